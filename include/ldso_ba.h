@@ -1,0 +1,222 @@
+/*
+ * ldso_ba.h -- C ABI of the MI355X-native LDSO photometric bundle-adjustment hot path.
+ *
+ * This header is the drop-in boundary.  It replaces, for the GPU, the C++ class surface
+ * the LDSO frontend drives once per Gauss-Newton iteration (reference paths are relative to
+ * n-lalanne/LDSO):
+ *
+ *   PointFrameResidual::linearize / applyRes / resetOOB      src/internal/Residuals.cc:15-217,
+ *                                                            include/internal/Residuals.h:61-88
+ *   FullSystem::linearizeAll(_Reductor), setNewFrameEnergyTH src/frontend/FullSystem.cc:1716-1823, 2078-2109
+ *   AccumulatedTopHessianSSE::addPoint<0> / stitchDoubleMT  src/internal/OptimizationBackend/AccumulatedTopHessian.cc:8-255
+ *   AccumulatedSCHessianSSE::addPoint / stitchDoubleMT      src/internal/OptimizationBackend/AccumulatedSCHessian.cc:9-177
+ *   EnergyFunctional::accumulate{AF,LF,SCF}_MT, solveSystemF, resubstituteF_MT
+ *                                                            src/internal/OptimizationBackend/EnergyFunctional.cc:280-471, 611-749
+ *   FrameFramePrecalc::Set, EnergyFunctional::setAdjointsF  src/internal/FrameFramePrecalc.cc:6-35,
+ *                                                            src/internal/OptimizationBackend/EnergyFunctional.cc:551-609
+ *
+ * Conventions (mirroring the reference):
+ *   - frame-pair index            pair = h + N*t      (AccumulatedTopHessian.cc:38)
+ *   - Hessian column blocks       [0,4) intrinsics, 4+8f+[0,6) xi_f, 4+8f+6 a_f, 4+8f+7 b_f
+ *   - residual states             IN = 0, OOB = 1, OUTLIER = 2 (Residuals.h:33)
+ *   - every matrix is row-major, every H is (8N+4)x(8N+4) double, every b is (8N+4) double.
+ *
+ * Error convention: every entry point returns 0 on success and a negative code on failure
+ * (never throws); ldso_ba_last_error() gives a message.  Non-finite numbers pass through as
+ * values, exactly as in the reference (the caller turns them into isLost).
+ * Threading: a context is bound to one HIP device and one HIP stream; entry points are not
+ * re-entrant (the reference runs them under FullSystem::mapMutex).
+ */
+#ifndef LDSO_BA_H_
+#define LDSO_BA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDSO_BA_ABI_VERSION 1
+
+#define LDSO_BA_PATTERN_NUM 8      /* patternNum, Settings.h:225 (staticPattern[8])     */
+#define LDSO_BA_CPARS 4            /* CPARS, NumTypes.h:25                              */
+#define LDSO_BA_MAX_FRAMES 16      /* window size supported by one context              */
+#define LDSO_BA_PRECALC_STRIDE 32  /* floats per FrameFramePrecalc record (see below)   */
+#define LDSO_BA_POINT_STRIDE 24    /* floats per PointHessian record (see below)        */
+
+/* Residual states, Residuals.h:33 */
+#define LDSO_BA_RES_IN 0
+#define LDSO_BA_RES_OOB 1
+#define LDSO_BA_RES_OUTLIER 2
+
+/* Residual flag bits */
+#define LDSO_BA_FLAG_ACTIVE 1u     /* PointFrameResidual::isActiveAndIsGoodNEW */
+#define LDSO_BA_FLAG_NEW 2u        /* PointFrameResidual::isNew                 */
+
+/*
+ * FrameFramePrecalc record (FrameFramePrecalc.h:35-44), LDSO_BA_PRECALC_STRIDE floats:
+ *   [0..8]  PRE_KRKiTll (3x3 row-major)   [9..11]  PRE_KtTll
+ *   [12..20] PRE_RTll_0 (3x3 row-major)   [21..23] PRE_tTll_0
+ *   [24..25] PRE_aff_mode                 [26]     PRE_b0_mode      [27..31] unused
+ *
+ * PointHessian record (PointHessian.h:83-131), LDSO_BA_POINT_STRIDE floats:
+ *   [0] u  [1] v  [2] idepth_scaled  [3] idepth_zero_scaled  [4] priorF  [5] deltaF
+ *   [6..7] unused  [8..15] color[8]  [16..23] weights[8]
+ */
+
+/* One sliding window (= one FullSystem / EnergyFunctional).  All pointers are host memory. */
+typedef struct ldso_ba_window {
+    int32_t n_frames;              /* N, 2 <= N <= LDSO_BA_MAX_FRAMES                        */
+    int32_t n_points;              /* P: EnergyFunctional::allPoints (makeIDX order)         */
+    int32_t n_residuals;           /* R: sum of PointHessian::residuals sizes                */
+    int32_t width, height;         /* wG[0], hG[0]                                           */
+    float calib[4];                /* CalibHessian::value_scaledf: fxl, fyl, cxl, cyl        */
+    const float *dI;               /* [N][height*width][3]: FrameHessian::dI = [I, dx, dy]   */
+    const float *frame_energy_th;  /* [N]: FrameHessian::frameEnergyTH                       */
+    const float *precalc;          /* [N*N][LDSO_BA_PRECALC_STRIDE], index h + N*t           */
+    const double *ad_host;         /* [N*N][64]: EnergyFunctional::adHost                    */
+    const double *ad_target;       /* [N*N][64]: EnergyFunctional::adTarget                  */
+    const double *c_prior;         /* [4]: EnergyFunctional::cPrior                          */
+    const float *c_delta;          /* [4]: EnergyFunctional::cDeltaF                         */
+    const double *frame_prior;     /* [N][8]: FrameHessian::prior                            */
+    const double *frame_delta_prior; /* [N][8]: FrameHessian::delta_prior                    */
+    const int32_t *point_host;     /* [P]: host frame index (FrameHessian::idx)              */
+    const float *point_data;       /* [P][LDSO_BA_POINT_STRIDE]                              */
+    const int32_t *point_res_begin;/* [P+1]: residuals of point p are [begin[p], begin[p+1]) */
+    const int32_t *res_target;     /* [R]: target frame index (PointFrameResidual::targetIDX)*/
+    const int8_t *res_state;       /* [R]: state_state                                       */
+    const float *res_energy;       /* [R]: state_energy                                      */
+    const uint8_t *res_flags;      /* [R]: LDSO_BA_FLAG_*                                    */
+} ldso_ba_window;
+
+/* Per-frame state needed by FrameFramePrecalc::Set / setAdjointsF / takeData. */
+typedef struct ldso_ba_frame_state {
+    double world_to_cam_evalpt[12]; /* FrameHessian::worldToCam_evalPT: R (3x3 row-major), t */
+    double state[10];               /* FrameHessian::state                                   */
+    double state_zero[10];          /* FrameHessian::state_zero                              */
+    double ab_exposure;             /* FrameHessian::ab_exposure                             */
+    int32_t is_first_frame;         /* frame->id == 0 (FrameHessian::getPrior)              */
+    int32_t pad_;
+} ldso_ba_frame_state;
+
+typedef struct ldso_ba_ctx ldso_ba_ctx;
+
+/* ---- host-side helpers (no GPU needed) ---------------------------------------------- */
+
+int ldso_ba_abi_version(void);
+const char *ldso_ba_last_error(void);
+
+/* FrameFramePrecalc::Set for every (h,t) pair and the per-frame PRE_worldToCam.
+ * precalc_out: [N*N][LDSO_BA_PRECALC_STRIDE] (index h + N*t).              FrameFramePrecalc.cc:6-35 */
+int ldso_ba_frame_precalc(int32_t n_frames, const ldso_ba_frame_state *frames, const float calib[4],
+                          float *precalc_out);
+
+/* EnergyFunctional::setAdjointsF (EnergyFunctional.cc:551-609): adHost/adTarget [N*N][64] and
+ * cPrior [4] (= setting_initialCalibHessian). */
+int ldso_ba_set_adjoints(int32_t n_frames, const ldso_ba_frame_state *frames, double *ad_host,
+                         double *ad_target, double *c_prior);
+
+/* FrameHessian::takeData (FrameHessian.cc:131-135): prior, delta, delta_prior [N][8]. */
+int ldso_ba_frame_take_data(int32_t n_frames, const ldso_ba_frame_state *frames, double *prior,
+                            double *delta, double *delta_prior);
+
+/* Solve assembly + Jacobi-scaled LDLT + optional nullspace projection, the non-VI branch of
+ * EnergyFunctional::solveSystemF (EnergyFunctional.cc:280-471).  Inputs are the stitched
+ * blocks; HM/bM may be NULL (no marginalisation prior).  nullspaces: [n_null][8N+4] column
+ * vectors (getNullspaces order) used when (iteration >= 2), may be NULL.  x_out: [8N+4]. */
+int ldso_ba_solve_system(int32_t n_frames, int32_t iteration, double lambda, const double *HA,
+                         const double *bA, const double *HL, const double *bL, const double *HM,
+                         const double *bM, const double *Hsc, const double *bsc,
+                         const double *nullspaces, int32_t n_null, double *x_out);
+
+/* FrameHessian::setStateZero nullspaces + FullSystem::getNullspaces (FullSystem.cc:2027-2076):
+ * out [7][8N+4] = the 6 pose nullspaces then the scale nullspace, the vectors
+ * EnergyFunctional::orthogonalize stacks (EnergyFunctional.cc:811-813). */
+int ldso_ba_nullspaces(int32_t n_frames, const ldso_ba_frame_state *frames, double *out);
+
+/* ---- device context --------------------------------------------------------------- */
+
+/* Create a context on HIP device `device` with its own non-blocking stream. */
+int ldso_ba_create(int32_t device, ldso_ba_ctx **out);
+void ldso_ba_destroy(ldso_ba_ctx *ctx);
+
+/* The HIP stream (hipStream_t) every kernel of this context is launched on. */
+void *ldso_ba_stream(ldso_ba_ctx *ctx);
+
+/* (Re)build the device mirror of n_windows windows (EnergyFunctional::insertFrame /
+ * insertResidual / dropResidual / makeIDX all end here).  shard_count > 1 keeps only the
+ * points with (p % shard_count) == shard_rank after host-frame ordering, for multi-GPU
+ * sharding (priors are then added by rank 0 only).  Every window must share width/height. */
+int ldso_ba_load(ldso_ba_ctx *ctx, int32_t n_windows, const ldso_ba_window *windows,
+                 int32_t shard_rank, int32_t shard_count);
+
+/* Refresh per-iteration state of window `win` after doStepFromBackup / setPrecalcValues:
+ * precalc, adjoints, priors, cDeltaF, frame_energy_th and point_data (idepth, deltaF).
+ * Structure (points, residual lists) must be unchanged. */
+int ldso_ba_update(ldso_ba_ctx *ctx, int32_t win, const ldso_ba_window *w);
+
+/* PointFrameResidual::resetOOB for every residual of window win (win < 0: all windows). */
+int ldso_ba_reset_oob(ldso_ba_ctx *ctx, int32_t win);
+
+/* One hot-path pass over all loaded windows, asynchronous on the context stream:
+ *   linearizeAll(fix) + applyRes(true) + setNewFrameEnergyTH, and if accumulate != 0
+ *   accumulateAF_MT + accumulateLF_MT + accumulateSCF_MT with both stitches.
+ * Mode-0 (active) accumulation uses the Jacobians of this same pass, exactly as the
+ * reference's solveSystemF uses those of the preceding linearizeAll + applyRes. */
+int ldso_ba_linearize(ldso_ba_ctx *ctx, int32_t fix, int32_t accumulate);
+
+int ldso_ba_sync(ldso_ba_ctx *ctx);
+
+/* Results of the last ldso_ba_linearize for window win (synchronising). */
+/* energy_out[3] = {sum of linearize() energies (double), 0, number of NewState == IN}.     */
+int ldso_ba_get_energy(ldso_ba_ctx *ctx, int32_t win, double *energy_out);
+/* Any output pointer may be NULL.  Sizes (8N+4)^2 and (8N+4). */
+int ldso_ba_get_system(ldso_ba_ctx *ctx, int32_t win, double *HA, double *bA, double *HL,
+                       double *bL, double *Hsc, double *bsc);
+/* Per residual, in the caller's point-major order. Any pointer may be NULL.
+ *   new_state/state [R], state_energy/new_energy_wo [R], center [R][3] (centerProjectedTo),
+ *   flags [R], jpjdf [R][8] (JpJdF), rel_bs [R] (linearizeAll_Reductor relBS, fix pass). */
+int ldso_ba_get_residuals(ldso_ba_ctx *ctx, int32_t win, int8_t *new_state, int8_t *state,
+                          float *state_energy, float *new_energy_wo, float *center,
+                          uint8_t *flags, float *jpjdf, float *rel_bs);
+/* Per point (caller order): HdiF, bdSumF, idepth_hessian, Hdd_accAF, bd_accAF, Hcd_accAF[4].
+ * Points with no active residual report HdiF = bdSumF = idepth_hessian = 0. */
+int ldso_ba_get_points(ldso_ba_ctx *ctx, int32_t win, float *HdiF, float *bdSumF,
+                       float *idepth_hessian, float *Hdd_acc, float *bd_acc, float *Hcd_acc);
+int ldso_ba_get_frame_energy_th(ldso_ba_ctx *ctx, int32_t win, float *th);
+
+/* solveSystemF on the stitched system of the last pass (get_system + ldso_ba_solve_system):
+ * priors come from the window's frame_prior / c_prior, HM = bM = 0. x_out [8N+4]. */
+int ldso_ba_solve(ldso_ba_ctx *ctx, int32_t win, int32_t iteration, double lambda,
+                  const double *nullspaces, int32_t n_null, double *x_out);
+
+/* EnergyFunctional::resubstituteF_MT (EnergyFunctional.cc:611-667) on the device for window
+ * win: x [8N+4], point_step_out [P] (PointHessian::step; NULL keeps it on the device). */
+int ldso_ba_resubstitute(ldso_ba_ctx *ctx, int32_t win, const double *x, double lambda,
+                         float *point_step_out);
+
+/* Device pointer of the packed per-window partial system used for multi-GPU all-reduce:
+ * [n_windows][sys_len] doubles, sys_len = 2*((8N+4)*(8N+5)/2 + (8N+4)) laid out as
+ * {HA upper-tri, bA, Hsc upper-tri, bsc}.  After an external all-reduce (sum) call
+ * ldso_ba_unpack_system so that get_system / solve read the reduced values. */
+int ldso_ba_packed_system(ldso_ba_ctx *ctx, void **dev_ptr, int64_t *n_doubles, int64_t *stride);
+int ldso_ba_unpack_system(ldso_ba_ctx *ctx);
+
+/* Per-kernel HIP-event timing (bench/profiling).  When enabled every kernel launch of
+ * ldso_ba_linearize is bracketed by events; get returns summed ms and launch counts for
+ * n_kernels <= 16 slots in the order of ldso_ba_kernel_name(i). */
+int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
+int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
+const char *ldso_ba_kernel_name(int32_t i);
+int32_t ldso_ba_num_kernels(void);
+
+/* Size of the device-resident data for the loaded windows (bytes) and total counts. */
+int ldso_ba_stats(ldso_ba_ctx *ctx, int64_t *device_bytes, int64_t *n_points,
+                  int64_t *n_residuals);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LDSO_BA_H_ */

@@ -1,0 +1,152 @@
+"""ctypes bindings of the C ABI in include/ldso_ba.h.
+
+The product path is the HIP library ``ldso_amd/lib/libldso_ba.so`` (built in-tree by
+``__graft_entry__.build()``).  There is no CPU fallback: if the library is missing the import
+fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libldso_ba.so")
+SYNTH_PATH = os.path.join(LIB_DIR, "libldso_synth.so")
+
+PATTERN_NUM = 8
+CPARS = 4
+MAX_FRAMES = 16
+PRECALC_STRIDE = 32
+POINT_STRIDE = 24
+RES_IN, RES_OOB, RES_OUTLIER = 0, 1, 2
+FLAG_ACTIVE, FLAG_NEW = 1, 2
+
+i32p = C.POINTER(C.c_int32)
+f32p = C.POINTER(C.c_float)
+f64p = C.POINTER(C.c_double)
+i8p = C.POINTER(C.c_int8)
+u8p = C.POINTER(C.c_uint8)
+i64p = C.POINTER(C.c_int64)
+
+FRAME_STATE_DTYPE = np.dtype(
+    [
+        ("world_to_cam_evalpt", np.float64, (12,)),
+        ("state", np.float64, (10,)),
+        ("state_zero", np.float64, (10,)),
+        ("ab_exposure", np.float64),
+        ("is_first_frame", np.int32),
+        ("pad_", np.int32),
+    ],
+    align=True,
+)
+assert FRAME_STATE_DTYPE.itemsize == 272
+
+
+class LdsoBaWindow(C.Structure):
+    _fields_ = [
+        ("n_frames", C.c_int32),
+        ("n_points", C.c_int32),
+        ("n_residuals", C.c_int32),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("calib", C.c_float * 4),
+        ("dI", f32p),
+        ("frame_energy_th", f32p),
+        ("precalc", f32p),
+        ("ad_host", f64p),
+        ("ad_target", f64p),
+        ("c_prior", f64p),
+        ("c_delta", f32p),
+        ("frame_prior", f64p),
+        ("frame_delta_prior", f64p),
+        ("point_host", i32p),
+        ("point_data", f32p),
+        ("point_res_begin", i32p),
+        ("res_target", i32p),
+        ("res_state", i8p),
+        ("res_energy", f32p),
+        ("res_flags", u8p),
+    ]
+
+
+def ptr(a, t):
+    if a is None:
+        return C.cast(None, t)
+    assert a.flags["C_CONTIGUOUS"], "arrays handed to the C ABI must be C-contiguous"
+    return a.ctypes.data_as(t)
+
+
+# (name, restype, argtypes) of every entry point declared in include/ldso_ba.h
+ABI = [
+    ("ldso_ba_abi_version", C.c_int, []),
+    ("ldso_ba_last_error", C.c_char_p, []),
+    ("ldso_ba_frame_precalc", C.c_int, [C.c_int32, C.c_void_p, f32p, f32p]),
+    ("ldso_ba_set_adjoints", C.c_int, [C.c_int32, C.c_void_p, f64p, f64p, f64p]),
+    ("ldso_ba_frame_take_data", C.c_int, [C.c_int32, C.c_void_p, f64p, f64p, f64p]),
+    ("ldso_ba_solve_system", C.c_int,
+     [C.c_int32, C.c_int32, C.c_double, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, C.c_int32, f64p]),
+    ("ldso_ba_nullspaces", C.c_int, [C.c_int32, C.c_void_p, f64p]),
+    ("ldso_ba_create", C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    ("ldso_ba_destroy", None, [C.c_void_p]),
+    ("ldso_ba_stream", C.c_void_p, [C.c_void_p]),
+    ("ldso_ba_load", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(LdsoBaWindow), C.c_int32, C.c_int32]),
+    ("ldso_ba_update", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(LdsoBaWindow)]),
+    ("ldso_ba_reset_oob", C.c_int, [C.c_void_p, C.c_int32]),
+    ("ldso_ba_linearize", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    ("ldso_ba_sync", C.c_int, [C.c_void_p]),
+    ("ldso_ba_get_energy", C.c_int, [C.c_void_p, C.c_int32, f64p]),
+    ("ldso_ba_get_system", C.c_int, [C.c_void_p, C.c_int32, f64p, f64p, f64p, f64p, f64p, f64p]),
+    ("ldso_ba_get_residuals", C.c_int, [C.c_void_p, C.c_int32, i8p, i8p, f32p, f32p, f32p, u8p, f32p, f32p]),
+    ("ldso_ba_get_points", C.c_int, [C.c_void_p, C.c_int32, f32p, f32p, f32p, f32p, f32p, f32p]),
+    ("ldso_ba_get_frame_energy_th", C.c_int, [C.c_void_p, C.c_int32, f32p]),
+    ("ldso_ba_solve", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_double, f64p, C.c_int32, f64p]),
+    ("ldso_ba_resubstitute", C.c_int, [C.c_void_p, C.c_int32, f64p, C.c_double, f32p]),
+    ("ldso_ba_packed_system", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), i64p, i64p]),
+    ("ldso_ba_unpack_system", C.c_int, [C.c_void_p]),
+    ("ldso_ba_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
+    ("ldso_ba_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),
+    ("ldso_ba_kernel_name", C.c_char_p, [C.c_int32]),
+    ("ldso_ba_num_kernels", C.c_int32, []),
+    ("ldso_ba_stats", C.c_int, [C.c_void_p, i64p, i64p, i64p]),
+]
+
+_lib = None
+_synth = None
+
+
+def lib():
+    """The product library.  Raises if it has not been built (no fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(make -C ldso_amd/csrc). The HIP path has no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in ABI:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(f"ldso_ba error {rc}: {lib().ldso_ba_last_error().decode()}")
+    return rc
+
+
+def synth_lib():
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise RuntimeError(f"{SYNTH_PATH} missing: run make -C ldso_amd/csrc")
+        S = C.CDLL(SYNTH_PATH)
+        S.ldso_synth_fill.restype = C.c_int
+        S.ldso_synth_fill.argtypes = [C.c_void_p, C.c_void_p, f32p, f32p, f32p, i32p, f32p, i32p, i32p, i8p, f32p, u8p]
+        _synth = S
+    return _synth

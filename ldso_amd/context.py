@@ -1,0 +1,143 @@
+"""Python face of the device context (one per FullSystem / group of windows).
+
+Mirrors the reference's per-iteration call sequence (FullSystem::optimize, FullSystem.cc:844-1007):
+
+    ctx.reset_oob()                         # PointFrameResidual::resetOOB for activeResiduals
+    ctx.linearize(fix=False)                # linearizeAll(false) + applyRes + accumulate{AF,LF,SCF}
+    x = ctx.solve(0, iteration, lam, ns)    # EnergyFunctional::solveSystemF (stitched system)
+    ctx.resubstitute(0, x, lam)             # resubstituteF_MT
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .window import Window
+
+
+class BAContext:
+    def __init__(self, device: int = 0):
+        self._lib = L.lib()
+        h = C.c_void_p()
+        L.check(self._lib.ldso_ba_create(int(device), C.byref(h)))
+        self._h = h
+        self.windows: list[Window] = []
+        self._structs = None
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.ldso_ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- structure ---------------------------------------------------------------------
+    def load(self, windows, shard_rank: int = 0, shard_count: int = 1):
+        if isinstance(windows, Window):
+            windows = [windows]
+        self.windows = list(windows)
+        structs = (L.LdsoBaWindow * len(self.windows))(*[w.c_struct() for w in self.windows])
+        L.check(self._lib.ldso_ba_load(self._h, len(self.windows), structs, int(shard_rank), int(shard_count)))
+        self._structs = structs
+        for w in self.windows:
+            w._keep = []  # host copies are no longer referenced by the device
+        return self
+
+    def update(self, win: int, window: Window):
+        s = window.c_struct()
+        L.check(self._lib.ldso_ba_update(self._h, int(win), C.byref(s)))
+
+    def reset_oob(self, win: int = -1):
+        L.check(self._lib.ldso_ba_reset_oob(self._h, int(win)))
+
+    # ---- hot path ----------------------------------------------------------------------
+    def linearize(self, fix: bool = False, accumulate: bool = True):
+        L.check(self._lib.ldso_ba_linearize(self._h, int(bool(fix)), int(bool(accumulate))))
+
+    def sync(self):
+        L.check(self._lib.ldso_ba_sync(self._h))
+
+    @property
+    def stream(self) -> int:
+        return int(self._lib.ldso_ba_stream(self._h) or 0)
+
+    # ---- results -----------------------------------------------------------------------
+    def energy(self, win: int = 0):
+        out = np.zeros(3, np.float64)
+        L.check(self._lib.ldso_ba_get_energy(self._h, int(win), L.ptr(out, L.f64p)))
+        return out
+
+    def system(self, win: int = 0) -> dict:
+        n = self.windows[win].dim
+        out = {k: np.zeros((n, n) if k.startswith("H") else n, np.float64) for k in ("HA", "bA", "HL", "bL", "Hsc", "bsc")}
+        L.check(self._lib.ldso_ba_get_system(self._h, int(win), *[L.ptr(out[k], L.f64p) for k in ("HA", "bA", "HL", "bL", "Hsc", "bsc")]))
+        return out
+
+    def residuals(self, win: int = 0) -> dict:
+        R = self.windows[win].n_residuals
+        o = dict(new_state=np.zeros(R, np.int8), state=np.zeros(R, np.int8), state_energy=np.zeros(R, np.float32),
+                 new_energy_wo=np.zeros(R, np.float32), center=np.zeros((R, 3), np.float32),
+                 flags=np.zeros(R, np.uint8), jpjdf=np.zeros((R, 8), np.float32), rel_bs=np.zeros(R, np.float32))
+        L.check(self._lib.ldso_ba_get_residuals(
+            self._h, int(win), L.ptr(o["new_state"], L.i8p), L.ptr(o["state"], L.i8p), L.ptr(o["state_energy"], L.f32p),
+            L.ptr(o["new_energy_wo"], L.f32p), L.ptr(o["center"], L.f32p), L.ptr(o["flags"], L.u8p),
+            L.ptr(o["jpjdf"], L.f32p), L.ptr(o["rel_bs"], L.f32p)))
+        return o
+
+    def points(self, win: int = 0) -> dict:
+        P = self.windows[win].n_points
+        o = dict(HdiF=np.zeros(P, np.float32), bdSumF=np.zeros(P, np.float32), idepth_hessian=np.zeros(P, np.float32),
+                 Hdd=np.zeros(P, np.float32), bd=np.zeros(P, np.float32), Hcd=np.zeros((P, 4), np.float32))
+        L.check(self._lib.ldso_ba_get_points(self._h, int(win), *[L.ptr(o[k], L.f32p) for k in
+                                                                  ("HdiF", "bdSumF", "idepth_hessian", "Hdd", "bd", "Hcd")]))
+        return o
+
+    def frame_energy_th(self, win: int = 0):
+        out = np.zeros(self.windows[win].n_frames, np.float32)
+        L.check(self._lib.ldso_ba_get_frame_energy_th(self._h, int(win), L.ptr(out, L.f32p)))
+        return out
+
+    def solve(self, win: int = 0, iteration: int = 0, lam: float = 1e-5, nullspaces=None):
+        x = np.zeros(self.windows[win].dim, np.float64)
+        ns = None if nullspaces is None else np.ascontiguousarray(nullspaces, np.float64)
+        L.check(self._lib.ldso_ba_solve(self._h, int(win), int(iteration), float(lam), L.ptr(ns, L.f64p),
+                                        0 if ns is None else ns.shape[0], L.ptr(x, L.f64p)))
+        return x
+
+    def resubstitute(self, win: int, x, lam: float = 1e-5, fetch: bool = True):
+        x = np.ascontiguousarray(x, np.float64)
+        step = np.zeros(self.windows[win].n_points, np.float32) if fetch else None
+        L.check(self._lib.ldso_ba_resubstitute(self._h, int(win), L.ptr(x, L.f64p), float(lam), L.ptr(step, L.f32p)))
+        return step
+
+    # ---- multi-GPU / profiling -----------------------------------------------------------
+    def packed_system(self):
+        p = C.c_void_p()
+        n = C.c_int64()
+        s = C.c_int64()
+        L.check(self._lib.ldso_ba_packed_system(self._h, C.byref(p), C.byref(n), C.byref(s)))
+        return int(p.value or 0), int(n.value), int(s.value)
+
+    def unpack_system(self):
+        L.check(self._lib.ldso_ba_unpack_system(self._h))
+
+    def set_kernel_timing(self, on: bool):
+        L.check(self._lib.ldso_ba_set_kernel_timing(self._h, int(bool(on))))
+
+    def kernel_times(self) -> dict:
+        n = int(self._lib.ldso_ba_num_kernels())
+        ms = np.zeros(n, np.float64)
+        cnt = np.zeros(n, np.int64)
+        L.check(self._lib.ldso_ba_get_kernel_times(self._h, L.ptr(ms, L.f64p), L.ptr(cnt, L.i64p), n))
+        return {self._lib.ldso_ba_kernel_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(n)}
+
+    def stats(self):
+        b, p, r = C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(self._lib.ldso_ba_stats(self._h, C.byref(b), C.byref(p), C.byref(r)))
+        return dict(device_bytes=b.value, points=p.value, residuals=r.value)

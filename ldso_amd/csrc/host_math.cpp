@@ -1,0 +1,421 @@
+// host_math.cpp -- host-side (double precision) pieces of the hot path that run once per
+// iteration on a handful of numbers: FrameFramePrecalc::Set, EnergyFunctional::setAdjointsF,
+// FrameHessian::takeData, getNullspaces and the solve of EnergyFunctional::solveSystemF.
+// They are O(N^2) or O((8N+4)^3) with N <= 16 and stay on the CPU next to the caller.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/ldso_ba.h"
+#include "ldso_ba_internal.h"
+
+namespace ldso_ba {
+
+namespace {
+
+constexpr double kScaleXiTrans = 0.5, kScaleXiRot = 1.0, kScaleA = 10.0, kScaleB = 1000.0;
+
+struct Mat3 {
+    double m[9];
+    double &operator()(int r, int c) { return m[r * 3 + c]; }
+    double operator()(int r, int c) const { return m[r * 3 + c]; }
+    static Mat3 eye() {
+        Mat3 a{};
+        a(0, 0) = a(1, 1) = a(2, 2) = 1;
+        return a;
+    }
+};
+Mat3 operator*(const Mat3 &a, const Mat3 &b) {
+    Mat3 c{};
+    for (int r = 0; r < 3; r++)
+        for (int k = 0; k < 3; k++)
+            for (int q = 0; q < 3; q++) c(r, q) += a(r, k) * b(k, q);
+    return c;
+}
+Mat3 skew(const double v[3]) {
+    Mat3 s{};
+    s(0, 1) = -v[2];
+    s(0, 2) = v[1];
+    s(1, 0) = v[2];
+    s(1, 2) = -v[0];
+    s(2, 0) = -v[1];
+    s(2, 1) = v[0];
+    return s;
+}
+
+struct Pose {  // rigid transform x -> R x + t (Sophus SE3 convention)
+    Mat3 R;
+    double t[3];
+    static Pose identity() {
+        Pose p;
+        p.R = Mat3::eye();
+        p.t[0] = p.t[1] = p.t[2] = 0;
+        return p;
+    }
+    Pose operator*(const Pose &b) const {
+        Pose c;
+        c.R = R * b.R;
+        for (int i = 0; i < 3; i++) c.t[i] = R(i, 0) * b.t[0] + R(i, 1) * b.t[1] + R(i, 2) * b.t[2] + t[i];
+        return c;
+    }
+    Pose inverse() const {
+        Pose c;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) c.R(i, j) = R(j, i);
+        for (int i = 0; i < 3; i++) c.t[i] = -(c.R(i, 0) * t[0] + c.R(i, 1) * t[1] + c.R(i, 2) * t[2]);
+        return c;
+    }
+    // exp of the tangent [upsilon(3), omega(3)] (thirdparty/Sophus/sophus/se3.hpp)
+    static Pose exp(const double xi[6]) {
+        const double *w = xi + 3;
+        double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2], th = std::sqrt(th2);
+        double a, b, c;
+        if (th < 1e-10) {
+            a = 1 - th2 / 6;
+            b = 0.5 - th2 / 24;
+            c = 1.0 / 6 - th2 / 120;
+        } else {
+            a = std::sin(th) / th;
+            b = (1 - std::cos(th)) / th2;
+            c = (th - std::sin(th)) / (th2 * th);
+        }
+        Mat3 W = skew(w), W2 = W * W, I = Mat3::eye();
+        Pose p;
+        Mat3 V;
+        for (int k = 0; k < 9; k++) {
+            p.R.m[k] = I.m[k] + a * W.m[k] + b * W2.m[k];
+            V.m[k] = I.m[k] + b * W.m[k] + c * W2.m[k];
+        }
+        for (int i = 0; i < 3; i++) p.t[i] = V(i, 0) * xi[0] + V(i, 1) * xi[1] + V(i, 2) * xi[2];
+        return p;
+    }
+    void log(double xi[6]) const {
+        double cs = std::max(-1.0, std::min(1.0, 0.5 * (R(0, 0) + R(1, 1) + R(2, 2) - 1)));
+        double th = std::acos(cs);
+        double f = th < 1e-10 ? 0.5 + th * th / 12 : th / (2 * std::sin(th));
+        double w[3] = {f * (R(2, 1) - R(1, 2)), f * (R(0, 2) - R(2, 0)), f * (R(1, 0) - R(0, 1))};
+        double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+        th = std::sqrt(th2);
+        double d = th < 1e-10 ? 1.0 / 12 + th2 / 720 : (1 - th * std::sin(th) / (2 * (1 - std::cos(th)))) / th2;
+        Mat3 W = skew(w), W2 = W * W;
+        for (int i = 0; i < 3; i++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += ((i == k ? 1.0 : 0.0) - 0.5 * W(i, k) + d * W2(i, k)) * t[k];
+            xi[i] = s;
+            xi[3 + i] = w[i];
+        }
+    }
+    // Adj = [R, [t]x R; 0, R]
+    void adjoint(double A[36]) const {
+        std::memset(A, 0, 36 * sizeof(double));
+        Mat3 tR = skew(t) * R;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                A[i * 6 + j] = R(i, j);
+                A[i * 6 + 3 + j] = tR(i, j);
+                A[(i + 3) * 6 + 3 + j] = R(i, j);
+            }
+    }
+};
+
+Pose eval_pose(const ldso_ba_frame_state &f) {
+    Pose p;
+    std::memcpy(p.R.m, f.world_to_cam_evalpt, 9 * sizeof(double));
+    std::memcpy(p.t, f.world_to_cam_evalpt + 9, 3 * sizeof(double));
+    return p;
+}
+// FrameHessian::setState (FrameHessian.h:95-114): PRE_worldToCam = exp(state_scaled[0:6]) * evalPT
+Pose current_pose(const ldso_ba_frame_state &f) {
+    double eps[6];
+    for (int i = 0; i < 6; i++) eps[i] = (i < 3 ? kScaleXiTrans : kScaleXiRot) * f.state[i];
+    return Pose::exp(eps) * eval_pose(f);
+}
+// AffLight::fromToVecExposure (include/AffLight.h:27-35), float arithmetic as in the reference
+void affine_from_to(float expF, float expT, float aF, float bF, float aT, float bT, float &a, float &b) {
+    if (expF == 0 || expT == 0) expF = expT = 1;
+    a = std::exp(aT - aF) * expT / expF;
+    b = bT - a * bF;
+}
+
+}  // namespace
+
+// FrameFramePrecalc::Set (src/internal/FrameFramePrecalc.cc:6-35) for all (h,t)
+int frame_precalc(int N, const ldso_ba_frame_state *fr, const float calib[4], float *out) {
+    const float fx = calib[0], fy = calib[1], cx = calib[2], cy = calib[3];
+    // K and Eigen's cofactor K.inverse() (InverseImpl.h, compute_inverse<.,.,3>)
+    const float K[9] = {fx, 0, cx, 0, fy, cy, 0, 0, 1};
+    const float invdet = 1.0f / (fy * fx);
+    const float Ki[9] = {fy * invdet, 0 * invdet, (0 * cy - cx * fy) * invdet,
+                         0 * invdet,  fx * invdet, (cx * 0 - fx * cy) * invdet,
+                         0 * invdet,  0 * invdet, (fx * fy - 0 * 0) * invdet};
+    std::vector<Pose> ev(N), cur(N);
+    for (int f = 0; f < N; f++) {
+        ev[f] = eval_pose(fr[f]);
+        cur[f] = current_pose(fr[f]);
+    }
+    for (int h = 0; h < N; h++) {
+        const Pose evInvH = ev[h].inverse(), curInvH = cur[h].inverse();
+        for (int t = 0; t < N; t++) {
+            float *o = out + (size_t)(h + N * t) * LDSO_BA_PRECALC_STRIDE;
+            std::memset(o, 0, LDSO_BA_PRECALC_STRIDE * sizeof(float));
+            const Pose l0 = ev[t] * evInvH;   // leftToLeft_0
+            const Pose l = cur[t] * curInvH;  // leftToLeft
+            float R[9], tt[3];
+            for (int k = 0; k < 9; k++) {
+                o[12 + k] = (float)l0.R.m[k];
+                R[k] = (float)l.R.m[k];
+            }
+            for (int k = 0; k < 3; k++) {
+                o[21 + k] = (float)l0.t[k];
+                tt[k] = (float)l.t[k];
+            }
+            float KR[9];
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++) KR[r * 3 + c] = K[r * 3] * R[c] + K[r * 3 + 1] * R[3 + c] + K[r * 3 + 2] * R[6 + c];
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++) o[r * 3 + c] = KR[r * 3] * Ki[c] + KR[r * 3 + 1] * Ki[3 + c] + KR[r * 3 + 2] * Ki[6 + c];
+            for (int r = 0; r < 3; r++) o[9 + r] = K[r * 3] * tt[0] + K[r * 3 + 1] * tt[1] + K[r * 3 + 2] * tt[2];
+            float a, b;
+            affine_from_to((float)fr[h].ab_exposure, (float)fr[t].ab_exposure, (float)(kScaleA * fr[h].state[6]),
+                           (float)(kScaleB * fr[h].state[7]), (float)(kScaleA * fr[t].state[6]),
+                           (float)(kScaleB * fr[t].state[7]), a, b);
+            o[24] = (float)(double)a;
+            o[25] = (float)(double)b;
+            o[26] = (float)(fr[h].state_zero[7] * kScaleB);  // PRE_b0_mode = aff_g2l_0().b
+        }
+    }
+    return 0;
+}
+
+// EnergyFunctional::setAdjointsF (EnergyFunctional.cc:551-609)
+int set_adjoints(int N, const ldso_ba_frame_state *fr, double *adH, double *adT, double *cPrior) {
+    std::vector<Pose> ev(N);
+    for (int f = 0; f < N; f++) ev[f] = eval_pose(fr[f]);
+    for (int h = 0; h < N; h++)
+        for (int t = 0; t < N; t++) {
+            double adj[36];
+            (ev[t] * ev[h].inverse()).adjoint(adj);
+            double *AH = adH + (size_t)(h + t * N) * 64, *AT = adT + (size_t)(h + t * N) * 64;
+            std::memset(AH, 0, 64 * sizeof(double));
+            std::memset(AT, 0, 64 * sizeof(double));
+            for (int i = 0; i < 8; i++) AH[i * 9] = AT[i * 9] = 1;
+            for (int r = 0; r < 6; r++)
+                for (int c = 0; c < 6; c++) AH[r * 8 + c] = -adj[c * 6 + r];  // -Adj^T
+            float a, b;
+            affine_from_to((float)fr[h].ab_exposure, (float)fr[t].ab_exposure, (float)(fr[h].state_zero[6] * kScaleA),
+                           (float)(fr[h].state_zero[7] * kScaleB), (float)(fr[t].state_zero[6] * kScaleA),
+                           (float)(fr[t].state_zero[7] * kScaleB), a, b);
+            (void)b;
+            AT[6 * 8 + 6] = -a;
+            AH[6 * 8 + 6] = a;
+            AT[7 * 8 + 7] = -1;
+            AH[7 * 8 + 7] = a;
+            const double rs[8] = {kScaleXiTrans, kScaleXiTrans, kScaleXiTrans, kScaleXiRot, kScaleXiRot, kScaleXiRot, kScaleA, kScaleB};
+            for (int r = 0; r < 8; r++)
+                for (int c = 0; c < 8; c++) {
+                    AH[r * 8 + c] *= rs[r];
+                    AT[r * 8 + c] *= rs[r];
+                }
+        }
+    if (cPrior)
+        for (int i = 0; i < 4; i++) cPrior[i] = kInitialCalibHessian;
+    return 0;
+}
+
+// FrameHessian::takeData / getPrior / get_state_minus_stateZero (FrameHessian.h:59-70,142-174)
+int frame_take_data(int N, const ldso_ba_frame_state *fr, double *prior, double *delta, double *delta_prior) {
+    for (int f = 0; f < N; f++) {
+        const ldso_ba_frame_state &F = fr[f];
+        double p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (F.is_first_frame) {
+            p[0] = p[1] = p[2] = kInitialTransPrior;
+            p[3] = p[4] = p[5] = kInitialRotPrior;
+            p[6] = kInitialAffAPrior;
+            p[7] = kInitialAffBPrior;
+        } else {
+            p[6] = kAffineOptModeA < 0 ? kInitialAffAPrior : kAffineOptModeA;
+            p[7] = kAffineOptModeB < 0 ? kInitialAffBPrior : kAffineOptModeB;
+        }
+        double mz[6], z[6], lg[6];
+        for (int i = 0; i < 6; i++) {
+            mz[i] = -F.state_zero[i];
+            z[i] = F.state[i];
+        }
+        if (prior) std::memcpy(prior + 8 * f, p, sizeof(p));
+        if (delta) {
+            (Pose::exp(mz) * Pose::exp(z)).log(lg);
+            for (int i = 0; i < 8; i++) delta[8 * f + i] = i < 6 ? lg[i] : F.state[i] - F.state_zero[i];
+        }
+        if (delta_prior) {
+            Pose::exp(z).log(lg);
+            for (int i = 0; i < 8; i++) delta_prior[8 * f + i] = i < 6 ? lg[i] : F.state[i];
+        }
+    }
+    return 0;
+}
+
+// FrameHessian::setStateZero nullspaces (FrameHessian.cc:26-57) + FullSystem::getNullspaces
+// (FullSystem.cc:2027-2076): out[7][8N+4] = pose x6 then scale, as orthogonalize() stacks them
+int nullspaces(int N, const ldso_ba_frame_state *fr, double *out) {
+    const int n = 8 * N + 4;
+    std::memset(out, 0, sizeof(double) * 7 * n);
+    const double unscale[6] = {1.0 / (double)0.5f, 1.0 / (double)0.5f, 1.0 / (double)0.5f, 1, 1, 1};
+    for (int f = 0; f < N; f++) {
+        Pose E = eval_pose(fr[f]), Ei = E.inverse();
+        for (int i = 0; i < 6; i++) {
+            double ep[6] = {0, 0, 0, 0, 0, 0}, em[6] = {0, 0, 0, 0, 0, 0}, lp[6], lm[6];
+            ep[i] = 1e-3;
+            em[i] = -1e-3;
+            ((E * Pose::exp(ep)) * Ei).log(lp);
+            ((E * Pose::exp(em)) * Ei).log(lm);
+            for (int k = 0; k < 6; k++) out[(size_t)i * n + 4 + 8 * f + k] = (lp[k] - lm[k]) / 2e-3 * unscale[k];
+        }
+        Pose P = E, M = E;
+        for (int k = 0; k < 3; k++) {
+            P.t[k] *= 1.00001;
+            M.t[k] /= 1.00001;
+        }
+        double lp[6], lm[6];
+        (P * Ei).log(lp);
+        (M * Ei).log(lm);
+        for (int k = 0; k < 6; k++) out[(size_t)6 * n + 4 + 8 * f + k] = (lp[k] - lm[k]) / 2e-3 * unscale[k];
+    }
+    return 0;
+}
+
+namespace {
+// In-place LDL^T with symmetric diagonal pivoting (Eigen::LDLT's strategy), then solve.
+void ldlt_solve(int n, std::vector<double> &A, std::vector<double> &b) {
+    std::vector<int> perm(n);
+    for (int i = 0; i < n; i++) perm[i] = i;
+    auto at = [&](int r, int c) -> double & { return A[(size_t)r * n + c]; };
+    for (int k = 0; k < n; k++) {
+        int piv = k;
+        for (int i = k + 1; i < n; i++)
+            if (std::fabs(at(i, i)) > std::fabs(at(piv, piv))) piv = i;
+        if (piv != k) {
+            std::swap(perm[k], perm[piv]);
+            for (int j = 0; j < n; j++) std::swap(at(k, j), at(piv, j));
+            for (int j = 0; j < n; j++) std::swap(at(j, k), at(j, piv));
+        }
+        const double d = at(k, k);
+        for (int i = k + 1; i < n; i++) {
+            const double l = d != 0 ? at(i, k) / d : 0.0;
+            for (int j = k + 1; j <= i; j++) at(i, j) -= l * at(j, k);
+            at(i, k) = l;
+        }
+        for (int i = k + 1; i < n; i++)
+            for (int j = k + 1; j < i; j++) at(j, i) = at(i, j);
+    }
+    std::vector<double> y(n);
+    for (int i = 0; i < n; i++) y[i] = b[perm[i]];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < i; j++) y[i] -= at(i, j) * y[j];
+    for (int i = 0; i < n; i++) y[i] = at(i, i) != 0 ? y[i] / at(i, i) : 0.0;
+    for (int i = n - 1; i >= 0; i--)
+        for (int j = i + 1; j < n; j++) y[i] -= at(j, i) * y[j];
+    for (int i = 0; i < n; i++) b[perm[i]] = y[i];
+}
+
+// x -= N (N^T N)^+ N^T x with columns normalised and singular values below
+// setting_solverModeDelta * max cut (EnergyFunctional::orthogonalize, EnergyFunctional.cc:809-841)
+void project_out(int n, const double *ns, int k, std::vector<double> &x) {
+    std::vector<double> Nm((size_t)n * k);
+    for (int c = 0; c < k; c++) {
+        double s = 0;
+        for (int i = 0; i < n; i++) s += ns[(size_t)c * n + i] * ns[(size_t)c * n + i];
+        s = std::sqrt(s);
+        for (int i = 0; i < n; i++) Nm[(size_t)i * k + c] = ns[(size_t)c * n + i] / s;
+    }
+    std::vector<double> G((size_t)k * k, 0.0), V((size_t)k * k, 0.0);
+    for (int a = 0; a < k; a++)
+        for (int c = 0; c < k; c++)
+            for (int i = 0; i < n; i++) G[(size_t)a * k + c] += Nm[(size_t)i * k + a] * Nm[(size_t)i * k + c];
+    for (int i = 0; i < k; i++) V[(size_t)i * k + i] = 1;
+    for (int sweep = 0; sweep < 64; sweep++) {  // cyclic Jacobi
+        double off = 0;
+        for (int p = 0; p < k; p++)
+            for (int q = p + 1; q < k; q++) off += G[(size_t)p * k + q] * G[(size_t)p * k + q];
+        if (off < 1e-30) break;
+        for (int p = 0; p < k; p++)
+            for (int q = p + 1; q < k; q++) {
+                const double apq = G[(size_t)p * k + q];
+                if (apq == 0) continue;
+                const double th = (G[(size_t)q * k + q] - G[(size_t)p * k + p]) / (2 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1));
+                const double c = 1 / std::sqrt(t * t + 1), s = t * c;
+                for (int r = 0; r < k; r++) {
+                    double gp = G[(size_t)r * k + p], gq = G[(size_t)r * k + q];
+                    G[(size_t)r * k + p] = c * gp - s * gq;
+                    G[(size_t)r * k + q] = s * gp + c * gq;
+                }
+                for (int r = 0; r < k; r++) {
+                    double gp = G[(size_t)p * k + r], gq = G[(size_t)q * k + r];
+                    G[(size_t)p * k + r] = c * gp - s * gq;
+                    G[(size_t)q * k + r] = s * gp + c * gq;
+                }
+                for (int r = 0; r < k; r++) {
+                    double vp = V[(size_t)r * k + p], vq = V[(size_t)r * k + q];
+                    V[(size_t)r * k + p] = c * vp - s * vq;
+                    V[(size_t)r * k + q] = s * vp + c * vq;
+                }
+            }
+    }
+    double smax = 0;
+    for (int e = 0; e < k; e++) smax = std::max(smax, std::sqrt(std::max(0.0, G[(size_t)e * k + e])));
+    std::vector<double> ntx(k, 0.0), coef(k, 0.0);
+    for (int a = 0; a < k; a++)
+        for (int i = 0; i < n; i++) ntx[a] += Nm[(size_t)i * k + a] * x[i];
+    for (int e = 0; e < k; e++) {
+        const double ev = G[(size_t)e * k + e];
+        if (!(std::sqrt(std::max(0.0, ev)) > kSolverModeDelta * smax)) continue;
+        double proj = 0;
+        for (int a = 0; a < k; a++) proj += V[(size_t)a * k + e] * ntx[a];
+        for (int a = 0; a < k; a++) coef[a] += V[(size_t)a * k + e] * proj / ev;
+    }
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int a = 0; a < k; a++) s += Nm[(size_t)i * k + a] * coef[a];
+        x[i] -= s;
+    }
+}
+}  // namespace
+
+// EnergyFunctional::solveSystemF, non-VI / FIX_LAMBDA / ORTHOGONALIZE_X_LATER branch
+// (EnergyFunctional.cc:282-283, 310, 342-378, 413-432)
+int solve_system(int N, int iteration, double lambda, const double *HA, const double *bA, const double *HL,
+                 const double *bL, const double *HM, const double *bM, const double *Hsc, const double *bsc,
+                 const double *ns, int n_null, double *x_out) {
+    const int n = 8 * N + 4;
+    (void)lambda;
+    lambda = 1e-5;  // SOLVER_FIX_LAMBDA
+    std::vector<double> H((size_t)n * n), b(n);
+    for (int i = 0; i < n; i++) {
+        for (int j = i; j < n; j++) {
+            const size_t q = (size_t)i * n + j;
+            H[q] = HL[q] + (HM ? HM[q] : 0.0) + HA[q];
+        }
+        b[i] = bL[i] + (bM ? bM[i] : 0.0) + bA[i] - bsc[i] / (1 + lambda);
+    }
+    for (int i = 0; i < n; i++) H[(size_t)i * n + i] *= (1 + lambda);
+    const double sc = 1.0f / (1 + lambda);
+    for (int i = 0; i < n; i++)
+        for (int j = i; j < n; j++) H[(size_t)i * n + j] -= Hsc[(size_t)i * n + j] * sc;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < i; j++) H[(size_t)i * n + j] = H[(size_t)j * n + i];
+    std::vector<double> s(n);
+    for (int i = 0; i < n; i++) s[i] = 1.0 / std::sqrt(H[(size_t)i * n + i] + 10);
+    for (int i = 0; i < n; i++) {
+        b[i] *= s[i];
+        for (int j = 0; j < n; j++) H[(size_t)i * n + j] *= s[i] * s[j];
+    }
+    ldlt_solve(n, H, b);
+    std::vector<double> x(n);
+    for (int i = 0; i < n; i++) x[i] = s[i] * b[i];
+    if (iteration >= 2 && ns && n_null > 0) project_out(n, ns, n_null, x);
+    std::memcpy(x_out, x.data(), n * sizeof(double));
+    return 0;
+}
+
+}  // namespace ldso_ba

@@ -1,0 +1,269 @@
+// synth.cpp -- seeded synthetic sliding windows for tests and bench (not part of the hot path).
+//
+// A window is N keyframes looking at one textured, tilted plane, rendered with per-frame
+// affine brightness (I_f = exp(a_f) * T + b_f, the model of AffLight, include/AffLight.h:27-35),
+// so residuals of correctly-placed points are photo-consistent and mostly inliers, like a real
+// DSO window.  Images follow FrameHessian::makeImages (src/internal/FrameHessian.cc:59-115);
+// point colours/weights follow ImmaturePoint::ImmaturePoint (src/internal/ImmaturePoint.cc:21-36)
+// via getInterpolatedElement33BiLin (include/internal/GlobalFuncs.h:185-207).
+//
+// The caller allocates every output (sizes are functions of N, P, w, h); R = P * (N - 1).
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/ldso_ba.h"
+
+namespace {
+
+struct Rng {  // splitmix64 + uniform helpers: fully deterministic across platforms
+    uint64_t s;
+    explicit Rng(uint64_t seed) : s(seed * 0x9E3779B97F4A7C15ull + 0x1D50ull) {}
+    uint64_t next() {
+        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    double uni() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+    double uni(double a, double b) { return a + (b - a) * uni(); }
+    double gauss() {
+        double u1 = uni(), u2 = uni();
+        if (u1 < 1e-300) u1 = 1e-300;
+        return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+    }
+};
+
+void rodrigues(const double w[3], double R[9]) {
+    double th = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    double k[3] = {0, 0, 1};
+    if (th > 1e-15) {
+        k[0] = w[0] / th;
+        k[1] = w[1] / th;
+        k[2] = w[2] / th;
+    }
+    double c = std::cos(th), s = std::sin(th), C = 1 - c;
+    R[0] = c + k[0] * k[0] * C;
+    R[1] = k[0] * k[1] * C - k[2] * s;
+    R[2] = k[0] * k[2] * C + k[1] * s;
+    R[3] = k[1] * k[0] * C + k[2] * s;
+    R[4] = c + k[1] * k[1] * C;
+    R[5] = k[1] * k[2] * C - k[0] * s;
+    R[6] = k[2] * k[0] * C - k[1] * s;
+    R[7] = k[2] * k[1] * C + k[0] * s;
+    R[8] = c + k[2] * k[2] * C;
+}
+
+struct Texture {
+    int n;
+    double extent;  // texture covers [-extent, extent]^2 metres of plane (X, Y)
+    std::vector<float> t;
+    float sample(double X, double Y) const {
+        double fx = (X + extent) / (2 * extent) * (n - 1), fy = (Y + extent) / (2 * extent) * (n - 1);
+        if (fx < 0) fx = 0;
+        if (fy < 0) fy = 0;
+        if (fx > n - 1.001) fx = n - 1.001;
+        if (fy > n - 1.001) fy = n - 1.001;
+        int ix = (int)fx, iy = (int)fy;
+        double dx = fx - ix, dy = fy - iy;
+        const float *p = &t[(size_t)iy * n + ix];
+        return (float)((1 - dx) * (1 - dy) * p[0] + dx * (1 - dy) * p[1] + (1 - dx) * dy * p[n] + dx * dy * p[n + 1]);
+    }
+};
+
+Texture make_texture(Rng &rng) {
+    Texture T;
+    T.n = 1024;
+    T.extent = 3.0;
+    const int n = T.n;
+    T.t.assign((size_t)n * n, 128.0f);
+    // coarse uniform noise (+-30) bilinearly upsampled (1/8 resolution)
+    const int g = n / 8 + 2;
+    std::vector<float> coarse((size_t)g * g);
+    for (auto &c : coarse) c = (float)rng.uni(-30, 30);
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) {
+            double fx = x / 8.0, fy = y / 8.0;
+            int ix = (int)fx, iy = (int)fy;
+            double dx = fx - ix, dy = fy - iy;
+            const float *p = &coarse[(size_t)iy * g + ix];
+            T.t[(size_t)y * n + x] += (float)((1 - dx) * (1 - dy) * p[0] + dx * (1 - dy) * p[1] + (1 - dx) * dy * p[g] + dx * dy * p[g + 1]);
+        }
+    // Gaussian blobs, sigma 3..34 texels, amplitude +-(20..120)
+    for (int b = 0; b < 600; b++) {
+        double cx = rng.uni(0, n), cy = rng.uni(0, n);
+        double sg = rng.uni(3.4, 34.0);
+        double amp = rng.uni(20, 120) * (rng.uni() < 0.5 ? -1 : 1);
+        int r = (int)(3 * sg) + 1;
+        int x0 = std::max(0, (int)cx - r), x1 = std::min(n - 1, (int)cx + r);
+        int y0 = std::max(0, (int)cy - r), y1 = std::min(n - 1, (int)cy + r);
+        double inv = 1.0 / (2 * sg * sg);
+        for (int y = y0; y <= y1; y++)
+            for (int x = x0; x <= x1; x++) {
+                double d2 = (x - cx) * (x - cx) + (y - cy) * (y - cy);
+                T.t[(size_t)y * n + x] += (float)(amp * std::exp(-d2 * inv));
+            }
+    }
+    return T;
+}
+
+// getInterpolatedElement33BiLin: include/internal/GlobalFuncs.h:185-207
+void interp33bilin(const float *mat, float x, float y, int width, float out[3]) {
+    int ix = (int)x;
+    int iy = (int)y;
+    const float *bp = mat + 3 * ((size_t)ix + (size_t)iy * width);
+    float tl = bp[0];
+    float tr = bp[3];
+    float bl = bp[3 * width];
+    float br = bp[3 * width + 3];
+    float dx = x - ix;
+    float dy = y - iy;
+    float topInt = dx * tr + (1 - dx) * tl;
+    float botInt = dx * br + (1 - dx) * bl;
+    float leftInt = dy * bl + (1 - dy) * tl;
+    float rightInt = dy * br + (1 - dy) * tr;
+    out[0] = dx * rightInt + (1 - dx) * leftInt;
+    out[1] = rightInt - leftInt;
+    out[2] = botInt - topInt;
+}
+
+}  // namespace
+
+extern "C" {
+
+typedef struct ldso_synth_params {
+    int32_t n_frames;
+    int32_t n_points;
+    int32_t width;
+    int32_t height;
+    uint64_t seed;
+    float outlier_frac;     /* fraction of points with a grossly wrong idepth      */
+    float idepth_noise;     /* relative gaussian noise on inlier idepths           */
+    float newest_perturb;   /* pose perturbation of the newest frame's state (rad/m) */
+    float baseline;         /* camera travel per keyframe along x (m)              */
+} ldso_synth_params;
+
+/* Fills a synthetic window.  Output sizes:
+ *   frames[N], dI[N*h*w*3], calib[4], frame_energy_th[N], point_host[P],
+ *   point_data[P*LDSO_BA_POINT_STRIDE], point_res_begin[P+1], res_target[R], res_state[R],
+ *   res_energy[R], res_flags[R] with R = P*(N-1).  Returns 0 on success. */
+int ldso_synth_fill(const ldso_synth_params *prm, ldso_ba_frame_state *frames, float *dI,
+                    float *calib, float *frame_energy_th, int32_t *point_host, float *point_data,
+                    int32_t *point_res_begin, int32_t *res_target, int8_t *res_state,
+                    float *res_energy, uint8_t *res_flags) {
+    const int N = prm->n_frames, P = prm->n_points, w = prm->width, h = prm->height;
+    if (N < 2 || N > LDSO_BA_MAX_FRAMES || P < 0 || w < 32 || h < 32) return -1;
+    Rng rng(prm->seed);
+    // EuRoC output intrinsics (examples/EUROC/EUROC.txt: 0.6 0.9 0.5 0.5 relative)
+    const double fx = 0.6 * w, fy = 0.9 * h, cx = 0.5 * w - 0.5, cy = 0.5 * h - 0.5;
+    calib[0] = (float)fx;
+    calib[1] = (float)fy;
+    calib[2] = (float)cx;
+    calib[3] = (float)cy;
+    // plane Z = Z0 + gx X + gy Y (world = first keyframe's camera)
+    const double Z0 = rng.uni(1.8, 2.4), gxp = rng.uni(-0.2, 0.2), gyp = rng.uni(-0.2, 0.2);
+    Texture tex = make_texture(rng);
+    std::vector<double> Rwc((size_t)N * 9), Cw((size_t)N * 3), affa(N), affb(N);
+    const double base = prm->baseline > 0 ? prm->baseline : 0.04;
+    for (int f = 0; f < N; f++) {
+        double om[3] = {0.01 * f + rng.uni(-0.002, 0.002), 0.02 * std::sin((double)f) + rng.uni(-0.002, 0.002), 0.005 * f};
+        rodrigues(om, &Rwc[f * 9]);
+        Cw[f * 3 + 0] = base * f + rng.uni(-0.005, 0.005);
+        Cw[f * 3 + 1] = 0.01 * std::sin((double)f);
+        Cw[f * 3 + 2] = 0.02 * f;
+        affa[f] = rng.uni(-0.05, 0.05);
+        affb[f] = rng.uni(-5, 5);
+        if (f == 0) affa[f] = affb[f] = 0;
+    }
+    for (int f = 0; f < N; f++) {
+        ldso_ba_frame_state &F = frames[f];
+        std::memset(&F, 0, sizeof(F));
+        const double *R = &Rwc[f * 9], *C = &Cw[f * 3];
+        // worldToCam: R^T, -R^T C
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) F.world_to_cam_evalpt[i * 3 + j] = R[j * 3 + i];
+        for (int i = 0; i < 3; i++)
+            F.world_to_cam_evalpt[9 + i] = -(R[0 * 3 + i] * C[0] + R[1 * 3 + i] * C[1] + R[2 * 3 + i] * C[2]);
+        F.state[6] = affa[f] / 10.0;   // aff_g2l().a = SCALE_A * state[6]
+        F.state[7] = affb[f] / 1000.0; // aff_g2l().b = SCALE_B * state[7]
+        for (int i = 0; i < 10; i++) F.state_zero[i] = F.state[i];
+        F.ab_exposure = 1.0;
+        F.is_first_frame = (f == 0);
+        if (f == N - 1 && prm->newest_perturb > 0)
+            for (int i = 0; i < 6; i++) F.state[i] = rng.uni(-prm->newest_perturb, prm->newest_perturb);
+        frame_energy_th[f] = 8 * 8 * 8;  // FrameHessian.h:194
+    }
+    // render + makeImages gradients
+    for (int f = 0; f < N; f++) {
+        const double *R = &Rwc[f * 9], *C = &Cw[f * 3];
+        float *img = dI + (size_t)f * w * h * 3;
+        const double ea = std::exp(affa[f]);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                double dc[3] = {(x - cx) / fx, (y - cy) / fy, 1.0};
+                double dw[3];
+                for (int i = 0; i < 3; i++) dw[i] = R[i * 3] * dc[0] + R[i * 3 + 1] * dc[1] + R[i * 3 + 2] * dc[2];
+                double s = (Z0 + gxp * C[0] + gyp * C[1] - C[2]) / (dw[2] - gxp * dw[0] - gyp * dw[1]);
+                double X = C[0] + s * dw[0], Y = C[1] + s * dw[1];
+                double I = ea * tex.sample(X, Y) + affb[f];
+                if (I < 0) I = 0;
+                if (I > 255) I = 255;
+                img[3 * ((size_t)y * w + x)] = (float)I;
+            }
+        for (size_t i = 0; i < (size_t)w * h; i++) img[3 * i + 1] = img[3 * i + 2] = 0;
+        for (int idx = w; idx < w * (h - 1); idx++) {  // FrameHessian.cc:96-105
+            float ddx = 0.5f * (img[3 * (idx + 1)] - img[3 * (idx - 1)]);
+            float ddy = 0.5f * (img[3 * (idx + w)] - img[3 * (idx - w)]);
+            if (std::isnan(ddx) || std::fabs(ddx) > 255.0) ddx = 0;
+            if (std::isnan(ddy) || std::fabs(ddy) > 255.0) ddy = 0;
+            img[3 * idx + 1] = ddx;
+            img[3 * idx + 2] = ddy;
+        }
+    }
+    // points
+    int rcount = 0;
+    for (int p = 0; p < P; p++) {
+        int hf = (int)(rng.uni() * N);
+        if (hf >= N) hf = N - 1;
+        point_host[p] = hf;
+        double u = rng.uni(8, w - 9), v = rng.uni(8, h - 9);
+        const double *R = &Rwc[hf * 9], *C = &Cw[hf * 3];
+        double dc[3] = {(u - cx) / fx, (v - cy) / fy, 1.0};
+        double dw[3];
+        for (int i = 0; i < 3; i++) dw[i] = R[i * 3] * dc[0] + R[i * 3 + 1] * dc[1] + R[i * 3 + 2] * dc[2];
+        double s = (Z0 + gxp * C[0] + gyp * C[1] - C[2]) / (dw[2] - gxp * dw[0] - gyp * dw[1]);
+        double idepth = 1.0 / s;  // camera-frame depth of the ray point is s (dc.z = 1)
+        if (rng.uni() < prm->outlier_frac) idepth *= rng.uni(0.5, 1.6);
+        else idepth *= 1.0 + prm->idepth_noise * rng.gauss();
+        float *d = point_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+        std::memset(d, 0, LDSO_BA_POINT_STRIDE * sizeof(float));
+        d[0] = (float)u;
+        d[1] = (float)v;
+        d[2] = (float)idepth;  // idepth_scaled = SCALE_IDEPTH * idepth
+        d[3] = (float)idepth;  // idepth_zero_scaled
+        d[4] = 0.0f;           // priorF (hasDepthPrior = false)
+        d[5] = 0.0f;           // deltaF = idepth - idepth_zero
+        const float *himg = dI + (size_t)hf * w * h * 3;
+        for (int i = 0; i < LDSO_BA_PATTERN_NUM; i++) {
+            static const int pat[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};
+            float ptc[3];
+            interp33bilin(himg, d[0] + pat[i][0], d[1] + pat[i][1], w, ptc);
+            d[8 + i] = ptc[0];
+            d[16 + i] = sqrtf(2500.0f / (2500.0f + (ptc[1] * ptc[1] + ptc[2] * ptc[2])));
+        }
+        point_res_begin[p] = rcount;
+        for (int t = 0; t < N; t++) {
+            if (t == hf) continue;
+            res_target[rcount] = t;
+            res_state[rcount] = LDSO_BA_RES_IN;  // resetOOB(): state_state = IN
+            res_energy[rcount] = 0;
+            res_flags[rcount] = LDSO_BA_FLAG_NEW;
+            rcount++;
+        }
+    }
+    point_res_begin[P] = rcount;
+    return 0;
+}
+
+}  // extern "C"

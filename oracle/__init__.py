@@ -1,0 +1,200 @@
+"""CPU restatement of LDSO's photometric-BA hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package,
+and only as the checker / CPU baseline.  The product path (ldso_amd) never touches it.
+
+Parity status: "parity unpinned" by the reference (n-lalanne/LDSO ships no golden vectors for
+this path and cannot be built here: Eigen3/glog/OpenCV/g2o/DBoW3 are absent).  The restatement
+is pinned by independent known-answer tests (tests/test_oracle_kat.py).  See ldso_oracle.cpp
+for the reference file:line of every function.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libldso_oracle.so")
+
+i32p = C.POINTER(C.c_int32)
+f32p = C.POINTER(C.c_float)
+f64p = C.POINTER(C.c_double)
+i8p = C.POINTER(C.c_int8)
+u8p = C.POINTER(C.c_uint8)
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        Lb = C.CDLL(LIB_PATH)
+        sig = {
+            "oracle_set_threads": (None, [C.c_int]),
+            "oracle_get_threads": (C.c_int, []),
+            "oracle_create": (C.c_void_p, [C.c_void_p]),
+            "oracle_destroy": (None, [C.c_void_p]),
+            "oracle_update": (C.c_int, [C.c_void_p, C.c_void_p]),
+            "oracle_reset_oob": (None, [C.c_void_p]),
+            "oracle_linearize_all": (C.c_int, [C.c_void_p, C.c_int, f64p]),
+            "oracle_apply_res": (None, [C.c_void_p]),
+            "oracle_accumulate": (C.c_int, [C.c_void_p, f64p, f64p, f64p, f64p, f64p, f64p]),
+            "oracle_iteration": (C.c_int, [C.c_void_p, f64p]),
+            "oracle_get_residuals": (None, [C.c_void_p, i8p, i8p, f32p, f32p, f32p, u8p, f32p, f32p]),
+            "oracle_get_jacobians": (None, [C.c_void_p, f32p]),
+            "oracle_get_points": (None, [C.c_void_p, f32p, f32p, f32p, f32p, f32p, f32p]),
+            "oracle_get_frame_energy_th": (None, [C.c_void_p, f32p]),
+            "oracle_solve_system": (C.c_int, [C.c_int, C.c_int, C.c_double] + [f64p] * 9 + [C.c_int, f64p]),
+            "oracle_resubstitute": (None, [C.c_void_p, f64p, C.c_double, f32p]),
+            "oracle_frame_precalc": (C.c_int, [C.c_int, C.c_void_p, f32p, f32p]),
+            "oracle_set_adjoints": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p]),
+            "oracle_frame_take_data": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p]),
+            "oracle_nullspaces": (C.c_int, [C.c_int, C.c_void_p, f64p]),
+            "oracle_time_iterations": (C.c_double, [C.c_void_p, C.c_int]),
+        }
+        for k, (res, args) in sig.items():
+            f = getattr(Lb, k)
+            f.restype = res
+            f.argtypes = args
+        _lib = Lb
+    return _lib
+
+
+def _p(a, t):
+    if a is None:
+        return C.cast(None, t)
+    return a.ctypes.data_as(t)
+
+
+def set_threads(n: int):
+    lib().oracle_set_threads(int(n))
+
+
+class OracleWindow:
+    """EnergyFunctional + FullSystem::linearizeAll restated on the CPU for one window."""
+
+    def __init__(self, window, threads=None):
+        if threads is not None:
+            set_threads(threads)
+        self.window = window
+        s = window.c_struct()
+        self._h = lib().oracle_create(C.byref(s))
+        if not self._h:
+            raise ValueError("oracle_create rejected the window")
+        window._keep = []
+
+    def close(self):
+        if self._h:
+            lib().oracle_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def update(self, window):
+        s = window.c_struct()
+        rc = lib().oracle_update(self._h, C.byref(s))
+        window._keep = []
+        assert rc == 0
+
+    def reset_oob(self):
+        lib().oracle_reset_oob(self._h)
+
+    def linearize_all(self, fix=False):
+        out = np.zeros(3, np.float64)
+        lib().oracle_linearize_all(self._h, int(bool(fix)), _p(out, f64p))
+        return out
+
+    def apply_res(self):
+        lib().oracle_apply_res(self._h)
+
+    def accumulate(self) -> dict:
+        n = self.window.dim
+        out = {k: np.zeros((n, n) if k.startswith("H") else n, np.float64) for k in ("HA", "bA", "HL", "bL", "Hsc", "bsc")}
+        lib().oracle_accumulate(self._h, *[_p(out[k], f64p) for k in ("HA", "bA", "HL", "bL", "Hsc", "bsc")])
+        return out
+
+    def iteration(self):
+        """linearizeAll(false) + applyRes + accumulate: the same pass as ldso_ba_linearize(0, 1)."""
+        e = self.linearize_all(False)
+        self.apply_res()
+        sysm = self.accumulate()
+        return e, sysm
+
+    def residuals(self) -> dict:
+        R = self.window.n_residuals
+        o = dict(new_state=np.zeros(R, np.int8), state=np.zeros(R, np.int8), state_energy=np.zeros(R, np.float32),
+                 new_energy_wo=np.zeros(R, np.float32), center=np.zeros((R, 3), np.float32),
+                 flags=np.zeros(R, np.uint8), jpjdf=np.zeros((R, 8), np.float32), rel_bs=np.zeros(R, np.float32))
+        lib().oracle_get_residuals(self._h, _p(o["new_state"], i8p), _p(o["state"], i8p), _p(o["state_energy"], f32p),
+                                   _p(o["new_energy_wo"], f32p), _p(o["center"], f32p), _p(o["flags"], u8p),
+                                   _p(o["jpjdf"], f32p), _p(o["rel_bs"], f32p))
+        return o
+
+    def jacobians(self) -> np.ndarray:
+        out = np.zeros((self.window.n_residuals, 78), np.float32)
+        lib().oracle_get_jacobians(self._h, _p(out, f32p))
+        return out
+
+    def points(self) -> dict:
+        P = self.window.n_points
+        o = dict(HdiF=np.zeros(P, np.float32), bdSumF=np.zeros(P, np.float32), idepth_hessian=np.zeros(P, np.float32),
+                 Hdd=np.zeros(P, np.float32), bd=np.zeros(P, np.float32), Hcd=np.zeros((P, 4), np.float32))
+        lib().oracle_get_points(self._h, *[_p(o[k], f32p) for k in ("HdiF", "bdSumF", "idepth_hessian", "Hdd", "bd", "Hcd")])
+        return o
+
+    def frame_energy_th(self):
+        out = np.zeros(self.window.n_frames, np.float32)
+        lib().oracle_get_frame_energy_th(self._h, _p(out, f32p))
+        return out
+
+    def resubstitute(self, x, lam=1e-5):
+        step = np.zeros(self.window.n_points, np.float32)
+        lib().oracle_resubstitute(self._h, _p(np.ascontiguousarray(x, np.float64), f64p), float(lam), _p(step, f32p))
+        return step
+
+    def time_iterations(self, iters: int) -> float:
+        return float(lib().oracle_time_iterations(self._h, int(iters)))
+
+
+def solve_system(n_frames, iteration, lam, sysm, HM=None, bM=None, nullspaces=None):
+    n = 8 * n_frames + 4
+    x = np.zeros(n, np.float64)
+    ns = None if nullspaces is None else np.ascontiguousarray(nullspaces, np.float64)
+    lib().oracle_solve_system(int(n_frames), int(iteration), float(lam), _p(sysm["HA"], f64p), _p(sysm["bA"], f64p),
+                              _p(sysm["HL"], f64p), _p(sysm["bL"], f64p), _p(HM, f64p), _p(bM, f64p),
+                              _p(sysm["Hsc"], f64p), _p(sysm["bsc"], f64p), _p(ns, f64p),
+                              0 if ns is None else ns.shape[0], _p(x, f64p))
+    return x
+
+
+def frame_terms(window):
+    """Oracle restatement of FrameFramePrecalc::Set / setAdjointsF / takeData / nullspaces."""
+    N = window.n_frames
+    fr = np.ascontiguousarray(window.frames)
+    pre = np.zeros((N * N, 32), np.float32)
+    lib().oracle_frame_precalc(N, fr.ctypes.data, _p(np.ascontiguousarray(window.calib, np.float32), f32p), _p(pre, f32p))
+    adH = np.zeros((N * N, 64))
+    adT = np.zeros((N * N, 64))
+    cp = np.zeros(4)
+    lib().oracle_set_adjoints(N, fr.ctypes.data, _p(adH, f64p), _p(adT, f64p), _p(cp, f64p))
+    prior = np.zeros((N, 8))
+    delta = np.zeros((N, 8))
+    dprior = np.zeros((N, 8))
+    lib().oracle_frame_take_data(N, fr.ctypes.data, _p(prior, f64p), _p(delta, f64p), _p(dprior, f64p))
+    ns = np.zeros((7, 8 * N + 4))
+    lib().oracle_nullspaces(N, fr.ctypes.data, _p(ns, f64p))
+    return dict(precalc=pre, ad_host=adH, ad_target=adT, c_prior=cp, frame_prior=prior, frame_delta=delta,
+                frame_delta_prior=dprior, nullspaces=ns)

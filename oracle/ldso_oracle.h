@@ -1,0 +1,84 @@
+/*
+ * ldso_oracle.h -- C API of the CPU restatement of LDSO's photometric-BA hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load this library, and only as the checker / CPU baseline, never as the product.
+ *
+ * Parity status: the reference (n-lalanne/LDSO) ships no golden vectors, KATs or fixtures for
+ * this path and cannot be built in this image (Eigen3, glog, OpenCV, g2o, DBoW3, Boost absent;
+ * SURVEY.md §8c), so this restatement is "parity unpinned" by the reference.  It is pinned
+ * instead by independent known-answer tests (finite-difference Jacobians, dense J^T W J and
+ * explicit Schur complements computed from first principles in tests/test_oracle_kat.py).
+ *
+ * Every function follows a reference file:line (see ldso_oracle.cpp).  Float arithmetic is
+ * compiled with -ffp-contract=off so that each statement rounds in the reference's source
+ * order (the reference itself, built with -march=native, lets GCC contract FMAs).
+ */
+#ifndef LDSO_ORACLE_H_
+#define LDSO_ORACLE_H_
+
+#include "../include/ldso_ba.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_window oracle_window;
+
+/* Number of IndexThreadReduce workers (reference NUM_THREADS = 6, Settings.h:11).
+ * 0 selects the reference's multiThreading=false path (single thread, tid = -1 stitch). */
+void oracle_set_threads(int n);
+int oracle_get_threads(void);
+
+oracle_window *oracle_create(const ldso_ba_window *w);
+void oracle_destroy(oracle_window *ow);
+
+/* per-iteration refresh (same fields as ldso_ba_update) */
+int oracle_update(oracle_window *ow, const ldso_ba_window *w);
+void oracle_reset_oob(oracle_window *ow);
+
+/* FullSystem::linearizeAll(fix) incl. setNewFrameEnergyTH; out[3] = {E, 0, nIN} */
+int oracle_linearize_all(oracle_window *ow, int fix, double *out);
+/* FullSystem::applyRes_Reductor(true) over all residuals */
+void oracle_apply_res(oracle_window *ow);
+/* accumulateAF_MT + accumulateLF_MT + accumulateSCF_MT (with stitches); any output may be NULL */
+int oracle_accumulate(oracle_window *ow, double *HA, double *bA, double *HL, double *bL,
+                      double *Hsc, double *bsc);
+/* one full hot-path GN pass, as the GPU's ldso_ba_linearize(fix=0, accumulate=1) */
+int oracle_iteration(oracle_window *ow, double *energy_out);
+
+void oracle_get_residuals(oracle_window *ow, int8_t *new_state, int8_t *state, float *state_energy,
+                          float *new_energy_wo, float *center, uint8_t *flags, float *jpjdf,
+                          float *rel_bs);
+/* RawResidualJacobian dump per residual: resF[8], Jpdxi[2][6], Jpdc[2][4], Jpdd[2], JIdx[2][8],
+ * JabF[2][8], JIdx2[4], JabJIdx[4], Jab2[4]  (= 78 floats) */
+void oracle_get_jacobians(oracle_window *ow, float *out78);
+void oracle_get_points(oracle_window *ow, float *HdiF, float *bdSumF, float *idepth_hessian,
+                       float *Hdd_acc, float *bd_acc, float *Hcd_acc);
+void oracle_get_frame_energy_th(oracle_window *ow, float *th);
+
+int oracle_solve_system(int n_frames, int iteration, double lambda, const double *HA,
+                        const double *bA, const double *HL, const double *bL, const double *HM,
+                        const double *bM, const double *Hsc, const double *bsc,
+                        const double *nullspaces, int n_null, double *x_out);
+void oracle_resubstitute(oracle_window *ow, const double *x, double lambda, float *point_step);
+
+/* host-side restatements of FrameFramePrecalc::Set, setAdjointsF, takeData, getNullspaces */
+int oracle_frame_precalc(int n_frames, const ldso_ba_frame_state *frames, const float calib[4],
+                         float *precalc_out);
+int oracle_set_adjoints(int n_frames, const ldso_ba_frame_state *frames, double *ad_host,
+                        double *ad_target, double *c_prior);
+int oracle_frame_take_data(int n_frames, const ldso_ba_frame_state *frames, double *prior,
+                           double *delta, double *delta_prior);
+/* FrameHessian::setStateZero nullspaces + FullSystem::getNullspaces (pose x6, scale x1):
+ * out [7][8N+4] in the order orthogonalize() stacks them. */
+int oracle_nullspaces(int n_frames, const ldso_ba_frame_state *frames, double *out);
+
+/* CPU-baseline timing: run `iters` oracle_iteration passes, return wall seconds. */
+double oracle_time_iterations(oracle_window *ow, int iters);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,216 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU restatement (oracle/) on the
+same seeded windows.
+
+Bars (SURVEY.md §7 "Hard parts", BASELINE.json north_star):
+  * per-residual arithmetic (states, energies, centerProjectedTo, JpJdF, per-point Hdd/bd/Hcd,
+    HdiF, frameEnergyTH) is bit-exact: both sides round every statement in the reference's
+    order with FMA contraction off;
+  * linearizeAll energy: relative 1e-12 (double sums, different order);
+  * stitched H, b (float accumulation reassociated on the GPU, then double): per 8x8 block
+    relative Frobenius error <= 1e-4 (the north star's tolerance is 1e-4 on the energy);
+  * solve: the product's solver matches the oracle's on the same system to 1e-9; end to end, x
+    stays within 20x the system's float-rounding sensitivity envelope (see sensitivity());
+  * resubstituted point steps: relative 1e-3 on the step vector.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from ldso_amd import BAContext, synth
+
+pytestmark = pytest.mark.gpu
+
+BLOCK_TOL = 1e-4
+
+
+def block_errors(G, O, N):
+    """max over the upper-triangle blocks of ||G-O||_F / ||O||_F (blocks: calib, frames)."""
+    edges = [0, 4] + [4 + 8 * (f + 1) for f in range(N)]
+    scale = np.linalg.norm(O)
+    worst = 0.0
+    for a in range(len(edges) - 1):
+        for b in range(a, len(edges) - 1):
+            g = G[edges[a]:edges[a + 1], edges[b]:edges[b + 1]]
+            o = O[edges[a]:edges[a + 1], edges[b]:edges[b + 1]]
+            if a == b:
+                g, o = np.triu(g), np.triu(o)
+            den = max(np.linalg.norm(o), 1e-12 * scale, 1e-300)
+            worst = max(worst, np.linalg.norm(g - o) / den)
+    return worst
+
+
+def vec_block_errors(g, o, N):
+    edges = [0, 4] + [4 + 8 * (f + 1) for f in range(N)]
+    scale = np.linalg.norm(o)
+    worst = 0.0
+    for a in range(len(edges) - 1):
+        gg, oo = g[edges[a]:edges[a + 1]], o[edges[a]:edges[a + 1]]
+        worst = max(worst, np.linalg.norm(gg - oo) / max(np.linalg.norm(oo), 1e-12 * scale, 1e-300))
+    return worst
+
+
+def sensitivity(N, it, sysm, ns, x0, eps=2.0 ** -20, trials=3):
+    rng = np.random.default_rng(0)
+    worst = 0.0
+    for _ in range(trials):
+        pert = {}
+        for k, v in sysm.items():
+            if k in ("HA", "Hsc"):
+                E = rng.standard_normal(v.shape)
+                pert[k] = v * (1 + eps * (E + E.T) / 2)
+            elif k in ("bA", "bsc"):
+                pert[k] = v * (1 + eps * rng.standard_normal(v.shape))
+            else:
+                pert[k] = v
+        x = oracle.solve_system(N, it, 1e-5, pert, nullspaces=ns)
+        worst = max(worst, np.linalg.norm(x - x0) / np.linalg.norm(x0))
+    return worst
+
+
+def compare_pass(ctx, ow, win_idx, e_cpu, s_cpu, check_system=True):
+    N = ow.window.n_frames
+    rg, rc = ctx.residuals(win_idx), ow.residuals()
+    assert np.array_equal(rg["new_state"], rc["new_state"])
+    assert np.array_equal(rg["state"], rc["state"])
+    assert np.array_equal(rg["flags"], rc["flags"])
+    assert np.array_equal(rg["state_energy"], rc["state_energy"])
+    assert np.array_equal(rg["new_energy_wo"], rc["new_energy_wo"])
+    assert np.array_equal(rg["center"], rc["center"])
+    act = (rc["flags"] & 1).astype(bool)
+    assert np.array_equal(rg["jpjdf"][act], rc["jpjdf"][act])
+    e_gpu = ctx.energy(win_idx)
+    assert e_gpu[2] == e_cpu[2]
+    assert abs(e_gpu[0] - e_cpu[0]) <= 1e-12 * abs(e_cpu[0]) + 1e-9
+    np.testing.assert_array_equal(ctx.frame_energy_th(win_idx), ow.frame_energy_th())
+    if not check_system:
+        return
+    pg, pc = ctx.points(win_idx), ow.points()
+    for k in ("Hdd", "bd", "Hcd", "HdiF", "bdSumF", "idepth_hessian"):
+        np.testing.assert_array_equal(pg[k], pc[k], err_msg=k)
+    s_gpu = ctx.system(win_idx)
+    errs = {k: block_errors(s_gpu[k], s_cpu[k], N) for k in ("HA", "Hsc")}
+    errs.update({k: vec_block_errors(s_gpu[k], s_cpu[k], N) for k in ("bA", "bsc")})
+    print("max block rel errors:", {k: f"{v:.2e}" for k, v in errs.items()})
+    assert block_errors(s_gpu["HA"], s_cpu["HA"], N) < BLOCK_TOL
+    assert block_errors(s_gpu["Hsc"], s_cpu["Hsc"], N) < BLOCK_TOL
+    assert vec_block_errors(s_gpu["bA"], s_cpu["bA"], N) < BLOCK_TOL
+    assert vec_block_errors(s_gpu["bsc"], s_cpu["bsc"], N) < BLOCK_TOL
+    np.testing.assert_array_equal(s_gpu["HL"], s_cpu["HL"])
+    np.testing.assert_array_equal(s_gpu["bL"], s_cpu["bL"])
+    return s_gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(built):
+    c = BAContext(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("cfg", [dict(n_frames=3, n_points=64, seed=11), dict(n_frames=5, n_points=400, seed=3),
+                                 dict(synth.S7, seed=1)], ids=["N3P64", "N5P400", "S7"])
+def test_single_pass_parity(ctx, cfg):
+    w = synth.make_window(**cfg)
+    ctx.load([w])
+    ctx.linearize(fix=False, accumulate=True)
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    e_cpu, s_cpu = ow.iteration()
+    s_gpu = compare_pass(ctx, ow, 0, e_cpu, s_cpu)
+    # solveSystemF and resubstituteF on both sides
+    ns = w.nullspaces()
+    for it in (0, 2):
+        xg = ctx.solve(0, it, 1e-5, ns)
+        # the product's solver on the GPU system == the oracle's solver on the same system
+        xo = oracle.solve_system(w.n_frames, it, 1e-5, s_gpu, nullspaces=ns)
+        assert np.linalg.norm(xg - xo) <= 1e-9 * np.linalg.norm(xo)
+        # end to end: float reassociation of H (~1e-6 relative) is amplified by the system's
+        # conditioning.  Bar: within 20x the shift of x under a random 2^-20 relative
+        # perturbation of the oracle's own H and b (its float-rounding sensitivity envelope).
+        xc = oracle.solve_system(w.n_frames, it, 1e-5, s_cpu, nullspaces=ns)
+        env = sensitivity(w.n_frames, it, s_cpu, ns, xc)
+        rel = np.linalg.norm(xg - xc) / np.linalg.norm(xc)
+        print(f"solve it={it}: |xg-xc|/|xc|={rel:.3e} envelope={env:.3e}")
+        assert rel <= max(1e-6, 20 * env)
+    xc = oracle.solve_system(w.n_frames, 0, 1e-5, s_cpu, nullspaces=ns)
+    stg = ctx.resubstitute(0, xc, 1e-5)
+    stc = ow.resubstitute(xc, 1e-5)
+    assert np.linalg.norm(stg - stc) <= 1e-3 * np.linalg.norm(stc) + 1e-12
+
+
+def test_repeated_passes_and_oob_stickiness(ctx):
+    """OOB is sticky inside optimize(): later passes return the stored state_energy."""
+    cfg = dict(n_frames=6, n_points=800, seed=5, baseline=0.12)
+    ctx.load([synth.make_window(**cfg)])
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    for _ in range(3):
+        ctx.linearize(fix=False, accumulate=True)
+        e_cpu, s_cpu = ow.iteration()
+        compare_pass(ctx, ow, 0, e_cpu, s_cpu)
+    ctx.reset_oob()
+    ow.reset_oob()
+    ctx.linearize(fix=True, accumulate=False)
+    e_cpu = ow.linearize_all(True)
+    compare_pass(ctx, ow, 0, e_cpu, None, check_system=False)
+    rg, rc = ctx.residuals(0), ow.residuals()
+    np.testing.assert_array_equal(rg["rel_bs"], rc["rel_bs"])
+
+
+def test_multi_window_batch(ctx):
+    cfgs = [dict(n_frames=7, n_points=500, seed=s) for s in (21, 22)] + [dict(n_frames=4, n_points=300, seed=23)]
+    ctx.load([synth.make_window(**c) for c in cfgs])
+    ctx.linearize(fix=False, accumulate=True)
+    for i, c in enumerate(cfgs):
+        ow = oracle.OracleWindow(synth.make_window(**c), threads=0)
+        e_cpu, s_cpu = ow.iteration()
+        compare_pass(ctx, ow, i, e_cpu, s_cpu)
+
+
+def test_state_update_between_passes(ctx):
+    """doStepFromBackup -> setPrecalcValues -> ldso_ba_update, then a fresh pass."""
+    cfg = dict(n_frames=5, n_points=600, seed=31)
+    w = synth.make_window(**cfg)
+    ctx.load([w])
+    ctx.linearize()
+    w2 = synth.make_window(**cfg)
+    w2.frames["state"][2, :6] += 2e-3
+    w2.point_data[:, 2] *= 1.01
+    w2.refresh_frame_terms()
+    ctx.update(0, w2)
+    ctx.linearize()
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    ow.iteration()
+    ow.update(w2)
+    e_cpu, s_cpu = ow.iteration()
+    compare_pass(ctx, ow, 0, e_cpu, s_cpu)
+
+
+def test_shards_sum_to_full(built):
+    """Host-frame ordered round-robin sharding: per-shard systems sum to the full system."""
+    cfg = dict(n_frames=7, n_points=900, seed=41)
+    full = BAContext(0).load([synth.make_window(**cfg)])
+    full.linearize()
+    s_full = full.system(0)
+    parts = []
+    for r in range(3):
+        c = BAContext(0).load([synth.make_window(**cfg)], shard_rank=r, shard_count=3)
+        c.linearize()
+        parts.append(c.system(0))
+        c.close()
+    N = cfg["n_frames"]
+    for k in ("HA", "Hsc"):
+        tot = sum(p[k] for p in parts)
+        assert block_errors(tot, s_full[k], N) < BLOCK_TOL
+    for k in ("bA", "bsc"):
+        assert vec_block_errors(sum(p[k] for p in parts), s_full[k], N) < BLOCK_TOL
+    np.testing.assert_array_equal(parts[0]["HL"], s_full["HL"])
+    assert not parts[1]["HL"].any()
+    full.close()
+
+
+def test_s11_window(ctx):
+    cfg = dict(synth.S11, seed=2)
+    ctx.load([synth.make_window(**cfg)])
+    ctx.linearize()
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    e_cpu, s_cpu = ow.iteration()
+    compare_pass(ctx, ow, 0, e_cpu, s_cpu)
