@@ -1,0 +1,251 @@
+"""Headline benchmark: point-residuals/sec per GN iteration on synthetic 7-keyframe windows.
+
+A *step* is one hot-path pass over every window resident on the GPU: linearizeAll + applyRes +
+setNewFrameEnergyTH + accumulate{AF,LF,SCF} + both stitches (one ldso_ba_linearize call,
+seven kernels on the context's stream).  Each GPU holds `--windows` independent S7 windows
+(7 keyframes, 2000 active points, 640x480, distinct seeds), so per-GPU work is fixed as GPUs
+are added ("scaling": "weak"; no collective is needed between independent windows).
+
+value  = residuals processed by all ranks per step / max-over-ranks step time.
+roofline: dominant kernel k_linearize, algorithmic bytes per residual
+          = 276 B (23 unique 12-B texels) + 8 B state + 88 B/(N-1) point data, times the
+          residuals that do gather (not OOB before the pass), / its mean HIP-event duration.
+cpu_baseline: the oracle restatement (oracle/, 6-thread IndexThreadReduce like the reference,
+          NUM_THREADS = 6) on one S7 window for ~10 s, same pass.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--windows B] [--mode replicas|shard]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "point-residuals/sec per GN iter (7-KF window) + ms/solve; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algo_bytes_per_residual(n_frames):
+    return 276.0 + 8.0 + 88.0 / (n_frames - 1)
+
+
+def load_pmc(workload):
+    """HBM traffic per k_linearize launch from a committed rocprofv3 --pmc summary, if one
+    exists for this exact workload (written by tools/pmc_traffic.py); else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_k_linearize.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(seconds=10.0, threads=6):
+    import oracle
+    from ldso_amd import synth
+
+    w = synth.make_window(**synth.S7, seed=1)
+    ow = oracle.OracleWindow(w, threads=threads)
+    ow.time_iterations(1)  # warm-up (thread pool spin-up, page faults)
+    iters, el = 0, 0.0
+    while el < seconds:
+        n = max(1, iters or 4)
+        el += ow.time_iterations(n)
+        iters += n
+    R = w.n_residuals
+    return {"value": R * iters / el, "unit": "point-residuals/s", "cores": threads, "kind": "port",
+            "sample": f"1 S7 window (seed 1, R={R}), {iters} passes of linearizeAll+applyRes+"
+                      f"accumulate{{AF,LF,SCF}}+stitch in {el:.1f} s, {threads}-thread IndexThreadReduce"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--windows", type=int, default=64, help="S7 windows per GPU")
+    ap.add_argument("--frames", type=int, default=7)
+    ap.add_argument("--points", type=int, default=2000)
+    ap.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+    import torch
+
+    from ldso_amd import BAContext, synth
+
+    B, N, P = args.windows, args.frames, args.points
+    if args.mode == "replicas":
+        seeds = [1000 + rank * B + i for i in range(B)]  # independent windows per rank
+        shard = (0, 1)
+    else:
+        seeds = [1000 + i for i in range(B)]  # same windows on every rank, points sharded
+        shard = (rank, world)
+    windows = [synth.make_window(n_frames=N, n_points=P, seed=s) for s in seeds]
+    ctx = BAContext(local_rank)
+    ctx.load(windows, shard_rank=shard[0], shard_count=shard[1])
+    for w in windows:
+        w.dI = None  # images now live in HBM only
+    R_rank = ctx.stats()["residuals"]
+
+    packed = None
+    if args.mode == "shard" and dist is not None:
+        from ldso_amd import dist as ldist
+
+        packed = ldist.PackedSystem(ctx)
+
+    def step():
+        ctx.linearize(fix=False, accumulate=True)
+        if packed is not None:
+            packed.allreduce(dist)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    # residuals that gather texels this pass (OOB is sticky within optimize())
+    n_gather = sum(int((ctx.residuals(i)["state"] != 1).sum()) for i in range(len(windows)))
+
+    ctx.set_kernel_timing(True)
+    if dist is not None:
+        dist.barrier()
+    ctx.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ktimes = ctx.kernel_times()
+    ctx.set_kernel_timing(False)
+
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        tot = torch.tensor([R_rank], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot)
+        R_total = float(tot.item())
+    else:
+        R_total = float(R_rank)
+    if args.mode == "shard":
+        R_job = float(sum(w.n_residuals for w in windows))  # each residual counted once
+    else:
+        R_job = R_total
+    ms_step = 1e3 * el / args.steps
+    value = R_job * args.steps / el
+
+    klin_ms, klin_n = ktimes["k_linearize"]
+    klin_avg_s = klin_ms / max(1, klin_n) / 1e3
+    bytes_per_launch = n_gather * algo_bytes_per_residual(N)
+    achieved = bytes_per_launch / klin_avg_s / 1e9 if klin_avg_s > 0 else 0.0
+    workload = f"{B} x S7 synthetic windows/GPU ({N} KF, {P} pts, 640x480)" if (N, P) == (7, 2000) else \
+        f"{B} x synthetic windows/GPU ({N} KF, {P} pts, 640x480)"
+    traffic = load_pmc(workload)
+
+    # ms/solve on one window: pass + stitched-system download + LDLT + resubstitute (host clock)
+    ms_solve = None
+    single = None
+    if rank == 0:
+        sw = synth.make_window(n_frames=N, n_points=P, seed=1)
+        ns = sw.nullspaces()
+        c1 = BAContext(local_rank)
+        c1.load([sw])
+        for i in range(5):
+            c1.linearize()
+            x = c1.solve(0, i, 1e-5, ns)
+            c1.resubstitute(0, x, 1e-5, fetch=True)
+        reps = 30
+        c1.sync()
+        t1 = time.perf_counter()
+        for i in range(reps):
+            c1.linearize()
+            x = c1.solve(0, 2, 1e-5, ns)
+            c1.resubstitute(0, x, 1e-5, fetch=True)
+        ms_solve = 1e3 * (time.perf_counter() - t1) / reps
+        c1.sync()
+        t1 = time.perf_counter()
+        for i in range(reps):
+            c1.linearize()
+        c1.sync()
+        sw_ms = 1e3 * (time.perf_counter() - t1) / reps
+        single = {"ms_per_pass": sw_ms, "point_residuals_per_s": sw.n_residuals / (sw_ms / 1e3)}
+        c1.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "point-residuals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "replicas" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded textured-plane windows, photo-consistent; no dataset)",
+            "config": {
+                "workload": workload,
+                "n_frames": N,
+                "points_per_window": P,
+                "windows_per_gpu": B,
+                "residuals_per_step": int(R_job),
+                "image": "640x480",
+                "parallelism": f"{args.mode}{world}" if world > 1 else "single",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_linearize",
+                "avg_launch_us": klin_avg_s * 1e6,
+                "algo_bytes_per_launch": bytes_per_launch,
+                "algo_bytes_per_residual": algo_bytes_per_residual(N),
+            },
+            "kernel_ms_per_step": {k: v[0] / max(1, v[1]) for k, v in ktimes.items() if v[1]},
+            "ms_per_solve": ms_solve,
+            "single_window": single,
+            "cpu_baseline": cpu,
+        }
+        if cpu is not None:
+            out["speedup_vs_cpu"] = value / cpu["value"]
+        print(json.dumps(out))
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

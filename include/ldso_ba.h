@@ -202,11 +202,30 @@ int ldso_ba_resubstitute(ldso_ba_ctx *ctx, int32_t win, const double *x, double 
  * ldso_ba_unpack_system so that get_system / solve read the reduced values. */
 int ldso_ba_packed_system(ldso_ba_ctx *ctx, void **dev_ptr, int64_t *n_doubles, int64_t *stride);
 int ldso_ba_unpack_system(ldso_ba_ctx *ctx);
+/* Device-to-device copy of the packed partial systems to (direction 0) or from (direction 1)
+ * a caller-owned device buffer of n_doubles (e.g. a torch tensor handed to RCCL); synchronises
+ * the context stream.  Direction 1 also invalidates cached host copies. */
+int ldso_ba_copy_packed(ldso_ba_ctx *ctx, void *dev_buf, int64_t n_doubles, int32_t direction);
 
 /* Per-kernel HIP-event timing (bench/profiling).  When enabled every kernel launch of
  * ldso_ba_linearize is bracketed by events; get returns summed ms and launch counts for
  * n_kernels <= 16 slots in the order of ldso_ba_kernel_name(i). */
 int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
+
+/* Tuning knobs (defaults are the measured best):
+ *   LDSO_BA_TUNE_LIN_VARIANT   k_linearize occupancy target in waves per SIMD (1 or 2)
+ *   LDSO_BA_TUNE_TILED_IMAGES  frames stored in 2x4-texel tiles (1) or row-major (0); set
+ *                              before ldso_ba_load
+ *   LDSO_BA_TUNE_LOAD3         texel loads as dwordx3 (1) or dwordx4 (0)
+ *   LDSO_BA_TUNE_XCD_REMAP     XCD-contiguous block->chunk mapping in k_linearize (1) or not
+ *   LDSO_BA_TUNE_CENTRE_FIRST  centre projection before the pattern gathers (1, reference order)
+ *                              or after them (0) */
+#define LDSO_BA_TUNE_LIN_VARIANT 1
+#define LDSO_BA_TUNE_TILED_IMAGES 2
+#define LDSO_BA_TUNE_LOAD3 3
+#define LDSO_BA_TUNE_XCD_REMAP 4
+#define LDSO_BA_TUNE_CENTRE_FIRST 5
+int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);
 int32_t ldso_ba_num_kernels(void);

@@ -106,7 +106,9 @@ ABI = [
     ("ldso_ba_resubstitute", C.c_int, [C.c_void_p, C.c_int32, f64p, C.c_double, f32p]),
     ("ldso_ba_packed_system", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), i64p, i64p]),
     ("ldso_ba_unpack_system", C.c_int, [C.c_void_p]),
+    ("ldso_ba_copy_packed", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
     ("ldso_ba_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
+    ("ldso_ba_set_tuning", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),
     ("ldso_ba_kernel_name", C.c_char_p, [C.c_int32]),
     ("ldso_ba_num_kernels", C.c_int32, []),

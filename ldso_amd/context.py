@@ -127,6 +127,9 @@ class BAContext:
     def unpack_system(self):
         L.check(self._lib.ldso_ba_unpack_system(self._h))
 
+    def set_tuning(self, key: int, value: int):
+        L.check(self._lib.ldso_ba_set_tuning(self._h, int(key), int(value)))
+
     def set_kernel_timing(self, on: bool):
         L.check(self._lib.ldso_ba_set_kernel_timing(self._h, int(bool(on))))
 

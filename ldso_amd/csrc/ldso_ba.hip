@@ -7,8 +7,8 @@
 //                 per-residual AccumulatorApprox terms (AccumulatedTopHessian.cc:66-99,
 //                 MatrixAccumulators.h:893-1045) reduced across the wavefront into a 96-float
 //                 partial per chunk.  The pair precalc, frame thresholds and image base are
-//                 wave-uniform (scalar loads); the only vector traffic is the point record and
-//                 32 texel gathers per residual.
+//                 wave-uniform (scalar loads); the vector traffic is the point record and the
+//                 32 bilinear taps per residual into 2x4-texel tiled [I, dx, dy, 0] frames.
 //   k_frame_th    FullSystem::setNewFrameEnergyTH (FullSystem.cc:2078-2109), radix select.
 //   k_point_sc    per point: Hdd/bd/Hcd sums (AccumulatedTopHessian.cc:94-116), HdiF
 //                 (AccumulatedSCHessian.cc:24-33); then the Schur terms of a 64-point chunk of one
@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -43,9 +44,8 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kTopVals = 96;    // 55 + 30 + 6 AccumulatorApprox entries, padded to 96
 constexpr int kMaxRes = LDSO_BA_MAX_FRAMES - 1;
-constexpr int kNumKernels = 8;
-const char *kKernelNames[kNumKernels] = {"k_linearize", "k_frame_th", "k_point_sc", "k_stitch_top",
-                                         "k_sc_reduce", "k_stitch_sc", "k_final", "k_resubstitute"};
+constexpr int kNumKernels = 4;
+const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch", "k_resubstitute"};
 
 thread_local std::string g_err;
 int fail(int code, const std::string &msg) {
@@ -87,7 +87,7 @@ __host__ __device__ inline long long sys_len(int D) { return 2 * (packed_len(D) 
 struct LinParams {
     const int4 *__restrict__ items;  // {res_begin, count, pair_global, win}
     const WinDev *__restrict__ wins;
-    const float4 *__restrict__ img;
+    const float4 *__restrict__ img;  // [I, dx, dy, 0] texels, 2x4-texel tiles (see tex())
     const float *__restrict__ precalc;
     const float *__restrict__ frame_th;
     const int *__restrict__ rs_point;
@@ -103,7 +103,9 @@ struct LinParams {
     float *top_slab;       // [items][96]
     double *item_energy;   // [items][2]
     int n_items;
-    int npix;
+    int n_blocks;
+    long long frame_stride;  // texels per tiled frame
+    int tiles_per_row;       // 2-wide tiles per tile row
     int fix;
     int accumulate;
 };
@@ -173,10 +175,25 @@ struct PhotoSums {
     float JI_r0, JI_r1, Jab_r0, Jab_r1, rr;  // AccumulatedTopHessian.cc:69-77 (mode 0: resApprox = resF)
 };
 
+// Image texel fetch.  Frames live in HBM as FrameHessian::dI texels [I, dx, dy, 0] (16 B),
+// tiled 2 (x) by 4 (y) texels per 128-byte line: the 8-pixel pattern's 32 bilinear taps then
+// touch ~6.3 lines per residual instead of ~8.1 for row-major (tools/ measurements).
+template <bool kTiled, bool kLoad3>
+__device__ inline float3 tex(const float4 *__restrict__ img, int tpr2, int x, int y) {
+    const int idx = kTiled ? (((y >> 2) * tpr2 + (x >> 1)) << 3) + ((y & 3) << 1) + (x & 1) : y * (tpr2 * 2) + x;
+    if constexpr (kLoad3) {
+        return *reinterpret_cast<const float3 *>(img + idx);  // dwordx3: pad never loaded
+    } else {
+        const float4 v = img[idx];
+        return make_float3(v.x, v.y, v.z);
+    }
+}
+
 // Pattern loop of Residuals.cc:128-190 with getInterpolatedElement33 (GlobalFuncs.h:89-103).
 // The JI_r / Jab_r / rr sums of the Top accumulation are folded into the same loop (same
 // order, so identical rounding to summing the stored J afterwards).
-__device__ inline bool pattern_loop(const float *__restrict__ pre, const float4 *__restrict__ img, int w,
+template <bool kTiled, bool kLoad3>
+__device__ inline bool pattern_loop(const float *__restrict__ pre, const float4 *__restrict__ img, int tpr2,
                                     float wM3, float hM3, float u, float v, float ids,
                                     const float *__restrict__ color, const float *__restrict__ weights,
                                     PhotoSums &s) {
@@ -188,7 +205,7 @@ __device__ inline bool pattern_loop(const float *__restrict__ pre, const float4 
     s.JabJIdx_00 = s.JabJIdx_01 = s.JabJIdx_10 = s.JabJIdx_11 = 0;
     s.Jab2_00 = s.Jab2_01 = s.Jab2_11 = 0;
     s.JI_r0 = s.JI_r1 = s.Jab_r0 = s.Jab_r1 = s.rr = 0;
-    // issue all eight projections first so the 32 texel loads can be in flight together
+    // all eight projections first: any OOB pattern pixel makes the residual OOB
     float Kus[8], Kvs[8];
     bool ok = true;
 #pragma unroll
@@ -202,22 +219,19 @@ __device__ inline bool pattern_loop(const float *__restrict__ pre, const float4 
         ok = ok && (Kus[idx] > 1.1f && Kvs[idx] > 1.1f && Kus[idx] < wM3 && Kvs[idx] < hM3);
     }
     if (!ok) return false;
-    float4 t00[8], t10[8], t01[8], t11[8];
-    float dxs[8], dys[8];
+    float3 t00[8], t10[8], t01[8], t11[8];
 #pragma unroll
-    for (int idx = 0; idx < 8; idx++) {
+    for (int idx = 0; idx < 8; idx++) {  // issue all 32 texel loads before any use
         const int ix = (int)Kus[idx], iy = (int)Kvs[idx];
-        dxs[idx] = Kus[idx] - ix;
-        dys[idx] = Kvs[idx] - iy;
-        const float4 *bp = img + ix + iy * w;
-        t00[idx] = bp[0];
-        t10[idx] = bp[1];
-        t01[idx] = bp[w];
-        t11[idx] = bp[w + 1];
+        t00[idx] = tex<kTiled, kLoad3>(img, tpr2, ix, iy);
+        t10[idx] = tex<kTiled, kLoad3>(img, tpr2, ix + 1, iy);
+        t01[idx] = tex<kTiled, kLoad3>(img, tpr2, ix, iy + 1);
+        t11[idx] = tex<kTiled, kLoad3>(img, tpr2, ix + 1, iy + 1);
     }
 #pragma unroll
     for (int idx = 0; idx < 8; idx++) {
-        const float dx = dxs[idx], dy = dys[idx], dxdy = dx * dy;
+        const int ix = (int)Kus[idx], iy = (int)Kvs[idx];
+        const float dx = Kus[idx] - ix, dy = Kvs[idx] - iy, dxdy = dx * dy;
         const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
         const float I = w11 * t11[idx].x + w01 * t01[idx].x + w10 * t10[idx].x + w00 * t00[idx].x;
         float gx = w11 * t11[idx].y + w01 * t01[idx].y + w10 * t10[idx].y + w00 * t00[idx].y;
@@ -287,10 +301,67 @@ __device__ inline void halve(float *v, int lane) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_linearize(LinParams P) {
+// Inputs of one residual's AccumulatorApprox contribution (x = [Jpdc0, Jpdxi0], y = [Jpdc1,
+// Jpdxi1]; a, b, c = JIdx2; tr = JabJIdx and JI_r; br = Jab2, Jab_r, rr).
+struct TopIn {
+    float x[10], y[10];
+    float a, b, c;
+    float tr[6], br[6];
+};
+// Element K of the 96-slot layout: [0,55) upper-triangular 10x10 row-major (Data[]),
+// [55,85) TopRight 10x3, [85,91) BotRight, [91,96) zero.  All index arithmetic is constexpr.
+constexpr int tri_row(int k) {
+    int r = 0;
+    while (k >= 10 - r) {
+        k -= 10 - r;
+        r++;
+    }
+    return r;
+}
+constexpr int tri_col(int k) {
+    int r = 0;
+    while (k >= 10 - r) {
+        k -= 10 - r;
+        r++;
+    }
+    return r + k;
+}
+template <int K>
+__device__ __forceinline__ float topval(const TopIn &t) {
+    if constexpr (K < 55) {
+        constexpr int r = tri_row(K), cc = tri_col(K);
+        return t.a * t.x[cc] * t.x[r] + t.c * t.y[cc] * t.y[r] + t.b * (t.x[cc] * t.y[r] + t.y[cc] * t.x[r]);
+    } else if constexpr (K < 85) {
+        constexpr int r = (K - 55) / 3, j = (K - 55) % 3;
+        return t.x[r] * t.tr[2 * j] + t.y[r] * t.tr[2 * j + 1];
+    } else if constexpr (K < 91) {
+        return t.br[K - 85];
+    } else {
+        return 0.0f;
+    }
+}
+// first recursive-halving step (lane mask 1) with the 96 terms generated on the fly
+template <int I>
+__device__ __forceinline__ void first_halve(const TopIn &t, float *v, bool upper) {
+    if constexpr (I < 48) {
+        const float lo = topval<I>(t), hi = topval<I + 48>(t);
+        const float send = upper ? lo : hi;
+        const float keep = upper ? hi : lo;
+        v[I] = keep + __shfl_xor(send, 1, kWave);
+        first_halve<I + 1>(t, v, upper);
+    }
+}
+
+template <int kMinWavesPerSimd, bool kTiled, bool kLoad3, bool kXcdRemap, bool kCentreFirst>
+__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_linearize(LinParams P) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int item = blockIdx.x * 4 + wave;
+    // XCD-aware mapping: blocks b, b+8, b+16, ... share an XCD (round-robin dispatch), so give
+    // each XCD one contiguous range of items.  Items are ordered by (window, target, host):
+    // all chunks reading one target frame then run on one XCD and share its L2.
+    const int nb = P.n_blocks, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+    const int lblock = kXcdRemap ? xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3) : (int)blockIdx.x;
+    const int item = lblock * 4 + wave;
     if (item >= P.n_items) return;
     const int4 it = P.items[item];
     const WinDev &W = P.wins[it.w];
@@ -298,7 +369,7 @@ __global__ __launch_bounds__(256) void k_linearize(LinParams P) {
     const int aidx = it.z - W.pair_base;
     const int h = aidx % N, t = aidx / N;
     const float *pre = P.precalc + (size_t)it.z * LDSO_BA_PRECALC_STRIDE;
-    const float4 *img = P.img + (size_t)(W.frame_base + t) * P.npix;
+    const float4 *img = P.img + (size_t)(W.frame_base + t) * P.frame_stride;
     const float th = fmaxf(P.frame_th[W.frame_base + h], P.frame_th[W.frame_base + t]);
 
     const bool valid = lane < it.y;
@@ -321,18 +392,33 @@ __global__ __launch_bounds__(256) void k_linearize(LinParams P) {
             const int p = P.rs_point[r];
             const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
             const float4 pd0 = *(const float4 *)pd;
-            float color[8], weights[8];
-            *(float4 *)&color[0] = *(const float4 *)(pd + 8);
-            *(float4 *)&color[4] = *(const float4 *)(pd + 12);
-            *(float4 *)&weights[0] = *(const float4 *)(pd + 16);
-            *(float4 *)&weights[4] = *(const float4 *)(pd + 20);
-            bool ok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
-                                        W.wM3, W.hM3, g);
-            if (ok) {
-                centre.x = g.Ku;
-                centre.y = g.Kv;
-                centre.z = g.new_idepth;
-                ok = pattern_loop(pre, img, W.width, W.wM3, W.hM3, pd0.x, pd0.y, pd0.z, color, weights, s);
+            bool ok;
+            if constexpr (kCentreFirst) {  // the reference's order (Residuals.cc:59-140)
+                float cw[16];
+#pragma unroll
+                for (int i = 0; i < 4; i++) *(float4 *)&cw[4 * i] = *(const float4 *)(pd + 8 + 4 * i);
+                ok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
+                                       W.wM3, W.hM3, g);
+                if (ok) {
+                    centre.x = g.Ku;
+                    centre.y = g.Kv;
+                    centre.z = g.new_idepth;
+                    ok = pattern_loop<kTiled, kLoad3>(pre, img, P.tiles_per_row, W.wM3, W.hM3, pd0.x, pd0.y, pd0.z,
+                                                      cw, cw + 8, s);
+                }
+            } else {
+                // gathers first, geometry after (not live across the 32 loads); same outcome: any
+                // failure -> OOB, centerProjectedTo set iff the centre projection succeeds
+                ok = pattern_loop<kTiled, kLoad3>(pre, img, P.tiles_per_row, W.wM3, W.hM3, pd0.x, pd0.y, pd0.z, pd + 8,
+                                                  pd + 16, s);
+                const bool cok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2],
+                                                   W.calib[3], W.wM3, W.hM3, g);
+                if (cok) {
+                    centre.x = g.Ku;
+                    centre.y = g.Kv;
+                    centre.z = g.new_idepth;
+                }
+                ok = ok && cok;
             }
             if (!ok) {
                 energy = state_energy;  // OOB: return state_energy, NewEnergy untouched
@@ -395,45 +481,44 @@ __global__ __launch_bounds__(256) void k_linearize(LinParams P) {
     }
     if (!P.accumulate) return;
 
-    // AccumulatorApprox::update / updateTopRight / updateBotRight terms (mode 0)
-    float v[kTopVals];
+    // AccumulatorApprox::update / updateTopRight / updateBotRight terms (mode 0), generated on
+    // the fly inside the first halving step so that only 48 partial sums are ever live.
+    TopIn tin;
     if (active) {
-        float x[10], y[10];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            x[i] = g.d_C_x[i];
-            y[i] = g.d_C_y[i];
+            tin.x[i] = g.d_C_x[i];
+            tin.y[i] = g.d_C_y[i];
         }
 #pragma unroll
         for (int i = 0; i < 6; i++) {
-            x[4 + i] = g.d_xi_x[i];
-            y[4 + i] = g.d_xi_y[i];
+            tin.x[4 + i] = g.d_xi_x[i];
+            tin.y[4 + i] = g.d_xi_y[i];
         }
-        const float a = s.JIdx2_00, b = s.JIdx2_10, c = s.JIdx2_11;
-        int q = 0;
-#pragma unroll
-        for (int rr = 0; rr < 10; rr++)
-#pragma unroll
-            for (int cc = rr; cc < 10; cc++) v[q++] = a * x[cc] * x[rr] + c * y[cc] * y[rr] + b * (x[cc] * y[rr] + y[cc] * x[rr]);
-#pragma unroll
-        for (int rr = 0; rr < 10; rr++) {
-            v[55 + 3 * rr] = x[rr] * s.JabJIdx_00 + y[rr] * s.JabJIdx_01;
-            v[56 + 3 * rr] = x[rr] * s.JabJIdx_10 + y[rr] * s.JabJIdx_11;
-            v[57 + 3 * rr] = x[rr] * s.JI_r0 + y[rr] * s.JI_r1;
-        }
-        v[85] = s.Jab2_00;
-        v[86] = s.Jab2_01;
-        v[87] = s.Jab_r0;
-        v[88] = s.Jab2_11;
-        v[89] = s.Jab_r1;
-        v[90] = s.rr;
-#pragma unroll
-        for (int i = 91; i < kTopVals; i++) v[i] = 0;
+        tin.a = s.JIdx2_00;
+        tin.b = s.JIdx2_10;
+        tin.c = s.JIdx2_11;
+        tin.tr[0] = s.JabJIdx_00;
+        tin.tr[1] = s.JabJIdx_01;
+        tin.tr[2] = s.JabJIdx_10;
+        tin.tr[3] = s.JabJIdx_11;
+        tin.tr[4] = s.JI_r0;
+        tin.tr[5] = s.JI_r1;
+        tin.br[0] = s.Jab2_00;
+        tin.br[1] = s.Jab2_01;
+        tin.br[2] = s.Jab_r0;
+        tin.br[3] = s.Jab2_11;
+        tin.br[4] = s.Jab_r1;
+        tin.br[5] = s.rr;
     } else {
 #pragma unroll
-        for (int i = 0; i < kTopVals; i++) v[i] = 0;
+        for (int i = 0; i < 10; i++) tin.x[i] = tin.y[i] = 0;
+        tin.a = tin.b = tin.c = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) tin.tr[i] = tin.br[i] = 0;
     }
-    halve<96, 1>(v, lane);
+    float v[48];
+    first_halve<0>(tin, v, (lane & 1) != 0);
     halve<48, 2>(v, lane);
     halve<24, 4>(v, lane);
     halve<12, 8>(v, lane);
@@ -447,67 +532,6 @@ __global__ __launch_bounds__(256) void k_linearize(LinParams P) {
         o[0] = v[0];
         o[1] = v[1];
         o[2] = v[2];
-    }
-}
-
-// ============================================================================================
-// k_frame_th: setNewFrameEnergyTH via an exact 4-pass radix select (nth_element semantics)
-// ============================================================================================
-__global__ __launch_bounds__(256) void k_frame_th(const WinDev *__restrict__ wins, const float *__restrict__ e_wo,
-                                                 float *frame_th) {
-    const WinDev &W = wins[blockIdx.x];
-    __shared__ unsigned hist[256];
-    __shared__ unsigned s_prefix, s_rank, s_count;
-    const int b = W.newest_begin, e = W.newest_end;
-    if (threadIdx.x == 0) s_count = 0;
-    __syncthreads();
-    unsigned cnt = 0;
-    for (int i = b + threadIdx.x; i < e; i += blockDim.x) cnt += (e_wo[i] >= 0);
-    atomicAdd(&s_count, cnt);
-    __syncthreads();
-    const unsigned n = s_count;
-    if (n == 0) {
-        if (threadIdx.x == 0) frame_th[W.frame_base + W.N - 1] = 12 * 12 * LDSO_BA_PATTERN_NUM;
-        return;
-    }
-    if (threadIdx.x == 0) {
-        s_prefix = 0;
-        s_rank = (unsigned)(int)(kFrameEnergyTHN * (float)n);
-    }
-    for (int pass = 0; pass < 4; pass++) {
-        const int shift = 24 - 8 * pass;
-        for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
-        __syncthreads();
-        const unsigned prefix = s_prefix;
-        const unsigned pmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
-        for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
-            const float x = e_wo[i];
-            if (!(x >= 0)) continue;
-            const unsigned key = __float_as_uint(x) & 0x7FFFFFFFu;  // -0.0 -> 0
-            if ((key & pmask) != (prefix & pmask)) continue;
-            atomicAdd(&hist[(key >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned rank = s_rank, acc = 0;
-            int d = 0;
-            for (; d < 256; d++) {
-                if (acc + hist[d] > rank) break;
-                acc += hist[d];
-            }
-            s_rank = rank - acc;
-            s_prefix = prefix | ((unsigned)d << shift);
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-#pragma clang fp contract(off)
-        const float nth = sqrtf(__uint_as_float(s_prefix));
-        float v = nth * kFrameEnergyTHFacMedian;
-        v = 26.0f * kFrameEnergyTHConstWeight + v * (1 - kFrameEnergyTHConstWeight);
-        v = v * v;
-        v *= kOverallEnergyTHWeight * kOverallEnergyTHWeight;
-        frame_th[W.frame_base + W.N - 1] = v;
     }
 }
 
@@ -627,331 +651,340 @@ __global__ __launch_bounds__(256) void k_point_sc(PointParams P) {
 }
 
 // ============================================================================================
-// k_stitch_top: per (h,t) pair, AccumulatedTopHessian.cc:213-239 (double)
+// k_stitch: one 256-thread block per frame pair (h,t) of every window, straight from the
+// partial slabs of k_linearize / k_point_sc, accumulating into the packed upper triangles of
+// {HA, bA, Hsc, bsc} with f64 atomics (zeroed before the pass):
+//   Top  bucket (h,t): sum the chunk partials, AccumulatorApprox::finish layout, adjoint
+//        sandwiches (AccumulatedTopHessian.cc:213-239), symmetrised as stitchDoubleMT does
+//        (H(a,b) = H(a,b) + H(b,a)^T, H(c,h) = H(h,c)^T; AccumulatedTopHessian.h:91-104)
+//   SC   host i = h, target j = t: rows of G_i for slot j (accD/accE/accEB of
+//        AccumulatedSCHessian.cc:35-50) summed from the SYRK chunk partials, then
+//        AccumulatedSCHessian.cc:80-114; only the upper triangle is produced (the solve reads
+//        only it, EnergyFunctional.cc:378) using D_kj = D_jk^T.
+// The diagonal (h == t) blocks have no residuals; block (0,0) of each window instead runs
+// setNewFrameEnergyTH (FullSystem.cc:2078-2109) and the linearizeAll energy sum.
+// Only the f64 summation order of the atomics varies between runs.
 // ============================================================================================
-struct TopStitchParams {
+constexpr int kStThreads = 256;
+constexpr int kThMaxLds = 8192;  // candidate energies staged in LDS; larger sets re-read HBM
+
+struct StitchParams {
     const WinDev *__restrict__ wins;
     const int *__restrict__ pair_win;
-    const int2 *__restrict__ pair_items;  // {first item, n items}
+    const float *__restrict__ e_wo;
+    float *frame_th;
+    const int2 *__restrict__ pair_items;  // per global pair: {first top item, n items}
     const float *__restrict__ top_slab;
-    const double *__restrict__ adH;
-    const double *__restrict__ adT;
-    double *top_rec;
-};
-
-__global__ __launch_bounds__(64) void k_stitch_top(TopStitchParams P) {
-    const int pair = blockIdx.x;
-    const WinDev &W = P.wins[P.pair_win[pair]];
-    const int N = W.N, aidx = pair - W.pair_base, h = aidx % N, t = aidx / N;
-    if (h == t) return;
-    __shared__ double acc[kTopVals];
-    __shared__ double A[13][13];
-    __shared__ double AH[64], AT[64], TH[64], TT[64];
-    const int tid = threadIdx.x;
-    const int2 pi = P.pair_items[pair];
-    for (int j = tid; j < kTopVals; j += 64) {
-        double s = 0;
-        for (int k = 0; k < pi.y; k++) s += (double)P.top_slab[(size_t)(pi.x + k) * kTopVals + j];
-        acc[j] = s;
-    }
-    AH[tid] = P.adH[(size_t)pair * 64 + tid];
-    AT[tid] = P.adT[(size_t)pair * 64 + tid];
-    __syncthreads();
-    if (tid == 0) {  // AccumulatorApprox::finish layout (MatrixAccumulators.h:771-800)
-        int q = 0;
-        for (int r = 0; r < 10; r++)
-            for (int c = r; c < 10; c++) {
-                A[r][c] = A[c][r] = acc[q];
-                q++;
-            }
-        for (int r = 0; r < 10; r++)
-            for (int c = 0; c < 3; c++) A[r][10 + c] = A[10 + c][r] = acc[55 + 3 * r + c];
-        A[10][10] = acc[85];
-        A[10][11] = A[11][10] = acc[86];
-        A[10][12] = A[12][10] = acc[87];
-        A[11][11] = acc[88];
-        A[11][12] = A[12][11] = acc[89];
-        A[12][12] = acc[90];
-    }
-    __syncthreads();
-    const int r = tid >> 3, c = tid & 7;
-    {
-        double sh = 0, st = 0;
-        for (int k = 0; k < 8; k++) {
-            sh += AH[r * 8 + k] * A[4 + k][4 + c];
-            st += AT[r * 8 + k] * A[4 + k][4 + c];
-        }
-        TH[tid] = sh;
-        TT[tid] = st;
-    }
-    __syncthreads();
-    double *rec = P.top_rec + W.top_rec_base + (size_t)aidx * kTopRecLen;
-    {
-        double hh = 0, tt = 0, ht = 0;
-        for (int k = 0; k < 8; k++) {
-            hh += TH[r * 8 + k] * AH[c * 8 + k];
-            tt += TT[r * 8 + k] * AT[c * 8 + k];
-            ht += TH[r * 8 + k] * AT[c * 8 + k];
-        }
-        rec[tid] = hh;
-        rec[64 + tid] = tt;
-        rec[128 + tid] = ht;
-    }
-    if (tid < 32) {  // H(h,c), H(t,c): 8x4
-        const int rr = tid >> 2, cc = tid & 3;
-        double sh = 0, st = 0;
-        for (int k = 0; k < 8; k++) {
-            sh += AH[rr * 8 + k] * A[4 + k][cc];
-            st += AT[rr * 8 + k] * A[4 + k][cc];
-        }
-        rec[192 + tid] = sh;
-        rec[224 + tid] = st;
-    }
-    if (tid < 16) rec[256 + tid] = A[tid >> 2][tid & 3];
-    if (tid < 8) {
-        double sh = 0, st = 0;
-        for (int k = 0; k < 8; k++) {
-            sh += AH[tid * 8 + k] * A[4 + k][12];
-            st += AT[tid * 8 + k] * A[4 + k][12];
-        }
-        rec[272 + tid] = sh;
-        rec[280 + tid] = st;
-    }
-    if (tid < 4) rec[288 + tid] = A[tid][12];
-}
-
-// ============================================================================================
-// k_sc_reduce: per (window, host) sum of the chunk partials into G_h (double, full symmetric)
-// ============================================================================================
-struct ScReduceParams {
-    const WinDev *__restrict__ wins;
-    const int *__restrict__ frame_win;
+    const double *__restrict__ item_energy;
     const int2 *__restrict__ host_items;  // per global frame: {first sc item, n items}
     const float *__restrict__ sc_slab;
-    double *G;
-};
-
-__global__ __launch_bounds__(256) void k_sc_reduce(ScReduceParams P) {
-    const int fg = blockIdx.x;
-    const WinDev &W = P.wins[P.frame_win[fg]];
-    const int host = fg - W.frame_base, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
-    const int2 hi = P.host_items[fg];
-    double *G = P.G + W.g_base + (size_t)host * KP * KP;
-    for (int e = threadIdx.x; e < ntiles * 16; e += blockDim.x) {
-        const int tile = e >> 4, ii = (e >> 2) & 3, jj = e & 3;
-        double s = 0;
-        for (int k = 0; k < hi.y; k++)
-            s += (double)P.sc_slab[W.sc_slab_base + (size_t)(hi.x - W.sc_item_base + k) * ntiles * 16 + e];
-        int a = 0, rem = tile;
-        while (rem >= nt - a) {
-            rem -= nt - a;
-            a++;
-        }
-        const int bb = a + rem;
-        const int row = 4 * a + ii, col = 4 * bb + jj;
-        G[(size_t)row * KP + col] = s;
-        G[(size_t)col * KP + row] = s;
-    }
-}
-
-// ============================================================================================
-// k_stitch_sc: per (host i, target j): AccumulatedSCHessian.cc:80-114 (double)
-// record: Hjk[N][64] | Hji[64] | Hii[64] | Hic[32] | Hjc[32] | bi[8] | bj[8]
-// ============================================================================================
-struct ScStitchParams {
-    const WinDev *__restrict__ wins;
-    const int *__restrict__ pair_win;
-    const double *__restrict__ G;
     const double *__restrict__ adH;
     const double *__restrict__ adT;
-    double *sc_rec;
-};
-
-__global__ __launch_bounds__(64) void k_stitch_sc(ScStitchParams P) {
-    const int pair = blockIdx.x;
-    const WinDev &W = P.wins[P.pair_win[pair]];
-    const int N = W.N, aidx = pair - W.pair_base, i = aidx % N, j = aidx / N;
-    if (i == j) return;
-    const int KP = W.KP, Kc = 8 * (N - 1), sj = j < i ? j : j - 1;
-    const double *G = P.G + W.g_base + (size_t)i * KP * KP;
-    __shared__ double AHij[64], ATij[64], AHik[64], ATik[64], Dm[64], X[64], S[64];
-    const int tid = threadIdx.x, r = tid >> 3, c = tid & 7;
-    AHij[tid] = P.adH[(size_t)pair * 64 + tid];
-    ATij[tid] = P.adT[(size_t)pair * 64 + tid];
-    double *rec = P.sc_rec + W.sc_rec_base + (size_t)aidx * sc_rec_len(N);
-    double sacc = 0;  // S = sum_k D_jk * AH_ik^T
-    for (int k = 0; k < N; k++) {
-        if (k == i) continue;
-        const int sk = k < i ? k : k - 1;
-        const int pik = W.pair_base + i + N * k;
-        __syncthreads();
-        Dm[tid] = G[(size_t)(8 * sj + r) * KP + 8 * sk + c];
-        AHik[tid] = P.adH[(size_t)pik * 64 + tid];
-        ATik[tid] = P.adT[(size_t)pik * 64 + tid];
-        __syncthreads();
-        double x = 0, sv = 0;
-        for (int q = 0; q < 8; q++) {
-            x += ATij[r * 8 + q] * Dm[q * 8 + c];
-            sv += Dm[r * 8 + q] * AHik[c * 8 + q];
-        }
-        X[tid] = x;
-        sacc += sv;
-        __syncthreads();
-        double hjk = 0;
-        for (int q = 0; q < 8; q++) hjk += X[r * 8 + q] * ATik[c * 8 + q];
-        rec[k * 64 + tid] = hjk;  // H(j,k) += AT_ij D AT_ik^T
-    }
-    __syncthreads();
-    S[tid] = sacc;
-    __syncthreads();
-    double hji = 0, hii = 0;
-    for (int q = 0; q < 8; q++) {
-        hji += ATij[r * 8 + q] * S[q * 8 + c];
-        hii += AHij[r * 8 + q] * S[q * 8 + c];
-    }
-    rec[N * 64 + tid] = hji;       // H(j,i) += sum_k AT_ij D AH_ik^T
-    rec[N * 64 + 64 + tid] = hii;  // H(i,i) += sum_k AH_ij D AH_ik^T
-    if (tid < 32) {
-        const int rr = tid >> 2, cc = tid & 3;
-        double hi = 0, hj = 0;
-        for (int q = 0; q < 8; q++) {
-            const double e = G[(size_t)(8 * sj + q) * KP + Kc + cc];
-            hi += AHij[rr * 8 + q] * e;
-            hj += ATij[rr * 8 + q] * e;
-        }
-        rec[N * 64 + 128 + tid] = hi;
-        rec[N * 64 + 160 + tid] = hj;
-    }
-    if (tid < 8) {
-        double bi = 0, bj = 0;
-        for (int q = 0; q < 8; q++) {
-            const double e = G[(size_t)(8 * sj + q) * KP + Kc + 4];
-            bi += AHij[tid * 8 + q] * e;
-            bj += ATij[tid * 8 + q] * e;
-        }
-        rec[N * 64 + 192 + tid] = bi;
-        rec[N * 64 + 200 + tid] = bj;
-    }
-}
-
-// ============================================================================================
-// k_final: per window, assemble the packed upper triangles of HA, Hsc and bA, bsc, and the
-// linearizeAll energy; symmetrisation as in AccumulatedTopHessian.h:91-104 / SC.h:91-97
-// ============================================================================================
-struct FinalParams {
-    const WinDev *__restrict__ wins;
-    const double *__restrict__ top_rec;
-    const double *__restrict__ sc_rec;
-    const double *__restrict__ G;
-    const double *__restrict__ item_energy;
     double *sys;
-    double *win_energy;  // [win][2]
+    double *win_energy;
     int accumulate;
 };
 
-__device__ inline void decode(int x, int &f, int &k) {  // H index -> (frame or -1 for calib, k)
-    if (x < 4) {
-        f = -1;
-        k = x;
+__device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row <= col
+    return (long long)row * D - (long long)row * (row - 1) / 2 + (col - row);
+}
+
+// setNewFrameEnergyTH as an exact 4-pass radix select (nth_element semantics) + energy sums
+__device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &W, int w, unsigned *keys) {
+    unsigned *hist = keys + kThMaxLds;
+    unsigned *sh = hist + 256;  // [0] count [1] prefix [2] rank
+    double *red = reinterpret_cast<double *>(sh + 8);
+    const int tid = threadIdx.x, N = W.N;
+    const int b = W.newest_begin, e = W.newest_end;
+    if (tid == 0) sh[0] = 0;
+    __syncthreads();
+    for (int i = b + tid; i < e; i += kStThreads) {
+        const float x = P.e_wo[i];
+        if (x >= 0) {
+            const unsigned slot = atomicAdd(&sh[0], 1u);
+            if (slot < (unsigned)kThMaxLds) keys[slot] = __float_as_uint(x) & 0x7FFFFFFFu;  // -0.0 -> 0
+        }
+    }
+    __syncthreads();
+    const unsigned n = sh[0];
+    if (n == 0) {
+        if (tid == 0) P.frame_th[W.frame_base + N - 1] = 12 * 12 * LDSO_BA_PATTERN_NUM;
     } else {
-        f = (x - 4) >> 3;
-        k = (x - 4) & 7;
+        const bool in_lds = n <= (unsigned)kThMaxLds;
+        if (tid == 0) {
+            sh[1] = 0;
+            sh[2] = (unsigned)(int)(kFrameEnergyTHN * (float)n);  // int nthIdx = 0.7f * size()
+        }
+        for (int pass = 0; pass < 4; pass++) {
+            const int shift = 24 - 8 * pass;
+            hist[tid] = 0;
+            __syncthreads();
+            const unsigned prefix = sh[1];
+            const unsigned pmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
+            if (in_lds) {
+                for (unsigned i = tid; i < n; i += kStThreads) {
+                    const unsigned key = keys[i];
+                    if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+                }
+            } else {
+                for (int i = b + tid; i < e; i += kStThreads) {
+                    const float x = P.e_wo[i];
+                    if (!(x >= 0)) continue;
+                    const unsigned key = __float_as_uint(x) & 0x7FFFFFFFu;
+                    if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+                }
+            }
+            __syncthreads();
+            if (tid < 64) {  // one wave: lane l owns bins 4l..4l+3
+                const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
+                unsigned incl = h0 + h1 + h2 + h3;
+#pragma unroll
+                for (int m = 1; m < 64; m <<= 1) {
+                    const unsigned y = __shfl_up(incl, m, kWave);
+                    if (tid >= m) incl += y;
+                }
+                const unsigned rank = sh[2];
+                const unsigned long long hit = __ballot(incl > rank);
+                const int first = __ffsll((long long)hit) - 1;
+                if (tid == first) {
+                    unsigned acc = incl - (h0 + h1 + h2 + h3);
+                    int d = 4 * tid;
+                    const unsigned hb[4] = {h0, h1, h2, h3};
+                    for (int k = 0; k < 4; k++, d++) {
+                        if (acc + hb[k] > rank) break;
+                        acc += hb[k];
+                    }
+                    sh[2] = rank - acc;
+                    sh[1] = prefix | ((unsigned)d << shift);
+                }
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+#pragma clang fp contract(off)
+            const float nth = sqrtf(__uint_as_float(sh[1]));
+            float v = nth * kFrameEnergyTHFacMedian;
+            v = 26.0f * kFrameEnergyTHConstWeight + v * (1 - kFrameEnergyTHConstWeight);
+            v = v * v;
+            v *= kOverallEnergyTHWeight * kOverallEnergyTHWeight;
+            P.frame_th[W.frame_base + N - 1] = v;
+        }
+    }
+    // linearizeAll: sum of returned energies and #IN, fixed order (strided, then thread 0)
+    double se = 0, sn = 0;
+    for (int k = tid; k < W.n_top_items; k += kStThreads) {
+        se += P.item_energy[2 * (W.top_item_base + k)];
+        sn += P.item_energy[2 * (W.top_item_base + k) + 1];
+    }
+    red[2 * tid] = se;
+    red[2 * tid + 1] = sn;
+    __syncthreads();
+    if (tid == 0) {
+        double a = 0, c = 0;
+        for (int k = 0; k < kStThreads; k++) {
+            a += red[2 * k];
+            c += red[2 * k + 1];
+        }
+        P.win_energy[2 * w] = a;
+        P.win_energy[2 * w + 1] = c;
     }
 }
 
-__global__ __launch_bounds__(256) void k_final(FinalParams P) {
-    const int w = blockIdx.x;
+// slot (r, c) of the 13x13 finish() matrix -> index into the 96-slot partial layout
+__device__ __forceinline__ int top_slot(int r, int c) {
+    if (r > c) {
+        const int t = r;
+        r = c;
+        c = t;
+    }
+    if (c < 10) return r * 10 - r * (r - 1) / 2 + (c - r);  // Data[] (upper row-major)
+    if (r < 10) return 55 + 3 * r + (c - 10);                // TopRight
+    const int a = r - 10, b = c - 10;                        // BotRight
+    return 85 + (a == 0 ? b : a == 1 ? 2 + b : 5);
+}
+
+// element (row, col) of G_h summed over the host's SYRK chunk partials (upper tiles only)
+__device__ __forceinline__ double g_elem(const float *__restrict__ slab, int n_items, int per, int nt, int row,
+                                         int col) {
+    if (row > col) {
+        const int t = row;
+        row = col;
+        col = t;
+    }
+    const int a = row >> 2, b = col >> 2;
+    const int tile = a * nt - a * (a - 1) / 2 + (b - a);
+    const float *src = slab + (size_t)tile * 16 + ((row & 3) << 2) + (col & 3);
+    double s = 0;
+    for (int k = 0; k < n_items; k++) s += (double)src[(size_t)k * per];
+    return s;
+}
+
+__global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
+    __shared__ double sm[5760];
+    const int pair = blockIdx.x;
+    const int w = P.pair_win[pair];
     const WinDev &W = P.wins[w];
-    if (threadIdx.x == 0) {
-        double e = 0, n = 0;
-        for (int k = 0; k < W.n_top_items; k++) {
-            e += P.item_energy[2 * (W.top_item_base + k)];
-            n += P.item_energy[2 * (W.top_item_base + k) + 1];
-        }
-        P.win_energy[2 * w] = e;
-        P.win_energy[2 * w + 1] = n;
+    const int N = W.N, D = W.D, aidx = pair - W.pair_base, h = aidx % N, t = aidx / N;
+    const int tid = threadIdx.x;
+    if (h == t) {
+        if (aidx == 0) frame_threshold_and_energy(P, W, w, reinterpret_cast<unsigned *>(sm));
+        return;
     }
     if (!P.accumulate) return;
-    const int N = W.N, D = W.D, KP = W.KP, Kc = 8 * (N - 1);
-    const int srl = sc_rec_len(N);
-    const double *trec = P.top_rec + W.top_rec_base;
-    const double *srec = P.sc_rec + W.sc_rec_base;
-    const double *G = P.G + W.g_base;
-    auto T = [&](int h, int t) { return trec + (size_t)(h + N * t) * kTopRecLen; };
-    auto S = [&](int i, int j) { return srec + (size_t)(i + N * j) * srl; };
     double *sys = P.sys + W.sys_base;
     const long long pl = packed_len(D);
-    for (long long q = threadIdx.x; q < pl + D; q += blockDim.x) {
-        double ha = 0, hs = 0;
-        long long out = q;
-        if (q < pl) {
-            // packed index -> (row, col >= row)
-            int row = (int)((2.0 * D + 1 - sqrt((2.0 * D + 1) * (2.0 * D + 1) - 8.0 * (double)q)) / 2);
-            while ((long long)row * D - (long long)row * (row - 1) / 2 > q) row--;
-            while ((long long)(row + 1) * D - (long long)(row + 1) * row / 2 <= q) row++;
-            const int col = row + (int)(q - ((long long)row * D - (long long)row * (row - 1) / 2));
-            int fa, ra, fb, cb;
-            decode(row, fa, ra);
-            decode(col, fb, cb);
-            if (fa < 0 && fb < 0) {
-                for (int k = 0; k < N * N; k++) {
-                    const int h = k % N, t = k / N;
-                    if (h != t) ha += T(h, t)[256 + ra * 4 + cb];
-                }
-                for (int i = 0; i < N; i++) hs += G[(size_t)i * KP * KP + (size_t)(Kc + ra) * KP + Kc + cb];
-            } else if (fa < 0) {  // H(c, frame b) = H(b, c)^T
-                const int b = fb;
-                for (int t = 0; t < N; t++)
-                    if (t != b) ha += T(b, t)[192 + cb * 4 + ra];
-                for (int h = 0; h < N; h++)
-                    if (h != b) ha += T(h, b)[224 + cb * 4 + ra];
-                for (int j = 0; j < N; j++)
-                    if (j != b) hs += S(b, j)[N * 64 + 128 + cb * 4 + ra];
-                for (int i = 0; i < N; i++)
-                    if (i != b) hs += S(i, b)[N * 64 + 160 + cb * 4 + ra];
-            } else if (fa == fb) {
-                const int a = fa, e = ra * 8 + cb;
-                for (int t = 0; t < N; t++)
-                    if (t != a) ha += T(a, t)[e];
-                for (int h = 0; h < N; h++)
-                    if (h != a) ha += T(h, a)[64 + e];
-                for (int i = 0; i < N; i++)
-                    if (i != a) hs += S(i, a)[a * 64 + e];
-                for (int j = 0; j < N; j++)
-                    if (j != a) hs += S(a, j)[N * 64 + 64 + e];
-            } else {  // a < b
-                const int a = fa, b = fb;
-                ha = T(a, b)[128 + ra * 8 + cb] + T(b, a)[128 + cb * 8 + ra];
-                for (int i = 0; i < N; i++)
-                    if (i != a && i != b) hs += S(i, a)[b * 64 + ra * 8 + cb];
-                hs += S(b, a)[N * 64 + ra * 8 + cb];
-                hs += S(a, b)[N * 64 + cb * 8 + ra];
+    double *HA = sys, *bA = sys + pl, *Hs = sys + pl + D, *bs = sys + 2 * pl + D;
+    const int hI = 4 + 8 * h, tI = 4 + 8 * t;
+
+    // ---------------- Top: bucket (h, t) ------------------------------------------------
+    double *acc = sm, *A = acc + 96, *AH = A + 169, *AT = AH + 64, *TH = AT + 64, *TT = TH + 64;
+    {
+        const int2 pi = P.pair_items[pair];
+        if (tid < kTopVals) {
+            const float *src = P.top_slab + (size_t)pi.x * kTopVals + tid;
+            double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+            int k = 0;
+            for (; k + 4 <= pi.y; k += 4) {  // 4 independent loads in flight
+                s0 += (double)src[(size_t)k * kTopVals];
+                s1 += (double)src[(size_t)(k + 1) * kTopVals];
+                s2 += (double)src[(size_t)(k + 2) * kTopVals];
+                s3 += (double)src[(size_t)(k + 3) * kTopVals];
             }
-        } else {
-            const int x = (int)(q - pl);
-            int fa, ra;
-            decode(x, fa, ra);
-            if (fa < 0) {
-                for (int k = 0; k < N * N; k++) {
-                    const int h = k % N, t = k / N;
-                    if (h != t) ha += T(h, t)[288 + ra];
-                }
-                for (int i = 0; i < N; i++) hs += G[(size_t)i * KP * KP + (size_t)(Kc + ra) * KP + Kc + 4];
-            } else {
-                const int a = fa;
-                for (int t = 0; t < N; t++)
-                    if (t != a) ha += T(a, t)[272 + ra];
-                for (int h = 0; h < N; h++)
-                    if (h != a) ha += T(h, a)[280 + ra];
-                for (int j = 0; j < N; j++)
-                    if (j != a) hs += S(a, j)[N * 64 + 192 + ra];
-                for (int i = 0; i < N; i++)
-                    if (i != a) hs += S(i, a)[N * 64 + 200 + ra];
-            }
-            out = pl + x;
+            for (; k < pi.y; k++) s0 += (double)src[(size_t)k * kTopVals];
+            acc[tid] = (s0 + s1) + (s2 + s3);
+        } else if (tid < kTopVals + 64) {
+            AH[tid - kTopVals] = P.adH[(size_t)pair * 64 + tid - kTopVals];
+        } else if (tid < kTopVals + 128) {
+            AT[tid - kTopVals - 64] = P.adT[(size_t)pair * 64 + tid - kTopVals - 64];
         }
-        sys[out] = ha;                 // {HA upper, bA}
-        sys[pl + D + out] = hs;        // {Hsc upper, bsc}
+        __syncthreads();
+        if (tid < 169) A[tid] = acc[top_slot(tid / 13, tid % 13)];
+        __syncthreads();
+        if (tid < 128) {
+            const int l = tid & 63, r = l >> 3, c = l & 7;
+            const double *Ad = tid < 64 ? AH : AT;
+            double sacc = 0;
+            for (int k = 0; k < 8; k++) sacc += Ad[r * 8 + k] * A[(4 + k) * 13 + 4 + c];
+            (tid < 64 ? TH : TT)[l] = sacc;
+        }
+        __syncthreads();
+        if (tid < 192) {
+            const int which = tid >> 6, l = tid & 63, r = l >> 3, c = l & 7;
+            double v = 0;
+            if (which == 0) {  // H(h,h) += AH A AH^T (upper half of the diagonal block)
+                for (int k = 0; k < 8; k++) v += TH[r * 8 + k] * AH[c * 8 + k];
+                if (c >= r) atomicAdd(&HA[pk_index(hI + r, hI + c, D)], v);
+            } else if (which == 1) {  // H(t,t) += AT A AT^T
+                for (int k = 0; k < 8; k++) v += TT[r * 8 + k] * AT[c * 8 + k];
+                if (c >= r) atomicAdd(&HA[pk_index(tI + r, tI + c, D)], v);
+            } else {  // H(h,t) += AH A AT^T; the (t,h) term folds in transposed (symmetrisation)
+                for (int k = 0; k < 8; k++) v += TH[r * 8 + k] * AT[c * 8 + k];
+                if (h < t) atomicAdd(&HA[pk_index(hI + r, tI + c, D)], v);
+                else atomicAdd(&HA[pk_index(tI + c, hI + r, D)], v);
+            }
+        } else {  // 64 threads: H(h,c) = AH A_8C and H(t,c) = AT A_8C, stored as H(c, frame)
+            const int l = tid - 192, which = l >> 5, rr = (l & 31) >> 2, cc = l & 3;
+            const double *Ad = which == 0 ? AH : AT;
+            double v = 0;
+            for (int k = 0; k < 8; k++) v += Ad[rr * 8 + k] * A[(4 + k) * 13 + cc];
+            atomicAdd(&HA[pk_index(cc, (which == 0 ? hI : tI) + rr, D)], v);
+        }
+        if (tid < 16) {
+            const int r = tid >> 2, c = tid & 3;
+            if (c >= r) atomicAdd(&HA[pk_index(r, c, D)], A[r * 13 + c]);
+        } else if (tid < 32) {
+            const int l = tid - 16, which = l >> 3, r = l & 7;
+            const double *Ad = which == 0 ? AH : AT;
+            double v = 0;
+            for (int k = 0; k < 8; k++) v += Ad[r * 8 + k] * A[(4 + k) * 13 + 12];
+            atomicAdd(&bA[(which == 0 ? hI : tI) + r], v);
+        } else if (tid < 36) {
+            atomicAdd(&bA[tid - 32], A[(tid - 32) * 13 + 12]);
+        }
+    }
+    __syncthreads();
+
+    // ---------------- SC: host i = h, target j = t ---------------------------------------
+    {
+        const int i = h, j = t, KP = W.KP, nt = KP / 4, per = W.ntiles * 16, Kc = 8 * (N - 1);
+        const int sj = j < i ? j : j - 1;
+        const int2 hi = P.host_items[W.frame_base + i];
+        const float *slab = P.sc_slab + W.sc_slab_base + (size_t)(hi.x - W.sc_item_base) * per;
+        double *Gj = sm;                       // [8][KP]: rows 8 sj.. of G_i
+        double *Ah = Gj + 8 * 128;             // AH_ij, AT_ij
+        double *At = Ah + 64;
+        double *AHk = At + 64;                 // [N-1][64] AH_ik
+        double *ATk = AHk + kMaxRes * 64;      // [N-1][64] AT_ik
+        double *X = ATk + kMaxRes * 64;        // [N-1][64]
+        double *Sk = X + kMaxRes * 64;         // [N-1][64]
+        double *Cc = Sk + kMaxRes * 64;        // [4][5]: G_i[Kc+r][Kc+c], bc
+        for (int e = tid; e < 8 * KP; e += kStThreads) {
+            const int r = e / KP, col = e % KP;
+            Gj[e] = col < Kc + 5 ? g_elem(slab, hi.y, per, nt, 8 * sj + r, col) : 0.0;
+        }
+        if (sj == 0 && tid < 20) {  // accHcc / accbc once per host (AccumulatedSCHessian.cc:105-113)
+            const int r = tid / 5, c = tid % 5;
+            Cc[tid] = g_elem(slab, hi.y, per, nt, Kc + r, Kc + c);
+        }
+        if (tid < 64) Ah[tid] = P.adH[(size_t)pair * 64 + tid];
+        else if (tid < 128) At[tid - 64] = P.adT[(size_t)pair * 64 + tid - 64];
+        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
+            const int s = e >> 6, k = s + (s >= i), pik = W.pair_base + i + N * k;
+            AHk[e] = P.adH[(size_t)pik * 64 + (e & 63)];
+            ATk[e] = P.adT[(size_t)pik * 64 + (e & 63)];
+        }
+        __syncthreads();
+        // per k != i: X_k = AT_ij D_jk, S_k = D_jk AH_ik^T
+        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
+            const int s = e >> 6, r = (e >> 3) & 7, c = e & 7;
+            const double *Dm = Gj + 8 * s;  // D_jk[r][c] = Gj[r * KP + 8 s + c]
+            double x = 0, sv = 0;
+            for (int q = 0; q < 8; q++) {
+                x += At[r * 8 + q] * Dm[q * KP + c];
+                sv += Dm[r * KP + q] * AHk[s * 64 + c * 8 + q];
+            }
+            X[e] = x;
+            Sk[e] = sv;
+        }
+        __syncthreads();
+        // H(j,k) += AT_ij D_jk AT_ik^T, upper triangle only (j < k, or the upper half at j == k)
+        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
+            const int s = e >> 6, k = s + (s >= i), r = (e >> 3) & 7, c = e & 7;
+            if (j > k || (j == k && c < r)) continue;
+            double v = 0;
+            for (int q = 0; q < 8; q++) v += X[s * 64 + r * 8 + q] * ATk[s * 64 + c * 8 + q];
+            atomicAdd(&Hs[pk_index(4 + 8 * j + r, 4 + 8 * k + c, D)], v);
+        }
+        if (tid < 64) {
+            const int r = tid >> 3, c = tid & 7;
+            double hji = 0, hii = 0;
+            for (int q = 0; q < 8; q++) {
+                double sq = 0;  // S = sum_k S_k, fixed order
+                for (int s = 0; s < N - 1; s++) sq += Sk[s * 64 + q * 8 + c];
+                hji += At[r * 8 + q] * sq;
+                hii += Ah[r * 8 + q] * sq;
+            }
+            // H(j,i) += sum_k AT_ij D AH_ik^T; its upper position is (j,i) or (i,j)^T
+            if (j < i) atomicAdd(&Hs[pk_index(4 + 8 * j + r, 4 + 8 * i + c, D)], hji);
+            else atomicAdd(&Hs[pk_index(4 + 8 * i + c, 4 + 8 * j + r, D)], hji);
+            if (c >= r) atomicAdd(&Hs[pk_index(4 + 8 * i + r, 4 + 8 * i + c, D)], hii);  // H(i,i)
+        } else if (tid < 128) {  // H(i,c) += AH_ij E, H(j,c) += AT_ij E (stored as H(c, frame))
+            const int l = tid - 64, which = l >> 5, rr = (l & 31) >> 2, cc = l & 3;
+            const double *Ad = which == 0 ? Ah : At;
+            double v = 0;
+            for (int q = 0; q < 8; q++) v += Ad[rr * 8 + q] * Gj[q * KP + Kc + cc];
+            atomicAdd(&Hs[pk_index(cc, 4 + 8 * (which == 0 ? i : j) + rr, D)], v);
+        } else if (tid < 144) {  // b(i) += AH_ij EB, b(j) += AT_ij EB
+            const int l = tid - 128, which = l >> 3, rr = l & 7;
+            const double *Ad = which == 0 ? Ah : At;
+            double v = 0;
+            for (int q = 0; q < 8; q++) v += Ad[rr * 8 + q] * Gj[q * KP + Kc + 4];
+            atomicAdd(&bs[4 + 8 * (which == 0 ? i : j) + rr], v);
+        } else if (sj == 0 && tid < 164) {  // H_cc += accHcc, b_c += accbc
+            const int l = tid - 144, r = l / 5, c = l % 5;
+            if (c == 4) atomicAdd(&bs[r], Cc[l]);
+            else if (c >= r) atomicAdd(&Hs[pk_index(r, c, D)], Cc[l]);
+        }
     }
 }
 
@@ -1000,10 +1033,45 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
     P.pt_step[p] = -b * po[0] / (1 + P.lambda);
 }
 
-// image repack: FrameHessian::dI AoS float3 -> float4 (16-B aligned texel loads)
-__global__ void k_repack(const float *__restrict__ src, float4 *dst, int npix) {
+// image ingest: FrameHessian::dI (AoS [I, dx, dy]) -> [I, dx, dy, 0] texels in 2x4 tiles
+__global__ void k_tile_image(const float *__restrict__ src, float4 *dst, int w, int h, int tpr2, int hp, int tiled) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npix) dst[i] = make_float4(src[3 * i], src[3 * i + 1], src[3 * i + 2], 0.f);
+    const int wp = tpr2 * 2;
+    if (i >= wp * hp) return;
+    const int x = i % wp, y = i / wp;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (x < w && y < h) {
+        const float *p = src + 3 * ((size_t)y * w + x);
+        v = make_float4(p[0], p[1], p[2], 0.f);
+    }
+    dst[tiled ? (((y >> 2) * tpr2 + (x >> 1)) << 3) + ((y & 3) << 1) + (x & 1) : y * wp + x] = v;
+}
+
+template <int W, bool T, bool L3>
+void launch_lin2(bool xcd, bool cf, int nb, hipStream_t st, const LinParams &L) {
+    if (xcd) {
+        if (cf) k_linearize<W, T, L3, true, true><<<nb, 256, 0, st>>>(L);
+        else k_linearize<W, T, L3, true, false><<<nb, 256, 0, st>>>(L);
+    } else {
+        if (cf) k_linearize<W, T, L3, false, true><<<nb, 256, 0, st>>>(L);
+        else k_linearize<W, T, L3, false, false><<<nb, 256, 0, st>>>(L);
+    }
+}
+template <int W>
+void launch_lin1(bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t st, const LinParams &L) {
+    if (tiled) {
+        if (load3) launch_lin2<W, true, true>(xcd, cf, nb, st, L);
+        else launch_lin2<W, true, false>(xcd, cf, nb, st, L);
+    } else {
+        if (load3) launch_lin2<W, false, true>(xcd, cf, nb, st, L);
+        else launch_lin2<W, false, false>(xcd, cf, nb, st, L);
+    }
+}
+// variant = occupancy target in waves per SIMD (see DESIGN.md for the measured choice)
+void launch_linearize(int variant, bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t st,
+                      const LinParams &L) {
+    if (variant == 2) launch_lin1<2>(tiled, load3, xcd, cf, nb, st, L);
+    else launch_lin1<1>(tiled, load3, xcd, cf, nb, st, L);
 }
 
 // ============================================================================================
@@ -1058,9 +1126,11 @@ struct ldso_ba_ctx {
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
     std::vector<WinDev> wd;
-    int n_top_items = 0, n_sc_items = 0, n_pairs = 0, n_frames = 0, P_tot = 0, R_tot = 0;
+    int n_top_items = 0, n_sc_items = 0, n_pairs = 0, n_frames = 0, P_tot = 0, R_tot = 0, max_frames = 0;
     DevBuf<WinDev> d_wins;
     DevBuf<float4> d_img;
+    int tiles_per_row = 0, padded_h = 0;
+    long long frame_stride = 0;
     DevBuf<float> d_precalc, d_frame_th, d_pt_data, d_pt_out, d_pt_step;
     DevBuf<double> d_adH, d_adT;
     DevBuf<int> d_rs_point, d_pt_nres, d_pt_res, d_pair_win, d_frame_win, d_pt_host;
@@ -1075,6 +1145,8 @@ struct ldso_ba_ctx {
     DevBuf<float> d_xad;
     size_t sc_smem_max = 0;
     bool timing = false;
+    int lin_variant = 1;
+    bool tiled = true, load3 = false, xcd_remap = true, centre_first = true;  // measured best
     std::vector<PendingEv> pending;
     std::vector<hipEvent_t> ev_pool;
     double kms[kNumKernels] = {0};
@@ -1208,6 +1280,8 @@ int ldso_ba_create(int32_t device, ldso_ba_ctx **out) {
         delete c;
         return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
+    if (const char *v = getenv("LDSO_BA_LIN_VARIANT")) c->lin_variant = atoi(v);
+    if (const char *v = getenv("LDSO_BA_TILED")) c->tiled = atoi(v) != 0;
     *out = c;
     return 0;
 }
@@ -1277,6 +1351,9 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     c->width = ws[0].width;
     c->height = ws[0].height;
     c->npix = c->width * c->height;
+    c->tiles_per_row = (c->width + 1) / 2;
+    c->padded_h = (c->height + 3) / 4 * 4;
+    c->frame_stride = (long long)c->tiles_per_row * 2 * c->padded_h;
     c->wh.assign(n_windows, WinHost());
     c->wd.assign(n_windows, WinDev());
     c->sys_host_valid = false;
@@ -1442,6 +1519,8 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     c->n_sc_items = (int)sc_items.size();
     c->n_pairs = pair_base;
     c->n_frames = frame_base;
+    c->max_frames = 0;
+    for (int w = 0; w < n_windows; w++) c->max_frames = std::max(c->max_frames, ws[w].n_frames);
     c->P_tot = point_base;
     c->R_tot = res_base;
     c->sc_smem_max = smem_max;
@@ -1453,7 +1532,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         if (rc) return rc;              \
     } while (0)
     ALLOC(c->d_wins, n_windows);
-    ALLOC(c->d_img, (size_t)c->n_frames * c->npix);
+    ALLOC(c->d_img, (size_t)c->n_frames * c->frame_stride);
     ALLOC(c->d_precalc, precalc.size());
     ALLOC(c->d_frame_th, frame_th.size());
     ALLOC(c->d_pt_data, std::max<size_t>(1, pt_data.size()));
@@ -1548,7 +1627,9 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
                     (void)hipFree(stage);
                     return fail(-2, std::string("image upload: ") + hipGetErrorString(e));
                 }
-                k_repack<<<(c->npix + 255) / 256, 256, 0, c->stream>>>(stage, c->d_img.p + (size_t)fb * c->npix, c->npix);
+                k_tile_image<<<(int)((c->frame_stride + 255) / 256), 256, 0, c->stream>>>(
+                    stage, c->d_img.p + (size_t)fb * c->frame_stride, c->width, c->height, c->tiles_per_row, c->padded_h,
+                    c->tiled ? 1 : 0);
             }
         hipError_t e = hipStreamSynchronize(c->stream);
         (void)hipFree(stage);
@@ -1622,6 +1703,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     c->sys_host_valid = false;
     c->energy_valid = false;
     int rc;
+    if (accumulate) HIP_TRY(hipMemsetAsync(c->d_sys.p, 0, c->d_sys.bytes(), c->stream));
     if (c->n_top_items > 0) {
         LinParams L;
         L.items = c->d_top_items.p;
@@ -1642,47 +1724,49 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         L.top_slab = c->d_top_slab.p;
         L.item_energy = c->d_item_energy.p;
         L.n_items = c->n_top_items;
-        L.npix = c->npix;
+        L.n_blocks = (c->n_top_items + 3) / 4;
+        L.frame_stride = c->frame_stride;
+        L.tiles_per_row = c->tiles_per_row;
         L.fix = fix;
         L.accumulate = accumulate;
-        rc = timed_launch(c, 0, [&] { k_linearize<<<(c->n_top_items + 3) / 4, 256, 0, c->stream>>>(L); });
+        const int nb = (c->n_top_items + 3) / 4;
+        rc = timed_launch(c, 0, [&] {
+            launch_linearize(c->lin_variant, c->tiled, c->load3, c->xcd_remap, c->centre_first, nb, c->stream, L);
+        });
         if (rc) return rc;
     }
-    rc = timed_launch(c, 1, [&] {
-        k_frame_th<<<c->n_win, 256, 0, c->stream>>>(c->d_wins.p, c->d_rs_energy_wo.p, c->d_frame_th.p);
-    });
-    if (rc) return rc;
-    if (accumulate) {
-        if (c->n_sc_items > 0) {
-            PointParams Pp;
-            Pp.items = c->d_sc_items.p;
-            Pp.wins = c->d_wins.p;
-            Pp.pt_data = c->d_pt_data.p;
-            Pp.pt_nres = c->d_pt_nres.p;
-            Pp.pt_res = c->d_pt_res.p;
-            Pp.rs_tgt = c->d_rs_tgt.p;
-            Pp.rs_flags = c->d_rs_flags.p;
-            Pp.rs_rec = c->d_rs_rec.p;
-            Pp.pt_out = c->d_pt_out.p;
-            Pp.sc_slab = c->d_sc_slab.p;
-            Pp.n_items = c->n_sc_items;
-            rc = timed_launch(c, 2, [&] { k_point_sc<<<c->n_sc_items, 256, c->sc_smem_max, c->stream>>>(Pp); });
-            if (rc) return rc;
-        }
-        TopStitchParams T{c->d_wins.p, c->d_pair_win.p, c->d_pair_items.p, c->d_top_slab.p, c->d_adH.p, c->d_adT.p,
-                          c->d_top_rec.p};
-        rc = timed_launch(c, 3, [&] { k_stitch_top<<<c->n_pairs, 64, 0, c->stream>>>(T); });
-        if (rc) return rc;
-        ScReduceParams Sr{c->d_wins.p, c->d_frame_win.p, c->d_host_items.p, c->d_sc_slab.p, c->d_G.p};
-        rc = timed_launch(c, 4, [&] { k_sc_reduce<<<c->n_frames, 256, 0, c->stream>>>(Sr); });
-        if (rc) return rc;
-        ScStitchParams Ss{c->d_wins.p, c->d_pair_win.p, c->d_G.p, c->d_adH.p, c->d_adT.p, c->d_sc_rec.p};
-        rc = timed_launch(c, 5, [&] { k_stitch_sc<<<c->n_pairs, 64, 0, c->stream>>>(Ss); });
+    if (accumulate && c->n_sc_items > 0) {
+        PointParams Pp;
+        Pp.items = c->d_sc_items.p;
+        Pp.wins = c->d_wins.p;
+        Pp.pt_data = c->d_pt_data.p;
+        Pp.pt_nres = c->d_pt_nres.p;
+        Pp.pt_res = c->d_pt_res.p;
+        Pp.rs_tgt = c->d_rs_tgt.p;
+        Pp.rs_flags = c->d_rs_flags.p;
+        Pp.rs_rec = c->d_rs_rec.p;
+        Pp.pt_out = c->d_pt_out.p;
+        Pp.sc_slab = c->d_sc_slab.p;
+        Pp.n_items = c->n_sc_items;
+        rc = timed_launch(c, 1, [&] { k_point_sc<<<c->n_sc_items, 256, c->sc_smem_max, c->stream>>>(Pp); });
         if (rc) return rc;
     }
-    FinalParams F{c->d_wins.p, c->d_top_rec.p, c->d_sc_rec.p, c->d_G.p, c->d_item_energy.p, c->d_sys.p,
-                  c->d_win_energy.p, accumulate};
-    rc = timed_launch(c, 6, [&] { k_final<<<c->n_win, 256, 0, c->stream>>>(F); });
+    StitchParams Sp;
+    Sp.wins = c->d_wins.p;
+    Sp.pair_win = c->d_pair_win.p;
+    Sp.e_wo = c->d_rs_energy_wo.p;
+    Sp.frame_th = c->d_frame_th.p;
+    Sp.pair_items = c->d_pair_items.p;
+    Sp.top_slab = c->d_top_slab.p;
+    Sp.item_energy = c->d_item_energy.p;
+    Sp.host_items = c->d_host_items.p;
+    Sp.sc_slab = c->d_sc_slab.p;
+    Sp.adH = c->d_adH.p;
+    Sp.adT = c->d_adT.p;
+    Sp.sys = c->d_sys.p;
+    Sp.win_energy = c->d_win_energy.p;
+    Sp.accumulate = accumulate;
+    rc = timed_launch(c, 2, [&] { k_stitch<<<c->n_pairs, kStThreads, 0, c->stream>>>(Sp); });
     return rc;
 }
 
@@ -1884,7 +1968,7 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
         R.count = D.P;
         R.N = N;
         R.lambda = (float)lambda;
-        int rc = timed_launch(c, 7, [&] { k_resubstitute<<<(D.P + 255) / 256, 256, 0, c->stream>>>(R); });
+        int rc = timed_launch(c, 3, [&] { k_resubstitute<<<(D.P + 255) / 256, 256, 0, c->stream>>>(R); });
         if (rc) return rc;
     }
     if (point_step_out) {
@@ -1910,6 +1994,45 @@ int ldso_ba_unpack_system(ldso_ba_ctx *c) {
     if (!c) return fail(-1, "null ctx");
     c->sys_host_valid = false;  // get_system re-reads the (externally reduced) device buffer
     return 0;
+}
+
+int ldso_ba_copy_packed(ldso_ba_ctx *c, void *buf, int64_t n, int32_t direction) {
+    if (!c || !buf || n != (int64_t)c->d_sys.n) return fail(-1, "bad arguments (size must equal the packed system)");
+    HIP_TRY(hipSetDevice(c->device));
+    if (direction == 0)
+        HIP_TRY(hipMemcpyAsync(buf, c->d_sys.p, c->d_sys.bytes(), hipMemcpyDeviceToDevice, c->stream));
+    else
+        HIP_TRY(hipMemcpyAsync(c->d_sys.p, buf, c->d_sys.bytes(), hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->sys_host_valid = false;
+    return 0;
+}
+
+int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
+    if (!c) return fail(-1, "null ctx");
+    if (key == LDSO_BA_TUNE_LIN_VARIANT) {
+        if (value != 1 && value != 2) return fail(-1, "lin variant must be 1 or 2");
+        c->lin_variant = value;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_TILED_IMAGES) {
+        if (c->n_win) return fail(-1, "image layout must be chosen before ldso_ba_load");
+        c->tiled = value != 0;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_LOAD3) {
+        c->load3 = value != 0;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_XCD_REMAP) {
+        c->xcd_remap = value != 0;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_CENTRE_FIRST) {
+        c->centre_first = value != 0;
+        return 0;
+    }
+    return fail(-1, "unknown tuning key");
 }
 
 int ldso_ba_set_kernel_timing(ldso_ba_ctx *c, int32_t enable) {
