@@ -112,12 +112,12 @@ def main():
     if args.mode == "shard" and dist is not None:
         from ldso_amd import dist as ldist
 
-        packed = ldist.PackedSystem(ctx)
+        packed = ldist.ShardExchange(ctx, dist)
 
     def step():
         ctx.linearize(fix=False, accumulate=True)
         if packed is not None:
-            packed.allreduce(dist)
+            packed()
 
     for _ in range(args.warmup):
         step()

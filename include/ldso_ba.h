@@ -135,6 +135,11 @@ int ldso_ba_solve_system(int32_t n_frames, int32_t iteration, double lambda, con
  * EnergyFunctional::orthogonalize stacks (EnergyFunctional.cc:811-813). */
 int ldso_ba_nullspaces(int32_t n_frames, const ldso_ba_frame_state *frames, double *out);
 
+/* Validate a window description without a GPU (what ldso_ba_load checks first): counts,
+ * pointers, host/target ranges, residual lists (no duplicate or self targets, <= N-1 per
+ * point).  Returns 0 or a negative code with ldso_ba_last_error() set. */
+int ldso_ba_validate_window(const ldso_ba_window *w);
+
 /* ---- device context --------------------------------------------------------------- */
 
 /* Create a context on HIP device `device` with its own non-blocking stream. */
@@ -206,6 +211,19 @@ int ldso_ba_unpack_system(ldso_ba_ctx *ctx);
  * a caller-owned device buffer of n_doubles (e.g. a torch tensor handed to RCCL); synchronises
  * the context stream.  Direction 1 also invalidates cached host copies. */
 int ldso_ba_copy_packed(ldso_ba_ctx *ctx, void *dev_buf, int64_t n_doubles, int32_t direction);
+
+/* Sharded setNewFrameEnergyTH (FullSystem.cc:459-482 over activeResiduals that target the
+ * newest frame).  With points sharded, each rank holds part of the newest frame's
+ * NewEnergyWithOutlier values; the exact nth_element needs all of them:
+ *   newest_stride       max over this context's windows of its newest-frame residual count
+ *                       (static after load; ranks agree on max-over-ranks as the slot size)
+ *   export_newest       writes [n_windows][stride] floats into a caller device buffer (-1 pads)
+ *   frame_threshold_gathered  takes the all-gathered [n_ranks][n_windows][stride] buffer and
+ *                       re-selects every window's newest-frame threshold on the device.
+ * All three synchronise the context stream.  Unsharded contexts never need them. */
+int ldso_ba_newest_stride(ldso_ba_ctx *ctx, int64_t *stride);
+int ldso_ba_export_newest(ldso_ba_ctx *ctx, float *dev_buf, int64_t stride);
+int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *ctx, const float *dev_buf, int32_t n_ranks, int64_t stride);
 
 /* Per-kernel HIP-event timing (bench/profiling).  When enabled every kernel launch of
  * ldso_ba_linearize is bracketed by events; get returns summed ms and launch counts for

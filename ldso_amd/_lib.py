@@ -89,6 +89,7 @@ ABI = [
     ("ldso_ba_solve_system", C.c_int,
      [C.c_int32, C.c_int32, C.c_double, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, C.c_int32, f64p]),
     ("ldso_ba_nullspaces", C.c_int, [C.c_int32, C.c_void_p, f64p]),
+    ("ldso_ba_validate_window", C.c_int, [C.POINTER(LdsoBaWindow)]),
     ("ldso_ba_create", C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
     ("ldso_ba_destroy", None, [C.c_void_p]),
     ("ldso_ba_stream", C.c_void_p, [C.c_void_p]),
@@ -107,6 +108,9 @@ ABI = [
     ("ldso_ba_packed_system", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), i64p, i64p]),
     ("ldso_ba_unpack_system", C.c_int, [C.c_void_p]),
     ("ldso_ba_copy_packed", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),
+    ("ldso_ba_newest_stride", C.c_int, [C.c_void_p, i64p]),
+    ("ldso_ba_export_newest", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    ("ldso_ba_frame_threshold_gathered", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64]),
     ("ldso_ba_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("ldso_ba_set_tuning", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),

@@ -44,8 +44,8 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kTopVals = 96;    // 55 + 30 + 6 AccumulatorApprox entries, padded to 96
 constexpr int kMaxRes = LDSO_BA_MAX_FRAMES - 1;
-constexpr int kNumKernels = 4;
-const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch", "k_resubstitute"};
+constexpr int kNumKernels = 5;
+const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch", "k_resubstitute", "k_frame_th"};
 
 thread_local std::string g_err;
 int fail(int code, const std::string &msg) {
@@ -689,17 +689,19 @@ __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row
     return (long long)row * D - (long long)row * (row - 1) / 2 + (col - row);
 }
 
-// setNewFrameEnergyTH as an exact 4-pass radix select (nth_element semantics) + energy sums
-__device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &W, int w, unsigned *keys) {
+// setNewFrameEnergyTH (FullSystem.cc:459-482) as an exact 4-pass radix select with
+// nth_element semantics over the candidates get(i), i in [0, n_cand), that are >= 0.
+// Candidates are staged in LDS when they fit; larger sets are re-read from global memory.
+// Every thread of the block must call it; thread 0 writes *th_out.
+template <class Get>
+__device__ void select_frame_th(Get get, int n_cand, unsigned *keys, float *th_out) {
     unsigned *hist = keys + kThMaxLds;
     unsigned *sh = hist + 256;  // [0] count [1] prefix [2] rank
-    double *red = reinterpret_cast<double *>(sh + 8);
-    const int tid = threadIdx.x, N = W.N;
-    const int b = W.newest_begin, e = W.newest_end;
+    const int tid = threadIdx.x;
     if (tid == 0) sh[0] = 0;
     __syncthreads();
-    for (int i = b + tid; i < e; i += kStThreads) {
-        const float x = P.e_wo[i];
+    for (int i = tid; i < n_cand; i += kStThreads) {
+        const float x = get(i);
         if (x >= 0) {
             const unsigned slot = atomicAdd(&sh[0], 1u);
             if (slot < (unsigned)kThMaxLds) keys[slot] = __float_as_uint(x) & 0x7FFFFFFFu;  // -0.0 -> 0
@@ -708,68 +710,78 @@ __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &
     __syncthreads();
     const unsigned n = sh[0];
     if (n == 0) {
-        if (tid == 0) P.frame_th[W.frame_base + N - 1] = 12 * 12 * LDSO_BA_PATTERN_NUM;
-    } else {
-        const bool in_lds = n <= (unsigned)kThMaxLds;
-        if (tid == 0) {
-            sh[1] = 0;
-            sh[2] = (unsigned)(int)(kFrameEnergyTHN * (float)n);  // int nthIdx = 0.7f * size()
-        }
-        for (int pass = 0; pass < 4; pass++) {
-            const int shift = 24 - 8 * pass;
-            hist[tid] = 0;
-            __syncthreads();
-            const unsigned prefix = sh[1];
-            const unsigned pmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
-            if (in_lds) {
-                for (unsigned i = tid; i < n; i += kStThreads) {
-                    const unsigned key = keys[i];
-                    if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
-                }
-            } else {
-                for (int i = b + tid; i < e; i += kStThreads) {
-                    const float x = P.e_wo[i];
-                    if (!(x >= 0)) continue;
-                    const unsigned key = __float_as_uint(x) & 0x7FFFFFFFu;
-                    if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
-                }
-            }
-            __syncthreads();
-            if (tid < 64) {  // one wave: lane l owns bins 4l..4l+3
-                const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
-                unsigned incl = h0 + h1 + h2 + h3;
-#pragma unroll
-                for (int m = 1; m < 64; m <<= 1) {
-                    const unsigned y = __shfl_up(incl, m, kWave);
-                    if (tid >= m) incl += y;
-                }
-                const unsigned rank = sh[2];
-                const unsigned long long hit = __ballot(incl > rank);
-                const int first = __ffsll((long long)hit) - 1;
-                if (tid == first) {
-                    unsigned acc = incl - (h0 + h1 + h2 + h3);
-                    int d = 4 * tid;
-                    const unsigned hb[4] = {h0, h1, h2, h3};
-                    for (int k = 0; k < 4; k++, d++) {
-                        if (acc + hb[k] > rank) break;
-                        acc += hb[k];
-                    }
-                    sh[2] = rank - acc;
-                    sh[1] = prefix | ((unsigned)d << shift);
-                }
-            }
-            __syncthreads();
-        }
-        if (tid == 0) {
-#pragma clang fp contract(off)
-            const float nth = sqrtf(__uint_as_float(sh[1]));
-            float v = nth * kFrameEnergyTHFacMedian;
-            v = 26.0f * kFrameEnergyTHConstWeight + v * (1 - kFrameEnergyTHConstWeight);
-            v = v * v;
-            v *= kOverallEnergyTHWeight * kOverallEnergyTHWeight;
-            P.frame_th[W.frame_base + N - 1] = v;
-        }
+        if (tid == 0) *th_out = 12 * 12 * LDSO_BA_PATTERN_NUM;
+        __syncthreads();
+        return;
     }
+    const bool in_lds = n <= (unsigned)kThMaxLds;
+    if (tid == 0) {
+        sh[1] = 0;
+        sh[2] = (unsigned)(int)(kFrameEnergyTHN * (float)n);  // int nthIdx = 0.7f * size()
+    }
+    for (int pass = 0; pass < 4; pass++) {
+        const int shift = 24 - 8 * pass;
+        hist[tid] = 0;
+        __syncthreads();
+        const unsigned prefix = sh[1];
+        const unsigned pmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
+        if (in_lds) {
+            for (unsigned i = tid; i < n; i += kStThreads) {
+                const unsigned key = keys[i];
+                if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+            }
+        } else {
+            for (int i = tid; i < n_cand; i += kStThreads) {
+                const float x = get(i);
+                if (!(x >= 0)) continue;
+                const unsigned key = __float_as_uint(x) & 0x7FFFFFFFu;
+                if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {  // one wave: lane l owns bins 4l..4l+3
+            const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
+            unsigned incl = h0 + h1 + h2 + h3;
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) {
+                const unsigned y = __shfl_up(incl, m, kWave);
+                if (tid >= m) incl += y;
+            }
+            const unsigned rank = sh[2];
+            const unsigned long long hit = __ballot(incl > rank);
+            const int first = __ffsll((long long)hit) - 1;
+            if (tid == first) {
+                unsigned acc = incl - (h0 + h1 + h2 + h3);
+                int d = 4 * tid;
+                const unsigned hb[4] = {h0, h1, h2, h3};
+                for (int k = 0; k < 4; k++, d++) {
+                    if (acc + hb[k] > rank) break;
+                    acc += hb[k];
+                }
+                sh[2] = rank - acc;
+                sh[1] = prefix | ((unsigned)d << shift);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+#pragma clang fp contract(off)
+        const float nth = sqrtf(__uint_as_float(sh[1]));
+        float v = nth * kFrameEnergyTHFacMedian;
+        v = 26.0f * kFrameEnergyTHConstWeight + v * (1 - kFrameEnergyTHConstWeight);
+        v = v * v;
+        v *= kOverallEnergyTHWeight * kOverallEnergyTHWeight;
+        *th_out = v;
+    }
+    __syncthreads();
+}
+
+__device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &W, int w, unsigned *keys) {
+    const int tid = threadIdx.x, N = W.N;
+    const float *e_wo = P.e_wo + W.newest_begin;
+    select_frame_th([&](int i) { return e_wo[i]; }, W.newest_end - W.newest_begin, keys,
+                    P.frame_th + W.frame_base + N - 1);
+    double *red = reinterpret_cast<double *>(keys + kThMaxLds + 256 + 8);
     // linearizeAll: sum of returned energies and #IN, fixed order (strided, then thread 0)
     double se = 0, sn = 0;
     for (int k = tid; k < W.n_top_items; k += kStThreads) {
@@ -991,6 +1003,34 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 // ============================================================================================
 // k_resubstitute: EnergyFunctional::resubstituteFPt (EnergyFunctional.cc:638-667)
 // ============================================================================================
+// ---- sharded setNewFrameEnergyTH ---------------------------------------
+// With points sharded over ranks, the newest frame's NewEnergyWithOutlier values are spread
+// over the ranks; nth_element needs all of them.  Each rank exports its newest-frame segment
+// of every window into a fixed-stride slot (padding -1, which the selection skips), the host
+// all-gathers the slots, and k_frame_th reruns the exact selection over all ranks' values.
+__global__ __launch_bounds__(256) void k_export_newest(const WinDev *__restrict__ wins, const float *__restrict__ e_wo,
+                                                       float *out, long long stride) {
+    const WinDev &W = wins[blockIdx.y];
+    const int n = W.newest_end - W.newest_begin;
+    float *dst = out + (size_t)blockIdx.y * stride;
+    for (long long i = blockIdx.x * 256 + threadIdx.x; i < stride; i += (long long)gridDim.x * 256)
+        dst[i] = i < n ? e_wo[W.newest_begin + i] : -1.0f;
+}
+
+__global__ __launch_bounds__(kStThreads) void k_frame_th(const WinDev *__restrict__ wins, const float *__restrict__ buf,
+                                                         int n_ranks, int n_win, long long stride, float *frame_th) {
+    __shared__ unsigned keys[kThMaxLds + 256 + 8];
+    const int w = blockIdx.x;
+    const WinDev &W = wins[w];
+    const long long n_cand = (long long)n_ranks * stride;
+    select_frame_th(
+        [&](int i) {
+            const int r = (int)(i / stride);
+            return buf[((size_t)r * n_win + w) * stride + (i - (long long)r * stride)];
+        },
+        (int)n_cand, keys, frame_th + W.frame_base + W.N - 1);
+}
+
 struct ResubParams {
     const float *__restrict__ xad;   // [N*N][8] for this window (index h*N + t)
     const float *__restrict__ xc;    // [4]
@@ -1264,6 +1304,11 @@ int ldso_ba_solve_system(int32_t n, int32_t it, double lambda, const double *HA,
     if (n < 1 || n > LDSO_BA_MAX_FRAMES || !HA || !bA || !HL || !bL || !Hsc || !bsc || !x)
         return fail(-1, "bad arguments");
     return solve_system(n, it, lambda, HA, bA, HL, bL, HM, bM, Hsc, bsc, ns, nn, x);
+}
+
+int ldso_ba_validate_window(const ldso_ba_window *w) {
+    if (!w) return fail(-1, "null window");
+    return check_window(*w);
 }
 
 int ldso_ba_create(int32_t device, ldso_ba_ctx **out) {
@@ -2005,6 +2050,39 @@ int ldso_ba_copy_packed(ldso_ba_ctx *c, void *buf, int64_t n, int32_t direction)
         HIP_TRY(hipMemcpyAsync(c->d_sys.p, buf, c->d_sys.bytes(), hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->sys_host_valid = false;
+    return 0;
+}
+
+int ldso_ba_newest_stride(ldso_ba_ctx *c, int64_t *stride) {
+    if (!c || !stride) return fail(-1, "bad arguments");
+    int64_t m = 0;
+    for (const WinDev &D : c->wd) m = std::max<int64_t>(m, D.newest_end - D.newest_begin);
+    *stride = m;
+    return 0;
+}
+
+int ldso_ba_export_newest(ldso_ba_ctx *c, float *dev_buf, int64_t stride) {
+    if (!c || !dev_buf || c->n_win == 0 || stride < 1) return fail(-1, "bad arguments");
+    for (const WinDev &D : c->wd)
+        if (D.newest_end - D.newest_begin > stride) return fail(-1, "stride smaller than a newest-frame segment");
+    HIP_TRY(hipSetDevice(c->device));
+    const dim3 grid((unsigned)std::min<int64_t>((stride + 255) / 256, 64), (unsigned)c->n_win);
+    k_export_newest<<<grid, 256, 0, c->stream>>>(c->d_wins.p, c->d_rs_energy_wo.p, dev_buf, (long long)stride);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *c, const float *dev_buf, int32_t n_ranks, int64_t stride) {
+    if (!c || !dev_buf || c->n_win == 0 || n_ranks < 1 || stride < 1) return fail(-1, "bad arguments");
+    if ((int64_t)n_ranks * stride > INT32_MAX) return fail(-1, "too many candidates");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = timed_launch(c, 4, [&] {
+        k_frame_th<<<c->n_win, kStThreads, 0, c->stream>>>(c->d_wins.p, dev_buf, n_ranks, c->n_win, (long long)stride,
+                                                           c->d_frame_th.p);
+    });
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
 }
 

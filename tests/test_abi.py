@@ -1,0 +1,127 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every entry point that
+include/ldso_ba.h declares, the host-side helpers (precalc, adjoints, priors, nullspaces,
+solve) agree with the oracle's independent restatement, and errors follow the reference's
+convention (negative status + message, never a crash)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from ldso_amd import _lib as L
+from ldso_amd import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ldso_ba.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(ldso_ba_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol(built):
+    syms = declared_symbols()
+    assert len(syms) >= 30
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (ldso_ba_\w+)", out))
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    bound = {name for name, _, _ in L.ABI}
+    assert set(syms) == bound, set(syms) ^ bound
+    lib = L.lib()
+    assert lib.ldso_ba_abi_version() == 1
+    assert lib.ldso_ba_num_kernels() >= 3
+
+
+def test_library_is_gfx950_only(built):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH], capture_output=True,
+                         text=True).stdout + subprocess.run(["strings", L.LIB_PATH], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+
+
+@pytest.mark.parametrize("cfg", [dict(n_frames=3, n_points=40, width=160, height=120, seed=5),
+                                 dict(n_frames=7, n_points=100, width=320, height=240, seed=9)])
+def test_host_helpers_match_oracle(built, cfg):
+    w = synth.make_window(**cfg)
+    ref = oracle.frame_terms(w)
+    np.testing.assert_array_equal(w.precalc, ref["precalc"])
+    np.testing.assert_allclose(w.ad_host, ref["ad_host"], rtol=0, atol=1e-12 * np.abs(ref["ad_host"]).max())
+    np.testing.assert_allclose(w.ad_target, ref["ad_target"], rtol=0, atol=0)
+    np.testing.assert_array_equal(w.c_prior, ref["c_prior"])
+    np.testing.assert_array_equal(w.frame_prior, ref["frame_prior"])
+    np.testing.assert_allclose(w.frame_delta, ref["frame_delta"], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(w.frame_delta_prior, ref["frame_delta_prior"], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(w.nullspaces(), ref["nullspaces"], rtol=0, atol=1e-9)
+
+
+def test_solver_matches_oracle_solver(built):
+    w = synth.make_window(n_frames=5, n_points=200, width=320, height=240, seed=3)
+    ow = oracle.OracleWindow(w, threads=0)
+    _, sysm = ow.iteration()
+    ns = w.nullspaces()
+    lib = L.lib()
+    n = w.dim
+    for it in (0, 3):
+        x = np.zeros(n)
+        args = [L.ptr(np.ascontiguousarray(sysm[k]), L.f64p) for k in ("HA", "bA", "HL", "bL")]
+        rc = lib.ldso_ba_solve_system(w.n_frames, it, 1e-5, *args, L.ptr(None, L.f64p), L.ptr(None, L.f64p),
+                                      L.ptr(np.ascontiguousarray(sysm["Hsc"]), L.f64p),
+                                      L.ptr(np.ascontiguousarray(sysm["bsc"]), L.f64p), L.ptr(ns, L.f64p), 7,
+                                      L.ptr(x, L.f64p))
+        assert rc == 0
+        xo = oracle.solve_system(w.n_frames, it, 1e-5, sysm, nullspaces=ns)
+        assert np.linalg.norm(x - xo) <= 1e-9 * np.linalg.norm(xo)
+    if True:  # orthogonalize(): x is orthogonal to the (normalised) gauge directions at it >= 2
+        xo = oracle.solve_system(w.n_frames, 2, 1e-5, sysm, nullspaces=ns)
+        Nn = ns / np.linalg.norm(ns, axis=1, keepdims=True)
+        assert np.abs(Nn @ xo).max() <= 1e-9 * np.linalg.norm(xo)
+
+
+def test_error_convention(built):
+    lib = L.lib()
+    assert lib.ldso_ba_frame_precalc(0, None, None, None) < 0
+    assert b"bad arguments" in lib.ldso_ba_last_error()
+    assert lib.ldso_ba_validate_window(None) < 0
+    w = synth.make_window(n_frames=3, n_points=10, width=160, height=120, seed=1)
+    s = w.c_struct()
+    assert lib.ldso_ba_validate_window(C.byref(s)) == 0
+    bad = w.copy_state()
+    bad.res_target = w.res_target.copy()
+    bad.res_target[0] = bad.point_host[0]  # a residual onto its own host
+    sb = bad.c_struct()
+    assert lib.ldso_ba_validate_window(C.byref(sb)) < 0
+    assert b"host" in lib.ldso_ba_last_error()
+    bad2 = w.copy_state()
+    bad2.point_host = w.point_host.copy()
+    bad2.point_host[1] = 7  # frame index out of range
+    sb2 = bad2.c_struct()
+    assert lib.ldso_ba_validate_window(C.byref(sb2)) < 0
+    bad3 = w.copy_state()
+    bad3.res_target = w.res_target.copy()
+    b0, b1 = w.point_res_begin[0], w.point_res_begin[1]
+    if b1 - b0 >= 2:
+        bad3.res_target[b0 + 1] = bad3.res_target[b0]  # duplicate (point, target)
+        sb3 = bad3.c_struct()
+        assert lib.ldso_ba_validate_window(C.byref(sb3)) < 0
+    h = C.c_void_p()
+    rc = lib.ldso_ba_create(1 << 20, C.byref(h))  # no such device: error, not a crash
+    assert rc < 0 and not h.value
+
+
+def test_synthetic_generator_is_deterministic(built):
+    a = synth.make_window(n_frames=4, n_points=50, width=160, height=120, seed=17)
+    b = synth.make_window(n_frames=4, n_points=50, width=160, height=120, seed=17)
+    c = synth.make_window(n_frames=4, n_points=50, width=160, height=120, seed=18)
+    for k in ("dI", "point_data", "point_host", "res_target", "precalc"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
+    assert not np.array_equal(a.dI, c.dI)
+    # FrameHessian::makeImages gradients (FrameHessian.cc:96-105) hold on the generated images
+    I = a.dI[0, :, 0].reshape(120, 160)
+    gx = 0.5 * (np.roll(I.ravel(), -1) - np.roll(I.ravel(), 1)).reshape(120, 160).astype(np.float32)
+    np.testing.assert_array_equal(a.dI[0, 160:160 * 119, 1], gx.ravel()[160:160 * 119])
+    assert (a.point_res_begin[1:] - a.point_res_begin[:-1] == 3).all()

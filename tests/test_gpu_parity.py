@@ -214,3 +214,41 @@ def test_s11_window(ctx):
     ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
     e_cpu, s_cpu = ow.iteration()
     compare_pass(ctx, ow, 0, e_cpu, s_cpu)
+
+
+def test_sharded_frame_threshold_exchange(built):
+    """ldso_ba_export_newest + ldso_ba_frame_threshold_gathered: three shards' newest-frame
+    slots concatenated as an all-gather would lay them out re-select the unsharded threshold,
+    for a batch of windows (also one whose newest segment exceeds the LDS staging size)."""
+    import ctypes as C
+
+    import torch
+
+    from ldso_amd import _lib as L
+
+    cfgs = [dict(n_frames=7, n_points=900, seed=43), dict(n_frames=5, n_points=12000, seed=44),
+            dict(n_frames=4, n_points=30, seed=45)]
+    full = BAContext(0).load([synth.make_window(**c) for c in cfgs])
+    full.linearize()
+    th_full = [full.frame_energy_th(i) for i in range(len(cfgs))]
+    world = 3
+    ctxs = [BAContext(0).load([synth.make_window(**c) for c in cfgs], shard_rank=r, shard_count=world)
+            for r in range(world)]
+    strides = []
+    for c in ctxs:
+        c.linearize()
+        s = C.c_int64()
+        L.check(c._lib.ldso_ba_newest_stride(c._h, C.byref(s)))
+        strides.append(s.value)
+    stride = max(strides)
+    nw = len(cfgs)
+    gathered = torch.empty(world * nw * stride, dtype=torch.float32, device="cuda")
+    for r, c in enumerate(ctxs):
+        L.check(c._lib.ldso_ba_export_newest(c._h, gathered[r * nw * stride:].data_ptr(), stride))
+    torch.cuda.synchronize()
+    for c in ctxs:
+        L.check(c._lib.ldso_ba_frame_threshold_gathered(c._h, gathered.data_ptr(), world, stride))
+        for i in range(nw):
+            np.testing.assert_array_equal(c.frame_energy_th(i), th_full[i])
+        c.close()
+    full.close()
