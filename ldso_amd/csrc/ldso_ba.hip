@@ -1,24 +1,28 @@
 // ldso_ba.hip -- MI355X (gfx950) kernels and C ABI of LDSO's photometric-BA hot path.
 //
-// One Gauss-Newton pass over every loaded window is seven stream-ordered launches:
+// One Gauss-Newton pass over every loaded window (ldso_ba_linearize) is three stream-ordered
+// launches plus a memset of the packed systems:
 //
-//   k_linearize   lane per PointFrameResidual, one wavefront per (host,target) bucket chunk.
-//                 linearize (Residuals.cc:15-217) + applyRes (Residuals.h:70-88) + the
-//                 per-residual AccumulatorApprox terms (AccumulatedTopHessian.cc:66-99,
-//                 MatrixAccumulators.h:893-1045) reduced across the wavefront into a 96-float
-//                 partial per chunk.  The pair precalc, frame thresholds and image base are
-//                 wave-uniform (scalar loads); the vector traffic is the point record and the
-//                 32 bilinear taps per residual into 2x4-texel tiled [I, dx, dy, 0] frames.
-//   k_frame_th    FullSystem::setNewFrameEnergyTH (FullSystem.cc:2078-2109), radix select.
+//   k_linearize   lane per PointFrameResidual, one wavefront per 64-residual chunk of one
+//                 (host,target) bucket.  linearize (Residuals.cc:15-217) + applyRes
+//                 (Residuals.h:70-88) + the per-residual AccumulatorApprox terms
+//                 (AccumulatedTopHessian.cc:66-99, MatrixAccumulators.h:893-1045) reduced across
+//                 the wavefront into a 96-float partial per chunk.  The pair precalc, frame
+//                 thresholds and image base are wave-uniform (scalar loads); the vector traffic is
+//                 the point record and the 32 bilinear taps per residual into 2x4-texel tiled
+//                 [I, dx, dy, 0] frames.
 //   k_point_sc    per point: Hdd/bd/Hcd sums (AccumulatedTopHessian.cc:94-116), HdiF
 //                 (AccumulatedSCHessian.cc:24-33); then the Schur terms of a 64-point chunk of one
 //                 host as one symmetric rank-64 update G += U^T diag(HdiF) U staged in LDS (the
 //                 accD/accE/accEB/accHcc/accbc sums of AccumulatedSCHessian.cc:35-50).
-//   k_stitch_top  per (h,t): adjoint sandwiches of AccumulatedTopHessian.cc:213-239 in double.
-//   k_sc_reduce   per host: chunk partials -> G_h (double).
-//   k_stitch_sc   per (host i, target j): AccumulatedSCHessian.cc:80-114 in double.
-//   k_final       per window: gathers the block records into HA, bA, Hsc, bsc (upper triangle,
-//                 symmetrised as stitchDoubleMT does) and the linearizeAll energy.
+//   k_stitch      block per (host,target) pair: the Top adjoint sandwiches
+//                 (AccumulatedTopHessian.cc:213-239) and the SC sandwiches for (i=h, j=t)
+//                 (AccumulatedSCHessian.cc:80-114) in double, f64 atomics into the packed upper
+//                 triangles; the (0,0) block also runs setNewFrameEnergyTH (FullSystem.cc:459-482)
+//                 as a radix select and sums the linearizeAll energy.
+//
+// Outside the pass: k_resubstitute (resubstituteFPt, EnergyFunctional.cc:638-667), k_tile_image
+// (image staging at load/update), k_export_newest + k_frame_th (sharded threshold exchange).
 //
 // The per-residual arithmetic of k_linearize is compiled with contraction off and follows the
 // reference's statement order, so states, energies, JpJdF and the per-point sums are
@@ -66,9 +70,6 @@ struct WinDev {
     int sc_item_base, n_sc_items;
     int K, KP, ntiles, pad0;
     long long sc_slab_base;  // floats
-    long long g_base;        // doubles: N * KP*KP
-    long long sc_rec_base;   // doubles: N*N * sc_rec_len
-    long long top_rec_base;  // doubles: N*N * kTopRecLen
     long long sys_base;      // doubles: packed system
     int newest_begin, newest_end;
     int width, height;
@@ -76,8 +77,6 @@ struct WinDev {
     float calib[4];
 };
 
-constexpr int kTopRecLen = 64 * 3 + 32 * 2 + 16 + 8 * 2 + 4;  // Hhh Htt Hht Hhc Htc Hcc bh bt bc = 292
-__host__ __device__ inline int sc_rec_len(int N) { return N * 64 + 64 + 64 + 32 + 32 + 8 + 8; }
 __host__ __device__ inline long long packed_len(int D) { return (long long)D * (D + 1) / 2; }
 __host__ __device__ inline long long sys_len(int D) { return 2 * (packed_len(D) + D); }
 
@@ -1181,7 +1180,7 @@ struct ldso_ba_ctx {
     DevBuf<int4> d_top_items, d_sc_items;
     DevBuf<int2> d_pair_items, d_host_items;
     DevBuf<float> d_top_slab, d_sc_slab;
-    DevBuf<double> d_item_energy, d_top_rec, d_sc_rec, d_G, d_sys, d_win_energy;
+    DevBuf<double> d_item_energy, d_sys, d_win_energy;
     DevBuf<float> d_xad;
     size_t sc_smem_max = 0;
     bool timing = false;
@@ -1368,9 +1367,6 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_top_slab.release();
     c->d_sc_slab.release();
     c->d_item_energy.release();
-    c->d_top_rec.release();
-    c->d_sc_rec.release();
-    c->d_G.release();
     c->d_sys.release();
     c->d_win_energy.release();
     c->d_xad.release();
@@ -1412,7 +1408,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     std::vector<int8_t> rs_state;
     std::vector<float> rs_energy, pt_data, precalc, frame_th;
     std::vector<double> adH, adT;
-    long long sc_slab_total = 0, g_total = 0, sc_rec_total = 0, top_rec_total = 0, sys_total = 0;
+    long long sc_slab_total = 0, sys_total = 0;
     int frame_base = 0, pair_base = 0, point_base = 0, res_base = 0;
     size_t smem_max = 0;
 
@@ -1540,12 +1536,6 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         D.n_sc_items = (int)sc_items.size() - D.sc_item_base;
         D.sc_slab_base = sc_slab_total;
         sc_slab_total += (long long)D.n_sc_items * D.ntiles * 16;
-        D.g_base = g_total;
-        g_total += (long long)N * D.KP * D.KP;
-        D.sc_rec_base = sc_rec_total;
-        sc_rec_total += (long long)N * N * sc_rec_len(N);
-        D.top_rec_base = top_rec_total;
-        top_rec_total += (long long)N * N * kTopRecLen;
         D.sys_base = sys_total;
         sys_total += sys_len(D.D);
         D.newest_begin = res_base + bucket_start[N * (N - 1)];
@@ -1607,9 +1597,6 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     ALLOC(c->d_top_slab, std::max<size_t>(1, top_items.size() * kTopVals));
     ALLOC(c->d_sc_slab, std::max<size_t>(1, (size_t)sc_slab_total));
     ALLOC(c->d_item_energy, std::max<size_t>(1, top_items.size() * 2));
-    ALLOC(c->d_top_rec, (size_t)top_rec_total);
-    ALLOC(c->d_sc_rec, (size_t)sc_rec_total);
-    ALLOC(c->d_G, (size_t)g_total);
     ALLOC(c->d_sys, (size_t)sys_total);
     ALLOC(c->d_win_energy, (size_t)n_windows * 2);
     ALLOC(c->d_xad, (size_t)LDSO_BA_MAX_FRAMES * LDSO_BA_MAX_FRAMES * 8 + 4);
@@ -1651,7 +1638,6 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     HIP_TRY(hipMemsetAsync(c->d_pt_out.p, 0, c->d_pt_out.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_pt_step.p, 0, c->d_pt_step.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_sys.p, 0, c->d_sys.bytes(), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_G.p, 0, c->d_G.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_rs_newstate.p, LDSO_BA_RES_OUTLIER, c->d_rs_newstate.bytes(), c->stream));
     {
         std::vector<float> neg(rs_energy.size(), -1.0f);
@@ -2143,8 +2129,7 @@ int ldso_ba_stats(ldso_ba_ctx *c, int64_t *device_bytes, int64_t *n_points, int6
     if (!c) return fail(-1, "null ctx");
     if (device_bytes)
         *device_bytes = (int64_t)(c->d_img.bytes() + c->d_precalc.bytes() + c->d_pt_data.bytes() + c->d_rs_rec.bytes() +
-                                  c->d_top_slab.bytes() + c->d_sc_slab.bytes() + c->d_G.bytes() + c->d_sys.bytes() +
-                                  c->d_top_rec.bytes() + c->d_sc_rec.bytes() + c->d_pt_res.bytes());
+                                  c->d_top_slab.bytes() + c->d_sc_slab.bytes() + c->d_sys.bytes() + c->d_pt_res.bytes());
     if (n_points) *n_points = c->P_tot;
     if (n_residuals) *n_residuals = c->R_tot;
     return 0;

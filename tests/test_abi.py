@@ -38,10 +38,16 @@ def test_library_exports_every_declared_symbol(built):
     assert lib.ldso_ba_num_kernels() >= 3
 
 
-def test_library_is_gfx950_only(built):
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH], capture_output=True,
-                         text=True).stdout + subprocess.run(["strings", L.LIB_PATH], capture_output=True, text=True).stdout
+def test_library_is_gfx950_only(built, tmp_path):
+    import shutil
+
+    lib = tmp_path / "libldso_ba.so"  # objdump --offloading extracts bundles next to its input
+    shutil.copy(L.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)], capture_output=True,
+                         text=True, cwd=tmp_path).stdout
+    out += subprocess.run(["strings", L.LIB_PATH], capture_output=True, text=True).stdout
     assert "gfx950" in out
+    assert not re.search(r"gfx9[0-4]\d\b|gfx1[01]\d\d", out.replace("gfx950", ""))
 
 
 @pytest.mark.parametrize("cfg", [dict(n_frames=3, n_points=40, width=160, height=120, seed=5),
