@@ -212,7 +212,7 @@ int ldso_ba_unpack_system(ldso_ba_ctx *ctx);
  * the context stream.  Direction 1 also invalidates cached host copies. */
 int ldso_ba_copy_packed(ldso_ba_ctx *ctx, void *dev_buf, int64_t n_doubles, int32_t direction);
 
-/* Sharded setNewFrameEnergyTH (FullSystem.cc:459-482 over activeResiduals that target the
+/* Sharded setNewFrameEnergyTH (FullSystem.cc:2078-2109 over activeResiduals that target the
  * newest frame).  With points sharded, each rank holds part of the newest frame's
  * NewEnergyWithOutlier values; the exact nth_element needs all of them:
  *   newest_stride       max over this context's windows of its newest-frame residual count

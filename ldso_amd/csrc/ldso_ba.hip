@@ -18,7 +18,7 @@
 //   k_stitch      block per (host,target) pair: the Top adjoint sandwiches
 //                 (AccumulatedTopHessian.cc:213-239) and the SC sandwiches for (i=h, j=t)
 //                 (AccumulatedSCHessian.cc:80-114) in double, f64 atomics into the packed upper
-//                 triangles; the (0,0) block also runs setNewFrameEnergyTH (FullSystem.cc:459-482)
+//                 triangles; the (0,0) block also runs setNewFrameEnergyTH (FullSystem.cc:2078-2109)
 //                 as a radix select and sums the linearizeAll energy.
 //
 // Outside the pass: k_resubstitute (resubstituteFPt, EnergyFunctional.cc:638-667), k_tile_image
@@ -688,7 +688,7 @@ __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row
     return (long long)row * D - (long long)row * (row - 1) / 2 + (col - row);
 }
 
-// setNewFrameEnergyTH (FullSystem.cc:459-482) as an exact 4-pass radix select with
+// setNewFrameEnergyTH (FullSystem.cc:2078-2109) as an exact 4-pass radix select with
 // nth_element semantics over the candidates get(i), i in [0, n_cand), that are >= 0.
 // Candidates are staged in LDS when they fit; larger sets are re-read from global memory.
 // Every thread of the block must call it; thread 0 writes *th_out.

@@ -56,7 +56,7 @@ def packed_upper(sysm):
 
 
 def frame_threshold(values):
-    """setNewFrameEnergyTH (FullSystem.cc:459-482) over NewEnergyWithOutlier values (host
+    """setNewFrameEnergyTH (FullSystem.cc:2078-2109) over NewEnergyWithOutlier values (host
     restatement for tests; the product selects on the device, ldso_ba_frame_threshold_gathered)."""
     v = np.asarray(values, np.float32)
     v = v[v >= 0]
