@@ -231,7 +231,8 @@ int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *ctx, const float *dev_buf, int
 int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
 
 /* Tuning knobs (defaults are the measured best):
- *   LDSO_BA_TUNE_LIN_VARIANT   k_linearize occupancy target in waves per SIMD (1 or 2)
+ *   LDSO_BA_TUNE_LIN_VARIANT   k_linearize form: 1 or 2 = lane per residual (occupancy target in
+ *                              waves per SIMD), 3 = sample-parallel (8 lanes per residual)
  *   LDSO_BA_TUNE_TILED_IMAGES  frames stored in 2x4-texel tiles (1) or row-major (0); set
  *                              before ldso_ba_load
  *   LDSO_BA_TUNE_LOAD3         texel loads as dwordx3 (1) or dwordx4 (0)

@@ -351,6 +351,38 @@ __device__ __forceinline__ void first_halve(const TopIn &t, float *v, bool upper
     }
 }
 
+// Two-pass form of the same reduction (48 slots per pass): only 24 partial sums are live
+// next to the TopIn operands, which keeps the kernel under 128 VGPRs.
+template <int Off, int I>
+__device__ __forceinline__ void first_halve24(const TopIn &t, float *v, bool upper) {
+    if constexpr (I < 24) {
+        const float lo = topval<Off + I>(t), hi = topval<Off + I + 24>(t);
+        const float send = upper ? lo : hi;
+        const float keep = upper ? hi : lo;
+        v[I] = keep + __shfl_xor(send, 1, kWave);
+        first_halve24<Off, I + 1>(t, v, upper);
+    }
+}
+template <int Off>
+__device__ __forceinline__ void reduce_top_pass(const TopIn &t, int lane, float *slab_item) {
+    float v[24];
+    first_halve24<Off, 0>(t, v, (lane & 1) != 0);
+    halve<24, 2>(v, lane);
+    halve<12, 4>(v, lane);
+    halve<6, 8>(v, lane);
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        v[i] += __shfl_xor(v[i], 16, kWave);
+        v[i] += __shfl_xor(v[i], 32, kWave);
+    }
+    if (lane < 16) {
+        const int base = Off + 24 * (lane & 1) + 12 * ((lane >> 1) & 1) + 6 * ((lane >> 2) & 1) + 3 * ((lane >> 3) & 1);
+        slab_item[base] = v[0];
+        slab_item[base + 1] = v[1];
+        slab_item[base + 2] = v[2];
+    }
+}
+
 template <int kMinWavesPerSimd, bool kTiled, bool kLoad3, bool kXcdRemap, bool kCentreFirst>
 __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_linearize(LinParams P) {
     const int lane = threadIdx.x & 63;
@@ -516,22 +548,333 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_linearize(LinParams P
 #pragma unroll
         for (int i = 0; i < 6; i++) tin.tr[i] = tin.br[i] = 0;
     }
-    float v[48];
-    first_halve<0>(tin, v, (lane & 1) != 0);
-    halve<48, 2>(v, lane);
-    halve<24, 4>(v, lane);
-    halve<12, 8>(v, lane);
-    halve<6, 16>(v, lane);
+    float *slab_item = P.top_slab + (size_t)item * kTopVals;
+    reduce_top_pass<0>(tin, lane, slab_item);
+    reduce_top_pass<48>(tin, lane, slab_item);
+}
+
+// ============================================================================================
+// k_linearize_sp: sample-parallel variant.  Phase A: 8 lanes per residual, one per pattern
+// pixel, so one wave-instruction's 64 taps belong to 8 residuals and coalesce into far fewer
+// cache lines, and only 4 taps per lane are live.  The 17 per-pixel sums of
+// Residuals.cc:128-190 are transposed through LDS and added in pattern order by one lane per
+// sum (same rounding as the sequential loop).  Phase B: lane per residual again (state,
+// applyRes, point terms, AccumulatorApprox terms and wave reduction, as k_linearize).
+// ============================================================================================
+constexpr int kSums = 17;      // energy, wJI2, JIdx2 (3), JabJIdx (4), Jab2 (3), JI_r (2), Jab_r (2), rr
+constexpr int kSumStride = 20; // floats per residual in the sums buffer ([17] = pattern ok flag)
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one pattern pixel of Residuals.cc:128-190: the 17 addends, in the reference's expression order
+__device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float color, float weight, float aff0,
+                                            float aff1, float b0, float t[kSums]) {
+#pragma clang fp contract(off)
+    const float residual = I - (float)(aff0 * color + aff1);
+    const float drdA = (color - b0);
+    float wg = sqrtf(kOutlierTHSumComponent / (kOutlierTHSumComponent + (gx * gx + gy * gy)));
+    wg = 0.5f * (wg + weight);
+    float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
+    t[0] = wg * wg * hw * residual * residual * (2 - hw);
+    if (hw < 1) hw = sqrtf(hw);
+    hw = hw * wg;
+    gx *= hw;
+    gy *= hw;
+    const float resF = residual * hw;
+    const float jab0 = drdA * hw;
+    t[2] = gx * gx;
+    t[4] = gy * gy;
+    t[3] = gx * gy;
+    t[5] = drdA * hw * gx;
+    t[6] = drdA * hw * gy;
+    t[7] = hw * gx;
+    t[8] = hw * gy;
+    t[9] = drdA * drdA * hw * hw;
+    t[10] = drdA * hw * hw;
+    t[11] = hw * hw;
+    t[1] = hw * hw * (gx * gx + gy * gy);
+    t[12] = resF * gx;
+    t[13] = resF * gy;
+    t[14] = resF * jab0;
+    t[15] = resF * hw;
+    t[16] = resF * resF;
+}
+
+template <bool kTiled, bool kXcdRemap>
+__global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
+    __shared__ float lds_terms[4][8][kSums][8];
+    __shared__ __attribute__((aligned(16))) float lds_sums[4][64][kSumStride];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nb = P.n_blocks, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
+    const int lblock = kXcdRemap ? xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3) : (int)blockIdx.x;
+    const int item = lblock * 4 + wave;
+    if (item >= P.n_items) return;
+    const int4 it = P.items[item];
+    const WinDev &W = P.wins[it.w];
+    const int N = W.N;
+    const int aidx = it.z - W.pair_base;
+    const int h = aidx % N, t = aidx / N;
+    const float *pre = P.precalc + (size_t)it.z * LDSO_BA_PRECALC_STRIDE;
+    const float4 *img = P.img + (size_t)(W.frame_base + t) * P.frame_stride;
+    const float th = fmaxf(P.frame_th[W.frame_base + h], P.frame_th[W.frame_base + t]);
+    const float wM3 = W.wM3, hM3 = W.hM3;
+
+    const bool valid = lane < it.y;
+    const int r = it.x + lane;
+    // Everything phase B needs is loaded up front (unconditionally, from a clamped index: a load
+    // inside a divergent branch is waited for at the branch's end) so it lands during phase A.
+    const int rq = valid ? r : it.x;
+    int my_state = P.rs_state[rq];
+    const int my_point = P.rs_point[rq];
+    uint8_t flags = P.rs_flags[rq];
+    float state_energy = P.rs_energy[rq];
+    float new_energy = P.rs_newenergy[rq];
+    float4 centre = P.rs_center[rq];
+    const float4 my_pd0 = *(const float4 *)(P.pt_data + (size_t)my_point * LDSO_BA_POINT_STRIDE);
+    if (!valid) my_state = LDSO_BA_RES_OOB;
+
+    // ---------------- phase A: pattern pixels, 8 residuals per step -------------------------
+    // One-step software pipeline: the projection and the 4 tap loads of step k+1 are issued
+    // before the arithmetic of step k.
+    {
+#pragma clang fp contract(off)
+        const int g = lane >> 3, sl = lane & 7;
+        // staticPattern[8] (Setting.cc:275) offset of this lane's pixel
+        const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
+        const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
+        const float aff0 = pre[24], aff1 = pre[25], b0 = pre[26];
+        float *T = &lds_terms[wave][g][0][0];
+        float *S = &lds_sums[wave][0][0];
+        const int nsteps = (it.y + 7) >> 3;
+        const int tpr2 = P.tiles_per_row;
+
+        struct Stage {
+            float Ku, Kv, color, weight;
+            float3 t00, t10, t01, t11;
+            bool gok;
+        };
+        auto issue = [&](int k, Stage &q) {
+            const int j = 8 * k + g;
+            const int st = __shfl(my_state, j, kWave);
+            const int p = __shfl(my_point, j, kWave);
+            const float pu = __shfl(my_pd0.x, j, kWave), pv = __shfl(my_pd0.y, j, kWave),
+                        pz = __shfl(my_pd0.z, j, kWave);
+            const bool go = j < it.y && st != LDSO_BA_RES_OOB;
+            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+            q.color = pd[8 + sl];
+            q.weight = pd[16 + sl];
+            const float up = pu + px, vp = pv + py;
+            float ptp[3];
 #pragma unroll
-    for (int i = 0; i < 3; i++) v[i] += __shfl_xor(v[i], 32, kWave);
-    if (lane < 32) {
-        const int base = 48 * (lane & 1) + 24 * ((lane >> 1) & 1) + 12 * ((lane >> 2) & 1) + 6 * ((lane >> 3) & 1) +
-                         3 * ((lane >> 4) & 1);
-        float *o = P.top_slab + (size_t)item * kTopVals + base;
-        o[0] = v[0];
-        o[1] = v[1];
-        o[2] = v[2];
+            for (int i = 0; i < 3; i++)
+                ptp[i] = (pre[3 * i] * up + pre[3 * i + 1] * vp + pre[3 * i + 2] * 1.0f) + pre[9 + i] * pz;
+            q.Ku = ptp[0] / ptp[2];
+            q.Kv = ptp[1] / ptp[2];
+            const bool pok = go && q.Ku > 1.1f && q.Kv > 1.1f && q.Ku < wM3 && q.Kv < hM3;
+            const unsigned long long m1 = __ballot(pok);
+            q.gok = ((m1 >> (8 * g)) & 0xFFull) == 0xFFull;
+            // taps of an in-bounds pixel are always addressable; others read texel (0, 0)
+            const int ix = pok ? (int)q.Ku : 0, iy = pok ? (int)q.Kv : 0;
+            q.t00 = tex<kTiled, false>(img, tpr2, ix, iy);
+            q.t10 = tex<kTiled, false>(img, tpr2, ix + 1, iy);
+            q.t01 = tex<kTiled, false>(img, tpr2, ix, iy + 1);
+            q.t11 = tex<kTiled, false>(img, tpr2, ix + 1, iy + 1);
+        };
+        auto consume = [&](int k, const Stage &q) {
+            const int j = 8 * k + g;
+            bool fin = false;
+            if (q.gok) {
+                const int ix = (int)q.Ku, iy = (int)q.Kv;
+                const float dx = q.Ku - ix, dy = q.Kv - iy, dxdy = dx * dy;
+                const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+                const float I = w11 * q.t11.x + w01 * q.t01.x + w10 * q.t10.x + w00 * q.t00.x;
+                const float gx = w11 * q.t11.y + w01 * q.t01.y + w10 * q.t10.y + w00 * q.t00.y;
+                const float gy = w11 * q.t11.z + w01 * q.t01.z + w10 * q.t10.z + w00 * q.t00.z;
+                fin = isfinite(I);
+                float tt[kSums];
+                pixel_terms(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt);
+#pragma unroll
+                for (int e = 0; e < kSums; e++) T[e * 8 + sl] = tt[e];
+            }
+            const unsigned long long m2 = __ballot(fin);
+            const bool rok = q.gok && ((m2 >> (8 * g)) & 0xFFull) == 0xFFull;
+            wave_lds_sync();
+            if (rok) {  // lane sl adds sums sl, sl+8 (and 16) over the 8 pixels in pattern order
+#pragma unroll
+                for (int e = 0; e < 3; e++) {
+                    const int qq = sl + 8 * e;
+                    if (qq < kSums) {
+                        const float4 a = *(const float4 *)&T[qq * 8], b = *(const float4 *)&T[qq * 8 + 4];
+                        float sum = 0.0f;
+                        sum += a.x;
+                        sum += a.y;
+                        sum += a.z;
+                        sum += a.w;
+                        sum += b.x;
+                        sum += b.y;
+                        sum += b.z;
+                        sum += b.w;
+                        S[j * kSumStride + qq] = sum;
+                    }
+                }
+            }
+            if (sl == 0 && j < it.y) S[j * kSumStride + kSums] = rok ? 1.0f : 0.0f;
+            wave_lds_sync();
+        };
+        // ping-pong stages, loads issued unconditionally (a step past the item's end has no valid
+        // group and reads texel (0, 0)), so no load result crosses a branch join
+        Stage A, B;
+        issue(0, A);
+        for (int k = 0; k < nsteps; k += 2) {
+            issue(k + 1, B);
+            consume(k, A);
+            issue(k + 2, A);
+            consume(k + 1, B);
+        }
     }
+
+    // ---------------- phase B: lane per residual ---------------------------------------------
+    double energy = 0;
+    bool isIN = false, active = false;
+    Geo g;
+    PhotoSums s;
+    if (valid) {
+        const int8_t old_state = (int8_t)my_state;
+        int8_t new_state = LDSO_BA_RES_OOB;
+        float e_wo = -1;
+        if (old_state == LDSO_BA_RES_OOB) {
+            energy = state_energy;
+        } else {
+            const float4 pd0 = my_pd0;
+            const float *Sr = &lds_sums[wave][lane][0];
+            const float4 s0 = *(const float4 *)(Sr), s1 = *(const float4 *)(Sr + 4), s2 = *(const float4 *)(Sr + 8),
+                         s3 = *(const float4 *)(Sr + 12), s4 = *(const float4 *)(Sr + 16);
+            s.energy = s0.x;
+            s.wJI2 = s0.y;
+            s.JIdx2_00 = s0.z;
+            s.JIdx2_10 = s0.w;
+            s.JIdx2_11 = s1.x;
+            s.JabJIdx_00 = s1.y;
+            s.JabJIdx_01 = s1.z;
+            s.JabJIdx_10 = s1.w;
+            s.JabJIdx_11 = s2.x;
+            s.Jab2_00 = s2.y;
+            s.Jab2_01 = s2.z;
+            s.Jab2_11 = s2.w;
+            s.JI_r0 = s3.x;
+            s.JI_r1 = s3.y;
+            s.Jab_r0 = s3.z;
+            s.Jab_r1 = s3.w;
+            s.rr = s4.x;
+            const bool pat_ok = s4.y != 0.0f;
+            bool ok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
+                                        wM3, hM3, g);
+            if (ok) {
+                centre.x = g.Ku;
+                centre.y = g.Kv;
+                centre.z = g.new_idepth;
+            }
+            ok = ok && pat_ok;
+            if (!ok) {
+                energy = state_energy;
+            } else {
+                e_wo = s.energy;
+                float el = s.energy;
+                if (el > th || s.wJI2 < 2) {
+                    el = th;
+                    new_state = LDSO_BA_RES_OUTLIER;
+                } else {
+                    new_state = LDSO_BA_RES_IN;
+                }
+                new_energy = el;
+                energy = el;
+            }
+            active = (new_state == LDSO_BA_RES_IN);
+            flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
+            state_energy = new_energy;
+            if (active) {
+                float jp[8], hc[4], hdd, bd;
+                point_terms(g, s, jp, hc, hdd, bd);
+                float4 *rec = P.rs_rec + (size_t)r * 4;
+                rec[0] = make_float4(jp[0], jp[1], jp[2], jp[3]);
+                rec[1] = make_float4(jp[4], jp[5], jp[6], jp[7]);
+                rec[2] = make_float4(hc[0], hc[1], hc[2], hc[3]);
+                rec[3] = make_float4(hdd, bd, 0.f, 0.f);
+            }
+            if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
+#pragma clang fp contract(off)
+                float pi[3], pr[3];
+#pragma unroll
+                for (int i = 0; i < 3; i++) {
+                    pi[i] = pre[3 * i] * pd0.x + pre[3 * i + 1] * pd0.y + pre[3 * i + 2] * 1.0f;
+                    pr[i] = pi[i] + pre[9 + i] * pd0.z;
+                }
+                const float dx = pi[0] / pi[2] - pr[0] / pr[2], dy = pi[1] / pi[2] - pr[1] / pr[2];
+                centre.w = 0.01f * sqrtf(dx * dx + dy * dy);
+            }
+            P.rs_state[r] = new_state;
+            P.rs_flags[r] = flags;
+            P.rs_energy[r] = state_energy;
+            P.rs_newenergy[r] = new_energy;
+            P.rs_center[r] = centre;
+        }
+        isIN = (new_state == LDSO_BA_RES_IN);
+        P.rs_newstate[r] = new_state;
+        P.rs_energy_wo[r] = e_wo;
+    }
+
+    double esum = energy;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
+    const unsigned long long inmask = __ballot(isIN);
+    if (lane == 0) {
+        P.item_energy[2 * item] = esum;
+        P.item_energy[2 * item + 1] = (double)__popcll(inmask);
+    }
+    if (!P.accumulate) return;
+
+    TopIn tin;
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            tin.x[i] = g.d_C_x[i];
+            tin.y[i] = g.d_C_y[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            tin.x[4 + i] = g.d_xi_x[i];
+            tin.y[4 + i] = g.d_xi_y[i];
+        }
+        tin.a = s.JIdx2_00;
+        tin.b = s.JIdx2_10;
+        tin.c = s.JIdx2_11;
+        tin.tr[0] = s.JabJIdx_00;
+        tin.tr[1] = s.JabJIdx_01;
+        tin.tr[2] = s.JabJIdx_10;
+        tin.tr[3] = s.JabJIdx_11;
+        tin.tr[4] = s.JI_r0;
+        tin.tr[5] = s.JI_r1;
+        tin.br[0] = s.Jab2_00;
+        tin.br[1] = s.Jab2_01;
+        tin.br[2] = s.Jab_r0;
+        tin.br[3] = s.Jab2_11;
+        tin.br[4] = s.Jab_r1;
+        tin.br[5] = s.rr;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 10; i++) tin.x[i] = tin.y[i] = 0;
+        tin.a = tin.b = tin.c = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) tin.tr[i] = tin.br[i] = 0;
+    }
+    float *slab_item = P.top_slab + (size_t)item * kTopVals;
+    reduce_top_pass<0>(tin, lane, slab_item);
+    reduce_top_pass<48>(tin, lane, slab_item);
 }
 
 // ============================================================================================
@@ -1109,7 +1452,15 @@ void launch_lin1(bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t 
 // variant = occupancy target in waves per SIMD (see DESIGN.md for the measured choice)
 void launch_linearize(int variant, bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t st,
                       const LinParams &L) {
-    if (variant == 2) launch_lin1<2>(tiled, load3, xcd, cf, nb, st, L);
+    if (variant == 3) {
+        if (tiled) {
+            if (xcd) k_linearize_sp<true, true><<<nb, 256, 0, st>>>(L);
+            else k_linearize_sp<true, false><<<nb, 256, 0, st>>>(L);
+        } else {
+            if (xcd) k_linearize_sp<false, true><<<nb, 256, 0, st>>>(L);
+            else k_linearize_sp<false, false><<<nb, 256, 0, st>>>(L);
+        }
+    } else if (variant == 2) launch_lin1<4>(tiled, load3, xcd, cf, nb, st, L);
     else launch_lin1<1>(tiled, load3, xcd, cf, nb, st, L);
 }
 
@@ -1184,7 +1535,7 @@ struct ldso_ba_ctx {
     DevBuf<float> d_xad;
     size_t sc_smem_max = 0;
     bool timing = false;
-    int lin_variant = 1;
+    int lin_variant = 3;
     bool tiled = true, load3 = false, xcd_remap = true, centre_first = true;  // measured best
     std::vector<PendingEv> pending;
     std::vector<hipEvent_t> ev_pool;
@@ -2075,7 +2426,7 @@ int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *c, const float *dev_buf, int32
 int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
     if (!c) return fail(-1, "null ctx");
     if (key == LDSO_BA_TUNE_LIN_VARIANT) {
-        if (value != 1 && value != 2) return fail(-1, "lin variant must be 1 or 2");
+        if (value < 1 || value > 3) return fail(-1, "lin variant must be 1, 2 or 3");
         c->lin_variant = value;
         return 0;
     }

@@ -17,7 +17,7 @@ for tiled in (0, 1):
     for _ in range(3):
         c.linearize()
     ctxs[tiled] = c
-combos = [(t, l3, x, 1, cf) for t in (0, 1) for l3 in (0, 1) for x in (0, 1) for cf in (0, 1)]
+combos = [(1, 0, 1, v, 1) for v in (1, 2, 3)] + [(0, 0, 1, 3, 1), (1, 0, 0, 3, 1)]
 res = {k: [] for k in combos}
 for rnd in range(3):
     for (tiled, load3, xcd, wv, cf) in combos:
@@ -34,4 +34,20 @@ for rnd in range(3):
         c.set_kernel_timing(False)
         res[(tiled, load3, xcd, wv, cf)].append(1e3 * ms / n)
 for k in sorted(res, key=lambda k: min(res[k])):
-    print(f"tiled={k[0]} load3={k[1]} xcd={k[2]} waves={k[3]} centre_first={k[4]}: best {min(res[k]):.1f} us  {['%.1f' % x for x in res[k]]}")
+    print(f"tiled={k[0]} load3={k[1]} xcd={k[2]} variant={k[3]} centre_first={k[4]}: best {min(res[k]):.1f} us  {['%.1f' % x for x in res[k]]}")
+
+# cost split: the same pass without the accumulation (k_linearize skips the Top terms/reduction)
+c = ctxs[1]
+for v in (1, 3):
+    c.set_tuning(1, v)
+    c.set_tuning(4, 1)
+    c.set_tuning(5, 1)
+    c.set_tuning(3, 0)
+    for acc in (True, False):
+        c.linearize(accumulate=acc)
+        c.set_kernel_timing(True)
+        for _ in range(20):
+            c.linearize(accumulate=acc)
+        ms, n = c.kernel_times()["k_linearize"]
+        c.set_kernel_timing(False)
+        print(f"variant={v} accumulate={acc}: {1e3 * ms / n:.1f} us")
