@@ -72,6 +72,7 @@ struct WinDev {
     long long sc_slab_base;  // floats
     long long sys_base;      // doubles: packed system
     int newest_begin, newest_end;
+    int rec_base;            // record slots: rec_base + s * P + q (s = target slot of host's point q)
     int width, height;
     float wM3, hM3;
     float calib[4];
@@ -90,6 +91,7 @@ struct LinParams {
     const float *__restrict__ precalc;
     const float *__restrict__ frame_th;
     const int *__restrict__ rs_point;
+    const int *__restrict__ rs_slot;   // record slot (WinDev::rec_base layout)
     const float *__restrict__ pt_data;
     int8_t *rs_state;
     int8_t *rs_newstate;
@@ -98,7 +100,7 @@ struct LinParams {
     float *rs_newenergy;   // state_NewEnergy (persists: applyRes copies it on a later OOB)
     float *rs_energy_wo;   // state_NewEnergyWithOutlier
     float4 *rs_center;     // centerProjectedTo, relBS
-    float4 *rs_rec;        // [R][4]: JpJdF[8], Hcd_r[4], Hdd_r, bd_r, -, -
+    float4 *pt_rec;        // [slots][4]: JpJdF[8], Hcd_r[4], (Hdd_r, bd_r, active, 0)
     float *top_slab;       // [items][96]
     double *item_energy;   // [items][2]
     int n_items;
@@ -285,6 +287,23 @@ __device__ inline void point_terms(const Geo &g, const PhotoSums &s, float jpjdf
     for (int i = 0; i < 4; i++) hcd[i] = g.d_C_x[i] * j0 + g.d_C_y[i] * j1;
 }
 
+// applyRes(true) + takeData record of one residual (Residuals.h:70-88, 120-129) at its slot
+// (target-slot major, point minor: a bucket chunk writes 64 consecutive records and a block of
+// k_point_sc reads them back coalesced): JpJdF and the point-side Top terms if active,
+// otherwise only the "not active" marker.
+__device__ __forceinline__ void write_record(float4 *rec, bool active, const Geo &g, const PhotoSums &s) {
+    if (active) {
+        float jp[8], hc[4], hdd, bd;
+        point_terms(g, s, jp, hc, hdd, bd);
+        rec[0] = make_float4(jp[0], jp[1], jp[2], jp[3]);
+        rec[1] = make_float4(jp[4], jp[5], jp[6], jp[7]);
+        rec[2] = make_float4(hc[0], hc[1], hc[2], hc[3]);
+        rec[3] = make_float4(hdd, bd, 1.f, 0.f);
+    } else {
+        rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
 // Recursive-halving wavefront reduction of 96 floats: 96 shuffles instead of 6*96.  On return
 // lane l (all 64) holds the full sums of elements base(l) + {0,1,2}, base = 48 b0 + 24 b1 +
 // 12 b2 + 6 b3 + 3 b4 (b = bits of the lane id).
@@ -419,6 +438,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_linearize(LinParams P
         float4 centre = P.rs_center[r];
         if (old_state == LDSO_BA_RES_OOB) {
             energy = state_energy;  // linearize returns state_energy; applyRes returns early
+            P.pt_rec[(size_t)P.rs_slot[r] * 4 + 3] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
         } else {
             const int p = P.rs_point[r];
             const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
@@ -469,15 +489,7 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_linearize(LinParams P
             active = (new_state == LDSO_BA_RES_IN);
             flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
             state_energy = new_energy;
-            if (active) {
-                float jp[8], hc[4], hdd, bd;
-                point_terms(g, s, jp, hc, hdd, bd);
-                float4 *rec = P.rs_rec + (size_t)r * 4;
-                rec[0] = make_float4(jp[0], jp[1], jp[2], jp[3]);
-                rec[1] = make_float4(jp[4], jp[5], jp[6], jp[7]);
-                rec[2] = make_float4(hc[0], hc[1], hc[2], hc[3]);
-                rec[3] = make_float4(hdd, bd, 0.f, 0.f);
-            }
+            write_record(P.pt_rec + (size_t)P.rs_slot[r] * 4, active, g, s);
             if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
                 // linearizeAll_Reductor relBS (FullSystem.cc:1800-1812)
 #pragma clang fp contract(off)
@@ -631,6 +643,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
     const int rq = valid ? r : it.x;
     int my_state = P.rs_state[rq];
     const int my_point = P.rs_point[rq];
+    const int my_slot = P.rs_slot[rq];
     uint8_t flags = P.rs_flags[rq];
     float state_energy = P.rs_energy[rq];
     float new_energy = P.rs_newenergy[rq];
@@ -749,6 +762,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
         float e_wo = -1;
         if (old_state == LDSO_BA_RES_OOB) {
             energy = state_energy;
+            P.pt_rec[(size_t)my_slot * 4 + 3] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
         } else {
             const float4 pd0 = my_pd0;
             const float *Sr = &lds_sums[wave][lane][0];
@@ -797,15 +811,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             active = (new_state == LDSO_BA_RES_IN);
             flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
             state_energy = new_energy;
-            if (active) {
-                float jp[8], hc[4], hdd, bd;
-                point_terms(g, s, jp, hc, hdd, bd);
-                float4 *rec = P.rs_rec + (size_t)r * 4;
-                rec[0] = make_float4(jp[0], jp[1], jp[2], jp[3]);
-                rec[1] = make_float4(jp[4], jp[5], jp[6], jp[7]);
-                rec[2] = make_float4(hc[0], hc[1], hc[2], hc[3]);
-                rec[3] = make_float4(hdd, bd, 0.f, 0.f);
-            }
+            write_record(P.pt_rec + (size_t)my_slot * 4, active, g, s);
             if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
 #pragma clang fp contract(off)
                 float pi[3], pr[3];
@@ -885,10 +891,8 @@ struct PointParams {
     const WinDev *__restrict__ wins;
     const float *__restrict__ pt_data;
     const int *__restrict__ pt_nres;
-    const int *__restrict__ pt_res;   // [P][kMaxRes]
-    const uint8_t *__restrict__ rs_tgt;
-    const uint8_t *__restrict__ rs_flags;
-    const float4 *__restrict__ rs_rec;
+    const unsigned long long *__restrict__ pt_tgt;  // [P]: residual targets, 4 bits each, caller order
+    const float4 *__restrict__ pt_rec;               // [slots][4] (WinDev::rec_base layout)
     float *pt_out;                     // [P][12]
     float *sc_slab;
     int n_items;
@@ -909,25 +913,43 @@ __global__ __launch_bounds__(256) void k_point_sc(PointParams P) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
         const int nres = P.pt_nres[p];
+        // one round of record loads (slot s of the block's 64 points is contiguous), then the
+        // sums in residual order exactly as AccumulatedTopHessian.cc:94-116 adds them
+        const unsigned long long tgs = P.pt_tgt[p];
+        const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * 4;
+        const size_t sstride = (size_t)W.P * 4;
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
         float *row = U + tid * KP;
-        for (int k = 0; k < nres; k++) {
-            const int r = P.pt_res[(size_t)p * kMaxRes + k];
-            if (!(P.rs_flags[r] & LDSO_BA_FLAG_ACTIVE)) continue;
-            ngood++;
-            const float4 *rec = P.rs_rec + (size_t)r * 4;
-            const float4 j0 = rec[0], j1 = rec[1], hc = rec[2], hb = rec[3];
-            bd += hb.y;
-            hdd += hb.x;
-            hcd[0] += hc.x;
-            hcd[1] += hc.y;
-            hcd[2] += hc.z;
-            hcd[3] += hc.w;
-            const int tg = P.rs_tgt[r];
-            const int slot = tg < host ? tg : tg - 1;
-            *(float4 *)(row + 8 * slot) = j0;
-            *(float4 *)(row + 8 * slot + 4) = j1;
+        for (int k0 = 0; k0 < nres; k0 += 4) {
+            float4 rec[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = min(k0 + u, nres - 1);
+                const int tg = (int)((tgs >> (4 * k)) & 15ull);
+                const float4 *q = rp + (tg < host ? tg : tg - 1) * sstride;
+                rec[u][0] = q[0];
+                rec[u][1] = q[1];
+                rec[u][2] = q[2];
+                rec[u][3] = q[3];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u;
+                if (k >= nres || rec[u][3].z == 0.0f) continue;
+                ngood++;
+                const float4 j0 = rec[u][0], j1 = rec[u][1], hc = rec[u][2], hb = rec[u][3];
+                bd += hb.y;
+                hdd += hb.x;
+                hcd[0] += hc.x;
+                hcd[1] += hc.y;
+                hcd[2] += hc.z;
+                hcd[3] += hc.w;
+                const int tg = (int)((tgs >> (4 * k)) & 15ull);
+                const int slot = tg < host ? tg : tg - 1;
+                *(float4 *)(row + 8 * slot) = j0;
+                *(float4 *)(row + 8 * slot + 4) = j1;
+            }
         }
         const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
         const float priorF = pd[4], deltaF = pd[5];
@@ -1008,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_point_sc(PointParams P) {
 // Only the f64 summation order of the atomics varies between runs.
 // ============================================================================================
 constexpr int kStThreads = 256;
-constexpr int kThMaxLds = 8192;  // candidate energies staged in LDS; larger sets re-read HBM
+constexpr int kThMaxLds = 8192;  // k_frame_th: candidate energies staged in LDS; larger sets re-read HBM
 
 struct StitchParams {
     const WinDev *__restrict__ wins;
@@ -1025,6 +1047,7 @@ struct StitchParams {
     double *sys;
     double *win_energy;
     int accumulate;
+    int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
 };
 
 __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row <= col
@@ -1036,8 +1059,8 @@ __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row
 // Candidates are staged in LDS when they fit; larger sets are re-read from global memory.
 // Every thread of the block must call it; thread 0 writes *th_out.
 template <class Get>
-__device__ void select_frame_th(Get get, int n_cand, unsigned *keys, float *th_out) {
-    unsigned *hist = keys + kThMaxLds;
+__device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, float *th_out) {
+    unsigned *hist = keys + cap;
     unsigned *sh = hist + 256;  // [0] count [1] prefix [2] rank
     const int tid = threadIdx.x;
     if (tid == 0) sh[0] = 0;
@@ -1046,7 +1069,7 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, float *th_o
         const float x = get(i);
         if (x >= 0) {
             const unsigned slot = atomicAdd(&sh[0], 1u);
-            if (slot < (unsigned)kThMaxLds) keys[slot] = __float_as_uint(x) & 0x7FFFFFFFu;  // -0.0 -> 0
+            if (slot < (unsigned)cap) keys[slot] = __float_as_uint(x) & 0x7FFFFFFFu;  // -0.0 -> 0
         }
     }
     __syncthreads();
@@ -1056,7 +1079,7 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, float *th_o
         __syncthreads();
         return;
     }
-    const bool in_lds = n <= (unsigned)kThMaxLds;
+    const bool in_lds = n <= (unsigned)cap;
     if (tid == 0) {
         sh[1] = 0;
         sh[2] = (unsigned)(int)(kFrameEnergyTHN * (float)n);  // int nthIdx = 0.7f * size()
@@ -1121,9 +1144,9 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, float *th_o
 __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &W, int w, unsigned *keys) {
     const int tid = threadIdx.x, N = W.N;
     const float *e_wo = P.e_wo + W.newest_begin;
-    select_frame_th([&](int i) { return e_wo[i]; }, W.newest_end - W.newest_begin, keys,
+    select_frame_th([&](int i) { return e_wo[i]; }, W.newest_end - W.newest_begin, keys, P.th_cap,
                     P.frame_th + W.frame_base + N - 1);
-    double *red = reinterpret_cast<double *>(keys + kThMaxLds + 256 + 8);
+    double *red = reinterpret_cast<double *>(keys + P.th_cap + 256 + 8);
     // linearizeAll: sum of returned energies and #IN, fixed order (strided, then thread 0)
     double se = 0, sn = 0;
     for (int k = tid; k < W.n_top_items; k += kStThreads) {
@@ -1174,7 +1197,7 @@ __device__ __forceinline__ double g_elem(const float *__restrict__ slab, int n_i
 }
 
 __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
-    __shared__ double sm[5760];
+    extern __shared__ double sm[];  // sized on the host for the largest window (stitch_smem_bytes)
     const int pair = blockIdx.x;
     const int w = P.pair_win[pair];
     const WinDev &W = P.wins[w];
@@ -1265,13 +1288,13 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
         const int2 hi = P.host_items[W.frame_base + i];
         const float *slab = P.sc_slab + W.sc_slab_base + (size_t)(hi.x - W.sc_item_base) * per;
         double *Gj = sm;                       // [8][KP]: rows 8 sj.. of G_i
-        double *Ah = Gj + 8 * 128;             // AH_ij, AT_ij
+        double *Ah = Gj + 8 * KP;              // AH_ij, AT_ij
         double *At = Ah + 64;
         double *AHk = At + 64;                 // [N-1][64] AH_ik
-        double *ATk = AHk + kMaxRes * 64;      // [N-1][64] AT_ik
-        double *X = ATk + kMaxRes * 64;        // [N-1][64]
-        double *Sk = X + kMaxRes * 64;         // [N-1][64]
-        double *Cc = Sk + kMaxRes * 64;        // [4][5]: G_i[Kc+r][Kc+c], bc
+        double *ATk = AHk + (N - 1) * 64;      // [N-1][64] AT_ik
+        double *X = ATk + (N - 1) * 64;        // [N-1][64]
+        double *Sk = X + (N - 1) * 64;         // [N-1][64]
+        double *Cc = Sk + (N - 1) * 64;        // [4][5]: G_i[Kc+r][Kc+c], bc
         for (int e = tid; e < 8 * KP; e += kStThreads) {
             const int r = e / KP, col = e % KP;
             Gj[e] = col < Kc + 5 ? g_elem(slab, hi.y, per, nt, 8 * sj + r, col) : 0.0;
@@ -1370,17 +1393,16 @@ __global__ __launch_bounds__(kStThreads) void k_frame_th(const WinDev *__restric
             const int r = (int)(i / stride);
             return buf[((size_t)r * n_win + w) * stride + (i - (long long)r * stride)];
         },
-        (int)n_cand, keys, frame_th + W.frame_base + W.N - 1);
+        (int)n_cand, keys, kThMaxLds, frame_th + W.frame_base + W.N - 1);
 }
 
 struct ResubParams {
     const float *__restrict__ xad;   // [N*N][8] for this window (index h*N + t)
     const float *__restrict__ xc;    // [4]
     const int *__restrict__ pt_nres;
-    const int *__restrict__ pt_res;
-    const uint8_t *__restrict__ rs_tgt;
-    const uint8_t *__restrict__ rs_flags;
-    const float4 *__restrict__ rs_rec;
+    const unsigned long long *__restrict__ pt_tgt;
+    const float4 *__restrict__ pt_rec;
+    int rec_base, P, point_base;
     const float *__restrict__ pt_out;
     const int *__restrict__ pt_host;
     float *pt_step;
@@ -1402,11 +1424,14 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
     const float d = P.xc[0] * po[5] + P.xc[1] * po[6] + P.xc[2] * po[7] + P.xc[3] * po[8];
     b -= d;
     const int h = P.pt_host[p];
+    const unsigned long long tgs = P.pt_tgt[p];
+    const float4 *rp = P.pt_rec + ((size_t)P.rec_base + (p - P.point_base)) * 4;
     for (int q = 0; q < P.pt_nres[p]; q++) {
-        const int r = P.pt_res[(size_t)p * kMaxRes + q];
-        if (!(P.rs_flags[r] & LDSO_BA_FLAG_ACTIVE)) continue;
-        const float *xa = P.xad + (size_t)(h * P.N + P.rs_tgt[r]) * 8;
-        const float4 j0 = P.rs_rec[(size_t)r * 4], j1 = P.rs_rec[(size_t)r * 4 + 1];
+        const int tg = (int)((tgs >> (4 * q)) & 15ull);
+        const float4 *rq = rp + (size_t)(tg < h ? tg : tg - 1) * P.P * 4;
+        if (rq[3].z == 0.0f) continue;  // not active
+        const float *xa = P.xad + (size_t)(h * P.N + tg) * 8;
+        const float4 j0 = rq[0], j1 = rq[1];
         const float dd = xa[0] * j0.x + xa[1] * j0.y + xa[2] * j0.z + xa[3] * j0.w + xa[4] * j1.x + xa[5] * j1.y +
                          xa[6] * j1.z + xa[7] * j1.w;
         b -= dd;
@@ -1496,6 +1521,7 @@ struct WinHost {
     int P_all, R_all;               // caller's counts
     std::vector<int> pt_orig;       // sorted -> caller point index
     std::vector<int> rs_orig;       // sorted -> caller residual index
+    std::vector<int> rs_slot;       // sorted residual -> record slot (global)
     std::vector<int> pt_host;       // sorted point host
     std::vector<double> c_prior, frame_prior, frame_delta_prior;
     std::vector<float> c_delta;
@@ -1523,11 +1549,12 @@ struct ldso_ba_ctx {
     long long frame_stride = 0;
     DevBuf<float> d_precalc, d_frame_th, d_pt_data, d_pt_out, d_pt_step;
     DevBuf<double> d_adH, d_adT;
-    DevBuf<int> d_rs_point, d_pt_nres, d_pt_res, d_pair_win, d_frame_win, d_pt_host;
+    DevBuf<int> d_rs_point, d_rs_slot, d_pt_nres, d_pair_win, d_frame_win, d_pt_host;
+    DevBuf<unsigned long long> d_pt_tgt;
     DevBuf<uint8_t> d_rs_tgt, d_rs_flags;
     DevBuf<int8_t> d_rs_state, d_rs_newstate;
     DevBuf<float> d_rs_energy, d_rs_newenergy, d_rs_energy_wo;
-    DevBuf<float4> d_rs_center, d_rs_rec;
+    DevBuf<float4> d_rs_center, d_pt_rec;
     DevBuf<int4> d_top_items, d_sc_items;
     DevBuf<int2> d_pair_items, d_host_items;
     DevBuf<float> d_top_slab, d_sc_slab;
@@ -1621,6 +1648,18 @@ int check_window(const ldso_ba_window &w) {
 }
 
 size_t sc_smem_bytes(int KP) { return (size_t)(64 * KP + 64) * sizeof(float); }
+// k_stitch dynamic LDS: max of the Top phase, the SC phase of the largest window, and the
+// frame-threshold staging (at least 1024 candidates; more if the SC phase leaves room)
+size_t stitch_smem_bytes(int KP, int N, int *th_cap) {
+    const size_t top = (96 + 169 + 4 * 64) * sizeof(double);
+    const size_t sc = (size_t)(8 * KP + 128 + 4 * (N - 1) * 64 + 20) * sizeof(double);
+    const size_t th_fixed = (256 + 8) * sizeof(unsigned) + 2 * kStThreads * sizeof(double);
+    size_t bytes = std::max(top, sc);
+    bytes = std::max(bytes, th_fixed + 1024 * sizeof(unsigned));
+    bytes = (bytes + 15) & ~(size_t)15;
+    *th_cap = (int)((bytes - th_fixed) / sizeof(unsigned)) & ~3;
+    return bytes;
+}
 
 }  // namespace
 
@@ -1697,8 +1736,9 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_adH.release();
     c->d_adT.release();
     c->d_rs_point.release();
+    c->d_rs_slot.release();
     c->d_pt_nres.release();
-    c->d_pt_res.release();
+    c->d_pt_tgt.release();
     c->d_pair_win.release();
     c->d_frame_win.release();
     c->d_pt_host.release();
@@ -1710,7 +1750,7 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_rs_newenergy.release();
     c->d_rs_energy_wo.release();
     c->d_rs_center.release();
-    c->d_rs_rec.release();
+    c->d_pt_rec.release();
     c->d_top_items.release();
     c->d_sc_items.release();
     c->d_pair_items.release();
@@ -1754,7 +1794,9 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     // host-side layout
     std::vector<int4> top_items, sc_items;
     std::vector<int2> pair_items, host_items;
-    std::vector<int> pair_win, frame_win, rs_point, pt_nres, pt_res, pt_host;
+    std::vector<int> pair_win, frame_win, rs_point, rs_slot, pt_nres, pt_host;
+    std::vector<unsigned long long> pt_tgt;
+    int rec_base = 0;
     std::vector<uint8_t> rs_tgt, rs_flags;
     std::vector<int8_t> rs_state;
     std::vector<float> rs_energy, pt_data, precalc, frame_th;
@@ -1824,7 +1866,9 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
             rs_state.push_back(in.res_state[k]);
             rs_energy.push_back(in.res_energy[k]);
             rs_point.push_back(0);
+            rs_slot.push_back(0);
         }
+        H.rs_slot.assign(R, 0);
         // per-point arrays
         H.pt_host.resize(P);
         for (int q = 0; q < P; q++) {
@@ -1835,11 +1879,17 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
                            in.point_data + (size_t)(p + 1) * LDSO_BA_POINT_STRIDE);
             const int b = in.point_res_begin[p], e = in.point_res_begin[p + 1];
             pt_nres.push_back(e - b);
-            for (int k = 0; k < kMaxRes; k++) {
-                const int pos = k < e - b ? res_pos_of[b + k] : 0;
-                pt_res.push_back(k < e - b ? res_base + pos : 0);
-                if (k < e - b) rs_point[res_base + pos] = point_base + q;
+            unsigned long long tg = 0;
+            for (int k = 0; k < e - b; k++) {
+                const int pos = res_pos_of[b + k];
+                rs_point[res_base + pos] = point_base + q;
+                const int tgk = in.res_target[b + k], hk = in.point_host[p];
+                const int slot = rec_base + (tgk < hk ? tgk : tgk - 1) * P + q;
+                rs_slot[res_base + pos] = slot;
+                H.rs_slot[pos] = slot;
+                tg |= (unsigned long long)in.res_target[b + k] << (4 * k);
             }
+            pt_tgt.push_back(tg);
         }
         // descriptors
         D.N = N;
@@ -1891,6 +1941,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         sys_total += sys_len(D.D);
         D.newest_begin = res_base + bucket_start[N * (N - 1)];
         D.newest_end = res_base + bucket_start[N * N];
+        D.rec_base = rec_base;
         // frame-level inputs
         precalc.insert(precalc.end(), in.precalc, in.precalc + (size_t)N * N * LDSO_BA_PRECALC_STRIDE);
         adH.insert(adH.end(), in.ad_host, in.ad_host + (size_t)N * N * 64);
@@ -1899,6 +1950,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         frame_base += N;
         pair_base += N * N;
         point_base += P;
+        rec_base += P * (N - 1);
         res_base += R;
     }
     c->n_top_items = (int)top_items.size();
@@ -1929,7 +1981,8 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     ALLOC(c->d_adT, adT.size());
     ALLOC(c->d_rs_point, std::max<size_t>(1, rs_point.size()));
     ALLOC(c->d_pt_nres, std::max<size_t>(1, pt_nres.size()));
-    ALLOC(c->d_pt_res, std::max<size_t>(1, pt_res.size()));
+    ALLOC(c->d_rs_slot, std::max<size_t>(1, rs_slot.size()));
+    ALLOC(c->d_pt_tgt, std::max<size_t>(1, pt_tgt.size()));
     ALLOC(c->d_pair_win, pair_win.size());
     ALLOC(c->d_frame_win, frame_win.size());
     ALLOC(c->d_rs_tgt, std::max<size_t>(1, rs_tgt.size()));
@@ -1940,7 +1993,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     ALLOC(c->d_rs_newenergy, std::max<size_t>(1, rs_energy.size()));
     ALLOC(c->d_rs_energy_wo, std::max<size_t>(1, rs_energy.size()));
     ALLOC(c->d_rs_center, std::max<size_t>(1, rs_energy.size()));
-    ALLOC(c->d_rs_rec, std::max<size_t>(1, rs_energy.size() * 4));
+    ALLOC(c->d_pt_rec, std::max<size_t>(1, (size_t)rec_base * 4));
     ALLOC(c->d_top_items, std::max<size_t>(1, top_items.size()));
     ALLOC(c->d_sc_items, std::max<size_t>(1, sc_items.size()));
     ALLOC(c->d_pair_items, pair_items.size());
@@ -1971,7 +2024,8 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     UP(c->d_adT, adT);
     UP(c->d_rs_point, rs_point);
     UP(c->d_pt_nres, pt_nres);
-    UP(c->d_pt_res, pt_res);
+    UP(c->d_rs_slot, rs_slot);
+    UP(c->d_pt_tgt, pt_tgt);
     UP(c->d_pair_win, pair_win);
     UP(c->d_frame_win, frame_win);
     UP(c->d_rs_tgt, rs_tgt);
@@ -1985,7 +2039,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     UP(c->d_host_items, host_items);
 #undef UP
     HIP_TRY(hipMemsetAsync(c->d_rs_center.p, 0, c->d_rs_center.bytes(), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_rs_rec.p, 0, c->d_rs_rec.bytes(), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_pt_rec.p, 0, c->d_pt_rec.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_pt_out.p, 0, c->d_pt_out.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_pt_step.p, 0, c->d_pt_step.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_sys.p, 0, c->d_sys.bytes(), c->stream));
@@ -2094,6 +2148,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         L.precalc = c->d_precalc.p;
         L.frame_th = c->d_frame_th.p;
         L.rs_point = c->d_rs_point.p;
+        L.rs_slot = c->d_rs_slot.p;
         L.pt_data = c->d_pt_data.p;
         L.rs_state = c->d_rs_state.p;
         L.rs_newstate = c->d_rs_newstate.p;
@@ -2102,7 +2157,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         L.rs_newenergy = c->d_rs_newenergy.p;
         L.rs_energy_wo = c->d_rs_energy_wo.p;
         L.rs_center = c->d_rs_center.p;
-        L.rs_rec = c->d_rs_rec.p;
+        L.pt_rec = c->d_pt_rec.p;
         L.top_slab = c->d_top_slab.p;
         L.item_energy = c->d_item_energy.p;
         L.n_items = c->n_top_items;
@@ -2123,10 +2178,8 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         Pp.wins = c->d_wins.p;
         Pp.pt_data = c->d_pt_data.p;
         Pp.pt_nres = c->d_pt_nres.p;
-        Pp.pt_res = c->d_pt_res.p;
-        Pp.rs_tgt = c->d_rs_tgt.p;
-        Pp.rs_flags = c->d_rs_flags.p;
-        Pp.rs_rec = c->d_rs_rec.p;
+        Pp.pt_tgt = c->d_pt_tgt.p;
+        Pp.pt_rec = c->d_pt_rec.p;
         Pp.pt_out = c->d_pt_out.p;
         Pp.sc_slab = c->d_sc_slab.p;
         Pp.n_items = c->n_sc_items;
@@ -2148,7 +2201,13 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.sys = c->d_sys.p;
     Sp.win_energy = c->d_win_energy.p;
     Sp.accumulate = accumulate;
-    rc = timed_launch(c, 2, [&] { k_stitch<<<c->n_pairs, kStThreads, 0, c->stream>>>(Sp); });
+    int kp_max = 0, n_max = 2;
+    for (const WinDev &D : c->wd) {
+        kp_max = std::max(kp_max, D.KP);
+        n_max = std::max(n_max, D.N);
+    }
+    const size_t st_smem = stitch_smem_bytes(kp_max, n_max, &Sp.th_cap);
+    rc = timed_launch(c, 2, [&] { k_stitch<<<c->n_pairs, kStThreads, st_smem, c->stream>>>(Sp); });
     return rc;
 }
 
@@ -2249,16 +2308,18 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
     std::vector<int8_t> ns(R), st(R);
     std::vector<uint8_t> fl(R);
     std::vector<float> se(R), ew(R);
-    std::vector<float4> ce(R), rec((size_t)R * 4);
+    std::vector<float4> ce(R), rec;
     HIP_TRY(hipMemcpy(ns.data(), c->d_rs_newstate.p + D.res_base, R, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(st.data(), c->d_rs_state.p + D.res_base, R, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fl.data(), c->d_rs_flags.p + D.res_base, R, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(se.data(), c->d_rs_energy.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(ew.data(), c->d_rs_energy_wo.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(ce.data(), c->d_rs_center.p + D.res_base, R * sizeof(float4), hipMemcpyDeviceToHost));
-    if (jpjdf)
-        HIP_TRY(hipMemcpy(rec.data(), c->d_rs_rec.p + (size_t)D.res_base * 4, (size_t)R * 4 * sizeof(float4),
-                          hipMemcpyDeviceToHost));
+    const size_t slot0 = (size_t)D.rec_base;
+    if (jpjdf && D.P > 0) {
+        rec.resize((size_t)D.P * (D.N - 1) * 4);
+        HIP_TRY(hipMemcpy(rec.data(), c->d_pt_rec.p + slot0 * 4, rec.size() * sizeof(float4), hipMemcpyDeviceToHost));
+    }
     for (int pos = 0; pos < R; pos++) {
         const int k = H.rs_orig[pos];
         if (new_state) new_state[k] = ns[pos];
@@ -2273,7 +2334,8 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
         if (flags) flags[k] = fl[pos];
         if (rel_bs) rel_bs[k] = ce[pos].w;
         if (jpjdf) {
-            const float4 a = rec[(size_t)pos * 4], b = rec[(size_t)pos * 4 + 1];
+            const size_t sl = (size_t)H.rs_slot[pos] - slot0;
+            const float4 a = rec[sl * 4], b = rec[sl * 4 + 1];
             const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
             std::memcpy(jpjdf + 8 * (size_t)k, v, sizeof(v));
         }
@@ -2339,10 +2401,11 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
         R.xad = c->d_xad.p;
         R.xc = c->d_xad.p + (size_t)N * N * 8;
         R.pt_nres = c->d_pt_nres.p;
-        R.pt_res = c->d_pt_res.p;
-        R.rs_tgt = c->d_rs_tgt.p;
-        R.rs_flags = c->d_rs_flags.p;
-        R.rs_rec = c->d_rs_rec.p;
+        R.pt_tgt = c->d_pt_tgt.p;
+        R.rec_base = D.rec_base;
+        R.P = D.P;
+        R.point_base = D.point_base;
+        R.pt_rec = c->d_pt_rec.p;
         R.pt_out = c->d_pt_out.p;
         R.pt_host = c->d_pt_host.p;
         R.pt_step = c->d_pt_step.p;
@@ -2479,8 +2542,8 @@ int32_t ldso_ba_num_kernels(void) { return kNumKernels; }
 int ldso_ba_stats(ldso_ba_ctx *c, int64_t *device_bytes, int64_t *n_points, int64_t *n_residuals) {
     if (!c) return fail(-1, "null ctx");
     if (device_bytes)
-        *device_bytes = (int64_t)(c->d_img.bytes() + c->d_precalc.bytes() + c->d_pt_data.bytes() + c->d_rs_rec.bytes() +
-                                  c->d_top_slab.bytes() + c->d_sc_slab.bytes() + c->d_sys.bytes() + c->d_pt_res.bytes());
+        *device_bytes = (int64_t)(c->d_img.bytes() + c->d_precalc.bytes() + c->d_pt_data.bytes() + c->d_pt_rec.bytes() +
+                                  c->d_top_slab.bytes() + c->d_sc_slab.bytes() + c->d_sys.bytes());
     if (n_points) *n_points = c->P_tot;
     if (n_residuals) *n_residuals = c->R_tot;
     return 0;
