@@ -233,8 +233,9 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
 /* Tuning knobs (defaults are the measured best):
  *   LDSO_BA_TUNE_LIN_VARIANT   k_linearize form: 1 or 2 = lane per residual (occupancy target in
  *                              waves per SIMD), 3 = sample-parallel (8 lanes per residual)
- *   LDSO_BA_TUNE_TILED_IMAGES  frames stored in 2x4-texel tiles (1) or row-major (0); set
- *                              before ldso_ba_load
+ *   LDSO_BA_TUNE_TILED_IMAGES  frame layout: 0 row-major [I,dx,dy,0] texels, 1 2x4-texel tiles,
+ *                              2 one 64-B bilinear quad record per pixel (needs LIN_VARIANT 3);
+ *                              set before ldso_ba_load
  *   LDSO_BA_TUNE_LOAD3         texel loads as dwordx3 (1) or dwordx4 (0)
  *   LDSO_BA_TUNE_XCD_REMAP     XCD-contiguous block->chunk mapping in k_linearize (1) or not
  *   LDSO_BA_TUNE_CENTRE_FIRST  centre projection before the pattern gathers (1, reference order)

@@ -616,8 +616,10 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
     t[16] = resF * resF;
 }
 
-template <bool kTiled, bool kXcdRemap>
+// kImg: 0 row-major float4 texels, 1 2x4-tiled float4 texels, 2 quad records (see k_tile_image)
+template <int kImg, bool kXcdRemap>
 __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
+    constexpr bool kTiled = kImg == 1;
     __shared__ float lds_terms[4][8][kSums][8];
     __shared__ __attribute__((aligned(16))) float lds_sums[4][64][kSumStride];
     const int lane = threadIdx.x & 63;
@@ -668,7 +670,8 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
 
         struct Stage {
             float Ku, Kv, color, weight;
-            float3 t00, t10, t01, t11;
+            float3 t00, t10, t01, t11;  // kImg 0/1: the four taps
+            float4 qi, qx, qy;          // kImg 2: I, dx, dy of the quad (00, 10, 01, 11)
             bool gok;
         };
         auto issue = [&](int k, Stage &q) {
@@ -693,10 +696,17 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             q.gok = ((m1 >> (8 * g)) & 0xFFull) == 0xFFull;
             // taps of an in-bounds pixel are always addressable; others read texel (0, 0)
             const int ix = pok ? (int)q.Ku : 0, iy = pok ? (int)q.Kv : 0;
-            q.t00 = tex<kTiled, false>(img, tpr2, ix, iy);
-            q.t10 = tex<kTiled, false>(img, tpr2, ix + 1, iy);
-            q.t01 = tex<kTiled, false>(img, tpr2, ix, iy + 1);
-            q.t11 = tex<kTiled, false>(img, tpr2, ix + 1, iy + 1);
+            if constexpr (kImg == 2) {  // one 64-byte record holds the whole 2x2 footprint
+                const float4 *rec = img + ((size_t)iy * W.width + ix) * 4;
+                q.qi = rec[0];
+                q.qx = rec[1];
+                q.qy = rec[2];
+            } else {
+                q.t00 = tex<kTiled, false>(img, tpr2, ix, iy);
+                q.t10 = tex<kTiled, false>(img, tpr2, ix + 1, iy);
+                q.t01 = tex<kTiled, false>(img, tpr2, ix, iy + 1);
+                q.t11 = tex<kTiled, false>(img, tpr2, ix + 1, iy + 1);
+            }
         };
         auto consume = [&](int k, const Stage &q) {
             const int j = 8 * k + g;
@@ -705,9 +715,16 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
                 const int ix = (int)q.Ku, iy = (int)q.Kv;
                 const float dx = q.Ku - ix, dy = q.Kv - iy, dxdy = dx * dy;
                 const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
-                const float I = w11 * q.t11.x + w01 * q.t01.x + w10 * q.t10.x + w00 * q.t00.x;
-                const float gx = w11 * q.t11.y + w01 * q.t01.y + w10 * q.t10.y + w00 * q.t00.y;
-                const float gy = w11 * q.t11.z + w01 * q.t01.z + w10 * q.t10.z + w00 * q.t00.z;
+                float I, gx, gy;
+                if constexpr (kImg == 2) {
+                    I = w11 * q.qi.w + w01 * q.qi.z + w10 * q.qi.y + w00 * q.qi.x;
+                    gx = w11 * q.qx.w + w01 * q.qx.z + w10 * q.qx.y + w00 * q.qx.x;
+                    gy = w11 * q.qy.w + w01 * q.qy.z + w10 * q.qy.y + w00 * q.qy.x;
+                } else {
+                    I = w11 * q.t11.x + w01 * q.t01.x + w10 * q.t10.x + w00 * q.t00.x;
+                    gx = w11 * q.t11.y + w01 * q.t01.y + w10 * q.t10.y + w00 * q.t00.y;
+                    gy = w11 * q.t11.z + w01 * q.t01.z + w10 * q.t10.z + w00 * q.t00.z;
+                }
                 fin = isfinite(I);
                 float tt[kSums];
                 pixel_terms(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt);
@@ -1441,6 +1458,24 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
 }
 
 // image ingest: FrameHessian::dI (AoS [I, dx, dy]) -> [I, dx, dy, 0] texels in 2x4 tiles
+// (tiled = 1), row-major (0), or (2) one 64-byte quad record per pixel (x, y) holding the
+// bilinear footprint {(x,y), (x+1,y), (x,y+1), (x+1,y+1)} as [I x4][dx x4][dy x4][pad]: every
+// pattern pixel's four taps then come from one record (3 dwordx4 loads in one 64-byte sector)
+// instead of up to four cache lines.  4x the bytes of dI, resident once per keyframe.
+__global__ void k_quad_image(const float *__restrict__ src, float4 *dst, int w, int h) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= w * h) return;
+    const int x = i % w, y = i / w;
+    const int x1 = min(x + 1, w - 1), y1 = min(y + 1, h - 1);
+    const float *a = src + 3 * ((size_t)y * w + x), *b = src + 3 * ((size_t)y * w + x1),
+                *c = src + 3 * ((size_t)y1 * w + x), *d = src + 3 * ((size_t)y1 * w + x1);
+    float4 *o = dst + (size_t)i * 4;
+    o[0] = make_float4(a[0], b[0], c[0], d[0]);
+    o[1] = make_float4(a[1], b[1], c[1], d[1]);
+    o[2] = make_float4(a[2], b[2], c[2], d[2]);
+    o[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __global__ void k_tile_image(const float *__restrict__ src, float4 *dst, int w, int h, int tpr2, int hp, int tiled) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int wp = tpr2 * 2;
@@ -1475,15 +1510,19 @@ void launch_lin1(bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t 
     }
 }
 // variant = occupancy target in waves per SIMD (see DESIGN.md for the measured choice)
-void launch_linearize(int variant, bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t st,
+void launch_linearize(int variant, int img_mode, bool load3, bool xcd, bool cf, int nb, hipStream_t st,
                       const LinParams &L) {
+    const bool tiled = img_mode == 1;
     if (variant == 3) {
-        if (tiled) {
-            if (xcd) k_linearize_sp<true, true><<<nb, 256, 0, st>>>(L);
-            else k_linearize_sp<true, false><<<nb, 256, 0, st>>>(L);
+        if (img_mode == 2) {
+            if (xcd) k_linearize_sp<2, true><<<nb, 256, 0, st>>>(L);
+            else k_linearize_sp<2, false><<<nb, 256, 0, st>>>(L);
+        } else if (tiled) {
+            if (xcd) k_linearize_sp<1, true><<<nb, 256, 0, st>>>(L);
+            else k_linearize_sp<1, false><<<nb, 256, 0, st>>>(L);
         } else {
-            if (xcd) k_linearize_sp<false, true><<<nb, 256, 0, st>>>(L);
-            else k_linearize_sp<false, false><<<nb, 256, 0, st>>>(L);
+            if (xcd) k_linearize_sp<0, true><<<nb, 256, 0, st>>>(L);
+            else k_linearize_sp<0, false><<<nb, 256, 0, st>>>(L);
         }
     } else if (variant == 2) launch_lin1<4>(tiled, load3, xcd, cf, nb, st, L);
     else launch_lin1<1>(tiled, load3, xcd, cf, nb, st, L);
@@ -1563,7 +1602,8 @@ struct ldso_ba_ctx {
     size_t sc_smem_max = 0;
     bool timing = false;
     int lin_variant = 3;
-    bool tiled = true, load3 = false, xcd_remap = true, centre_first = true;  // measured best
+    int img_mode = 1;  // 0 row-major, 1 2x4 tiles, 2 quad records (LDSO_BA_TUNE_TILED_IMAGES)
+    bool load3 = false, xcd_remap = true, centre_first = true;  // measured best
     std::vector<PendingEv> pending;
     std::vector<hipEvent_t> ev_pool;
     double kms[kNumKernels] = {0};
@@ -1715,7 +1755,7 @@ int ldso_ba_create(int32_t device, ldso_ba_ctx **out) {
         return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
     if (const char *v = getenv("LDSO_BA_LIN_VARIANT")) c->lin_variant = atoi(v);
-    if (const char *v = getenv("LDSO_BA_TILED")) c->tiled = atoi(v) != 0;
+    if (const char *v = getenv("LDSO_BA_TILED")) c->img_mode = atoi(v);
     *out = c;
     return 0;
 }
@@ -1785,7 +1825,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     c->npix = c->width * c->height;
     c->tiles_per_row = (c->width + 1) / 2;
     c->padded_h = (c->height + 3) / 4 * 4;
-    c->frame_stride = (long long)c->tiles_per_row * 2 * c->padded_h;
+    c->frame_stride = c->img_mode == 2 ? (long long)c->npix * 4 : (long long)c->tiles_per_row * 2 * c->padded_h;
     c->wh.assign(n_windows, WinHost());
     c->wd.assign(n_windows, WinDev());
     c->sys_host_valid = false;
@@ -2063,9 +2103,13 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
                     (void)hipFree(stage);
                     return fail(-2, std::string("image upload: ") + hipGetErrorString(e));
                 }
-                k_tile_image<<<(int)((c->frame_stride + 255) / 256), 256, 0, c->stream>>>(
-                    stage, c->d_img.p + (size_t)fb * c->frame_stride, c->width, c->height, c->tiles_per_row, c->padded_h,
-                    c->tiled ? 1 : 0);
+                if (c->img_mode == 2)
+                    k_quad_image<<<(c->npix + 255) / 256, 256, 0, c->stream>>>(
+                        stage, c->d_img.p + (size_t)fb * c->frame_stride, c->width, c->height);
+                else
+                    k_tile_image<<<(int)((c->frame_stride + 255) / 256), 256, 0, c->stream>>>(
+                        stage, c->d_img.p + (size_t)fb * c->frame_stride, c->width, c->height, c->tiles_per_row,
+                        c->padded_h, c->img_mode);
             }
         hipError_t e = hipStreamSynchronize(c->stream);
         (void)hipFree(stage);
@@ -2135,6 +2179,7 @@ int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
 
 int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
+    if (c->img_mode == 2 && c->lin_variant != 3) return fail(-1, "quad image records need LIN_VARIANT 3");
     HIP_TRY(hipSetDevice(c->device));
     c->sys_host_valid = false;
     c->energy_valid = false;
@@ -2168,7 +2213,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         L.accumulate = accumulate;
         const int nb = (c->n_top_items + 3) / 4;
         rc = timed_launch(c, 0, [&] {
-            launch_linearize(c->lin_variant, c->tiled, c->load3, c->xcd_remap, c->centre_first, nb, c->stream, L);
+            launch_linearize(c->lin_variant, c->img_mode, c->load3, c->xcd_remap, c->centre_first, nb, c->stream, L);
         });
         if (rc) return rc;
     }
@@ -2495,7 +2540,8 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
     }
     if (key == LDSO_BA_TUNE_TILED_IMAGES) {
         if (c->n_win) return fail(-1, "image layout must be chosen before ldso_ba_load");
-        c->tiled = value != 0;
+        if (value < 0 || value > 2) return fail(-1, "image layout must be 0, 1 or 2");
+        c->img_mode = value;
         return 0;
     }
     if (key == LDSO_BA_TUNE_LOAD3) {

@@ -252,3 +252,29 @@ def test_sharded_frame_threshold_exchange(built):
             np.testing.assert_array_equal(c.frame_energy_th(i), th_full[i])
         c.close()
     full.close()
+
+
+@pytest.mark.parametrize("variant,layout", [(1, 0), (1, 1), (3, 0), (3, 1), (3, 2)])
+def test_kernel_forms_and_image_layouts_agree(built, variant, layout):
+    """Every k_linearize form (lane per residual / sample-parallel) on every frame layout
+    (row-major, 2x4 tiles, quad records) is bit-exact on the per-residual outputs."""
+    cfg = dict(n_frames=6, n_points=700, seed=23)
+    c = BAContext(0)
+    c.set_tuning(2, layout)  # LDSO_BA_TUNE_TILED_IMAGES, before load
+    c.set_tuning(1, variant)
+    c.load([synth.make_window(**cfg)])
+    c.linearize(fix=False, accumulate=True)
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    e_cpu, s_cpu = ow.iteration()
+    compare_pass(c, ow, 0, e_cpu, s_cpu)
+    c.close()
+
+
+def test_quad_layout_requires_sample_parallel_form(built):
+    c = BAContext(0)
+    c.set_tuning(2, 2)
+    c.set_tuning(1, 1)
+    c.load([synth.make_window(n_frames=3, n_points=20, seed=2)])
+    with pytest.raises(RuntimeError, match="quad"):
+        c.linearize()
+    c.close()
