@@ -1077,78 +1077,89 @@ __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row
 // Every thread of the block must call it; thread 0 writes *th_out.
 template <class Get>
 __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, float *th_out) {
+    // LDS: keys[cap] | hist[4 waves][256] | sh[8]
     unsigned *hist = keys + cap;
-    unsigned *sh = hist + 256;  // [0] count [1] prefix [2] rank
-    const int tid = threadIdx.x;
-    if (tid == 0) sh[0] = 0;
-    __syncthreads();
-    for (int i = tid; i < n_cand; i += kStThreads) {
-        const float x = get(i);
-        if (x >= 0) {
-            const unsigned slot = atomicAdd(&sh[0], 1u);
-            if (slot < (unsigned)cap) keys[slot] = __float_as_uint(x) & 0x7FFFFFFFu;  // -0.0 -> 0
+    unsigned *sh = hist + 4 * 256;  // [0..3] per-wave valid counts, [4] prefix, [5] rank
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool in_lds = n_cand <= cap;
+    // stage every candidate at its own index (no compaction, so no dependent slot atomics):
+    // an invalid one (NewEnergyWithOutlier < 0) becomes 0xFFFFFFFF, above every valid key, and
+    // is never selected because the rank is taken among the valid ones only
+    constexpr int kU = 8;
+    unsigned cnt = 0;
+    for (int i0 = 0; i0 < n_cand; i0 += kStThreads * kU) {
+        float x[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) x[u] = get(min(i0 + u * kStThreads + tid, n_cand - 1));  // loads in flight
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int idx = i0 + u * kStThreads + tid;
+            const bool ok = idx < n_cand && x[u] >= 0;
+            cnt += ok ? 1u : 0u;
+            if (in_lds && idx < n_cand) keys[idx] = ok ? (__float_as_uint(x[u]) & 0x7FFFFFFFu) : 0xFFFFFFFFu;
         }
     }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) cnt += __shfl_xor(cnt, m, kWave);
+    if (lane == 0) sh[wid] = cnt;
     __syncthreads();
-    const unsigned n = sh[0];
+    const unsigned n = sh[0] + sh[1] + sh[2] + sh[3];
     if (n == 0) {
         if (tid == 0) *th_out = 12 * 12 * LDSO_BA_PATTERN_NUM;
         __syncthreads();
         return;
     }
-    const bool in_lds = n <= (unsigned)cap;
-    if (tid == 0) {
-        sh[1] = 0;
-        sh[2] = (unsigned)(int)(kFrameEnergyTHN * (float)n);  // int nthIdx = 0.7f * size()
-    }
+    unsigned prefix = 0, rank = (unsigned)(int)(kFrameEnergyTHN * (float)n);  // int nthIdx = 0.7f * size()
+    unsigned *wh = hist + 256 * wid;  // per-wave sub-histogram: 4x less same-address contention
     for (int pass = 0; pass < 4; pass++) {
         const int shift = 24 - 8 * pass;
-        hist[tid] = 0;
-        __syncthreads();
-        const unsigned prefix = sh[1];
         const unsigned pmask = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
+        for (int b = lane; b < 256; b += 64) wh[b] = 0;
+        __syncthreads();
         if (in_lds) {
-            for (unsigned i = tid; i < n; i += kStThreads) {
+            for (int i = tid; i < n_cand; i += kStThreads) {
                 const unsigned key = keys[i];
-                if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+                if ((key & pmask) == (prefix & pmask)) atomicAdd(&wh[(key >> shift) & 255u], 1u);
             }
         } else {
             for (int i = tid; i < n_cand; i += kStThreads) {
                 const float x = get(i);
-                if (!(x >= 0)) continue;
-                const unsigned key = __float_as_uint(x) & 0x7FFFFFFFu;
-                if ((key & pmask) == (prefix & pmask)) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+                const unsigned key = x >= 0 ? (__float_as_uint(x) & 0x7FFFFFFFu) : 0xFFFFFFFFu;
+                if ((key & pmask) == (prefix & pmask)) atomicAdd(&wh[(key >> shift) & 255u], 1u);
             }
         }
         __syncthreads();
         if (tid < 64) {  // one wave: lane l owns bins 4l..4l+3
-            const unsigned h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
-            unsigned incl = h0 + h1 + h2 + h3;
+            unsigned hb[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                hb[q] = hist[4 * tid + q] + hist[256 + 4 * tid + q] + hist[512 + 4 * tid + q] + hist[768 + 4 * tid + q];
+            unsigned incl = hb[0] + hb[1] + hb[2] + hb[3];
 #pragma unroll
             for (int m = 1; m < 64; m <<= 1) {
                 const unsigned y = __shfl_up(incl, m, kWave);
                 if (tid >= m) incl += y;
             }
-            const unsigned rank = sh[2];
             const unsigned long long hit = __ballot(incl > rank);
             const int first = __ffsll((long long)hit) - 1;
             if (tid == first) {
-                unsigned acc = incl - (h0 + h1 + h2 + h3);
+                unsigned acc = incl - (hb[0] + hb[1] + hb[2] + hb[3]);
                 int d = 4 * tid;
-                const unsigned hb[4] = {h0, h1, h2, h3};
-                for (int k = 0; k < 4; k++, d++) {
-                    if (acc + hb[k] > rank) break;
-                    acc += hb[k];
+                for (int q = 0; q < 4; q++, d++) {
+                    if (acc + hb[q] > rank) break;
+                    acc += hb[q];
                 }
-                sh[2] = rank - acc;
-                sh[1] = prefix | ((unsigned)d << shift);
+                sh[5] = rank - acc;
+                sh[4] = prefix | ((unsigned)d << shift);
             }
         }
         __syncthreads();
+        prefix = sh[4];
+        rank = sh[5];
     }
     if (tid == 0) {
 #pragma clang fp contract(off)
-        const float nth = sqrtf(__uint_as_float(sh[1]));
+        const float nth = sqrtf(__uint_as_float(prefix));
         float v = nth * kFrameEnergyTHFacMedian;
         v = 26.0f * kFrameEnergyTHConstWeight + v * (1 - kFrameEnergyTHConstWeight);
         v = v * v;
@@ -1163,24 +1174,27 @@ __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &
     const float *e_wo = P.e_wo + W.newest_begin;
     select_frame_th([&](int i) { return e_wo[i]; }, W.newest_end - W.newest_begin, keys, P.th_cap,
                     P.frame_th + W.frame_base + N - 1);
-    double *red = reinterpret_cast<double *>(keys + P.th_cap + 256 + 8);
-    // linearizeAll: sum of returned energies and #IN, fixed order (strided, then thread 0)
+    double *red = reinterpret_cast<double *>(keys + P.th_cap + 4 * 256 + 8);
+    // linearizeAll: sum of returned energies and #IN in a fixed order (strided per thread, then
+    // a fixed tree), so repeated passes give identical sums
     double se = 0, sn = 0;
     for (int k = tid; k < W.n_top_items; k += kStThreads) {
         se += P.item_energy[2 * (W.top_item_base + k)];
         sn += P.item_energy[2 * (W.top_item_base + k) + 1];
     }
-    red[2 * tid] = se;
-    red[2 * tid + 1] = sn;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        se += __shfl_xor(se, m, kWave);
+        sn += __shfl_xor(sn, m, kWave);
+    }
+    if ((tid & 63) == 0) {
+        red[2 * (tid >> 6)] = se;
+        red[2 * (tid >> 6) + 1] = sn;
+    }
     __syncthreads();
     if (tid == 0) {
-        double a = 0, c = 0;
-        for (int k = 0; k < kStThreads; k++) {
-            a += red[2 * k];
-            c += red[2 * k + 1];
-        }
-        P.win_energy[2 * w] = a;
-        P.win_energy[2 * w + 1] = c;
+        P.win_energy[2 * w] = (red[0] + red[2]) + (red[4] + red[6]);
+        P.win_energy[2 * w + 1] = (red[1] + red[3]) + (red[5] + red[7]);
     }
 }
 
@@ -1208,9 +1222,16 @@ __device__ __forceinline__ double g_elem(const float *__restrict__ slab, int n_i
     const int a = row >> 2, b = col >> 2;
     const int tile = a * nt - a * (a - 1) / 2 + (b - a);
     const float *src = slab + (size_t)tile * 16 + ((row & 3) << 2) + (col & 3);
-    double s = 0;
-    for (int k = 0; k < n_items; k++) s += (double)src[(size_t)k * per];
-    return s;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // 4 independent loads in flight
+    int k = 0;
+    for (; k + 4 <= n_items; k += 4) {
+        s0 += (double)src[(size_t)k * per];
+        s1 += (double)src[(size_t)(k + 1) * per];
+        s2 += (double)src[(size_t)(k + 2) * per];
+        s3 += (double)src[(size_t)(k + 3) * per];
+    }
+    for (; k < n_items; k++) s0 += (double)src[(size_t)k * per];
+    return (s0 + s1) + (s2 + s3);
 }
 
 __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
@@ -1231,6 +1252,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     const int hI = 4 + 8 * h, tI = 4 + 8 * t;
 
     // ---------------- Top: bucket (h, t) ------------------------------------------------
+    {
     double *acc = sm, *A = acc + 96, *AH = A + 169, *AT = AH + 64, *TH = AT + 64, *TT = TH + 64;
     {
         const int2 pi = P.pair_items[pair];
@@ -1295,6 +1317,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
         } else if (tid < 36) {
             atomicAdd(&bA[tid - 32], A[(tid - 32) * 13 + 12]);
         }
+    }
     }
     __syncthreads();
 
@@ -1401,7 +1424,7 @@ __global__ __launch_bounds__(256) void k_export_newest(const WinDev *__restrict_
 
 __global__ __launch_bounds__(kStThreads) void k_frame_th(const WinDev *__restrict__ wins, const float *__restrict__ buf,
                                                          int n_ranks, int n_win, long long stride, float *frame_th) {
-    __shared__ unsigned keys[kThMaxLds + 256 + 8];
+    __shared__ unsigned keys[kThMaxLds + 4 * 256 + 8];
     const int w = blockIdx.x;
     const WinDev &W = wins[w];
     const long long n_cand = (long long)n_ranks * stride;
@@ -1693,7 +1716,7 @@ size_t sc_smem_bytes(int KP) { return (size_t)(64 * KP + 64) * sizeof(float); }
 size_t stitch_smem_bytes(int KP, int N, int *th_cap) {
     const size_t top = (96 + 169 + 4 * 64) * sizeof(double);
     const size_t sc = (size_t)(8 * KP + 128 + 4 * (N - 1) * 64 + 20) * sizeof(double);
-    const size_t th_fixed = (256 + 8) * sizeof(unsigned) + 2 * kStThreads * sizeof(double);
+    const size_t th_fixed = (4 * 256 + 8) * sizeof(unsigned) + 8 * sizeof(double);
     size_t bytes = std::max(top, sc);
     bytes = std::max(bytes, th_fixed + 1024 * sizeof(unsigned));
     bytes = (bytes + 15) & ~(size_t)15;
