@@ -616,7 +616,8 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
     t[16] = resF * resF;
 }
 
-// kImg: 0 row-major float4 texels, 1 2x4-tiled float4 texels, 2 quad records (see k_tile_image)
+// kImg: 0 row-major float4 texels, 1 2x4-tiled float4 texels, 2 quad records (see k_tile_image),
+// 3 intensity only in 8x4-float tiles with the gradients recomputed (see k_intensity_image)
 template <int kImg, bool kXcdRemap>
 __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
     constexpr bool kTiled = kImg == 1;
@@ -672,6 +673,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             float Ku, Kv, color, weight;
             float3 t00, t10, t01, t11;  // kImg 0/1: the four taps
             float4 qi, qx, qy;          // kImg 2: I, dx, dy of the quad (00, 10, 01, 11)
+            float iv[12];               // kImg 3: I at rows y-1 (x, x+1), y and y+1 (x-1..x+2), y+2 (x, x+1)
             bool gok;
         };
         auto issue = [&](int k, Stage &q) {
@@ -694,9 +696,26 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             const bool pok = go && q.Ku > 1.1f && q.Kv > 1.1f && q.Ku < wM3 && q.Kv < hM3;
             const unsigned long long m1 = __ballot(pok);
             q.gok = ((m1 >> (8 * g)) & 0xFFull) == 0xFFull;
-            // taps of an in-bounds pixel are always addressable; others read texel (0, 0)
-            const int ix = pok ? (int)q.Ku : 0, iy = pok ? (int)q.Kv : 0;
-            if constexpr (kImg == 2) {  // one 64-byte record holds the whole 2x2 footprint
+            // taps of an in-bounds pixel are always addressable; others read texel (1, 1)
+            const int ix = pok ? (int)q.Ku : 1, iy = pok ? (int)q.Kv : 1;
+            if constexpr (kImg == 3) {
+                const float *imf = reinterpret_cast<const float *>(img);
+                auto at = [&](int x, int y) {
+                    return imf[(((y >> 2) * tpr2 + (x >> 3)) << 5) + ((y & 3) << 3) + (x & 7)];
+                };
+                q.iv[0] = at(ix, iy - 1);
+                q.iv[1] = at(ix + 1, iy - 1);
+                q.iv[2] = at(ix - 1, iy);
+                q.iv[3] = at(ix, iy);
+                q.iv[4] = at(ix + 1, iy);
+                q.iv[5] = at(ix + 2, iy);
+                q.iv[6] = at(ix - 1, iy + 1);
+                q.iv[7] = at(ix, iy + 1);
+                q.iv[8] = at(ix + 1, iy + 1);
+                q.iv[9] = at(ix + 2, iy + 1);
+                q.iv[10] = at(ix, iy + 2);
+                q.iv[11] = at(ix + 1, iy + 2);
+            } else if constexpr (kImg == 2) {  // one 64-byte record holds the whole 2x2 footprint
                 const float4 *rec = img + ((size_t)iy * W.width + ix) * 4;
                 q.qi = rec[0];
                 q.qx = rec[1];
@@ -716,7 +735,21 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
                 const float dx = q.Ku - ix, dy = q.Kv - iy, dxdy = dx * dy;
                 const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
                 float I, gx, gy;
-                if constexpr (kImg == 2) {
+                if constexpr (kImg == 3) {
+                    // FrameHessian::makeImages gradients (FrameHessian.cc:96-101), recomputed
+                    auto grad = [](float a, float b) {
+                        const float d = 0.5f * (a - b);
+                        return (isnan(d) || fabsf(d) > 255.0f) ? 0.0f : d;
+                    };
+                    const float *v = q.iv;
+                    const float3 t00 = make_float3(v[3], grad(v[4], v[2]), grad(v[7], v[0]));
+                    const float3 t10 = make_float3(v[4], grad(v[5], v[3]), grad(v[8], v[1]));
+                    const float3 t01 = make_float3(v[7], grad(v[8], v[6]), grad(v[10], v[3]));
+                    const float3 t11 = make_float3(v[8], grad(v[9], v[7]), grad(v[11], v[4]));
+                    I = w11 * t11.x + w01 * t01.x + w10 * t10.x + w00 * t00.x;
+                    gx = w11 * t11.y + w01 * t01.y + w10 * t10.y + w00 * t00.y;
+                    gy = w11 * t11.z + w01 * t01.z + w10 * t10.z + w00 * t00.z;
+                } else if constexpr (kImg == 2) {
                     I = w11 * q.qi.w + w01 * q.qi.z + w10 * q.qi.y + w00 * q.qi.x;
                     gx = w11 * q.qx.w + w01 * q.qx.z + w10 * q.qx.y + w00 * q.qx.x;
                     gy = w11 * q.qy.w + w01 * q.qy.z + w10 * q.qy.y + w00 * q.qy.x;
@@ -758,6 +791,19 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
         };
         // ping-pong stages, loads issued unconditionally (a step past the item's end has no valid
         // group and reads texel (0, 0)), so no load result crosses a branch join
+#if LDSO_LIN_PIPE3
+        Stage A, B, C;
+        issue(0, A);
+        issue(1, B);
+        for (int k = 0; k < nsteps; k += 3) {
+            issue(k + 2, C);
+            consume(k, A);
+            issue(k + 3, A);
+            consume(k + 1, B);
+            issue(k + 4, B);
+            consume(k + 2, C);
+        }
+#else
         Stage A, B;
         issue(0, A);
         for (int k = 0; k < nsteps; k += 2) {
@@ -766,6 +812,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             issue(k + 2, A);
             consume(k + 1, B);
         }
+#endif
     }
 
     // ---------------- phase B: lane per residual ---------------------------------------------
@@ -1499,6 +1546,32 @@ __global__ void k_quad_image(const float *__restrict__ src, float4 *dst, int w, 
     o[3] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// image layout 3: the intensity channel only, in 8x4-float tiles (one 128-byte line each, 1/4
+// of the float4 texel bytes); k_linearize_sp recomputes the gradients with makeImages' rule.
+// That is exact only if the caller's gradients ARE makeImages' (FrameHessian.cc:96-101): every
+// pixel the taps can reach (x in [1, w-2], y in [1, h-2]) is checked and *mismatch is set if not.
+__global__ void k_intensity_image(const float *__restrict__ src, float *dst, int w, int h, int tpr8, int hp,
+                                  int *mismatch) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int wp = tpr8 * 8;
+    if (i >= wp * hp) return;
+    const int x = i % wp, y = i / wp;
+    float v = 0.f;
+    if (x < w && y < h) {
+        const float *p = src + 3 * ((size_t)y * w + x);
+        v = p[0];
+        if (x >= 1 && x <= w - 2 && y >= 1 && y <= h - 2) {
+            float dx = 0.5f * (p[3] - p[-3]);
+            float dy = 0.5f * (p[3 * w] - p[-3 * w]);
+            if (isnan(dx) || fabsf(dx) > 255.0f) dx = 0;
+            if (isnan(dy) || fabsf(dy) > 255.0f) dy = 0;
+            if (__float_as_uint(dx) != __float_as_uint(p[1]) || __float_as_uint(dy) != __float_as_uint(p[2]))
+                atomicOr(mismatch, 1);
+        }
+    }
+    dst[(((y >> 2) * tpr8 + (x >> 3)) << 5) + ((y & 3) << 3) + (x & 7)] = v;
+}
+
 __global__ void k_tile_image(const float *__restrict__ src, float4 *dst, int w, int h, int tpr2, int hp, int tiled) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int wp = tpr2 * 2;
@@ -1537,7 +1610,10 @@ void launch_linearize(int variant, int img_mode, bool load3, bool xcd, bool cf, 
                       const LinParams &L) {
     const bool tiled = img_mode == 1;
     if (variant == 3) {
-        if (img_mode == 2) {
+        if (img_mode == 3) {
+            if (xcd) k_linearize_sp<3, true><<<nb, 256, 0, st>>>(L);
+            else k_linearize_sp<3, false><<<nb, 256, 0, st>>>(L);
+        } else if (img_mode == 2) {
             if (xcd) k_linearize_sp<2, true><<<nb, 256, 0, st>>>(L);
             else k_linearize_sp<2, false><<<nb, 256, 0, st>>>(L);
         } else if (tiled) {
@@ -1625,7 +1701,7 @@ struct ldso_ba_ctx {
     size_t sc_smem_max = 0;
     bool timing = false;
     int lin_variant = 3;
-    int img_mode = 1;  // 0 row-major, 1 2x4 tiles, 2 quad records (LDSO_BA_TUNE_TILED_IMAGES)
+    int img_mode = 3;  // 0 row-major, 1 2x4 tiles, 2 quad records, 3 intensity only (LDSO_BA_TUNE_TILED_IMAGES)
     bool load3 = false, xcd_remap = true, centre_first = true;  // measured best
     std::vector<PendingEv> pending;
     std::vector<hipEvent_t> ev_pool;
@@ -1711,6 +1787,57 @@ int check_window(const ldso_ba_window &w) {
 }
 
 size_t sc_smem_bytes(int KP) { return (size_t)(64 * KP + 64) * sizeof(float); }
+
+// frame geometry of the image layout (all strides in float4 units)
+void image_geometry(ldso_ba_ctx *c) {
+    c->padded_h = (c->height + 3) / 4 * 4;
+    if (c->img_mode == 3) {
+        c->tiles_per_row = (c->width + 7) / 8;
+        c->frame_stride = (long long)c->tiles_per_row * 8 * c->padded_h / 4;
+    } else if (c->img_mode == 2) {
+        c->tiles_per_row = (c->width + 1) / 2;
+        c->frame_stride = (long long)c->npix * 4;
+    } else {
+        c->tiles_per_row = (c->width + 1) / 2;
+        c->frame_stride = (long long)c->tiles_per_row * 2 * c->padded_h;
+    }
+}
+
+int stage_images(ldso_ba_ctx *c, const ldso_ba_window *ws, int n_windows, int *mismatch) {
+    float *stage = nullptr;
+    int *flag = nullptr;
+    HIP_TRY(hipMalloc(&stage, (size_t)c->npix * 3 * sizeof(float)));
+    if (hipMalloc(&flag, sizeof(int)) != hipSuccess) {
+        (void)hipFree(stage);
+        return fail(-3, "hipMalloc failed");
+    }
+    hipError_t e = hipMemsetAsync(flag, 0, sizeof(int), c->stream);
+    int fb = 0;
+    for (int w = 0; w < n_windows && e == hipSuccess; w++)
+        for (int f = 0; f < ws[w].n_frames && e == hipSuccess; f++, fb++) {
+            e = hipMemcpyAsync(stage, ws[w].dI + (size_t)f * c->npix * 3, (size_t)c->npix * 3 * sizeof(float),
+                               hipMemcpyHostToDevice, c->stream);
+            if (e != hipSuccess) break;
+            float4 *dst = c->d_img.p + (size_t)fb * c->frame_stride;
+            if (c->img_mode == 3) {
+                const long long n = (long long)c->tiles_per_row * 8 * c->padded_h;
+                k_intensity_image<<<(int)((n + 255) / 256), 256, 0, c->stream>>>(
+                    stage, reinterpret_cast<float *>(dst), c->width, c->height, c->tiles_per_row, c->padded_h, flag);
+            } else if (c->img_mode == 2) {
+                k_quad_image<<<(c->npix + 255) / 256, 256, 0, c->stream>>>(stage, dst, c->width, c->height);
+            } else {
+                k_tile_image<<<(int)((c->frame_stride + 255) / 256), 256, 0, c->stream>>>(
+                    stage, dst, c->width, c->height, c->tiles_per_row, c->padded_h, c->img_mode);
+            }
+            e = hipGetLastError();
+        }
+    if (e == hipSuccess) e = hipMemcpyAsync(mismatch, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(stage);
+    (void)hipFree(flag);
+    if (e != hipSuccess) return fail(-2, std::string("image staging: ") + hipGetErrorString(e));
+    return 0;
+}
 // k_stitch dynamic LDS: max of the Top phase, the SC phase of the largest window, and the
 // frame-threshold staging (at least 1024 candidates; more if the SC phase leaves room)
 size_t stitch_smem_bytes(int KP, int N, int *th_cap) {
@@ -1846,9 +1973,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     c->width = ws[0].width;
     c->height = ws[0].height;
     c->npix = c->width * c->height;
-    c->tiles_per_row = (c->width + 1) / 2;
-    c->padded_h = (c->height + 3) / 4 * 4;
-    c->frame_stride = c->img_mode == 2 ? (long long)c->npix * 4 : (long long)c->tiles_per_row * 2 * c->padded_h;
+    image_geometry(c);
     c->wh.assign(n_windows, WinHost());
     c->wd.assign(n_windows, WinDev());
     c->sys_host_valid = false;
@@ -2113,30 +2238,21 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         if (rc) return rc;
         HIP_TRY(hipStreamSynchronize(c->stream));
     }
-    // images: per frame through a float3 staging buffer, repacked to float4 on the device
+    // images: per frame through a float3 staging buffer, repacked on the device; the
+    // intensity-only layout falls back to 2x4 float4 tiles if the caller's gradients are not
+    // makeImages' (then recomputing them would not be exact)
     {
-        float *stage = nullptr;
-        HIP_TRY(hipMalloc(&stage, (size_t)c->npix * 3 * sizeof(float)));
-        int fb = 0;
-        for (int w = 0; w < n_windows; w++)
-            for (int f = 0; f < ws[w].n_frames; f++, fb++) {
-                hipError_t e = hipMemcpyAsync(stage, ws[w].dI + (size_t)f * c->npix * 3, (size_t)c->npix * 3 * sizeof(float),
-                                              hipMemcpyHostToDevice, c->stream);
-                if (e != hipSuccess) {
-                    (void)hipFree(stage);
-                    return fail(-2, std::string("image upload: ") + hipGetErrorString(e));
-                }
-                if (c->img_mode == 2)
-                    k_quad_image<<<(c->npix + 255) / 256, 256, 0, c->stream>>>(
-                        stage, c->d_img.p + (size_t)fb * c->frame_stride, c->width, c->height);
-                else
-                    k_tile_image<<<(int)((c->frame_stride + 255) / 256), 256, 0, c->stream>>>(
-                        stage, c->d_img.p + (size_t)fb * c->frame_stride, c->width, c->height, c->tiles_per_row,
-                        c->padded_h, c->img_mode);
-            }
-        hipError_t e = hipStreamSynchronize(c->stream);
-        (void)hipFree(stage);
-        if (e != hipSuccess) return fail(-2, std::string("image repack: ") + hipGetErrorString(e));
+        int mismatch = 0;
+        rc = stage_images(c, ws, n_windows, &mismatch);
+        if (rc) return rc;
+        if (c->img_mode == 3 && mismatch) {
+            c->img_mode = 1;
+            image_geometry(c);
+            rc = c->d_img.alloc((size_t)c->n_frames * c->frame_stride);
+            if (rc) return rc;
+            rc = stage_images(c, ws, n_windows, &mismatch);
+            if (rc) return rc;
+        }
     }
     if (c->sc_smem_max > 64 * 1024) {
         HIP_TRY(hipFuncSetAttribute((const void *)k_point_sc, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2202,7 +2318,8 @@ int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
 
 int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
-    if (c->img_mode == 2 && c->lin_variant != 3) return fail(-1, "quad image records need LIN_VARIANT 3");
+    if (c->img_mode >= 2 && c->lin_variant != 3)
+        return fail(-1, "quad / intensity-only image layouts need LIN_VARIANT 3");
     HIP_TRY(hipSetDevice(c->device));
     c->sys_host_valid = false;
     c->energy_valid = false;
@@ -2563,7 +2680,7 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
     }
     if (key == LDSO_BA_TUNE_TILED_IMAGES) {
         if (c->n_win) return fail(-1, "image layout must be chosen before ldso_ba_load");
-        if (value < 0 || value > 2) return fail(-1, "image layout must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(-1, "image layout must be 0, 1, 2 or 3");
         c->img_mode = value;
         return 0;
     }

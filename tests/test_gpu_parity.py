@@ -254,10 +254,11 @@ def test_sharded_frame_threshold_exchange(built):
     full.close()
 
 
-@pytest.mark.parametrize("variant,layout", [(1, 0), (1, 1), (3, 0), (3, 1), (3, 2)])
+@pytest.mark.parametrize("variant,layout", [(1, 0), (1, 1), (3, 0), (3, 1), (3, 2), (3, 3)])
 def test_kernel_forms_and_image_layouts_agree(built, variant, layout):
     """Every k_linearize form (lane per residual / sample-parallel) on every frame layout
-    (row-major, 2x4 tiles, quad records) is bit-exact on the per-residual outputs."""
+    (row-major, 2x4 tiles, quad records, intensity-only with recomputed gradients) is bit-exact
+    on the per-residual outputs."""
     cfg = dict(n_frames=6, n_points=700, seed=23)
     c = BAContext(0)
     c.set_tuning(2, layout)  # LDSO_BA_TUNE_TILED_IMAGES, before load
@@ -277,4 +278,23 @@ def test_quad_layout_requires_sample_parallel_form(built):
     c.load([synth.make_window(n_frames=3, n_points=20, seed=2)])
     with pytest.raises(RuntimeError, match="quad"):
         c.linearize()
+    c.close()
+
+
+def test_intensity_layout_falls_back_when_gradients_are_not_makeimages(built):
+    """Layout 3 recomputes gradients with makeImages' rule; a caller whose dI gradients differ
+    (here: every dx nudged) must still get results from ITS gradients."""
+    cfg = dict(n_frames=4, n_points=300, seed=29)
+    w = synth.make_window(**cfg)
+    w.dI = w.dI.copy()
+    w.dI[:, :, 1] += np.float32(0.125)
+    c = BAContext(0)
+    c.set_tuning(2, 3)
+    c.load([w])
+    c.linearize()
+    w2 = synth.make_window(**cfg)
+    w2.dI = w.dI.copy()
+    ow = oracle.OracleWindow(w2, threads=0)
+    e_cpu, s_cpu = ow.iteration()
+    compare_pass(c, ow, 0, e_cpu, s_cpu)
     c.close()

@@ -10,14 +10,14 @@ from ldso_amd import BAContext, synth  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 ws = [synth.make_window(**synth.S7, seed=1000 + i) for i in range(B)]
 ctxs = {}
-for tiled in (0, 1, 2):
+for tiled in (1, 2, 3):
     c = BAContext(0)
     c.set_tuning(2, tiled)
     c.load(ws)
     for _ in range(3):
         c.linearize()
     ctxs[tiled] = c
-combos = [(1, 0, 1, v, 1) for v in (1, 3)] + [(0, 0, 1, 3, 1), (2, 0, 1, 3, 1), (2, 0, 0, 3, 1)]
+combos = [(1, 0, 1, 3, 1), (2, 0, 1, 3, 1), (3, 0, 1, 3, 1), (3, 0, 0, 3, 1)]
 res = {k: [] for k in combos}
 for rnd in range(3):
     for (tiled, load3, xcd, wv, cf) in combos:
