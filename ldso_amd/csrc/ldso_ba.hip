@@ -962,7 +962,8 @@ struct PointParams {
     int n_items;
 };
 
-__global__ __launch_bounds__(256) void k_point_sc(PointParams P) {
+constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
+__global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int4 it = P.items[blockIdx.x];
     const WinDev &W = P.wins[it.w];
     const int host = it.z, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
@@ -985,10 +986,10 @@ __global__ __launch_bounds__(256) void k_point_sc(PointParams P) {
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
         float *row = U + tid * KP;
-        for (int k0 = 0; k0 < nres; k0 += 4) {
-            float4 rec[4][4];
+        for (int k0 = 0; k0 < nres; k0 += 2) {
+            float4 rec[2][4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 2; u++) {
                 const int k = min(k0 + u, nres - 1);
                 const int tg = (int)((tgs >> (4 * k)) & 15ull);
                 const float4 *q = rp + (tg < host ? tg : tg - 1) * sstride;
@@ -998,7 +999,7 @@ __global__ __launch_bounds__(256) void k_point_sc(PointParams P) {
                 rec[u][3] = q[3];
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 2; u++) {
                 const int k = k0 + u;
                 if (k >= nres || rec[u][3].z == 0.0f) continue;
                 ngood++;
@@ -2368,7 +2369,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         Pp.pt_out = c->d_pt_out.p;
         Pp.sc_slab = c->d_sc_slab.p;
         Pp.n_items = c->n_sc_items;
-        rc = timed_launch(c, 1, [&] { k_point_sc<<<c->n_sc_items, 256, c->sc_smem_max, c->stream>>>(Pp); });
+        rc = timed_launch(c, 1, [&] { k_point_sc<<<c->n_sc_items, kScThreads, c->sc_smem_max, c->stream>>>(Pp); });
         if (rc) return rc;
     }
     StitchParams Sp;
