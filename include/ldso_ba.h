@@ -239,12 +239,16 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *   LDSO_BA_TUNE_LOAD3         texel loads as dwordx3 (1) or dwordx4 (0)
  *   LDSO_BA_TUNE_XCD_REMAP     XCD-contiguous block->chunk mapping in k_linearize (1) or not
  *   LDSO_BA_TUNE_CENTRE_FIRST  centre projection before the pattern gathers (1, reference order)
- *                              or after them (0) */
+ *                              or after them (0)
+ *   LDSO_BA_TUNE_TOP_CHUNK     residuals per k_linearize wavefront: 16, 32, 64, or 0 = automatic
+ *                              (64 for large batches, shorter for a single window); set before
+ *                              ldso_ba_load */
 #define LDSO_BA_TUNE_LIN_VARIANT 1
 #define LDSO_BA_TUNE_TILED_IMAGES 2
 #define LDSO_BA_TUNE_LOAD3 3
 #define LDSO_BA_TUNE_XCD_REMAP 4
 #define LDSO_BA_TUNE_CENTRE_FIRST 5
+#define LDSO_BA_TUNE_TOP_CHUNK 6
 int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);

@@ -1702,6 +1702,7 @@ struct ldso_ba_ctx {
     size_t sc_smem_max = 0;
     bool timing = false;
     int lin_variant = 3;
+    int top_chunk = 0;  // residuals per k_linearize wave (0 = automatic); LDSO_BA_TUNE_TOP_CHUNK
     int img_mode = 3;  // 0 row-major, 1 2x4 tiles, 2 quad records, 3 intensity only (LDSO_BA_TUNE_TILED_IMAGES)
     bool load3 = false, xcd_remap = true, centre_first = true;  // measured best
     std::vector<PendingEv> pending;
@@ -1991,6 +1992,12 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     std::vector<float> rs_energy, pt_data, precalc, frame_th;
     std::vector<double> adH, adT;
     long long sc_slab_total = 0, sys_total = 0;
+    // residuals per k_linearize wave: 64 when the grid is large anyway; small workloads (one
+    // window) use shorter chunks so more waves start at once (latency, not throughput, bound)
+    long long r_est = 0;
+    for (int w = 0; w < n_windows; w++) r_est += ws[w].n_residuals;
+    r_est /= shard_count;
+    const int chunk = c->top_chunk ? c->top_chunk : r_est >= 64LL * 4096 ? 64 : r_est >= 32LL * 2048 ? 32 : 16;
     int frame_base = 0, pair_base = 0, point_base = 0, res_base = 0;
     size_t smem_max = 0;
 
@@ -2099,12 +2106,12 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         const int nt = D.KP / 4;
         D.ntiles = nt * (nt + 1) / 2;
         smem_max = std::max(smem_max, sc_smem_bytes(D.KP));
-        // top items: chunks of 64 residuals of one bucket
+        // top items: chunks of `chunk` residuals of one bucket (one wave each)
         D.top_item_base = (int)top_items.size();
         for (int b = 0; b < N * N; b++) {
             const int first = (int)top_items.size();
-            for (int s = bucket_start[b]; s < bucket_start[b + 1]; s += kWave)
-                top_items.push_back(make_int4(res_base + s, std::min(kWave, bucket_start[b + 1] - s), pair_base + b, w));
+            for (int s = bucket_start[b]; s < bucket_start[b + 1]; s += chunk)
+                top_items.push_back(make_int4(res_base + s, std::min(chunk, bucket_start[b + 1] - s), pair_base + b, w));
             pair_items.push_back(make_int2(first, (int)top_items.size() - first));
             pair_win.push_back(w);
         }
@@ -2683,6 +2690,12 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
         if (c->n_win) return fail(-1, "image layout must be chosen before ldso_ba_load");
         if (value < 0 || value > 3) return fail(-1, "image layout must be 0, 1, 2 or 3");
         c->img_mode = value;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_TOP_CHUNK) {
+        if (value != 0 && value != 16 && value != 32 && value != 64) return fail(-1, "chunk must be 0, 16, 32 or 64");
+        if (c->n_win) return fail(-1, "chunk size must be chosen before ldso_ba_load");
+        c->top_chunk = value;
         return 0;
     }
     if (key == LDSO_BA_TUNE_LOAD3) {

@@ -298,3 +298,16 @@ def test_intensity_layout_falls_back_when_gradients_are_not_makeimages(built):
     e_cpu, s_cpu = ow.iteration()
     compare_pass(c, ow, 0, e_cpu, s_cpu)
     c.close()
+
+
+@pytest.mark.parametrize("chunk", [16, 32, 64])
+def test_chunk_sizes_agree(built, chunk):
+    cfg = dict(n_frames=5, n_points=500, seed=37)
+    c = BAContext(0)
+    c.set_tuning(6, chunk)  # LDSO_BA_TUNE_TOP_CHUNK
+    c.load([synth.make_window(**cfg)])
+    c.linearize()
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    e_cpu, s_cpu = ow.iteration()
+    compare_pass(c, ow, 0, e_cpu, s_cpu)
+    c.close()
