@@ -1095,6 +1095,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
 // Only the f64 summation order of the atomics varies between runs.
 // ============================================================================================
 constexpr int kStThreads = 256;
+constexpr int kStTopLds = 528;  // doubles of k_stitch LDS used by the Top half (521, padded)
 constexpr int kThMaxLds = 8192;  // k_frame_th: candidate energies staged in LDS; larger sets re-read HBM
 
 struct StitchParams {
@@ -1299,9 +1300,18 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     double *HA = sys, *bA = sys + pl, *Hs = sys + pl + D, *bs = sys + 2 * pl + D;
     const int hI = 4 + 8 * h, tI = 4 + 8 * t;
 
-    // ---------------- Top: bucket (h, t) ------------------------------------------------
-    {
-    double *acc = sm, *A = acc + 96, *AH = A + 169, *AT = AH + 64, *TH = AT + 64, *TT = TH + 64;
+    // All global loads of both halves are issued first (one round trip for the block): the
+    // Top bucket partial sums and pair adjoints, and the SC rows of G_i with the host's adjoints.
+    double *acc = sm, *A = acc + 96, *AH = A + 169, *AT = AH + 64, *TH = AT + 64, *TT = TH + 64;  // 521
+    const int i = h, j = t, KP = W.KP, nt = KP / 4, per = W.ntiles * 16, Kc = 8 * (N - 1);
+    const int sj = j < i ? j : j - 1;
+    double *Gj = sm + kStTopLds;           // [8][KP]: rows 8 sj.. of G_i
+    double *AHk = Gj + 8 * KP;             // [N-1][64] AH_ik
+    double *ATk = AHk + (N - 1) * 64;      // [N-1][64] AT_ik
+    double *X = ATk + (N - 1) * 64;        // [N-1][64]
+    double *Sk = X + (N - 1) * 64;         // [N-1][64]
+    double *Cc = Sk + (N - 1) * 64;        // [4][5]: G_i[Kc+r][Kc+c], bc
+    const double *Ah = AH, *At = AT;       // AH_ij, AT_ij are the Top pair's adjoints
     {
         const int2 pi = P.pair_items[pair];
         if (tid < kTopVals) {
@@ -1321,7 +1331,26 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
         } else if (tid < kTopVals + 128) {
             AT[tid - kTopVals - 64] = P.adT[(size_t)pair * 64 + tid - kTopVals - 64];
         }
-        __syncthreads();
+        const int2 hi = P.host_items[W.frame_base + i];
+        const float *slab = P.sc_slab + W.sc_slab_base + (size_t)(hi.x - W.sc_item_base) * per;
+        for (int e = tid; e < 8 * KP; e += kStThreads) {
+            const int r = e / KP, col = e % KP;
+            Gj[e] = col < Kc + 5 ? g_elem(slab, hi.y, per, nt, 8 * sj + r, col) : 0.0;
+        }
+        if (sj == 0 && tid < 20) {  // accHcc / accbc once per host (AccumulatedSCHessian.cc:105-113)
+            const int r = tid / 5, c = tid % 5;
+            Cc[tid] = g_elem(slab, hi.y, per, nt, Kc + r, Kc + c);
+        }
+        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
+            const int s = e >> 6, k = s + (s >= i), pik = W.pair_base + i + N * k;
+            AHk[e] = P.adH[(size_t)pik * 64 + (e & 63)];
+            ATk[e] = P.adT[(size_t)pik * 64 + (e & 63)];
+        }
+    }
+    __syncthreads();
+
+    // ---------------- Top: bucket (h, t) ------------------------------------------------
+    {
         if (tid < 169) A[tid] = acc[top_slot(tid / 13, tid % 13)];
         __syncthreads();
         if (tid < 128) {
@@ -1366,39 +1395,9 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
             atomicAdd(&bA[tid - 32], A[(tid - 32) * 13 + 12]);
         }
     }
-    }
-    __syncthreads();
 
     // ---------------- SC: host i = h, target j = t ---------------------------------------
     {
-        const int i = h, j = t, KP = W.KP, nt = KP / 4, per = W.ntiles * 16, Kc = 8 * (N - 1);
-        const int sj = j < i ? j : j - 1;
-        const int2 hi = P.host_items[W.frame_base + i];
-        const float *slab = P.sc_slab + W.sc_slab_base + (size_t)(hi.x - W.sc_item_base) * per;
-        double *Gj = sm;                       // [8][KP]: rows 8 sj.. of G_i
-        double *Ah = Gj + 8 * KP;              // AH_ij, AT_ij
-        double *At = Ah + 64;
-        double *AHk = At + 64;                 // [N-1][64] AH_ik
-        double *ATk = AHk + (N - 1) * 64;      // [N-1][64] AT_ik
-        double *X = ATk + (N - 1) * 64;        // [N-1][64]
-        double *Sk = X + (N - 1) * 64;         // [N-1][64]
-        double *Cc = Sk + (N - 1) * 64;        // [4][5]: G_i[Kc+r][Kc+c], bc
-        for (int e = tid; e < 8 * KP; e += kStThreads) {
-            const int r = e / KP, col = e % KP;
-            Gj[e] = col < Kc + 5 ? g_elem(slab, hi.y, per, nt, 8 * sj + r, col) : 0.0;
-        }
-        if (sj == 0 && tid < 20) {  // accHcc / accbc once per host (AccumulatedSCHessian.cc:105-113)
-            const int r = tid / 5, c = tid % 5;
-            Cc[tid] = g_elem(slab, hi.y, per, nt, Kc + r, Kc + c);
-        }
-        if (tid < 64) Ah[tid] = P.adH[(size_t)pair * 64 + tid];
-        else if (tid < 128) At[tid - 64] = P.adT[(size_t)pair * 64 + tid - 64];
-        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
-            const int s = e >> 6, k = s + (s >= i), pik = W.pair_base + i + N * k;
-            AHk[e] = P.adH[(size_t)pik * 64 + (e & 63)];
-            ATk[e] = P.adT[(size_t)pik * 64 + (e & 63)];
-        }
-        __syncthreads();
         // per k != i: X_k = AT_ij D_jk, S_k = D_jk AH_ik^T
         for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
             const int s = e >> 6, r = (e >> 3) & 7, c = e & 7;
@@ -1844,7 +1843,7 @@ int stage_images(ldso_ba_ctx *c, const ldso_ba_window *ws, int n_windows, int *m
 // frame-threshold staging (at least 1024 candidates; more if the SC phase leaves room)
 size_t stitch_smem_bytes(int KP, int N, int *th_cap) {
     const size_t top = (96 + 169 + 4 * 64) * sizeof(double);
-    const size_t sc = (size_t)(8 * KP + 128 + 4 * (N - 1) * 64 + 20) * sizeof(double);
+    const size_t sc = (size_t)(kStTopLds + 8 * KP + 4 * (N - 1) * 64 + 20) * sizeof(double);
     const size_t th_fixed = (4 * 256 + 8) * sizeof(unsigned) + 8 * sizeof(double);
     size_t bytes = std::max(top, sc);
     bytes = std::max(bytes, th_fixed + 1024 * sizeof(unsigned));
