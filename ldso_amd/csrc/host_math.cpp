@@ -288,6 +288,7 @@ namespace {
 // In-place LDL^T with symmetric diagonal pivoting (Eigen::LDLT's strategy), then solve.
 void ldlt_solve(int n, std::vector<double> &A, std::vector<double> &b) {
     std::vector<int> perm(n);
+    std::vector<double> col(n, 0.0);
     for (int i = 0; i < n; i++) perm[i] = i;
     auto at = [&](int r, int c) -> double & { return A[(size_t)r * n + c]; };
     for (int k = 0; k < n; k++) {
@@ -300,9 +301,11 @@ void ldlt_solve(int n, std::vector<double> &A, std::vector<double> &b) {
             for (int j = 0; j < n; j++) std::swap(at(j, k), at(j, piv));
         }
         const double d = at(k, k);
+        // trailing update with the unscaled column k: A(i,j) -= (A(i,k) / d) A(j,k), then L(i,k)
+        for (int i = k + 1; i < n; i++) col[i] = at(i, k);
         for (int i = k + 1; i < n; i++) {
-            const double l = d != 0 ? at(i, k) / d : 0.0;
-            for (int j = k + 1; j <= i; j++) at(i, j) -= l * at(j, k);
+            const double l = d != 0 ? col[i] / d : 0.0;
+            for (int j = k + 1; j <= i; j++) at(i, j) -= l * col[j];
             at(i, k) = l;
         }
         for (int i = k + 1; i < n; i++)

@@ -1370,9 +1370,12 @@ static bool ldlt_solve(int n, std::vector<double> A, std::vector<double> b, std:
             for (int j = 0; j < n; j++) std::swap(A[(size_t)j * n + k], A[(size_t)j * n + piv]);
         }
         double d = A[(size_t)k * n + k];
+        // trailing update A(i,j) -= A(i,k) A(j,k) / d with the UNSCALED column k, then L(i,k) = A(i,k) / d
+        std::vector<double> col(n, 0.0);
+        for (int i = k + 1; i < n; i++) col[i] = A[(size_t)i * n + k];
         for (int i = k + 1; i < n; i++) {
-            double l = (d != 0) ? A[(size_t)i * n + k] / d : 0.0;
-            for (int j = k + 1; j <= i; j++) A[(size_t)i * n + j] -= l * A[(size_t)j * n + k];
+            double l = (d != 0) ? col[i] / d : 0.0;
+            for (int j = k + 1; j <= i; j++) A[(size_t)i * n + j] -= l * col[j];
             A[(size_t)i * n + k] = l;
         }
         for (int i = k + 1; i < n; i++)

@@ -131,3 +131,26 @@ def test_synthetic_generator_is_deterministic(built):
     gx = 0.5 * (np.roll(I.ravel(), -1) - np.roll(I.ravel(), 1)).reshape(120, 160).astype(np.float32)
     np.testing.assert_array_equal(a.dI[0, 160:160 * 119, 1], gx.ravel()[160:160 * 119])
     assert (a.point_res_begin[1:] - a.point_res_begin[:-1] == 3).all()
+
+
+def test_product_solver_known_answer(built):
+    """ldso_ba_solve_system on an SPD system that needs pivoting equals numpy's solve."""
+    rng = np.random.default_rng(7)
+    N = 4
+    n = 8 * N + 4
+    A = rng.standard_normal((n, n))
+    D = np.diag(10.0 ** rng.uniform(-3, 6, n))
+    H = np.ascontiguousarray(D @ (A @ A.T + n * np.eye(n)) @ D)
+    b = rng.standard_normal(n)
+    Z = np.zeros((n, n))
+    z = np.zeros(n)
+    x = np.zeros(n)
+    lib = L.lib()
+    rc = lib.ldso_ba_solve_system(N, 0, 1e-5, L.ptr(H, L.f64p), L.ptr(b, L.f64p), L.ptr(Z, L.f64p), L.ptr(z, L.f64p),
+                                  L.ptr(None, L.f64p), L.ptr(None, L.f64p), L.ptr(Z, L.f64p), L.ptr(z, L.f64p),
+                                  L.ptr(None, L.f64p), 0, L.ptr(x, L.f64p))
+    assert rc == 0
+    Hl = H.copy()
+    Hl[np.diag_indices(n)] *= 1 + 1e-5
+    xr = np.linalg.solve(Hl, b)
+    assert np.linalg.norm(x - xr) <= 1e-9 * np.linalg.norm(xr)

@@ -208,3 +208,56 @@ def test_single_and_multi_thread_paths_agree():
     for k in ("HA", "bA", "Hsc", "bsc"):
         assert rel(s6[k], s1[k]) < 1e-6
     np.testing.assert_array_equal(o1.residuals()["new_state"], o6.residuals()["new_state"])
+
+
+def _solve_inputs(H, b, n):
+    Z = np.zeros((n, n))
+    z = np.zeros(n)
+    return dict(HA=H, bA=b, HL=Z, bL=z, Hsc=Z, bsc=z)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_ldlt_solver_known_answer(seed):
+    """solveSystemF's LDLT (Eigen::LDLT, symmetric pivoting) against numpy on SPD systems that
+    need pivoting (diagonal spanning 1e-3..1e6): x = (H (1+lambda on diag))^-1 b."""
+    rng = np.random.default_rng(seed)
+    N = 4
+    n = 8 * N + 4
+    A = rng.standard_normal((n, n))
+    D = np.diag(10.0 ** rng.uniform(-3, 6, n))
+    H = D @ (A @ A.T + n * np.eye(n)) @ D
+    b = rng.standard_normal(n)
+    x = oracle.solve_system(N, 0, 1e-5, _solve_inputs(H, b, n))
+    Hl = H.copy()
+    Hl[np.diag_indices(n)] *= 1 + 1e-5
+    xr = np.linalg.solve(Hl, b)
+    assert np.linalg.norm(x - xr) <= 1e-9 * np.linalg.norm(xr)
+
+
+def test_orthogonalize_known_answer():
+    """orthogonalize (EnergyFunctional.cc:809-841): x minus its projection on span(N)."""
+    rng = np.random.default_rng(5)
+    N = 3
+    n = 8 * N + 4
+    A = rng.standard_normal((n, n))
+    H = A @ A.T + n * np.eye(n)
+    b = rng.standard_normal(n)
+    ns = rng.standard_normal((7, n))
+    x0 = oracle.solve_system(N, 0, 1e-5, _solve_inputs(H, b, n))
+    x2 = oracle.solve_system(N, 2, 1e-5, _solve_inputs(H, b, n), nullspaces=ns)
+    Q, _ = np.linalg.qr(ns.T)
+    assert np.linalg.norm(x2 - (x0 - Q @ (Q.T @ x0))) <= 1e-10 * np.linalg.norm(x0)
+
+
+def test_solver_backward_stable_on_ba_system(win):
+    """On the (gauge-deficient) BA system itself: the Jacobi-scaled solve has a small backward
+    error, ||H x - b|| <= 1e-12 ||H|| ||x||."""
+    w, s = win["w"], win["sys"]
+    n = w.dim
+    x = oracle.solve_system(w.n_frames, 0, 1e-5, s)
+    sym = lambda M: np.triu(M) + np.triu(M, 1).T  # the solve reads the upper triangles
+    H = sym(s["HL"] + s["HA"])
+    H[np.diag_indices(n)] *= 1 + 1e-5
+    H -= sym(s["Hsc"]) * (1.0 / (1 + 1e-5))
+    b = s["bL"] + s["bA"] - s["bsc"] / (1 + 1e-5)
+    assert np.linalg.norm(H @ x - b) <= 1e-12 * np.linalg.norm(H, 2) * np.linalg.norm(x)
