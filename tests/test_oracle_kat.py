@@ -88,8 +88,9 @@ def test_geometric_jacobians_match_finite_differences(win):
     assert checked == 40
 
 
-def dense_system(w, J, res):
-    """J^T J, J^T r and the explicit Schur complement, rebuilt from per-residual Jacobians."""
+def dense_system(w, J, res, points=None):
+    """J^T J, J^T r and the explicit Schur complement, rebuilt from per-residual Jacobians
+    (optionally also each point's coupling row h_pd, H_dd and b_d into `points`)."""
     N, D = w.n_frames, w.dim
     HA = np.zeros((D, D))
     bA = np.zeros(D)
@@ -123,6 +124,8 @@ def dense_system(w, J, res):
         if hdd > 0:
             Hsc += np.outer(hpd, hpd) / hdd
             bsc += hpd * bd / hdd
+        if points is not None:
+            points.append((hpd, hdd, bd))
     return HA, bA, Hsc, bsc
 
 
@@ -261,3 +264,20 @@ def test_solver_backward_stable_on_ba_system(win):
     H -= sym(s["Hsc"]) * (1.0 / (1 + 1e-5))
     b = s["bL"] + s["bA"] - s["bsc"] / (1 + 1e-5)
     assert np.linalg.norm(H @ x - b) <= 1e-12 * np.linalg.norm(H, 2) * np.linalg.norm(x)
+
+
+def test_resubstitute_known_answer(win):
+    """resubstituteFPt (EnergyFunctional.cc:638-667): step_p = -(b_d - h_pd . x) / H_dd / (1 + lambda),
+    with h_pd, H_dd, b_d rebuilt densely from the Jacobians (priorF = 0 in the synthetic set)."""
+    w, J, res = win["w"], win["J"], win["res"]
+    pts = []
+    dense_system(w, J, res, pts)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(w.dim) * 1e-3
+    ow = oracle.OracleWindow(synth.make_window(n_frames=5, n_points=300, width=320, height=240, seed=13), threads=0)
+    ow.iteration()
+    step = ow.resubstitute(x, 1e-5)
+    exp = np.array([-(bd - hpd @ x) / hdd / (1 + 1e-5) if hdd > 0 else 0.0 for hpd, hdd, bd in pts])
+    act = np.array([hdd > 0 for _, hdd, _ in pts])
+    assert np.array_equal(step[~act], np.zeros((~act).sum()))
+    assert np.linalg.norm(step[act] - exp[act]) <= 1e-5 * np.linalg.norm(exp[act])
