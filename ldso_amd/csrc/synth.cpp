@@ -13,7 +13,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../../include/ldso_ba.h"
+#include "synth.h"
 
 namespace {
 
@@ -132,22 +132,6 @@ void interp33bilin(const float *mat, float x, float y, int width, float out[3]) 
 
 extern "C" {
 
-typedef struct ldso_synth_params {
-    int32_t n_frames;
-    int32_t n_points;
-    int32_t width;
-    int32_t height;
-    uint64_t seed;
-    float outlier_frac;     /* fraction of points with a grossly wrong idepth      */
-    float idepth_noise;     /* relative gaussian noise on inlier idepths           */
-    float newest_perturb;   /* pose perturbation of the newest frame's state (rad/m) */
-    float baseline;         /* camera travel per keyframe along x (m)              */
-} ldso_synth_params;
-
-/* Fills a synthetic window.  Output sizes:
- *   frames[N], dI[N*h*w*3], calib[4], frame_energy_th[N], point_host[P],
- *   point_data[P*LDSO_BA_POINT_STRIDE], point_res_begin[P+1], res_target[R], res_state[R],
- *   res_energy[R], res_flags[R] with R = P*(N-1).  Returns 0 on success. */
 int ldso_synth_fill(const ldso_synth_params *prm, ldso_ba_frame_state *frames, float *dI,
                     float *calib, float *frame_energy_th, int32_t *point_host, float *point_data,
                     int32_t *point_res_begin, int32_t *res_target, int8_t *res_state,

@@ -1,0 +1,28 @@
+"""The C++ host face (include/ldso_amd/energy_functional.h: FrameHessian, PointHessian,
+PointFrameResidual, EnergyFunctional with insert*/makeIDX/linearizeAll/solveSystemF/
+resubstituteF_MT) exercised by its own C++ test program, tests/cpp/test_energy_functional.cpp,
+against the oracle on the same synthetic window."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_energy_functional")
+
+
+def run(*args):
+    p = subprocess.run([BIN, *args], capture_output=True, text=True, timeout=600)
+    print(p.stdout[-4000:], p.stderr[-2000:])
+    return p
+
+
+def test_cpp_host_structure_and_errors(built):
+    p = run("--cpu")
+    assert p.returncode == 0 and "0 failure(s)" in p.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_host_gn_iterations_match_oracle(built):
+    p = run()
+    assert p.returncode == 0 and "0 failure(s)" in p.stdout
