@@ -242,13 +242,16 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              or after them (0)
  *   LDSO_BA_TUNE_TOP_CHUNK     residuals per k_linearize wavefront: 16, 32, 64, or 0 = automatic
  *                              (64 for large batches, shorter for a single window); set before
- *                              ldso_ba_load */
+ *                              ldso_ba_load
+ *   LDSO_BA_TUNE_TIMING_MASK   bit i: bracket kernel slot i with events when timing is enabled
+ *                              (default all; each event pair costs the stream a few us) */
 #define LDSO_BA_TUNE_LIN_VARIANT 1
 #define LDSO_BA_TUNE_TILED_IMAGES 2
 #define LDSO_BA_TUNE_LOAD3 3
 #define LDSO_BA_TUNE_XCD_REMAP 4
 #define LDSO_BA_TUNE_CENTRE_FIRST 5
 #define LDSO_BA_TUNE_TOP_CHUNK 6
+#define LDSO_BA_TUNE_TIMING_MASK 7
 int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);

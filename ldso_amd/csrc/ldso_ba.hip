@@ -1700,6 +1700,7 @@ struct ldso_ba_ctx {
     DevBuf<float> d_xad;
     size_t sc_smem_max = 0;
     bool timing = false;
+    unsigned timing_mask = ~0u;  // kernel slots bracketed by events when timing is on
     int lin_variant = 3;
     int top_chunk = 0;  // residuals per k_linearize wave (0 = automatic); LDSO_BA_TUNE_TOP_CHUNK
     int img_mode = 3;  // 0 row-major, 1 2x4 tiles, 2 quad records, 3 intensity only (LDSO_BA_TUNE_TILED_IMAGES)
@@ -1743,7 +1744,8 @@ void drain_events(ldso_ba_ctx *c) {
 template <typename F>
 int timed_launch(ldso_ba_ctx *c, int slot, F &&launch) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (c->timing) {
+    const bool timed = c->timing && ((c->timing_mask >> slot) & 1u);
+    if (timed) {
         a = get_event(c);
         b = get_event(c);
         (void)hipEventRecord(a, c->stream);
@@ -1751,7 +1753,7 @@ int timed_launch(ldso_ba_ctx *c, int slot, F &&launch) {
     launch();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(-2, std::string("launch ") + kKernelNames[slot] + ": " + hipGetErrorString(e));
-    if (c->timing) {
+    if (timed) {
         (void)hipEventRecord(b, c->stream);
         c->pending.push_back({slot, a, b});
     }
@@ -2689,6 +2691,10 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
         if (c->n_win) return fail(-1, "image layout must be chosen before ldso_ba_load");
         if (value < 0 || value > 3) return fail(-1, "image layout must be 0, 1, 2 or 3");
         c->img_mode = value;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_TIMING_MASK) {
+        c->timing_mask = (unsigned)value;
         return 0;
     }
     if (key == LDSO_BA_TUNE_TOP_CHUNK) {
