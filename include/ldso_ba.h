@@ -244,7 +244,10 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              (64 for large batches, shorter for a single window); set before
  *                              ldso_ba_load
  *   LDSO_BA_TUNE_TIMING_MASK   bit i: bracket kernel slot i with events when timing is enabled
- *                              (default all; each event pair costs the stream a few us) */
+ *                              (default all; each event pair costs the stream a few us)
+ *   LDSO_BA_TUNE_PIPELINE_GROUPS  window groups pipelined over two streams in a pass (one group's
+ *                              k_point_sc/k_stitch overlap the next group's k_linearize);
+ *                              0 = default 1 (measured: 2/4/8 groups are 15-60% slower) */
 #define LDSO_BA_TUNE_LIN_VARIANT 1
 #define LDSO_BA_TUNE_TILED_IMAGES 2
 #define LDSO_BA_TUNE_LOAD3 3
@@ -252,6 +255,7 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
 #define LDSO_BA_TUNE_CENTRE_FIRST 5
 #define LDSO_BA_TUNE_TOP_CHUNK 6
 #define LDSO_BA_TUNE_TIMING_MASK 7
+#define LDSO_BA_TUNE_PIPELINE_GROUPS 8
 int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);

@@ -103,7 +103,8 @@ struct LinParams {
     float4 *pt_rec;        // [slots][4]: JpJdF[8], Hcd_r[4], (Hdd_r, bd_r, active, 0)
     float *top_slab;       // [items][96]
     double *item_energy;   // [items][2]
-    int n_items;
+    int n_items;             // chunks of this launch: [item_base, item_base + n_items)
+    int item_base;
     int n_blocks;
     long long frame_stride;  // texels per tiled frame
     int tiles_per_row;       // 2-wide tiles per tile row
@@ -411,8 +412,8 @@ __global__ __launch_bounds__(256, kMinWavesPerSimd) void k_linearize(LinParams P
     // all chunks reading one target frame then run on one XCD and share its L2.
     const int nb = P.n_blocks, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
     const int lblock = kXcdRemap ? xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3) : (int)blockIdx.x;
-    const int item = lblock * 4 + wave;
-    if (item >= P.n_items) return;
+    if (lblock * 4 + wave >= P.n_items) return;
+    const int item = P.item_base + lblock * 4 + wave;  // global chunk index
     const int4 it = P.items[item];
     const WinDev &W = P.wins[it.w];
     const int N = W.N;
@@ -627,8 +628,8 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nb = P.n_blocks, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
     const int lblock = kXcdRemap ? xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3) : (int)blockIdx.x;
-    const int item = lblock * 4 + wave;
-    if (item >= P.n_items) return;
+    if (lblock * 4 + wave >= P.n_items) return;
+    const int item = P.item_base + lblock * 4 + wave;  // global chunk index
     const int4 it = P.items[item];
     const WinDev &W = P.wins[it.w];
     const int N = W.N;
@@ -960,11 +961,13 @@ struct PointParams {
     float *pt_out;                     // [P][12]
     float *sc_slab;
     int n_items;
+    int item_base;
 };
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
-    const int4 it = P.items[blockIdx.x];
+    const int item = P.item_base + blockIdx.x;
+    const int4 it = P.items[item];
     const WinDev &W = P.wins[it.w];
     const int host = it.z, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
     const int Kj = 8 * (W.N - 1);
@@ -1049,7 +1052,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     __syncthreads();
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
     const int cnt = it.y;
-    float *slab = P.sc_slab + W.sc_slab_base + (size_t)(blockIdx.x - W.sc_item_base) * ntiles * 16;
+    float *slab = P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16;
     for (int tile = tid; tile < ntiles; tile += blockDim.x) {
         int a = 0, rem = tile;
         while (rem >= nt - a) {
@@ -1114,6 +1117,7 @@ struct StitchParams {
     double *win_energy;
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
+    int pair_base;  // first global pair of this launch
 };
 
 __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row <= col
@@ -1285,7 +1289,7 @@ __device__ __forceinline__ double g_elem(const float *__restrict__ slab, int n_i
 
 __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     extern __shared__ double sm[];  // sized on the host for the largest window (stitch_smem_bytes)
-    const int pair = blockIdx.x;
+    const int pair = P.pair_base + blockIdx.x;
     const int w = P.pair_win[pair];
     const WinDev &W = P.wins[w];
     const int N = W.N, D = W.D, aidx = pair - W.pair_base, h = aidx % N, t = aidx / N;
@@ -1677,6 +1681,10 @@ struct PendingEv {
 struct ldso_ba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;  // second stream of the pipelined window groups
+    hipEvent_t ev_fork = nullptr, ev_lin0 = nullptr, ev_join = nullptr;
+    int groups_req = 0;             // LDSO_BA_TUNE_PIPELINE_GROUPS (0 = automatic)
+    int groups = 1;                 // pipelined window groups per pass
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
     std::vector<WinDev> wd;
@@ -1742,19 +1750,19 @@ void drain_events(ldso_ba_ctx *c) {
 }
 
 template <typename F>
-int timed_launch(ldso_ba_ctx *c, int slot, F &&launch) {
+int timed_launch(ldso_ba_ctx *c, int slot, hipStream_t st, F &&launch) {
     hipEvent_t a = nullptr, b = nullptr;
     const bool timed = c->timing && ((c->timing_mask >> slot) & 1u);
     if (timed) {
         a = get_event(c);
         b = get_event(c);
-        (void)hipEventRecord(a, c->stream);
+        (void)hipEventRecord(a, st);
     }
     launch();
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(-2, std::string("launch ") + kKernelNames[slot] + ": " + hipGetErrorString(e));
     if (timed) {
-        (void)hipEventRecord(b, c->stream);
+        (void)hipEventRecord(b, st);
         c->pending.push_back({slot, a, b});
     }
     return 0;
@@ -1903,7 +1911,13 @@ int ldso_ba_create(int32_t device, ldso_ba_ctx **out) {
     ldso_ba_ctx *c = new ldso_ba_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_lin0, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (c->stream2) (void)hipStreamDestroy(c->stream2);
         delete c;
         return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
@@ -1917,8 +1931,12 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     drain_events(c);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_fork, c->ev_lin0, c->ev_join})
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     c->d_wins.release();
     c->d_img.release();
     c->d_precalc.release();
@@ -1977,6 +1995,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     c->height = ws[0].height;
     c->npix = c->width * c->height;
     image_geometry(c);
+    c->groups = c->groups_req ? c->groups_req : 1;
     c->wh.assign(n_windows, WinHost());
     c->wd.assign(n_windows, WinDev());
     c->sys_host_valid = false;
@@ -2334,52 +2353,39 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     c->energy_valid = false;
     int rc;
     if (accumulate) HIP_TRY(hipMemsetAsync(c->d_sys.p, 0, c->d_sys.bytes(), c->stream));
-    if (c->n_top_items > 0) {
-        LinParams L;
-        L.items = c->d_top_items.p;
-        L.wins = c->d_wins.p;
-        L.img = c->d_img.p;
-        L.precalc = c->d_precalc.p;
-        L.frame_th = c->d_frame_th.p;
-        L.rs_point = c->d_rs_point.p;
-        L.rs_slot = c->d_rs_slot.p;
-        L.pt_data = c->d_pt_data.p;
-        L.rs_state = c->d_rs_state.p;
-        L.rs_newstate = c->d_rs_newstate.p;
-        L.rs_flags = c->d_rs_flags.p;
-        L.rs_energy = c->d_rs_energy.p;
-        L.rs_newenergy = c->d_rs_newenergy.p;
-        L.rs_energy_wo = c->d_rs_energy_wo.p;
-        L.rs_center = c->d_rs_center.p;
-        L.pt_rec = c->d_pt_rec.p;
-        L.top_slab = c->d_top_slab.p;
-        L.item_energy = c->d_item_energy.p;
-        L.n_items = c->n_top_items;
-        L.n_blocks = (c->n_top_items + 3) / 4;
-        L.frame_stride = c->frame_stride;
-        L.tiles_per_row = c->tiles_per_row;
-        L.fix = fix;
-        L.accumulate = accumulate;
-        const int nb = (c->n_top_items + 3) / 4;
-        rc = timed_launch(c, 0, [&] {
-            launch_linearize(c->lin_variant, c->img_mode, c->load3, c->xcd_remap, c->centre_first, nb, c->stream, L);
-        });
-        if (rc) return rc;
-    }
-    if (accumulate && c->n_sc_items > 0) {
-        PointParams Pp;
-        Pp.items = c->d_sc_items.p;
-        Pp.wins = c->d_wins.p;
-        Pp.pt_data = c->d_pt_data.p;
-        Pp.pt_nres = c->d_pt_nres.p;
-        Pp.pt_tgt = c->d_pt_tgt.p;
-        Pp.pt_rec = c->d_pt_rec.p;
-        Pp.pt_out = c->d_pt_out.p;
-        Pp.sc_slab = c->d_sc_slab.p;
-        Pp.n_items = c->n_sc_items;
-        rc = timed_launch(c, 1, [&] { k_point_sc<<<c->n_sc_items, kScThreads, c->sc_smem_max, c->stream>>>(Pp); });
-        if (rc) return rc;
-    }
+
+    LinParams L;
+    L.items = c->d_top_items.p;
+    L.wins = c->d_wins.p;
+    L.img = c->d_img.p;
+    L.precalc = c->d_precalc.p;
+    L.frame_th = c->d_frame_th.p;
+    L.rs_point = c->d_rs_point.p;
+    L.rs_slot = c->d_rs_slot.p;
+    L.pt_data = c->d_pt_data.p;
+    L.rs_state = c->d_rs_state.p;
+    L.rs_newstate = c->d_rs_newstate.p;
+    L.rs_flags = c->d_rs_flags.p;
+    L.rs_energy = c->d_rs_energy.p;
+    L.rs_newenergy = c->d_rs_newenergy.p;
+    L.rs_energy_wo = c->d_rs_energy_wo.p;
+    L.rs_center = c->d_rs_center.p;
+    L.pt_rec = c->d_pt_rec.p;
+    L.top_slab = c->d_top_slab.p;
+    L.item_energy = c->d_item_energy.p;
+    L.frame_stride = c->frame_stride;
+    L.tiles_per_row = c->tiles_per_row;
+    L.fix = fix;
+    L.accumulate = accumulate;
+    PointParams Pp;
+    Pp.items = c->d_sc_items.p;
+    Pp.wins = c->d_wins.p;
+    Pp.pt_data = c->d_pt_data.p;
+    Pp.pt_nres = c->d_pt_nres.p;
+    Pp.pt_tgt = c->d_pt_tgt.p;
+    Pp.pt_rec = c->d_pt_rec.p;
+    Pp.pt_out = c->d_pt_out.p;
+    Pp.sc_slab = c->d_sc_slab.p;
     StitchParams Sp;
     Sp.wins = c->d_wins.p;
     Sp.pair_win = c->d_pair_win.p;
@@ -2401,8 +2407,51 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         n_max = std::max(n_max, D.N);
     }
     const size_t st_smem = stitch_smem_bytes(kp_max, n_max, &Sp.th_cap);
-    rc = timed_launch(c, 2, [&] { k_stitch<<<c->n_pairs, kStThreads, st_smem, c->stream>>>(Sp); });
-    return rc;
+
+    // Window groups pipelined over two streams: group g runs its three kernels in order on
+    // stream g % 2, and stream 1 starts after group 0's k_linearize, so one group's k_point_sc
+    // and k_stitch (latency-bound, few waves) overlap the next group's k_linearize (HBM-bound).
+    const int G = std::max(1, std::min(c->groups, c->n_win));
+    if (G > 1) {
+        HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+    }
+    for (int g = 0; g < G; g++) {
+        const int w0 = (int)((long long)c->n_win * g / G), w1 = (int)((long long)c->n_win * (g + 1) / G);
+        const WinDev &A = c->wd[w0], &B = c->wd[w1 - 1];
+        hipStream_t st = (g & 1) ? c->stream2 : c->stream;
+        const int ti0 = A.top_item_base, ti1 = B.top_item_base + B.n_top_items;
+        const int si0 = A.sc_item_base, si1 = B.sc_item_base + B.n_sc_items;
+        const int p0 = A.pair_base, p1 = B.pair_base + B.N * B.N;
+        if (ti1 > ti0) {
+            L.item_base = ti0;
+            L.n_items = ti1 - ti0;
+            L.n_blocks = (L.n_items + 3) / 4;
+            rc = timed_launch(c, 0, st, [&] {
+                launch_linearize(c->lin_variant, c->img_mode, c->load3, c->xcd_remap, c->centre_first, L.n_blocks, st,
+                                 L);
+            });
+            if (rc) return rc;
+        }
+        if (G > 1 && g == 0) {  // stream 1 starts once group 0 is past its gather
+            HIP_TRY(hipEventRecord(c->ev_lin0, c->stream));
+            HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_lin0, 0));
+        }
+        if (accumulate && si1 > si0) {
+            Pp.item_base = si0;
+            Pp.n_items = si1 - si0;
+            rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
+            if (rc) return rc;
+        }
+        Sp.pair_base = p0;
+        rc = timed_launch(c, 2, st, [&] { k_stitch<<<p1 - p0, kStThreads, st_smem, st>>>(Sp); });
+        if (rc) return rc;
+    }
+    if (G > 1) {  // join: the context stream orders everything that follows
+        HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    }
+    return 0;
 }
 
 int ldso_ba_sync(ldso_ba_ctx *c) {
@@ -2607,7 +2656,7 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
         R.count = D.P;
         R.N = N;
         R.lambda = (float)lambda;
-        int rc = timed_launch(c, 3, [&] { k_resubstitute<<<(D.P + 255) / 256, 256, 0, c->stream>>>(R); });
+        int rc = timed_launch(c, 3, c->stream, [&] { k_resubstitute<<<(D.P + 255) / 256, 256, 0, c->stream>>>(R); });
         if (rc) return rc;
     }
     if (point_step_out) {
@@ -2671,7 +2720,7 @@ int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *c, const float *dev_buf, int32
     if (!c || !dev_buf || c->n_win == 0 || n_ranks < 1 || stride < 1) return fail(-1, "bad arguments");
     if ((int64_t)n_ranks * stride > INT32_MAX) return fail(-1, "too many candidates");
     HIP_TRY(hipSetDevice(c->device));
-    int rc = timed_launch(c, 4, [&] {
+    int rc = timed_launch(c, 4, c->stream, [&] {
         k_frame_th<<<c->n_win, kStThreads, 0, c->stream>>>(c->d_wins.p, dev_buf, n_ranks, c->n_win, (long long)stride,
                                                            c->d_frame_th.p);
     });
@@ -2691,6 +2740,12 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
         if (c->n_win) return fail(-1, "image layout must be chosen before ldso_ba_load");
         if (value < 0 || value > 3) return fail(-1, "image layout must be 0, 1, 2 or 3");
         c->img_mode = value;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_PIPELINE_GROUPS) {
+        if (value < 0 || value > 64) return fail(-1, "groups must be in [0, 64]");
+        c->groups_req = value;
+        c->groups = value ? value : 1;
         return 0;
     }
     if (key == LDSO_BA_TUNE_TIMING_MASK) {

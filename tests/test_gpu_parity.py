@@ -311,3 +311,20 @@ def test_chunk_sizes_agree(built, chunk):
     e_cpu, s_cpu = ow.iteration()
     compare_pass(c, ow, 0, e_cpu, s_cpu)
     c.close()
+
+
+@pytest.mark.parametrize("groups", [1, 2, 3])
+def test_pipelined_groups_agree(built, groups):
+    """Window groups pipelined over two streams give the same per-window results."""
+    cfgs = [dict(n_frames=4 + (i % 3), n_points=150 + 40 * i, seed=60 + i) for i in range(5)]
+    c = BAContext(0)
+    c.load([synth.make_window(**cf) for cf in cfgs])
+    c.set_tuning(8, groups)
+    c.linearize()
+    c.linearize()
+    for i, cf in enumerate(cfgs):
+        ow = oracle.OracleWindow(synth.make_window(**cf), threads=0)
+        ow.iteration()
+        e_cpu, s_cpu = ow.iteration()
+        compare_pass(c, ow, i, e_cpu, s_cpu)
+    c.close()
