@@ -285,31 +285,36 @@ int nullspaces(int N, const ldso_ba_frame_state *fr, double *out) {
 }
 
 namespace {
-// In-place LDL^T with symmetric diagonal pivoting (Eigen::LDLT's strategy), then solve.
+// In-place LDL^T with symmetric diagonal pivoting (Eigen::LDLT's strategy), then solve.  Only
+// the lower triangle is kept: a symmetric swap of k < p touches (k,j)<->(p,j) for j < k,
+// (i,k)<->(p,i) for k < i < p, (i,k)<->(i,p) for i > p and the two diagonals; every element
+// sees the same operations as with a full symmetric matrix.
 void ldlt_solve(int n, std::vector<double> &A, std::vector<double> &b) {
     std::vector<int> perm(n);
     std::vector<double> col(n, 0.0);
     for (int i = 0; i < n; i++) perm[i] = i;
-    auto at = [&](int r, int c) -> double & { return A[(size_t)r * n + c]; };
+    double *a = A.data();
+    auto at = [a, n](int r, int c) -> double & { return a[(size_t)r * n + c]; };
     for (int k = 0; k < n; k++) {
         int piv = k;
         for (int i = k + 1; i < n; i++)
             if (std::fabs(at(i, i)) > std::fabs(at(piv, piv))) piv = i;
         if (piv != k) {
             std::swap(perm[k], perm[piv]);
-            for (int j = 0; j < n; j++) std::swap(at(k, j), at(piv, j));
-            for (int j = 0; j < n; j++) std::swap(at(j, k), at(j, piv));
+            for (int j = 0; j < k; j++) std::swap(at(k, j), at(piv, j));
+            for (int i = k + 1; i < piv; i++) std::swap(at(i, k), at(piv, i));
+            for (int i = piv + 1; i < n; i++) std::swap(at(i, k), at(i, piv));
+            std::swap(at(k, k), at(piv, piv));
         }
         const double d = at(k, k);
         // trailing update with the unscaled column k: A(i,j) -= (A(i,k) / d) A(j,k), then L(i,k)
         for (int i = k + 1; i < n; i++) col[i] = at(i, k);
         for (int i = k + 1; i < n; i++) {
             const double l = d != 0 ? col[i] / d : 0.0;
-            for (int j = k + 1; j <= i; j++) at(i, j) -= l * col[j];
-            at(i, k) = l;
+            double *row = &at(i, 0);
+            for (int j = k + 1; j <= i; j++) row[j] -= l * col[j];
+            row[k] = l;
         }
-        for (int i = k + 1; i < n; i++)
-            for (int j = k + 1; j < i; j++) at(j, i) = at(i, j);
     }
     std::vector<double> y(n);
     for (int i = 0; i < n; i++) y[i] = b[perm[i]];

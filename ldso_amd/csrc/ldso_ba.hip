@@ -1717,8 +1717,14 @@ struct ldso_ba_ctx {
     std::vector<hipEvent_t> ev_pool;
     double kms[kNumKernels] = {0};
     long long kcount[kNumKernels] = {0};
-    std::vector<double> sys_host;  // last downloaded packed systems
-    bool sys_host_valid = false;
+    std::vector<double> sys_host;  // last downloaded packed systems (per window, see sys_valid)
+    std::vector<char> sys_valid;
+    bool sys_host_valid = false;   // false => every window's host copy is stale
+    // pinned staging for the per-iteration host round trips (system download, xAd upload,
+    // point-step download): async copies with one synchronisation each
+    double *pin_sys = nullptr;
+    float *pin_xad = nullptr, *pin_step = nullptr;
+    size_t pin_sys_n = 0, pin_step_n = 0;
     std::vector<double> energy_host;
     bool energy_valid = false;
 };
@@ -1937,6 +1943,9 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     for (hipEvent_t e : {c->ev_fork, c->ev_lin0, c->ev_join})
         if (e) (void)hipEventDestroy(e);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->pin_sys) (void)hipHostFree(c->pin_sys);
+    if (c->pin_xad) (void)hipHostFree(c->pin_xad);
+    if (c->pin_step) (void)hipHostFree(c->pin_step);
     c->d_wins.release();
     c->d_img.release();
     c->d_precalc.release();
@@ -2474,13 +2483,28 @@ int ldso_ba_get_energy(ldso_ba_ctx *c, int32_t win, double *out) {
     return 0;
 }
 
-static int fetch_sys(ldso_ba_ctx *c) {
-    if (c->sys_host_valid) return 0;
+// download one window's packed system (through pinned staging) unless the host copy is fresh
+static int fetch_sys(ldso_ba_ctx *c, int win) {
+    if (!c->sys_host_valid) {
+        c->sys_valid.assign(c->n_win, 0);
+        c->sys_host.resize(c->d_sys.n);
+        c->sys_host_valid = true;
+    }
+    if (c->sys_valid[win]) return 0;
+    const WinDev &D = c->wd[win];
+    const size_t n = (size_t)sys_len(D.D);
+    if (c->pin_sys_n < n) {
+        if (c->pin_sys) (void)hipHostFree(c->pin_sys);
+        c->pin_sys = nullptr;
+        HIP_TRY(hipHostMalloc(&c->pin_sys, n * sizeof(double), hipHostMallocDefault));
+        c->pin_sys_n = n;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(c->pin_sys, c->d_sys.p + D.sys_base, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     int rc = ldso_ba_sync(c);
     if (rc) return rc;
-    c->sys_host.resize(c->d_sys.n);
-    HIP_TRY(hipMemcpy(c->sys_host.data(), c->d_sys.p, c->d_sys.bytes(), hipMemcpyDeviceToHost));
-    c->sys_host_valid = true;
+    std::memcpy(c->sys_host.data() + D.sys_base, c->pin_sys, n * sizeof(double));
+    c->sys_valid[win] = 1;
     return 0;
 }
 
@@ -2493,7 +2517,7 @@ static void expand(const double *packed, int D, double *full) {
 int ldso_ba_get_system(ldso_ba_ctx *c, int32_t win, double *HA, double *bA, double *HL, double *bL, double *Hsc,
                        double *bsc) {
     if (!c || win < 0 || win >= c->n_win) return fail(-1, "bad arguments");
-    int rc = fetch_sys(c);
+    int rc = fetch_sys(c, win);
     if (rc) return rc;
     const WinDev &D = c->wd[win];
     const WinHost &H = c->wh[win];
@@ -2625,7 +2649,13 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
     const WinHost &H = c->wh[win];
     const int N = H.N;
     // xAd[N*h + t] = x_h^T adHostF[h + N t] + x_t^T adTargetF[h + N t] (EnergyFunctional.cc:624-632)
-    std::vector<float> xF(D.D), host((size_t)N * N * 8 + 4);
+    const size_t nx = (size_t)N * N * 8 + 4;
+    if (!c->pin_xad)
+        HIP_TRY(hipHostMalloc(&c->pin_xad, ((size_t)LDSO_BA_MAX_FRAMES * LDSO_BA_MAX_FRAMES * 8 + 4) * sizeof(float),
+                              hipHostMallocDefault));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // a previous upload from pin_xad has completed
+    std::vector<float> xF(D.D);
+    float *host = c->pin_xad;
     for (int i = 0; i < D.D; i++) xF[i] = (float)x[i];
     for (int h = 0; h < N; h++)
         for (int t = 0; t < N; t++) {
@@ -2638,7 +2668,7 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
             }
         }
     for (int i = 0; i < 4; i++) host[(size_t)N * N * 8 + i] = xF[i];
-    HIP_TRY(hipMemcpyAsync(c->d_xad.p, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_xad.p, host, nx * sizeof(float), hipMemcpyHostToDevice, c->stream));
     if (D.P > 0) {
         ResubParams R;
         R.xad = c->d_xad.p;
@@ -2660,12 +2690,18 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
         if (rc) return rc;
     }
     if (point_step_out) {
+        if (c->pin_step_n < (size_t)D.P) {
+            if (c->pin_step) (void)hipHostFree(c->pin_step);
+            c->pin_step = nullptr;
+            HIP_TRY(hipHostMalloc(&c->pin_step, std::max<size_t>(1, D.P) * sizeof(float), hipHostMallocDefault));
+            c->pin_step_n = D.P;
+        }
+        if (D.P)
+            HIP_TRY(hipMemcpyAsync(c->pin_step, c->d_pt_step.p + D.point_base, D.P * sizeof(float),
+                                   hipMemcpyDeviceToHost, c->stream));
         int rc = ldso_ba_sync(c);
         if (rc) return rc;
-        std::vector<float> st(D.P);
-        if (D.P)
-            HIP_TRY(hipMemcpy(st.data(), c->d_pt_step.p + D.point_base, D.P * sizeof(float), hipMemcpyDeviceToHost));
-        for (int q = 0; q < D.P; q++) point_step_out[H.pt_orig[q]] = st[q];
+        for (int q = 0; q < D.P; q++) point_step_out[H.pt_orig[q]] = c->pin_step[q];
     }
     return 0;
 }
