@@ -1060,20 +1060,36 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
             a++;
         }
         const int bb = a + rem;
-        float acc[16];
+        // G += U^T diag(HdiF) U on 4x4 tiles: 16 products per point as 8 packed FMAs on
+        // diagonal pairs (after 2 packed weight multiplies), e.g. {acc00, acc11} +=
+        // {ua.x, ua.y} * {ub.x, ub.y} and {acc01, acc10} += {ua.x, ua.y} * {ub.y, ub.x}: both
+        // operands are natural register pairs (or a swapped one), so no broadcast moves
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 c[8];
 #pragma unroll
-        for (int i = 0; i < 16; i++) acc[i] = 0;
-        for (int p = 0; p < cnt; p++) {
-            const float wgt = Wt[p];
-            const float4 ua = *(const float4 *)(U + p * KP + 4 * a);
-            const float4 ub = *(const float4 *)(U + p * KP + 4 * bb);
-            const float wa[4] = {wgt * ua.x, wgt * ua.y, wgt * ua.z, wgt * ua.w};
-            const float ubv[4] = {ub.x, ub.y, ub.z, ub.w};
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) acc[i * 4 + j] += wa[i] * ubv[j];
+        for (int i = 0; i < 8; i++) c[i] = f2{0.f, 0.f};
+        const float *pa = U + 4 * a, *pb = U + 4 * bb;
+#pragma unroll 4
+        for (int p = 0; p < cnt; p++, pa += KP, pb += KP) {
+            const float w = Wt[p];
+            const float4 ua = *(const float4 *)pa;
+            const float4 ub = *(const float4 *)pb;
+            const f2 a01 = f2{ua.x, ua.y} * w, a23 = f2{ua.z, ua.w} * w;
+            const f2 b01 = {ub.x, ub.y}, b10 = {ub.y, ub.x}, b23 = {ub.z, ub.w}, b32 = {ub.w, ub.z};
+            c[0] += a01 * b01;  // (0,0) (1,1)
+            c[1] += a01 * b10;  // (0,1) (1,0)
+            c[2] += a01 * b23;  // (0,2) (1,3)
+            c[3] += a01 * b32;  // (0,3) (1,2)
+            c[4] += a23 * b01;  // (2,0) (3,1)
+            c[5] += a23 * b10;  // (2,1) (3,0)
+            c[6] += a23 * b23;  // (2,2) (3,3)
+            c[7] += a23 * b32;  // (2,3) (3,2)
         }
+        float acc[16];
+        acc[0] = c[0].x, acc[5] = c[0].y, acc[1] = c[1].x, acc[4] = c[1].y;
+        acc[2] = c[2].x, acc[7] = c[2].y, acc[3] = c[3].x, acc[6] = c[3].y;
+        acc[8] = c[4].x, acc[13] = c[4].y, acc[9] = c[5].x, acc[12] = c[5].y;
+        acc[10] = c[6].x, acc[15] = c[6].y, acc[11] = c[7].x, acc[14] = c[7].y;
         float4 *o = (float4 *)(slab + (size_t)tile * 16);
         o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
         o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
