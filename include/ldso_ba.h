@@ -225,6 +225,22 @@ int ldso_ba_newest_stride(ldso_ba_ctx *ctx, int64_t *stride);
 int ldso_ba_export_newest(ldso_ba_ctx *ctx, float *dev_buf, int64_t stride);
 int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *ctx, const float *dev_buf, int32_t n_ranks, int64_t stride);
 
+/* Device-side solve and resubstitution, every loaded window at once:
+ *   solve_device         EnergyFunctional::solveSystemF on the GPU, one wavefront per window,
+ *                        statement for statement ldso_ba_solve (bit-identical x); windows of up to
+ *                        11 keyframes.  ns: every window's [n_null][8N+4] nullspaces back to back
+ *                        (used at iteration >= 2), x_out: every window's x back to back (or NULL:
+ *                        x stays on the device for resubstitute_device).
+ *   resubstitute_device  resubstituteF_MT from the device x; point_step_out (or NULL): every
+ *                        window's points back to back, each in its caller order.
+ *   iterate              linearize(fix=0, accumulate=1) + solve_device + resubstitute_device with
+ *                        one synchronisation; energy_out: [n_windows][3] as ldso_ba_get_energy. */
+int ldso_ba_solve_device(ldso_ba_ctx *ctx, int32_t iteration, double lambda, const double *ns, int32_t n_null,
+                         double *x_out);
+int ldso_ba_resubstitute_device(ldso_ba_ctx *ctx, double lambda, float *point_step_out);
+int ldso_ba_iterate(ldso_ba_ctx *ctx, int32_t iteration, double lambda, const double *ns, int32_t n_null,
+                    double *x_out, float *point_step_out, double *energy_out);
+
 /* Per-kernel HIP-event timing (bench/profiling).  When enabled every kernel launch of
  * ldso_ba_linearize is bracketed by events; get returns summed ms and launch counts for
  * n_kernels <= 16 slots in the order of ldso_ba_kernel_name(i). */

@@ -105,6 +105,9 @@ ABI = [
     ("ldso_ba_get_frame_energy_th", C.c_int, [C.c_void_p, C.c_int32, f32p]),
     ("ldso_ba_solve", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_double, f64p, C.c_int32, f64p]),
     ("ldso_ba_resubstitute", C.c_int, [C.c_void_p, C.c_int32, f64p, C.c_double, f32p]),
+    ("ldso_ba_solve_device", C.c_int, [C.c_void_p, C.c_int32, C.c_double, f64p, C.c_int32, f64p]),
+    ("ldso_ba_resubstitute_device", C.c_int, [C.c_void_p, C.c_double, f32p]),
+    ("ldso_ba_iterate", C.c_int, [C.c_void_p, C.c_int32, C.c_double, f64p, C.c_int32, f64p, f32p, f64p]),
     ("ldso_ba_packed_system", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), i64p, i64p]),
     ("ldso_ba_unpack_system", C.c_int, [C.c_void_p]),
     ("ldso_ba_copy_packed", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]),

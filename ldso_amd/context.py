@@ -116,6 +116,46 @@ class BAContext:
         L.check(self._lib.ldso_ba_resubstitute(self._h, int(win), L.ptr(x, L.f64p), float(lam), L.ptr(step, L.f32p)))
         return step
 
+    # ---- device-side solve ---------------------------------------------
+    def _ns_all(self, nullspaces):
+        if nullspaces is None:
+            return None
+        return np.ascontiguousarray(np.concatenate([np.asarray(n, np.float64).ravel() for n in nullspaces]))
+
+    def _split(self, flat, sizes):
+        out, o = [], 0
+        for n in sizes:
+            out.append(flat[o:o + n])
+            o += n
+        return out
+
+    def solve_device(self, iteration: int = 0, lam: float = 1e-5, nullspaces=None):
+        """x of every window (solveSystemF on the GPU); nullspaces: list of [7][8N+4] arrays."""
+        ns = self._ns_all(nullspaces)
+        x = np.zeros(sum(w.dim for w in self.windows), np.float64)
+        L.check(self._lib.ldso_ba_solve_device(self._h, int(iteration), float(lam), L.ptr(ns, L.f64p),
+                                               0 if ns is None else 7, L.ptr(x, L.f64p)))
+        return self._split(x, [w.dim for w in self.windows])
+
+    def resubstitute_device(self, lam: float = 1e-5):
+        """Point steps of every window from the device x (caller point order per window)."""
+        st = np.zeros(sum(w.n_points for w in self.windows), np.float32)
+        L.check(self._lib.ldso_ba_resubstitute_device(self._h, float(lam), L.ptr(st, L.f32p)))
+        return self._split(st, [w.n_points for w in self.windows])
+
+    def iterate(self, iteration: int = 0, lam: float = 1e-5, nullspaces=None, fetch_steps: bool = True):
+        """One fused GN iteration on the device: pass + solve + resubstitute, one synchronisation."""
+        ns = self._ns_all(nullspaces)
+        x = np.zeros(sum(w.dim for w in self.windows), np.float64)
+        st = np.zeros(sum(w.n_points for w in self.windows), np.float32) if fetch_steps else None
+        e = np.zeros((len(self.windows), 3), np.float64)
+        L.check(self._lib.ldso_ba_iterate(self._h, int(iteration), float(lam), L.ptr(ns, L.f64p),
+                                          0 if ns is None else 7, L.ptr(x, L.f64p), L.ptr(st, L.f32p),
+                                          L.ptr(e, L.f64p)))
+        xs = self._split(x, [w.dim for w in self.windows])
+        sts = self._split(st, [w.n_points for w in self.windows]) if fetch_steps else None
+        return e, xs, sts
+
     # ---- multi-GPU / profiling -----------------------------------------------------------
     def packed_system(self):
         p = C.c_void_p()

@@ -321,8 +321,9 @@ void ldlt_solve(int n, std::vector<double> &A, std::vector<double> &b) {
     for (int i = 0; i < n; i++)
         for (int j = 0; j < i; j++) y[i] -= at(i, j) * y[j];
     for (int i = 0; i < n; i++) y[i] = at(i, i) != 0 ? y[i] / at(i, i) : 0.0;
-    for (int i = n - 1; i >= 0; i--)
-        for (int j = i + 1; j < n; j++) y[i] -= at(j, i) * y[j];
+    // back substitution column by column (j descending), the order k_solve uses on the GPU
+    for (int j = n - 1; j >= 0; j--)
+        for (int i = 0; i < j; i++) y[i] -= at(j, i) * y[j];
     for (int i = 0; i < n; i++) b[perm[i]] = y[i];
 }
 

@@ -48,8 +48,9 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kTopVals = 96;    // 55 + 30 + 6 AccumulatorApprox entries, padded to 96
 constexpr int kMaxRes = LDSO_BA_MAX_FRAMES - 1;
-constexpr int kNumKernels = 5;
-const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch", "k_resubstitute", "k_frame_th"};
+constexpr int kNumKernels = 6;
+const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch", "k_resubstitute", "k_frame_th",
+                                         "k_solve"};
 
 thread_local std::string g_err;
 int fail(int code, const std::string &msg) {
@@ -73,6 +74,7 @@ struct WinDev {
     long long sys_base;      // doubles: packed system
     int newest_begin, newest_end;
     int rec_base;            // record slots: rec_base + s * P + q (s = target slot of host's point q)
+    int vec_base;            // per-window (8N+4)-vectors (priors, x): vec_base + i
     int width, height;
     float wM3, hM3;
     float calib[4];
@@ -1473,6 +1475,217 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 }
 
 // ============================================================================================
+// k_solve: EnergyFunctional::solveSystemF on the GPU, one wavefront per window.
+// Statement for statement the host solver (host_math.cpp solve_system: assembly with the
+// FIX_LAMBDA damping, Jacobi scaling, lower-triangle LDL^T with diagonal pivoting, column
+// substitutions, orthogonalize); each lane owns the matrix rows i = lane (mod 64) and every
+// element sees the host's operations in the host's order, so x is bit-identical to
+// ldso_ba_solve's.  H lives in LDS (n <= kSolveMaxDim).
+// ============================================================================================
+constexpr int kSolveMaxDim = 8 * 11 + 4;  // windows up to 11 keyframes (68 KB of LDS for H)
+struct SolveParams {
+    const WinDev *__restrict__ wins;
+    const double *__restrict__ sys;
+    const double *__restrict__ prior;  // [vec][2]: HL diagonal, bL
+    const double *__restrict__ ns;     // [win][7][n] nullspaces (iteration >= 2)
+    double *x;                         // [vec]
+    int iteration, n_null;
+};
+size_t solve_smem_bytes(int n) { return ((size_t)n * n + 7 * (size_t)n + 8 * (size_t)n + 7 * 7 * 3 + 64) * sizeof(double); }
+
+__global__ __launch_bounds__(64) void k_solve(SolveParams P) {
+#pragma clang fp contract(off)
+    extern __shared__ double lds[];
+    const WinDev &W = P.wins[blockIdx.x];
+    const int n = W.D, lane = threadIdx.x;
+    const long long pl = packed_len(n);
+    const double *HA = P.sys + W.sys_base, *bA = HA + pl, *Hs = HA + pl + n, *bs = HA + 2 * pl + n;
+    double *H = lds;                  // [n][n] row-major, as the host's std::vector
+    double *b = H + (size_t)n * n;    // [n]
+    double *sc = b + n, *y = sc + n, *col = y + n;
+    double *Nm = col + n;             // [n][7]
+    double *G = Nm + 7 * (size_t)n, *V = G + 49, *misc = V + 49;  // misc: ntx[7], coef[7]
+    int *perm = reinterpret_cast<int *>(misc + 16);
+    const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
+    auto at = [&](int r, int c) -> double & { return H[(size_t)r * n + c]; };
+    // ---- assembly (EnergyFunctional.cc:342-378), upper triangle then mirrored
+    for (int i = lane; i < n; i += 64) {
+        const double hl = P.prior[2 * (W.vec_base + i)], bl = P.prior[2 * (W.vec_base + i) + 1];
+        for (int j = i; j < n; j++) at(i, j) = ((i == j ? hl : 0.0) + 0.0) + HA[pk_index(i, j, n)];
+        b[i] = ((bl + 0.0) + bA[i]) - bs[i] / (1 + lambda);
+    }
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) at(i, i) *= (1 + lambda);
+    const double scl = 1.0f / (1 + lambda);
+    for (int i = lane; i < n; i += 64)
+        for (int j = i; j < n; j++) at(i, j) -= Hs[pk_index(i, j, n)] * scl;
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64)
+        for (int j = 0; j < i; j++) at(i, j) = at(j, i);
+    for (int i = lane; i < n; i += 64) sc[i] = 1.0 / sqrt(at(i, i) + 10);
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) {
+        b[i] *= sc[i];
+        for (int j = 0; j < n; j++) at(i, j) *= sc[i] * sc[j];
+        perm[i] = i;
+    }
+    wave_lds_sync();
+    // ---- LDL^T with symmetric diagonal pivoting (lower triangle)
+    for (int k = 0; k < n; k++) {
+        double best = -1.0;
+        int bi = n;
+        for (int i = k + lane; i < n; i += 64) {  // first index of the largest |diag|
+            const double v = fabs(at(i, i));
+            if (v > best) {
+                best = v;
+                bi = i;
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const double ob = __shfl_xor(best, m, kWave);
+            const int oi = __shfl_xor(bi, m, kWave);
+            if (ob > best || (ob == best && oi < bi)) {
+                best = ob;
+                bi = oi;
+            }
+        }
+        const int piv = bi;
+        if (piv != k) {
+            for (int j = lane; j < k; j += 64) {
+                const double t = at(k, j);
+                at(k, j) = at(piv, j);
+                at(piv, j) = t;
+            }
+            for (int i = k + 1 + lane; i < piv; i += 64) {
+                const double t = at(i, k);
+                at(i, k) = at(piv, i);
+                at(piv, i) = t;
+            }
+            for (int i = piv + 1 + lane; i < n; i += 64) {
+                const double t = at(i, k);
+                at(i, k) = at(i, piv);
+                at(i, piv) = t;
+            }
+            if (lane == 0) {
+                const double t = at(k, k);
+                at(k, k) = at(piv, piv);
+                at(piv, piv) = t;
+                const int pt = perm[k];
+                perm[k] = perm[piv];
+                perm[piv] = pt;
+            }
+        }
+        wave_lds_sync();
+        const double d = at(k, k);
+        for (int i = k + 1 + lane; i < n; i += 64) col[i] = at(i, k);
+        wave_lds_sync();
+        for (int i = k + 1 + lane; i < n; i += 64) {
+            const double l = d != 0 ? col[i] / d : 0.0;
+            double *row = &at(i, 0);
+            for (int j = k + 1; j <= i; j++) row[j] -= l * col[j];
+            row[k] = l;
+        }
+        wave_lds_sync();
+    }
+    // ---- substitutions (column by column, as the host)
+    for (int i = lane; i < n; i += 64) y[i] = b[perm[i]];
+    wave_lds_sync();
+    for (int j = 0; j < n; j++) {
+        const double yj = y[j];
+        for (int i = j + 1 + lane; i < n; i += 64) y[i] -= at(i, j) * yj;
+        wave_lds_sync();
+    }
+    for (int i = lane; i < n; i += 64) y[i] = at(i, i) != 0 ? y[i] / at(i, i) : 0.0;
+    wave_lds_sync();
+    for (int j = n - 1; j >= 0; j--) {
+        const double yj = y[j];
+        for (int i = lane; i < j; i += 64) y[i] -= at(j, i) * yj;
+        wave_lds_sync();
+    }
+    for (int i = lane; i < n; i += 64) b[perm[i]] = y[i];
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) y[i] = sc[i] * b[i];  // x
+    wave_lds_sync();
+    // ---- orthogonalize (EnergyFunctional.cc:809-841), iteration >= 2
+    const int kk = P.n_null;
+    if (P.iteration >= 2 && kk > 0) {
+        const double *ns = P.ns + (size_t)7 * W.vec_base;
+        if (lane < kk) {
+            double s2 = 0;
+            for (int i = 0; i < n; i++) s2 += ns[(size_t)lane * n + i] * ns[(size_t)lane * n + i];
+            s2 = sqrt(s2);
+            for (int i = 0; i < n; i++) Nm[(size_t)i * kk + lane] = ns[(size_t)lane * n + i] / s2;
+        }
+        wave_lds_sync();
+        if (lane < kk * kk) {
+            const int a = lane / kk, c = lane % kk;
+            double g = 0.0;
+            for (int i = 0; i < n; i++) g += Nm[(size_t)i * kk + a] * Nm[(size_t)i * kk + c];
+            G[lane] = g;
+            V[lane] = a == c ? 1.0 : 0.0;
+        }
+        double *ntx = misc, *coef = misc + 8;
+        if (lane < kk) {
+            double t = 0.0;
+            for (int i = 0; i < n; i++) t += Nm[(size_t)i * kk + lane] * y[i];
+            ntx[lane] = t;
+            coef[lane] = 0.0;
+        }
+        wave_lds_sync();
+        if (lane == 0) {  // cyclic Jacobi on the k x k Gram matrix, as the host
+            const int k = kk;
+            for (int sweep = 0; sweep < 64; sweep++) {
+                double off = 0;
+                for (int p = 0; p < k; p++)
+                    for (int q = p + 1; q < k; q++) off += G[p * k + q] * G[p * k + q];
+                if (off < 1e-30) break;
+                for (int p = 0; p < k; p++)
+                    for (int q = p + 1; q < k; q++) {
+                        const double apq = G[p * k + q];
+                        if (apq == 0) continue;
+                        const double th = (G[q * k + q] - G[p * k + p]) / (2 * apq);
+                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+                        const double c = 1 / sqrt(t * t + 1), s = t * c;
+                        for (int r = 0; r < k; r++) {
+                            const double gp = G[r * k + p], gq = G[r * k + q];
+                            G[r * k + p] = c * gp - s * gq;
+                            G[r * k + q] = s * gp + c * gq;
+                        }
+                        for (int r = 0; r < k; r++) {
+                            const double gp = G[p * k + r], gq = G[q * k + r];
+                            G[p * k + r] = c * gp - s * gq;
+                            G[q * k + r] = s * gp + c * gq;
+                        }
+                        for (int r = 0; r < k; r++) {
+                            const double vp = V[r * k + p], vq = V[r * k + q];
+                            V[r * k + p] = c * vp - s * vq;
+                            V[r * k + q] = s * vp + c * vq;
+                        }
+                    }
+            }
+            double smax = 0;
+            for (int e = 0; e < k; e++) smax = fmax(smax, sqrt(fmax(0.0, G[e * k + e])));
+            for (int e = 0; e < k; e++) {
+                const double ev = G[e * k + e];
+                if (!(sqrt(fmax(0.0, ev)) > kSolverModeDelta * smax)) continue;
+                double proj = 0;
+                for (int a = 0; a < k; a++) proj += V[a * k + e] * ntx[a];
+                for (int a = 0; a < k; a++) coef[a] += V[a * k + e] * proj / ev;
+            }
+        }
+        wave_lds_sync();
+        for (int i = lane; i < n; i += 64) {
+            double t = 0;
+            for (int a = 0; a < kk; a++) t += Nm[(size_t)i * kk + a] * coef[a];
+            y[i] -= t;
+        }
+        wave_lds_sync();
+    }
+    for (int i = lane; i < n; i += 64) P.x[W.vec_base + i] = y[i];
+}
+
+// ============================================================================================
 // k_resubstitute: EnergyFunctional::resubstituteFPt (EnergyFunctional.cc:638-667)
 // ============================================================================================
 // ---- sharded setNewFrameEnergyTH ---------------------------------------
@@ -1503,19 +1716,41 @@ __global__ __launch_bounds__(kStThreads) void k_frame_th(const WinDev *__restric
         (int)n_cand, keys, kThMaxLds, frame_th + W.frame_base + W.N - 1);
 }
 
+constexpr int kXadStride = LDSO_BA_MAX_FRAMES * LDSO_BA_MAX_FRAMES * 8 + 4;  // floats per window
 struct ResubParams {
-    const float *__restrict__ xad;   // [N*N][8] for this window (index h*N + t)
-    const float *__restrict__ xc;    // [4]
+    const float *__restrict__ xad;   // [win][kXadStride]: xAd[h*N + t][8], then x_c[4]
+    const WinDev *__restrict__ wins;
+    const int *__restrict__ pt_win;
     const int *__restrict__ pt_nres;
     const unsigned long long *__restrict__ pt_tgt;
     const float4 *__restrict__ pt_rec;
-    int rec_base, P, point_base;
     const float *__restrict__ pt_out;
     const int *__restrict__ pt_host;
     float *pt_step;
-    int begin, count, N;
+    int begin, count;
     float lambda;
 };
+
+// xAd[N*h + t] = x_h^T adHostF[h + N t] + x_t^T adTargetF[h + N t] in float (EnergyFunctional.cc:
+// 624-632), from the device solution; same statements as the host path of ldso_ba_resubstitute
+__global__ __launch_bounds__(256) void k_xad(const WinDev *__restrict__ wins, const double *__restrict__ x,
+                                             const double *__restrict__ adH, const double *__restrict__ adT,
+                                             float *xad) {
+#pragma clang fp contract(off)
+    const WinDev &W = wins[blockIdx.x];
+    const int N = W.N;
+    const double *xw = x + W.vec_base;
+    float *o = xad + (size_t)blockIdx.x * kXadStride;
+    for (int e = threadIdx.x; e < N * N * 8; e += blockDim.x) {
+        const int cc = e & 7, ht = e >> 3, h = ht / N, t = ht % N;
+        const double *AH = adH + (size_t)(W.pair_base + h + N * t) * 64, *AT = adT + (size_t)(W.pair_base + h + N * t) * 64;
+        float s1 = 0, s2 = 0;
+        for (int k = 0; k < 8; k++) s1 += (float)xw[4 + 8 * h + k] * (float)AH[k * 8 + cc];
+        for (int k = 0; k < 8; k++) s2 += (float)xw[4 + 8 * t + k] * (float)AT[k * 8 + cc];
+        o[(size_t)(N * h + t) * 8 + cc] = s1 + s2;
+    }
+    if (threadIdx.x < 4) o[(size_t)N * N * 8 + threadIdx.x] = (float)xw[threadIdx.x];
+}
 
 __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
 #pragma clang fp contract(off)
@@ -1527,17 +1762,21 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
         P.pt_step[p] = 0;
         return;
     }
+    const int w = P.pt_win[p];
+    const WinDev &W = P.wins[w];
+    const int N = W.N;
+    const float *xad = P.xad + (size_t)w * kXadStride, *xc = xad + (size_t)N * N * 8;
     float b = po[1];
-    const float d = P.xc[0] * po[5] + P.xc[1] * po[6] + P.xc[2] * po[7] + P.xc[3] * po[8];
+    const float d = xc[0] * po[5] + xc[1] * po[6] + xc[2] * po[7] + xc[3] * po[8];
     b -= d;
     const int h = P.pt_host[p];
     const unsigned long long tgs = P.pt_tgt[p];
-    const float4 *rp = P.pt_rec + ((size_t)P.rec_base + (p - P.point_base)) * 4;
+    const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * 4;
     for (int q = 0; q < P.pt_nres[p]; q++) {
         const int tg = (int)((tgs >> (4 * q)) & 15ull);
-        const float4 *rq = rp + (size_t)(tg < h ? tg : tg - 1) * P.P * 4;
+        const float4 *rq = rp + (size_t)(tg < h ? tg : tg - 1) * W.P * 4;
         if (rq[3].z == 0.0f) continue;  // not active
-        const float *xa = P.xad + (size_t)(h * P.N + tg) * 8;
+        const float *xa = xad + (size_t)(h * N + tg) * 8;
         const float4 j0 = rq[0], j1 = rq[1];
         const float dd = xa[0] * j0.x + xa[1] * j0.y + xa[2] * j0.z + xa[3] * j0.w + xa[4] * j1.x + xa[5] * j1.y +
                          xa[6] * j1.z + xa[7] * j1.w;
@@ -1721,7 +1960,10 @@ struct ldso_ba_ctx {
     DevBuf<int2> d_pair_items, d_host_items;
     DevBuf<float> d_top_slab, d_sc_slab;
     DevBuf<double> d_item_energy, d_sys, d_win_energy;
-    DevBuf<float> d_xad;
+    DevBuf<float> d_xad;            // [win][kXadStride]
+    DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
+    DevBuf<int> d_pt_win;
+    int vec_total = 0;
     size_t sc_smem_max = 0;
     bool timing = false;
     unsigned timing_mask = ~0u;  // kernel slots bracketed by events when timing is on
@@ -1870,6 +2112,47 @@ int stage_images(ldso_ba_ctx *c, const ldso_ba_window *ws, int n_windows, int *m
     (void)hipFree(flag);
     if (e != hipSuccess) return fail(-2, std::string("image staging: ") + hipGetErrorString(e));
     return 0;
+}
+
+// HL diagonal and bL of one window (the priors accumulateLF_MT stitches, AccumulatedTopHessian.cc:
+// 241-250) as the device solver reads them; zero on ranks other than 0 of a sharded window
+int upload_priors(ldso_ba_ctx *c, int win) {
+    const WinHost &H = c->wh[win];
+    const WinDev &D = c->wd[win];
+    std::vector<double> pr((size_t)2 * D.D, 0.0);
+    if (H.add_priors) {
+        for (int i = 0; i < 4; i++) {
+            pr[2 * i] = H.c_prior[i];
+            pr[2 * i + 1] = H.c_prior[i] * (double)H.c_delta[i];
+        }
+        for (int f = 0; f < H.N; f++)
+            for (int i = 0; i < 8; i++) {
+                const int q = 4 + 8 * f + i;
+                pr[2 * q] = H.frame_prior[8 * f + i];
+                pr[2 * q + 1] = H.frame_prior[8 * f + i] * H.frame_delta_prior[8 * f + i];
+            }
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_prior.p + (size_t)2 * D.vec_base, pr.data(), pr.size() * sizeof(double),
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int launch_resubstitute(ldso_ba_ctx *c, int begin, int count, double lambda) {
+    ResubParams R;
+    R.xad = c->d_xad.p;
+    R.wins = c->d_wins.p;
+    R.pt_win = c->d_pt_win.p;
+    R.pt_nres = c->d_pt_nres.p;
+    R.pt_tgt = c->d_pt_tgt.p;
+    R.pt_rec = c->d_pt_rec.p;
+    R.pt_out = c->d_pt_out.p;
+    R.pt_host = c->d_pt_host.p;
+    R.pt_step = c->d_pt_step.p;
+    R.begin = begin;
+    R.count = count;
+    R.lambda = (float)lambda;
+    return timed_launch(c, 3, c->stream, [&] { k_resubstitute<<<(count + 255) / 256, 256, 0, c->stream>>>(R); });
 }
 // k_stitch dynamic LDS: max of the Top phase, the SC phase of the largest window, and the
 // frame-threshold staging (at least 1024 candidates; more if the SC phase leaves room)
@@ -2037,6 +2320,8 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     std::vector<float> rs_energy, pt_data, precalc, frame_th;
     std::vector<double> adH, adT;
     long long sc_slab_total = 0, sys_total = 0;
+    int vec_total = 0;
+    std::vector<int> pt_win;
     // residuals per k_linearize wave: 64 when the grid is large anyway; small workloads (one
     // window) use shorter chunks so more waves start at once (latency, not throughput, bound)
     long long r_est = 0;
@@ -2183,6 +2468,9 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         D.newest_begin = res_base + bucket_start[N * (N - 1)];
         D.newest_end = res_base + bucket_start[N * N];
         D.rec_base = rec_base;
+        D.vec_base = vec_total;
+        vec_total += D.D;
+        pt_win.insert(pt_win.end(), P, w);
         // frame-level inputs
         precalc.insert(precalc.end(), in.precalc, in.precalc + (size_t)N * N * LDSO_BA_PRECALC_STRIDE);
         adH.insert(adH.end(), in.ad_host, in.ad_host + (size_t)N * N * 64);
@@ -2201,6 +2489,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     c->max_frames = 0;
     for (int w = 0; w < n_windows; w++) c->max_frames = std::max(c->max_frames, ws[w].n_frames);
     c->P_tot = point_base;
+    c->vec_total = vec_total;
     c->R_tot = res_base;
     c->sc_smem_max = smem_max;
 
@@ -2244,7 +2533,11 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     ALLOC(c->d_item_energy, std::max<size_t>(1, top_items.size() * 2));
     ALLOC(c->d_sys, (size_t)sys_total);
     ALLOC(c->d_win_energy, (size_t)n_windows * 2);
-    ALLOC(c->d_xad, (size_t)LDSO_BA_MAX_FRAMES * LDSO_BA_MAX_FRAMES * 8 + 4);
+    ALLOC(c->d_xad, (size_t)n_windows * kXadStride);
+    ALLOC(c->d_prior, (size_t)2 * vec_total);
+    ALLOC(c->d_x, (size_t)vec_total);
+    ALLOC(c->d_ns, (size_t)7 * vec_total);
+    ALLOC(c->d_pt_win, std::max<size_t>(1, pt_win.size()));
 #undef ALLOC
     auto up = [&](void *dst, const void *src, size_t bytes) -> int {
         if (bytes == 0) return 0;
@@ -2267,6 +2560,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     UP(c->d_pt_nres, pt_nres);
     UP(c->d_rs_slot, rs_slot);
     UP(c->d_pt_tgt, pt_tgt);
+    UP(c->d_pt_win, pt_win);
     UP(c->d_pair_win, pair_win);
     UP(c->d_frame_win, frame_win);
     UP(c->d_rs_tgt, rs_tgt);
@@ -2311,6 +2605,10 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         HIP_TRY(hipFuncSetAttribute((const void *)k_point_sc, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)c->sc_smem_max));
     }
+    for (int w = 0; w < n_windows; w++) {
+        rc = upload_priors(c, w);
+        if (rc) return rc;
+    }
     return 0;
 }
 
@@ -2350,7 +2648,7 @@ int ldso_ba_update(ldso_ba_ctx *c, int32_t win, const ldso_ba_window *w) {
                                pd.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->sys_host_valid = false;
-    return 0;
+    return upload_priors(c, win);
 }
 
 int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
@@ -2684,25 +2982,10 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
             }
         }
     for (int i = 0; i < 4; i++) host[(size_t)N * N * 8 + i] = xF[i];
-    HIP_TRY(hipMemcpyAsync(c->d_xad.p, host, nx * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_xad.p + (size_t)win * kXadStride, host, nx * sizeof(float), hipMemcpyHostToDevice,
+                           c->stream));
     if (D.P > 0) {
-        ResubParams R;
-        R.xad = c->d_xad.p;
-        R.xc = c->d_xad.p + (size_t)N * N * 8;
-        R.pt_nres = c->d_pt_nres.p;
-        R.pt_tgt = c->d_pt_tgt.p;
-        R.rec_base = D.rec_base;
-        R.P = D.P;
-        R.point_base = D.point_base;
-        R.pt_rec = c->d_pt_rec.p;
-        R.pt_out = c->d_pt_out.p;
-        R.pt_host = c->d_pt_host.p;
-        R.pt_step = c->d_pt_step.p;
-        R.begin = D.point_base;
-        R.count = D.P;
-        R.N = N;
-        R.lambda = (float)lambda;
-        int rc = timed_launch(c, 3, c->stream, [&] { k_resubstitute<<<(D.P + 255) / 256, 256, 0, c->stream>>>(R); });
+        int rc = launch_resubstitute(c, D.point_base, D.P, lambda);
         if (rc) return rc;
     }
     if (point_step_out) {
@@ -2720,6 +3003,103 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
         for (int q = 0; q < D.P; q++) point_step_out[H.pt_orig[q]] = c->pin_step[q];
     }
     return 0;
+}
+
+// ---- device-side solve / resubstitute ----------------------------------
+int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const double *ns, int32_t n_null,
+                         double *x_out) {
+    (void)lambda;  // SOLVER_FIX_LAMBDA, as the host solver
+    if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
+    if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
+    int dmax = 0;
+    for (const WinDev &D : c->wd) dmax = std::max(dmax, D.D);
+    if (dmax > kSolveMaxDim) return fail(-1, "device solve supports windows of up to 11 keyframes");
+    HIP_TRY(hipSetDevice(c->device));
+    if (iteration >= 2 && ns && n_null > 0) {
+        // caller layout: every window's [7][D] back to back -> device [7 * vec_total] (same order)
+        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
+                               c->stream));
+    }
+    SolveParams S;
+    S.wins = c->d_wins.p;
+    S.sys = c->d_sys.p;
+    S.prior = c->d_prior.p;
+    S.ns = c->d_ns.p;
+    S.x = c->d_x.p;
+    S.iteration = iteration;
+    S.n_null = (iteration >= 2 && ns) ? n_null : 0;
+    const size_t smem = solve_smem_bytes(dmax);
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void *)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)solve_smem_bytes(kSolveMaxDim));
+    });
+    int rc = timed_launch(c, 5, c->stream, [&] { k_solve<<<c->n_win, 64, smem, c->stream>>>(S); });
+    if (rc) return rc;
+    if (x_out) {
+        HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream));
+        rc = ldso_ba_sync(c);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int ldso_ba_resubstitute_device(ldso_ba_ctx *c, double lambda, float *point_step_out) {
+    if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
+    HIP_TRY(hipSetDevice(c->device));
+    k_xad<<<c->n_win, 256, 0, c->stream>>>(c->d_wins.p, c->d_x.p, c->d_adH.p, c->d_adT.p, c->d_xad.p);
+    HIP_TRY(hipGetLastError());
+    if (c->P_tot > 0) {
+        int rc = launch_resubstitute(c, 0, c->P_tot, lambda);
+        if (rc) return rc;
+    }
+    if (point_step_out) {
+        if (c->pin_step_n < (size_t)c->P_tot) {
+            if (c->pin_step) (void)hipHostFree(c->pin_step);
+            c->pin_step = nullptr;
+            HIP_TRY(hipHostMalloc(&c->pin_step, std::max<size_t>(1, c->P_tot) * sizeof(float), hipHostMallocDefault));
+            c->pin_step_n = c->P_tot;
+        }
+        if (c->P_tot)
+            HIP_TRY(hipMemcpyAsync(c->pin_step, c->d_pt_step.p, c->P_tot * sizeof(float), hipMemcpyDeviceToHost,
+                                   c->stream));
+        int rc = ldso_ba_sync(c);
+        if (rc) return rc;
+        long long out_base = 0;  // windows back to back, each in its caller point order
+        for (int w = 0; w < c->n_win; w++) {
+            const WinDev &D = c->wd[w];
+            const WinHost &H = c->wh[w];
+            for (int q = 0; q < D.P; q++) point_step_out[out_base + H.pt_orig[q]] = c->pin_step[D.point_base + q];
+            out_base += H.P_all;
+        }
+    }
+    return 0;
+}
+
+int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const double *ns, int32_t n_null, double *x_out,
+                    float *point_step_out, double *energy_out) {
+    int rc = ldso_ba_linearize(c, 0, 1);
+    if (rc) return rc;
+    rc = ldso_ba_solve_device(c, iteration, lambda, ns, n_null, nullptr);
+    if (rc) return rc;
+    if (x_out)
+        HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream));
+    rc = ldso_ba_resubstitute_device(c, lambda, point_step_out);
+    if (rc) return rc;
+    if (energy_out) {
+        rc = ldso_ba_sync(c);
+        if (rc) return rc;
+        std::vector<double> e((size_t)2 * c->n_win);
+        HIP_TRY(hipMemcpy(e.data(), c->d_win_energy.p, e.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int w = 0; w < c->n_win; w++) {
+            energy_out[3 * w] = e[2 * w];
+            energy_out[3 * w + 1] = 0;
+            energy_out[3 * w + 2] = e[2 * w + 1];
+        }
+    }
+    return ldso_ba_sync(c);
 }
 
 int ldso_ba_packed_system(ldso_ba_ctx *c, void **dev_ptr, int64_t *n_doubles, int64_t *stride) {

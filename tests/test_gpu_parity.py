@@ -328,3 +328,44 @@ def test_pipelined_groups_agree(built, groups):
         e_cpu, s_cpu = ow.iteration()
         compare_pass(c, ow, i, e_cpu, s_cpu)
     c.close()
+
+
+def test_device_solve_and_resubstitute_match_host_path(built):
+    """ldso_ba_solve_device / resubstitute_device (one wavefront per window) reproduce the host
+    solver and the host-staged resubstitution bit for bit, for a batch of windows of different
+    sizes, at iteration 0 (no orthogonalisation) and 2 (nullspace projection)."""
+    cfgs = [dict(n_frames=3, n_points=120, seed=70), dict(n_frames=7, n_points=900, seed=71),
+            dict(n_frames=11, n_points=1200, seed=72), dict(n_frames=5, n_points=400, seed=73)]
+    ws = [synth.make_window(**cf) for cf in cfgs]
+    ns = [w.nullspaces() for w in ws]
+    c = BAContext(0).load(ws)
+    c.linearize()
+    for it in (0, 2):
+        xd = c.solve_device(it, 1e-5, ns)
+        for i in range(len(ws)):
+            xh = c.solve(i, it, 1e-5, ns[i])
+            np.testing.assert_array_equal(xd[i], xh)
+        sd = c.resubstitute_device(1e-5)
+        for i in range(len(ws)):
+            sh = c.resubstitute(i, xd[i], 1e-5)
+            np.testing.assert_array_equal(sd[i], sh)
+    # fused iteration == the separate calls (a new pass: the f64-atomic stitch sums in a
+    # different order each pass, so x agrees to rounding, not bitwise)
+    c.linearize()
+    xs_ref = c.solve_device(2, 1e-5, ns)
+    st_ref = c.resubstitute_device(1e-5)
+    e_ref = [c.energy(i) for i in range(len(ws))]
+    e, xs, sts = c.iterate(2, 1e-5, ns)
+    for i in range(len(ws)):
+        assert np.linalg.norm(xs[i] - xs_ref[i]) <= 1e-9 * np.linalg.norm(xs_ref[i])
+        assert np.linalg.norm(sts[i] - st_ref[i]) <= 1e-5 * np.linalg.norm(st_ref[i]) + 1e-12
+        assert e[i][2] == e_ref[i][2] and abs(e[i][0] - e_ref[i][0]) <= 1e-12 * abs(e_ref[i][0])
+    c.close()
+
+
+def test_device_solve_rejects_windows_above_eleven_keyframes(built):
+    c = BAContext(0).load([synth.make_window(n_frames=12, n_points=200, seed=74)])
+    c.linearize()
+    with pytest.raises(RuntimeError, match="11 keyframes"):
+        c.solve_device(0)
+    c.close()
