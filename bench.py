@@ -151,6 +151,19 @@ def main():
     ctx.sync()
     kall = ctx.kernel_times()
     ctx.set_kernel_timing(False)
+    # every resident window through a full device GN iteration (pass + solve + resubstitute)
+    gn = None
+    if args.mode == "replicas" and max(w.n_frames for w in windows) <= 11:
+        nss = [w.nullspaces() for w in windows]
+        for _ in range(3):
+            ctx.iterate(2, 1e-5, nss, fetch_steps=False)
+        ctx.sync()
+        t1 = time.perf_counter()
+        it_reps = min(args.steps, 20)
+        for _ in range(it_reps):
+            ctx.iterate(2, 1e-5, nss, fetch_steps=False)
+        gn_ms = 1e3 * (time.perf_counter() - t1) / it_reps
+        gn = {"ms_per_iteration": gn_ms, "windows": B, "windows_per_s": B / (gn_ms / 1e3)}
 
     if dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
@@ -202,7 +215,16 @@ def main():
             c1.linearize()
         c1.sync()
         sw_ms = 1e3 * (time.perf_counter() - t1) / reps
-        single = {"ms_per_pass": sw_ms, "point_residuals_per_s": sw.n_residuals / (sw_ms / 1e3)}
+        # the same GN iteration with the solve and resubstitution on the device (ldso_ba_iterate:
+        # pass + solve + resubstitute, x and point steps back on the host, one synchronisation)
+        for i in range(5):
+            c1.iterate(2, 1e-5, [ns])
+        t1 = time.perf_counter()
+        for i in range(reps):
+            c1.iterate(2, 1e-5, [ns])
+        ms_solve_dev = 1e3 * (time.perf_counter() - t1) / reps
+        single = {"ms_per_pass": sw_ms, "point_residuals_per_s": sw.n_residuals / (sw_ms / 1e3),
+                  "ms_per_solve_device": ms_solve_dev}
         c1.close()
 
     cpu = None
@@ -246,6 +268,7 @@ def main():
             },
             "kernel_ms_per_step": {k: v[0] / max(1, v[1]) for k, v in kall.items() if v[1]},
             "ms_per_solve": ms_solve,
+            "gn_iteration_batched": gn,
             "single_window": single,
             "cpu_baseline": cpu,
         }

@@ -342,46 +342,77 @@ void project_out(int n, const double *ns, int k, std::vector<double> &x) {
         for (int c = 0; c < k; c++)
             for (int i = 0; i < n; i++) G[(size_t)a * k + c] += Nm[(size_t)i * k + a] * Nm[(size_t)i * k + c];
     for (int i = 0; i < k; i++) V[(size_t)i * k + i] = 1;
-    for (int sweep = 0; sweep < 64; sweep++) {  // cyclic Jacobi
-        double off = 0;
-        for (int p = 0; p < k; p++)
-            for (int q = p + 1; q < k; q++) off += G[(size_t)p * k + q] * G[(size_t)p * k + q];
-        if (off < 1e-30) break;
-        for (int p = 0; p < k; p++)
-            for (int q = p + 1; q < k; q++) {
-                const double apq = G[(size_t)p * k + q];
-                if (apq == 0) continue;
-                const double th = (G[(size_t)q * k + q] - G[(size_t)p * k + p]) / (2 * apq);
-                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1));
-                const double c = 1 / std::sqrt(t * t + 1), s = t * c;
-                for (int r = 0; r < k; r++) {
-                    double gp = G[(size_t)r * k + p], gq = G[(size_t)r * k + q];
-                    G[(size_t)r * k + p] = c * gp - s * gq;
-                    G[(size_t)r * k + q] = s * gp + c * gq;
-                }
-                for (int r = 0; r < k; r++) {
-                    double gp = G[(size_t)p * k + r], gq = G[(size_t)q * k + r];
-                    G[(size_t)p * k + r] = c * gp - s * gq;
-                    G[(size_t)q * k + r] = s * gp + c * gq;
-                }
-                for (int r = 0; r < k; r++) {
-                    double vp = V[(size_t)r * k + p], vq = V[(size_t)r * k + q];
-                    V[(size_t)r * k + p] = c * vp - s * vq;
-                    V[(size_t)r * k + q] = s * vp + c * vq;
-                }
-            }
-    }
-    double smax = 0;
-    for (int e = 0; e < k; e++) smax = std::max(smax, std::sqrt(std::max(0.0, G[(size_t)e * k + e])));
     std::vector<double> ntx(k, 0.0), coef(k, 0.0);
     for (int a = 0; a < k; a++)
         for (int i = 0; i < n; i++) ntx[a] += Nm[(size_t)i * k + a] * x[i];
-    for (int e = 0; e < k; e++) {
-        const double ev = G[(size_t)e * k + e];
-        if (!(std::sqrt(std::max(0.0, ev)) > kSolverModeDelta * smax)) continue;
-        double proj = 0;
-        for (int a = 0; a < k; a++) proj += V[(size_t)a * k + e] * ntx[a];
-        for (int a = 0; a < k; a++) coef[a] += V[(size_t)a * k + e] * proj / ev;
+    bool fast = false;
+    if (k == 7) {
+        double g7[7][7], n7[7], c7[7];
+        for (int a = 0; a < 7; a++) {
+            n7[a] = ntx[a];
+            for (int c = 0; c < 7; c++) g7[a][c] = G[(size_t)a * 7 + c];
+        }
+        fast = gram_inverse_coef7(g7, n7, c7);
+        if (fast)
+            for (int a = 0; a < 7; a++) coef[a] = c7[a];
+    }
+    // Jacobi sweeps in round-robin order (circle method): 7 rounds of 3 disjoint rotations; in a
+    // round all angles come from the round's starting G, then every column update, then every row
+    // update (disjoint pairs make both phases order-free).  k_solve runs the same rounds.
+    if (!fast) {
+        static constexpr int kRounds[7][3][2] = {
+            {{1, 6}, {2, 5}, {3, 4}}, {{0, 2}, {3, 6}, {4, 5}}, {{1, 3}, {0, 4}, {5, 6}}, {{2, 4}, {1, 5}, {0, 6}},
+            {{3, 5}, {2, 6}, {0, 1}}, {{4, 6}, {0, 3}, {1, 2}}, {{0, 5}, {1, 4}, {2, 3}}};
+        for (int sweep = 0; sweep < 64; sweep++) {
+            double off = 0;
+            for (int p = 0; p < k; p++)
+                for (int q = p + 1; q < k; q++) off += G[(size_t)p * k + q] * G[(size_t)p * k + q];
+            if (off < 1e-30) break;
+            for (int rd = 0; rd < 7; rd++) {
+                double c[3], s[3];
+                bool on[3];
+                for (int e = 0; e < 3; e++) {
+                    const int p = kRounds[rd][e][0], q = kRounds[rd][e][1];
+                    on[e] = q < k && G[(size_t)p * k + q] != 0;
+                    if (!on[e]) continue;
+                    const double apq = G[(size_t)p * k + q];
+                    const double th = (G[(size_t)q * k + q] - G[(size_t)p * k + p]) / (2 * apq);
+                    const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1));
+                    c[e] = 1 / std::sqrt(t * t + 1);
+                    s[e] = t * c[e];
+                }
+                for (int e = 0; e < 3; e++) {
+                    if (!on[e]) continue;
+                    const int p = kRounds[rd][e][0], q = kRounds[rd][e][1];
+                    for (int r = 0; r < k; r++) {
+                        const double gp = G[(size_t)r * k + p], gq = G[(size_t)r * k + q];
+                        G[(size_t)r * k + p] = c[e] * gp - s[e] * gq;
+                        G[(size_t)r * k + q] = s[e] * gp + c[e] * gq;
+                    }
+                }
+                for (int e = 0; e < 3; e++) {
+                    if (!on[e]) continue;
+                    const int p = kRounds[rd][e][0], q = kRounds[rd][e][1];
+                    for (int r = 0; r < k; r++) {
+                        const double gp = G[(size_t)p * k + r], gq = G[(size_t)q * k + r];
+                        G[(size_t)p * k + r] = c[e] * gp - s[e] * gq;
+                        G[(size_t)q * k + r] = s[e] * gp + c[e] * gq;
+                        const double vp = V[(size_t)r * k + p], vq = V[(size_t)r * k + q];
+                        V[(size_t)r * k + p] = c[e] * vp - s[e] * vq;
+                        V[(size_t)r * k + q] = s[e] * vp + c[e] * vq;
+                    }
+                }
+            }
+        }
+        double smax = 0;
+        for (int e = 0; e < k; e++) smax = std::max(smax, std::sqrt(std::max(0.0, G[(size_t)e * k + e])));
+        for (int e = 0; e < k; e++) {
+            const double ev = G[(size_t)e * k + e];
+            if (!(std::sqrt(std::max(0.0, ev)) > kSolverModeDelta * smax)) continue;
+            double proj = 0;
+            for (int a = 0; a < k; a++) proj += V[(size_t)a * k + e] * ntx[a];
+            for (int a = 0; a < k; a++) coef[a] += V[(size_t)a * k + e] * proj / ev;
+        }
     }
     for (int i = 0; i < n; i++) {
         double s = 0;

@@ -1483,6 +1483,11 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 // ldso_ba_solve's.  H lives in LDS (n <= kSolveMaxDim).
 // ============================================================================================
 constexpr int kSolveMaxDim = 8 * 11 + 4;  // windows up to 11 keyframes (68 KB of LDS for H)
+// Round-robin (circle method) schedule of the 7 x 7 Jacobi sweep: 7 rounds of 3 disjoint pairs
+// (p < q); player r sits out round r.  Shared with host_math.cpp's project_out.
+__device__ constexpr int kJacobiRounds[7][3][2] = {
+    {{1, 6}, {2, 5}, {3, 4}}, {{0, 2}, {3, 6}, {4, 5}}, {{1, 3}, {0, 4}, {5, 6}}, {{2, 4}, {1, 5}, {0, 6}},
+    {{3, 5}, {2, 6}, {0, 1}}, {{4, 6}, {0, 3}, {1, 2}}, {{0, 5}, {1, 4}, {2, 3}}};
 struct SolveParams {
     const WinDev *__restrict__ wins;
     const double *__restrict__ sys;
@@ -1491,7 +1496,46 @@ struct SolveParams {
     double *x;                         // [vec]
     int iteration, n_null;
 };
-size_t solve_smem_bytes(int n) { return ((size_t)n * n + 7 * (size_t)n + 8 * (size_t)n + 7 * 7 * 3 + 64) * sizeof(double); }
+// H's row stride in LDS: odd (in doubles), so a column walk touches 32 distinct bank pairs
+__host__ __device__ inline int solve_ld(int n) { return n | 1; }
+size_t solve_smem_bytes(int n) {
+    return ((size_t)n * solve_ld(n) + 7 * (size_t)n + 9 * (size_t)n + 7 * 7 * 3 + 64) * sizeof(double) +
+           ((size_t)n * (n + 1) / 2 + 1) * sizeof(int) + 64 * sizeof(double);
+}
+
+// wave-wide maximum of a 64-bit key, broadcast to every lane: inclusive max-scan within each
+// row of 16 (row_shr 1/2/4/8), then row_bcast15 / row_bcast31 carry rows 0-2 into lane 63.
+// Keys >= 0 with 0 as identity; every lane of the wave must be active.
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
+#define LDSO_DPP_MAX(CTRL, ROWS)                                                                  \
+    {                                                                                             \
+        const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)x, CTRL, ROWS, 0xF, true); \
+        const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(x >> 32), CTRL, ROWS, 0xF, true); \
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;                         \
+        x = o > x ? o : x;                                                                        \
+    }
+    LDSO_DPP_MAX(0x111, 0xF)
+    LDSO_DPP_MAX(0x112, 0xF)
+    LDSO_DPP_MAX(0x114, 0xF)
+    LDSO_DPP_MAX(0x118, 0xF)
+    LDSO_DPP_MAX(0x142, 0xA)
+    LDSO_DPP_MAX(0x143, 0xC)
+#undef LDSO_DPP_MAX
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// |v| as an order-preserving key; NaN never wins (the host's '>' never selects one)
+__device__ __forceinline__ unsigned long long abs_key(double v) {
+    const double a = fabs(v);
+    return a == a ? (unsigned long long)__double_as_longlong(a) : 0ull;
+}
 
 __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
 #pragma clang fp contract(off)
@@ -1500,110 +1544,154 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     const int n = W.D, lane = threadIdx.x;
     const long long pl = packed_len(n);
     const double *HA = P.sys + W.sys_base, *bA = HA + pl, *Hs = HA + pl + n, *bs = HA + 2 * pl + n;
-    double *H = lds;                  // [n][n] row-major, as the host's std::vector
-    double *b = H + (size_t)n * n;    // [n]
+    const int ld = solve_ld(n);
+    double *H = lds;                  // [n][ld] row-major (the host's [n][n]); lower triangle used
+    double *b = H + (size_t)n * ld;   // [n]
     double *sc = b + n, *y = sc + n, *col = y + n;
     double *Nm = col + n;             // [n][7]
-    double *G = Nm + 7 * (size_t)n, *V = G + 49, *misc = V + 49;  // misc: ntx[7], coef[7]
+    double *lr = Nm + 7 * (size_t)n;  // [n]: L(i,k) of the current step
+    double *G = lr + n, *V = G + 49, *misc = V + 49;  // misc: ntx[7], coef[7]
     int *perm = reinterpret_cast<int *>(misc + 16);
+    // lower-triangle elements (i, j), j <= i, ordered by column j descending: the elements the
+    // LDL^T step k updates (k < j <= i) are exactly a prefix, so every step is element-parallel.
+    // Entry: the element's offset in H (16 bits) | i << 16 | j << 23 (n <= 92 < 128).
+    // Columns n-1, n-2, ... hold 1, 2, ... elements: e lies in column n-1-m with m(m+1)/2 <= e.
+    int *tri = perm + n;
+    const int ntri = n * (n + 1) / 2;
+    // one private dummy slot per lane: masked-off update elements land there (no branches)
+    double *dummy = reinterpret_cast<double *>(tri + ((ntri + 1) & ~1)) + lane;
+    for (int e = lane; e < ntri; e += 64) {
+        int m = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
+        while (m * (m + 1) / 2 > e) m--;
+        while ((m + 1) * (m + 2) / 2 <= e) m++;
+        const int j = n - 1 - m, rem = e - m * (m + 1) / 2;
+        tri[e] = ((j + rem) * ld + j) | ((j + rem) << 16) | (j << 23);  // LDS offset of (i, j) | i | j
+    }
     const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
-    auto at = [&](int r, int c) -> double & { return H[(size_t)r * n + c]; };
-    // ---- assembly (EnergyFunctional.cc:342-378), upper triangle then mirrored
+    const double scl = 1.0f / (1 + lambda);
+    auto at = [&](int r, int c) -> double & { return H[r * ld + c]; };
+    // ---- assembly (EnergyFunctional.cc:342-378), each element in the host's order of operations:
+    // H = (HL + 0) + HA, diagonal *= (1 + lambda), H -= Hsc * scl, mirror, H(i,j) *= s_i s_j.
+    // The diagonal first (the Jacobi scale needs it), then every packed upper element (r, c)
+    // straight into its scaled lower position (c, r); products of two scales commute exactly.
+    auto element = [&](int r, int c, double ha, double hs) {
+        double h = ((r == c ? P.prior[2 * (W.vec_base + r)] : 0.0) + 0.0) + ha;
+        if (r == c) h *= (1 + lambda);
+        return h - hs * scl;
+    };
     for (int i = lane; i < n; i += 64) {
-        const double hl = P.prior[2 * (W.vec_base + i)], bl = P.prior[2 * (W.vec_base + i) + 1];
-        for (int j = i; j < n; j++) at(i, j) = ((i == j ? hl : 0.0) + 0.0) + HA[pk_index(i, j, n)];
-        b[i] = ((bl + 0.0) + bA[i]) - bs[i] / (1 + lambda);
+        const long long q = pk_index(i, i, n);
+        sc[i] = 1.0 / sqrt(element(i, i, HA[q], Hs[q]) + 10);
+        perm[i] = i;
     }
     wave_lds_sync();
-    for (int i = lane; i < n; i += 64) at(i, i) *= (1 + lambda);
-    const double scl = 1.0f / (1 + lambda);
-    for (int i = lane; i < n; i += 64)
-        for (int j = i; j < n; j++) at(i, j) -= Hs[pk_index(i, j, n)] * scl;
-    wave_lds_sync();
-    for (int i = lane; i < n; i += 64)
-        for (int j = 0; j < i; j++) at(i, j) = at(j, i);
-    for (int i = lane; i < n; i += 64) sc[i] = 1.0 / sqrt(at(i, i) + 10);
-    wave_lds_sync();
     for (int i = lane; i < n; i += 64) {
-        b[i] *= sc[i];
-        for (int j = 0; j < n; j++) at(i, j) *= sc[i] * sc[j];
-        perm[i] = i;
+        const double bl = P.prior[2 * (W.vec_base + i) + 1];
+        b[i] = (((bl + 0.0) + bA[i]) - bs[i] / (1 + lambda)) * sc[i];
+    }
+    constexpr int kAsmBatch = 8;
+    const int n2 = 2 * n + 1;
+    for (int f0 = lane; f0 < pl; f0 += 64 * kAsmBatch) {
+        double ha[kAsmBatch], hs[kAsmBatch];
+#pragma unroll
+        for (int u = 0; u < kAsmBatch; u++) {
+            const int f = f0 + 64 * u;
+            ha[u] = f < pl ? HA[f] : 0.0;
+            hs[u] = f < pl ? Hs[f] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kAsmBatch; u++) {
+            const int f = f0 + 64 * u;
+            if (f >= pl) break;
+            // row r of the row-major packed upper triangle: r (2n - r + 1) / 2 <= f
+            int r = (int)((n2 - sqrtf(fmaxf(0.0f, (float)(n2 * n2) - 8.0f * f))) * 0.5f);
+            r = r < 0 ? 0 : (r > n - 1 ? n - 1 : r);
+            while (r < n - 1 && pk_index(r + 1, r + 1, n) <= f) r++;
+            while (r > 0 && pk_index(r, r, n) > f) r--;
+            const int c = r + (int)(f - pk_index(r, r, n));
+            at(c, r) = element(r, c, ha[u], hs[u]) * (sc[c] * sc[r]);
+        }
     }
     wave_lds_sync();
     // ---- LDL^T with symmetric diagonal pivoting (lower triangle)
     for (int k = 0; k < n; k++) {
-        double best = -1.0;
-        int bi = n;
-        for (int i = k + lane; i < n; i += 64) {  // first index of the largest |diag|
-            const double v = fabs(at(i, i));
-            if (v > best) {
-                best = v;
-                bi = i;
-            }
+        // pivot = first index of the largest |diag| (the host's strict '>' scan from k: a NaN
+        // never wins, except that a NaN at k itself keeps k)
+        int piv;
+        {
+            const int i0 = k + lane, i1 = k + 64 + lane;
+            const double v0 = at(min(i0, n - 1), min(i0, n - 1)), v1 = at(min(i1, n - 1), min(i1, n - 1));
+            const unsigned long long k0 = i0 >= n ? 0ull : (v0 != v0 && i0 == k) ? ~0ull : abs_key(v0);
+            const unsigned long long k1 = i1 < n ? abs_key(v1) : 0ull;
+            const unsigned long long mx = wave_max_u64(k0 > k1 ? k0 : k1);
+            const unsigned long long b0 = __ballot(i0 < n && k0 == mx);
+            piv = b0 ? k + __builtin_ctzll(b0) : k + 64 + __builtin_ctzll(__ballot(i1 < n && k1 == mx));
         }
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            const double ob = __shfl_xor(best, m, kWave);
-            const int oi = __shfl_xor(bi, m, kWave);
-            if (ob > best || (ob == best && oi < bi)) {
-                best = ob;
-                bi = oi;
-            }
-        }
-        const int piv = bi;
-        if (piv != k) {
+        // symmetric swap k <-> piv (lower triangle: (k,j)<->(piv,j) for j < k, (i,k)<->(piv,i) for
+        // k < i < piv, (i,k)<->(i,piv) for i > piv, the two diagonals), fused with taking column k:
+        // col = the new A(i,k), lr = L(i,k) = col / d, written back as L
+        const double d = at(piv, piv), dkk = at(k, k);
+        if (piv != k)
             for (int j = lane; j < k; j += 64) {
-                const double t = at(k, j);
-                at(k, j) = at(piv, j);
+                const double t = at(k, j), u = at(piv, j);
+                at(k, j) = u;
                 at(piv, j) = t;
             }
-            for (int i = k + 1 + lane; i < piv; i += 64) {
-                const double t = at(i, k);
-                at(i, k) = at(piv, i);
-                at(piv, i) = t;
-            }
-            for (int i = piv + 1 + lane; i < n; i += 64) {
-                const double t = at(i, k);
-                at(i, k) = at(i, piv);
-                at(i, piv) = t;
-            }
-            if (lane == 0) {
-                const double t = at(k, k);
-                at(k, k) = at(piv, piv);
-                at(piv, piv) = t;
-                const int pt = perm[k];
-                perm[k] = perm[piv];
-                perm[piv] = pt;
-            }
-        }
-        wave_lds_sync();
-        const double d = at(k, k);
-        for (int i = k + 1 + lane; i < n; i += 64) col[i] = at(i, k);
-        wave_lds_sync();
         for (int i = k + 1 + lane; i < n; i += 64) {
-            const double l = d != 0 ? col[i] / d : 0.0;
-            double *row = &at(i, 0);
-            for (int j = k + 1; j <= i; j++) row[j] -= l * col[j];
-            row[k] = l;
+            double *own = &at(i, k);
+            double *src = piv == k || i == piv ? own : (i < piv ? &at(piv, i) : &at(i, piv));
+            const double old = *own, v = *src;
+            *(src != own ? src : dummy) = old;
+            const double l = d != 0 ? v / d : 0.0;
+            col[i] = v;
+            lr[i] = l;
+            *own = l;
+        }
+        if (lane == 0 && piv != k) {
+            at(k, k) = d;
+            at(piv, piv) = dkk;
+            const int pt = perm[k];
+            perm[k] = perm[piv];
+            perm[piv] = pt;
+        }
+        wave_lds_sync();
+        const int m = (n - k - 1) * (n - k) / 2;  // elements with k < j <= i
+        constexpr int kUpdBatch = 8;
+        for (int e0 = lane; e0 < m; e0 += 64 * kUpdBatch) {
+            int ij[kUpdBatch];
+            double a[kUpdBatch], l[kUpdBatch], cj[kUpdBatch], *dst[kUpdBatch];
+#pragma unroll
+            for (int u = 0; u < kUpdBatch; u++) ij[u] = tri[min(e0 + 64 * u, m - 1)];
+#pragma unroll
+            for (int u = 0; u < kUpdBatch; u++) {
+                const int off = ij[u] & 0xFFFF, i = (ij[u] >> 16) & 0x7F, j = ij[u] >> 23;
+                l[u] = lr[i];
+                cj[u] = col[j];
+                a[u] = H[off];
+                dst[u] = e0 + 64 * u < m ? H + off : dummy;
+            }
+#pragma unroll
+            for (int u = 0; u < kUpdBatch; u++) *dst[u] = a[u] - l[u] * cj[u];
         }
         wave_lds_sync();
     }
-    // ---- substitutions (column by column, as the host)
-    for (int i = lane; i < n; i += 64) y[i] = b[perm[i]];
-    wave_lds_sync();
+    // ---- substitutions (column by column, as the host); y[i] lives in lane i (mod 64)
+    const int ia = lane, ib = lane + 64;
+    double ya = ia < n ? b[perm[ia]] : 0.0, yb = ib < n ? b[perm[ib]] : 0.0;
     for (int j = 0; j < n; j++) {
-        const double yj = y[j];
-        for (int i = j + 1 + lane; i < n; i += 64) y[i] -= at(i, j) * yj;
-        wave_lds_sync();
+        const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+        if (ia > j && ia < n) ya -= at(ia, j) * yj;
+        if (ib > j && ib < n) yb -= at(ib, j) * yj;
     }
-    for (int i = lane; i < n; i += 64) y[i] = at(i, i) != 0 ? y[i] / at(i, i) : 0.0;
-    wave_lds_sync();
+    if (ia < n) ya = at(ia, ia) != 0 ? ya / at(ia, ia) : 0.0;
+    if (ib < n) yb = at(ib, ib) != 0 ? yb / at(ib, ib) : 0.0;
     for (int j = n - 1; j >= 0; j--) {
-        const double yj = y[j];
-        for (int i = lane; i < j; i += 64) y[i] -= at(j, i) * yj;
-        wave_lds_sync();
+        const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+        if (ia < j) ya -= at(j, ia) * yj;
+        if (ib < j) yb -= at(j, ib) * yj;
     }
-    for (int i = lane; i < n; i += 64) b[perm[i]] = y[i];
+    if (ia < n) b[perm[ia]] = ya;
+    if (ib < n) b[perm[ib]] = yb;
     wave_lds_sync();
     for (int i = lane; i < n; i += 64) y[i] = sc[i] * b[i];  // x
     wave_lds_sync();
@@ -1611,11 +1699,18 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     const int kk = P.n_null;
     if (P.iteration >= 2 && kk > 0) {
         const double *ns = P.ns + (size_t)7 * W.vec_base;
+        double *raw = H;  // H is free after the substitutions: raw nullspaces [kk][n], coalesced
+        for (int e = lane; e < kk * n; e += 64) raw[e] = ns[e];
+        wave_lds_sync();
         if (lane < kk) {
             double s2 = 0;
-            for (int i = 0; i < n; i++) s2 += ns[(size_t)lane * n + i] * ns[(size_t)lane * n + i];
-            s2 = sqrt(s2);
-            for (int i = 0; i < n; i++) Nm[(size_t)i * kk + lane] = ns[(size_t)lane * n + i] / s2;
+            for (int i = 0; i < n; i++) s2 += raw[lane * n + i] * raw[lane * n + i];
+            lr[lane] = sqrt(s2);
+        }
+        wave_lds_sync();
+        for (int e = lane; e < kk * n; e += 64) {
+            const int i = e / kk, a = e - i * kk;
+            Nm[e] = raw[a * n + i] / lr[a];
         }
         wave_lds_sync();
         if (lane < kk * kk) {
@@ -1633,45 +1728,91 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
             coef[lane] = 0.0;
         }
         wave_lds_sync();
-        if (lane == 0) {  // cyclic Jacobi on the k x k Gram matrix, as the host
-            const int k = kk;
-            for (int sweep = 0; sweep < 64; sweep++) {
+        {  // (NtN)^+ NtX in registers, every lane redundantly (no LDS traffic, no synchronisation):
+            // the Cholesky fast path when G is well conditioned, else the round-robin Jacobi of
+            // host_math.cpp project_out
+            double g[7][7], v[7][7], nt[7], cf[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int r = 0; r < 7; r++)
+#pragma unroll
+                for (int q = 0; q < 7; q++) {
+                    g[r][q] = r < kk && q < kk ? G[r * kk + q] : 0.0;
+                    v[r][q] = r == q ? 1.0 : 0.0;
+                }
+#pragma unroll
+            for (int a = 0; a < 7; a++) nt[a] = a < kk ? ntx[a] : 0.0;
+            const bool fast = kk == 7 && gram_inverse_coef7(g, nt, cf);
+            for (int sweep = 0; sweep < 64 && !fast; sweep++) {
                 double off = 0;
-                for (int p = 0; p < k; p++)
-                    for (int q = p + 1; q < k; q++) off += G[p * k + q] * G[p * k + q];
+#pragma unroll
+                for (int p = 0; p < 7; p++)
+#pragma unroll
+                    for (int q = p + 1; q < 7; q++)
+                        if (q < kk) off += g[p][q] * g[p][q];
                 if (off < 1e-30) break;
-                for (int p = 0; p < k; p++)
-                    for (int q = p + 1; q < k; q++) {
-                        const double apq = G[p * k + q];
-                        if (apq == 0) continue;
-                        const double th = (G[q * k + q] - G[p * k + p]) / (2 * apq);
+#pragma unroll
+                for (int rd = 0; rd < 7; rd++) {
+                    double c[3], sn[3];
+                    bool on[3];
+#pragma unroll
+                    for (int e = 0; e < 3; e++) {
+                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
+                        const double apq = g[p][q];
+                        on[e] = q < kk && apq != 0;
+                        const double th = (g[q][q] - g[p][p]) / (2 * apq);
                         const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
-                        const double c = 1 / sqrt(t * t + 1), s = t * c;
-                        for (int r = 0; r < k; r++) {
-                            const double gp = G[r * k + p], gq = G[r * k + q];
-                            G[r * k + p] = c * gp - s * gq;
-                            G[r * k + q] = s * gp + c * gq;
-                        }
-                        for (int r = 0; r < k; r++) {
-                            const double gp = G[p * k + r], gq = G[q * k + r];
-                            G[p * k + r] = c * gp - s * gq;
-                            G[q * k + r] = s * gp + c * gq;
-                        }
-                        for (int r = 0; r < k; r++) {
-                            const double vp = V[r * k + p], vq = V[r * k + q];
-                            V[r * k + p] = c * vp - s * vq;
-                            V[r * k + q] = s * vp + c * vq;
+                        c[e] = 1 / sqrt(t * t + 1);
+                        sn[e] = t * c[e];
+                    }
+#pragma unroll
+                    for (int e = 0; e < 3; e++) {  // column phase
+                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
+                        if (!on[e]) continue;
+#pragma unroll
+                        for (int r = 0; r < 7; r++) {
+                            const double gp = g[r][p], gq = g[r][q];
+                            g[r][p] = c[e] * gp - sn[e] * gq;
+                            g[r][q] = sn[e] * gp + c[e] * gq;
                         }
                     }
+#pragma unroll
+                    for (int e = 0; e < 3; e++) {  // row phase, then V
+                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
+                        if (!on[e]) continue;
+#pragma unroll
+                        for (int r = 0; r < 7; r++) {
+                            const double gp = g[p][r], gq = g[q][r];
+                            g[p][r] = c[e] * gp - sn[e] * gq;
+                            g[q][r] = sn[e] * gp + c[e] * gq;
+                            const double vp = v[r][p], vq = v[r][q];
+                            v[r][p] = c[e] * vp - sn[e] * vq;
+                            v[r][q] = sn[e] * vp + c[e] * vq;
+                        }
+                    }
+                }
             }
             double smax = 0;
-            for (int e = 0; e < k; e++) smax = fmax(smax, sqrt(fmax(0.0, G[e * k + e])));
-            for (int e = 0; e < k; e++) {
-                const double ev = G[e * k + e];
+#pragma unroll
+            for (int e = 0; e < 7; e++)
+                if (e < kk) smax = fmax(smax, sqrt(fmax(0.0, g[e][e])));
+#pragma unroll
+            for (int e = 0; e < 7; e++) {
+                if (fast || e >= kk) continue;
+                const double ev = g[e][e];
                 if (!(sqrt(fmax(0.0, ev)) > kSolverModeDelta * smax)) continue;
                 double proj = 0;
-                for (int a = 0; a < k; a++) proj += V[a * k + e] * ntx[a];
-                for (int a = 0; a < k; a++) coef[a] += V[a * k + e] * proj / ev;
+#pragma unroll
+                for (int a = 0; a < 7; a++)
+                    if (a < kk) proj += v[a][e] * nt[a];
+#pragma unroll
+                for (int a = 0; a < 7; a++)
+                    if (a < kk) cf[a] += v[a][e] * proj / ev;
+            }
+            if (lane < kk) {
+                double mine = 0;
+#pragma unroll
+                for (int a = 0; a < 7; a++) mine = a == lane ? cf[a] : mine;
+                coef[lane] = mine;
             }
         }
         wave_lds_sync();

@@ -3,6 +3,12 @@
 #pragma once
 #include "../../include/ldso_ba.h"
 
+#if defined(__HIP__)
+#define LDSO_HD __host__ __device__
+#else
+#define LDSO_HD
+#endif
+
 namespace ldso_ba {
 
 // include/Settings.h:28-35
@@ -24,6 +30,57 @@ constexpr float kInitialTransPrior = 1e10f;                // :19
 constexpr float kInitialAffBPrior = 1e14f;                 // :20
 constexpr float kInitialAffAPrior = 1e14f;                 // :21
 constexpr double kSolverModeDelta = 0.00001;               // :24
+
+// Fast path of the nullspace projection (EnergyFunctional::orthogonalize, EnergyFunctional.cc:809-841)
+// for 7 nullspaces: when the Gram matrix G = N^T N of the normalised nullspaces is so well
+// conditioned that no singular value of N can fall under kSolverModeDelta * max (checked with
+// lambda_min >= 1 / |G^-1|_F and lambda_max <= trace G, with a factor 2 margin), the
+// pseudo-inverse is the inverse: coef = G^-1 N^T x via Cholesky.  Returns false (coef untouched)
+// otherwise, and the caller runs the Jacobi eigen-decomposition.  One definition for the host
+// solver and k_solve, so both produce the same bits.
+LDSO_HD inline bool gram_inverse_coef7(const double (&G)[7][7], const double (&ntx)[7], double (&coef)[7]) {
+#pragma clang fp contract(off)
+    double L[7][7], Li[7][7];
+    for (int j = 0; j < 7; j++) {
+        double s = G[j][j];
+        for (int p = 0; p < j; p++) s -= L[j][p] * L[j][p];
+        if (!(s > 0)) return false;
+        L[j][j] = sqrt(s);
+        for (int i = j + 1; i < 7; i++) {
+            double t = G[i][j];
+            for (int p = 0; p < j; p++) t -= L[i][p] * L[j][p];
+            L[i][j] = t / L[j][j];
+        }
+        for (int i = 0; i < j; i++) L[i][j] = 0;
+    }
+    for (int c = 0; c < 7; c++)  // L^-1, column by column (forward substitution on e_c)
+        for (int i = 0; i < 7; i++) {
+            if (i < c) {
+                Li[i][c] = 0;
+                continue;
+            }
+            double t = i == c ? 1.0 : 0.0;
+            for (int p = c; p < i; p++) t -= L[i][p] * Li[p][c];
+            Li[i][c] = t / L[i][i];
+        }
+    double Gi[7][7], f2 = 0, tr = 0;
+    for (int a = 0; a < 7; a++) {
+        tr += G[a][a];
+        for (int b = 0; b < 7; b++) {
+            double t = 0;
+            for (int i = (a > b ? a : b); i < 7; i++) t += Li[i][a] * Li[i][b];
+            Gi[a][b] = t;
+            f2 += t * t;
+        }
+    }
+    if (!(kSolverModeDelta * kSolverModeDelta * tr * sqrt(f2) < 0.5)) return false;
+    for (int a = 0; a < 7; a++) {
+        double t = 0;
+        for (int b = 0; b < 7; b++) t += Gi[a][b] * ntx[b];
+        coef[a] = t;
+    }
+    return true;
+}
 
 int frame_precalc(int N, const ldso_ba_frame_state *fr, const float calib[4], float *out);
 int set_adjoints(int N, const ldso_ba_frame_state *fr, double *adH, double *adT, double *cPrior);

@@ -154,3 +154,32 @@ def test_product_solver_known_answer(built):
     Hl[np.diag_indices(n)] *= 1 + 1e-5
     xr = np.linalg.solve(Hl, b)
     assert np.linalg.norm(x - xr) <= 1e-9 * np.linalg.norm(xr)
+
+
+@pytest.mark.parametrize("degenerate", [False, True])
+def test_product_solver_projection_known_answer(built, degenerate):
+    """Iteration >= 2 projects the step out of the nullspace span (EnergyFunctional::orthogonalize):
+    x = (I - N N^+) x0.  Well-conditioned nullspaces take the Cholesky path; a rank-deficient set
+    (two equal columns) takes the Jacobi path, whose cut drops the zero singular value."""
+    rng = np.random.default_rng(8)
+    N = 3
+    n = 8 * N + 4
+    A = rng.standard_normal((n, n))
+    H = np.ascontiguousarray(A @ A.T + n * np.eye(n))
+    b = rng.standard_normal(n)
+    ns = rng.standard_normal((7, n))
+    if degenerate:
+        ns[6] = ns[5]
+    ns = np.ascontiguousarray(ns)
+    Z, z = np.zeros((n, n)), np.zeros(n)
+    x0, x2 = np.zeros(n), np.zeros(n)
+    lib = L.lib()
+    for it, x in ((0, x0), (2, x2)):
+        rc = lib.ldso_ba_solve_system(N, it, 1e-5, L.ptr(H, L.f64p), L.ptr(b, L.f64p), L.ptr(Z, L.f64p),
+                                      L.ptr(z, L.f64p), L.ptr(None, L.f64p), L.ptr(None, L.f64p), L.ptr(Z, L.f64p),
+                                      L.ptr(z, L.f64p), L.ptr(ns, L.f64p), 7, L.ptr(x, L.f64p))
+        assert rc == 0
+    Nm = (ns / np.linalg.norm(ns, axis=1, keepdims=True)).T
+    xr = x0 - Nm @ (np.linalg.pinv(Nm, rcond=1e-10) @ x0)
+    assert np.linalg.norm(x2 - xr) <= 1e-9 * np.linalg.norm(x0)
+    assert np.abs(Nm.T @ x2).max() <= 1e-9 * np.linalg.norm(x0)

@@ -333,7 +333,8 @@ def test_pipelined_groups_agree(built, groups):
 def test_device_solve_and_resubstitute_match_host_path(built):
     """ldso_ba_solve_device / resubstitute_device (one wavefront per window) reproduce the host
     solver and the host-staged resubstitution bit for bit, for a batch of windows of different
-    sizes, at iteration 0 (no orthogonalisation) and 2 (nullspace projection)."""
+    sizes, at iteration 0 (no orthogonalisation) and 2 (nullspace projection: the Cholesky path,
+    and the Jacobi path for a rank-deficient nullspace set)."""
     cfgs = [dict(n_frames=3, n_points=120, seed=70), dict(n_frames=7, n_points=900, seed=71),
             dict(n_frames=11, n_points=1200, seed=72), dict(n_frames=5, n_points=400, seed=73)]
     ws = [synth.make_window(**cf) for cf in cfgs]
@@ -349,6 +350,13 @@ def test_device_solve_and_resubstitute_match_host_path(built):
         for i in range(len(ws)):
             sh = c.resubstitute(i, xd[i], 1e-5)
             np.testing.assert_array_equal(sd[i], sh)
+    # rank-deficient nullspaces: the Jacobi fallback of the projection, also bit for bit
+    ns_deg = [a.copy() for a in ns]
+    for a in ns_deg:
+        a[6] = a[5]
+    xd = c.solve_device(2, 1e-5, ns_deg)
+    for i in range(len(ws)):
+        np.testing.assert_array_equal(xd[i], c.solve(i, 2, 1e-5, ns_deg[i]))
     # fused iteration == the separate calls (a new pass: the f64-atomic stitch sums in a
     # different order each pass, so x agrees to rounding, not bitwise)
     c.linearize()
