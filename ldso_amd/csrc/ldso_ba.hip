@@ -1475,14 +1475,14 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 }
 
 // ============================================================================================
-// k_solve: EnergyFunctional::solveSystemF on the GPU, one wavefront per window.
-// Statement for statement the host solver (host_math.cpp solve_system: assembly with the
-// FIX_LAMBDA damping, Jacobi scaling, lower-triangle LDL^T with diagonal pivoting, column
-// substitutions, orthogonalize); each lane owns the matrix rows i = lane (mod 64) and every
-// element sees the host's operations in the host's order, so x is bit-identical to
-// ldso_ba_solve's.  H lives in LDS (n <= kSolveMaxDim).
+// k_solve: EnergyFunctional::solveSystemF on the GPU, one workgroup of 4 wavefronts per window
+// (SURVEY §8f row 1).  Statement for statement the host solver (host_math.cpp solve_system:
+// assembly with the FIX_LAMBDA damping, Jacobi scaling, lower-triangle LDL^T with diagonal
+// pivoting, column substitutions, orthogonalize); every element sees the host's operations in
+// the host's order, so x is bit-identical to ldso_ba_solve's.  H lives in LDS (n <= kSolveMaxDim).
 // ============================================================================================
 constexpr int kSolveMaxDim = 8 * 11 + 4;  // windows up to 11 keyframes (68 KB of LDS for H)
+constexpr int kSolveThreads = 256;        // 4 wavefronts share the assembly and the LDL^T updates
 // Round-robin (circle method) schedule of the 7 x 7 Jacobi sweep: 7 rounds of 3 disjoint pairs
 // (p < q); player r sits out round r.  Shared with host_math.cpp's project_out.
 __device__ constexpr int kJacobiRounds[7][3][2] = {
@@ -1500,7 +1500,7 @@ struct SolveParams {
 __host__ __device__ inline int solve_ld(int n) { return n | 1; }
 size_t solve_smem_bytes(int n) {
     return ((size_t)n * solve_ld(n) + 7 * (size_t)n + 9 * (size_t)n + 7 * 7 * 3 + 64) * sizeof(double) +
-           ((size_t)n * (n + 1) / 2 + 1) * sizeof(int) + 64 * sizeof(double);
+           ((size_t)n + 1) * sizeof(int) + kSolveThreads * sizeof(double);
 }
 
 // wave-wide maximum of a 64-bit key, broadcast to every lane: inclusive max-scan within each
@@ -1537,11 +1537,11 @@ __device__ __forceinline__ unsigned long long abs_key(double v) {
     return a == a ? (unsigned long long)__double_as_longlong(a) : 0ull;
 }
 
-__global__ __launch_bounds__(64) void k_solve(SolveParams P) {
+__global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
     const WinDev &W = P.wins[blockIdx.x];
-    const int n = W.D, lane = threadIdx.x;
+    const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long pl = packed_len(n);
     const double *HA = P.sys + W.sys_base, *bA = HA + pl, *Hs = HA + pl + n, *bs = HA + 2 * pl + n;
     const int ld = solve_ld(n);
@@ -1552,20 +1552,24 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
     double *lr = Nm + 7 * (size_t)n;  // [n]: L(i,k) of the current step
     double *G = lr + n, *V = G + 49, *misc = V + 49;  // misc: ntx[7], coef[7]
     int *perm = reinterpret_cast<int *>(misc + 16);
-    // lower-triangle elements (i, j), j <= i, ordered by column j descending: the elements the
-    // LDL^T step k updates (k < j <= i) are exactly a prefix, so every step is element-parallel.
-    // Entry: the element's offset in H (16 bits) | i << 16 | j << 23 (n <= 92 < 128).
-    // Columns n-1, n-2, ... hold 1, 2, ... elements: e lies in column n-1-m with m(m+1)/2 <= e.
-    int *tri = perm + n;
-    const int ntri = n * (n + 1) / 2;
-    // one private dummy slot per lane: masked-off update elements land there (no branches)
-    double *dummy = reinterpret_cast<double *>(tri + ((ntri + 1) & ~1)) + lane;
-    for (int e = lane; e < ntri; e += 64) {
-        int m = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
-        while (m * (m + 1) / 2 > e) m--;
-        while ((m + 1) * (m + 2) / 2 <= e) m++;
-        const int j = n - 1 - m, rem = e - m * (m + 1) / 2;
-        tri[e] = ((j + rem) * ld + j) | ((j + rem) << 16) | (j << 23);  // LDS offset of (i, j) | i | j
+    // one private dummy slot per thread: masked-off update elements land there (no branches)
+    double *dummy = reinterpret_cast<double *>(perm + (n + 1) / 2 * 2) + tid;
+    // Strictly-lower elements (i, j), j < i, ordered by column j descending: the elements LDL^T
+    // step k updates (k < j < i) are exactly a prefix, so every step is element-parallel.  Wave w
+    // lane l always owns the elements e = l + 64 (w + 4 t).  Column n-2-mm holds mm+1 elements
+    // and starts at e = mm (mm + 1) / 2.  Entry: offset of (i, j) in H (16 bits) | i << 16 | j << 23.
+    constexpr int kWaves = kSolveThreads / 64;
+    constexpr int kOffRegs = ((kSolveMaxDim - 1) * kSolveMaxDim / 2 + 64 * kWaves - 1) / (64 * kWaves);
+    int tri[kOffRegs];
+    const int noff = n * (n - 1) / 2;
+#pragma unroll
+    for (int t = 0; t < kOffRegs; t++) {
+        const int e = lane + 64 * (wave + kWaves * t);
+        int mm = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
+        if (mm * (mm + 1) / 2 > e) mm--;
+        if ((mm + 1) * (mm + 2) / 2 <= e) mm++;
+        const int j = n - 2 - mm, i = j + 1 + (e - mm * (mm + 1) / 2);
+        tri[t] = e < noff ? ((i * ld + j) | (i << 16) | (j << 23)) : 0;  // padding: (0, 0), never stored
     }
     const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
     const double scl = 1.0f / (1 + lambda);
@@ -1579,29 +1583,29 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
         if (r == c) h *= (1 + lambda);
         return h - hs * scl;
     };
-    for (int i = lane; i < n; i += 64) {
+    for (int i = tid; i < n; i += kSolveThreads) {
         const long long q = pk_index(i, i, n);
         sc[i] = 1.0 / sqrt(element(i, i, HA[q], Hs[q]) + 10);
         perm[i] = i;
     }
-    wave_lds_sync();
-    for (int i = lane; i < n; i += 64) {
+    __syncthreads();
+    for (int i = tid; i < n; i += kSolveThreads) {
         const double bl = P.prior[2 * (W.vec_base + i) + 1];
         b[i] = (((bl + 0.0) + bA[i]) - bs[i] / (1 + lambda)) * sc[i];
     }
-    constexpr int kAsmBatch = 8;
+    constexpr int kAsmBatch = 4;
     const int n2 = 2 * n + 1;
-    for (int f0 = lane; f0 < pl; f0 += 64 * kAsmBatch) {
+    for (int f0 = tid; f0 < pl; f0 += kSolveThreads * kAsmBatch) {
         double ha[kAsmBatch], hs[kAsmBatch];
 #pragma unroll
         for (int u = 0; u < kAsmBatch; u++) {
-            const int f = f0 + 64 * u;
+            const int f = f0 + kSolveThreads * u;
             ha[u] = f < pl ? HA[f] : 0.0;
             hs[u] = f < pl ? Hs[f] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < kAsmBatch; u++) {
-            const int f = f0 + 64 * u;
+            const int f = f0 + kSolveThreads * u;
             if (f >= pl) break;
             // row r of the row-major packed upper triangle: r (2n - r + 1) / 2 <= f
             int r = (int)((n2 - sqrtf(fmaxf(0.0f, (float)(n2 * n2) - 8.0f * f))) * 0.5f);
@@ -1612,83 +1616,128 @@ __global__ __launch_bounds__(64) void k_solve(SolveParams P) {
             at(c, r) = element(r, c, ha[u], hs[u]) * (sc[c] * sc[r]);
         }
     }
-    wave_lds_sync();
-    // ---- LDL^T with symmetric diagonal pivoting (lower triangle)
+    __syncthreads();
+    // ---- LDL^T with symmetric diagonal pivoting (lower triangle).  Wave 0 runs the serial part
+    // of each step (pivot, swap, column k) with the diagonal in its registers (lane i mod 64); all
+    // waves then share the trailing update.
+    double dg0 = lane < n ? at(lane, lane) : 0.0, dg1 = lane + 64 < n ? at(lane + 64, lane + 64) : 0.0;
     for (int k = 0; k < n; k++) {
-        // pivot = first index of the largest |diag| (the host's strict '>' scan from k: a NaN
-        // never wins, except that a NaN at k itself keeps k)
-        int piv;
-        {
-            const int i0 = k + lane, i1 = k + 64 + lane;
-            const double v0 = at(min(i0, n - 1), min(i0, n - 1)), v1 = at(min(i1, n - 1), min(i1, n - 1));
-            const unsigned long long k0 = i0 >= n ? 0ull : (v0 != v0 && i0 == k) ? ~0ull : abs_key(v0);
-            const unsigned long long k1 = i1 < n ? abs_key(v1) : 0ull;
-            const unsigned long long mx = wave_max_u64(k0 > k1 ? k0 : k1);
-            const unsigned long long b0 = __ballot(i0 < n && k0 == mx);
-            piv = b0 ? k + __builtin_ctzll(b0) : k + 64 + __builtin_ctzll(__ballot(i1 < n && k1 == mx));
-        }
-        // symmetric swap k <-> piv (lower triangle: (k,j)<->(piv,j) for j < k, (i,k)<->(piv,i) for
-        // k < i < piv, (i,k)<->(i,piv) for i > piv, the two diagonals), fused with taking column k:
-        // col = the new A(i,k), lr = L(i,k) = col / d, written back as L
-        const double d = at(piv, piv), dkk = at(k, k);
-        if (piv != k)
-            for (int j = lane; j < k; j += 64) {
-                const double t = at(k, j), u = at(piv, j);
-                at(k, j) = u;
-                at(piv, j) = t;
+        if (wave == 0) {
+            // pivot = first index of the largest |diag| (the host's strict '>' scan from k: a NaN
+            // never wins, except that a NaN at k itself keeps k)
+            int piv;
+            {
+                const int i0 = lane, i1 = lane + 64;
+                const bool c0 = i0 >= k && i0 < n, c1 = i1 >= k && i1 < n;
+                const unsigned long long k0 = !c0 ? 0ull : (dg0 != dg0 && i0 == k) ? ~0ull : abs_key(dg0);
+                const unsigned long long k1 = !c1 ? 0ull : (dg1 != dg1 && i1 == k) ? ~0ull : abs_key(dg1);
+                const unsigned long long mx = wave_max_u64(k0 > k1 ? k0 : k1);
+                const unsigned long long b0 = __ballot(c0 && k0 == mx);
+                piv = b0 ? __builtin_ctzll(b0) : 64 + __builtin_ctzll(__ballot(c1 && k1 == mx));
             }
-        for (int i = k + 1 + lane; i < n; i += 64) {
-            double *own = &at(i, k);
-            double *src = piv == k || i == piv ? own : (i < piv ? &at(piv, i) : &at(i, piv));
-            const double old = *own, v = *src;
-            *(src != own ? src : dummy) = old;
-            const double l = d != 0 ? v / d : 0.0;
-            col[i] = v;
-            lr[i] = l;
-            *own = l;
+            // symmetric swap k <-> piv (lower triangle: (k,j)<->(piv,j) for j < k, (i,k)<->(piv,i)
+            // for k < i < piv, (i,k)<->(i,piv) for i > piv, the two diagonals), fused with taking
+            // column k: col = the new A(i,k), lr = L(i,k) = col / d, written back as L; the
+            // diagonal's share of the trailing update (A(i,i) -= L(i,k) col_i) happens here
+            const double dk = readlane_f64(k < 64 ? dg0 : dg1, k & 63);
+            const double d = readlane_f64(piv < 64 ? dg0 : dg1, piv & 63);
+            if (piv != k) {
+                if (lane == (k & 63)) (k < 64 ? dg0 : dg1) = d;
+                if (lane == (piv & 63)) (piv < 64 ? dg0 : dg1) = dk;
+                for (int j = lane; j < k; j += 64) {
+                    const double t = at(k, j), u = at(piv, j);
+                    at(k, j) = u;
+                    at(piv, j) = t;
+                }
+            }
+#pragma unroll
+            for (int sgm = 0; sgm < 2; sgm++) {
+                const int i = lane + 64 * sgm;
+                if (i <= k || i >= n) continue;
+                double *own = &at(i, k);
+                double *src = piv == k || i == piv ? own : (i < piv ? &at(piv, i) : &at(i, piv));
+                const double old = *own, v = *src;
+                *(src != own ? src : dummy) = old;
+                const double l = d != 0 ? v / d : 0.0;
+                col[i] = v;
+                lr[i] = l;
+                *own = l;
+                (sgm == 0 ? dg0 : dg1) -= l * v;
+            }
+            if (lane == 0 && piv != k) {
+                const int pt = perm[k];
+                perm[k] = perm[piv];
+                perm[piv] = pt;
+            }
         }
-        if (lane == 0 && piv != k) {
-            at(k, k) = d;
-            at(piv, piv) = dkk;
-            const int pt = perm[k];
-            perm[k] = perm[piv];
-            perm[piv] = pt;
-        }
-        wave_lds_sync();
-        const int m = (n - k - 1) * (n - k) / 2;  // elements with k < j <= i
-        constexpr int kUpdBatch = 8;
-        for (int e0 = lane; e0 < m; e0 += 64 * kUpdBatch) {
-            int ij[kUpdBatch];
+        __syncthreads();
+        const int m = (n - k - 2) * (n - k - 1) / 2;  // off-diagonal elements with k < j < i
+        constexpr int kUpdBatch = 6;
+#pragma unroll
+        for (int t0 = 0; t0 < kOffRegs; t0 += kUpdBatch) {
+            if (64 * (wave + kWaves * t0) >= m) continue;  // uniform per wave: chunks past the prefix
             double a[kUpdBatch], l[kUpdBatch], cj[kUpdBatch], *dst[kUpdBatch];
 #pragma unroll
-            for (int u = 0; u < kUpdBatch; u++) ij[u] = tri[min(e0 + 64 * u, m - 1)];
-#pragma unroll
             for (int u = 0; u < kUpdBatch; u++) {
-                const int off = ij[u] & 0xFFFF, i = (ij[u] >> 16) & 0x7F, j = ij[u] >> 23;
+                if (t0 + u >= kOffRegs) continue;
+                const int x = tri[t0 + u], off = x & 0xFFFF, i = (x >> 16) & 0x7F, j = x >> 23;
                 l[u] = lr[i];
                 cj[u] = col[j];
                 a[u] = H[off];
-                dst[u] = e0 + 64 * u < m ? H + off : dummy;
+                dst[u] = lane + 64 * (wave + kWaves * (t0 + u)) < m ? H + off : dummy;
             }
 #pragma unroll
-            for (int u = 0; u < kUpdBatch; u++) *dst[u] = a[u] - l[u] * cj[u];
+            for (int u = 0; u < kUpdBatch; u++) {
+                if (t0 + u >= kOffRegs) continue;
+                *dst[u] = a[u] - l[u] * cj[u];
+            }
         }
-        wave_lds_sync();
+        __syncthreads();
     }
-    // ---- substitutions (column by column, as the host); y[i] lives in lane i (mod 64)
-    const int ia = lane, ib = lane + 64;
+    if (wave != 0) return;  // the rest is one wavefront's work (wave-level synchronisation only)
+    if (lane < n) at(lane, lane) = dg0;
+    if (lane + 64 < n) at(lane + 64, lane + 64) = dg1;
+    wave_lds_sync();
+    // ---- substitutions (column by column, as the host); y[i] lives in lane i (mod 64); the
+    // matrix entries of the next 4 columns are loaded ahead of the dependent chain
+    const int ia = lane, ib = lane + 64, ra = min(ia, n - 1), rb = min(ib, n - 1);
     double ya = ia < n ? b[perm[ia]] : 0.0, yb = ib < n ? b[perm[ib]] : 0.0;
-    for (int j = 0; j < n; j++) {
-        const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
-        if (ia > j && ia < n) ya -= at(ia, j) * yj;
-        if (ib > j && ib < n) yb -= at(ib, j) * yj;
+    constexpr int kSubAhead = 4;
+    for (int j0 = 0; j0 < n; j0 += kSubAhead) {
+        double fa[kSubAhead], fb[kSubAhead];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = min(j0 + u, n - 1);
+            fa[u] = at(ra, j);
+            fb[u] = at(rb, j);
+        }
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = j0 + u;
+            if (j >= n) break;
+            const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+            if (ia > j && ia < n) ya -= fa[u] * yj;
+            if (ib > j && ib < n) yb -= fb[u] * yj;
+        }
     }
     if (ia < n) ya = at(ia, ia) != 0 ? ya / at(ia, ia) : 0.0;
     if (ib < n) yb = at(ib, ib) != 0 ? yb / at(ib, ib) : 0.0;
-    for (int j = n - 1; j >= 0; j--) {
-        const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
-        if (ia < j) ya -= at(j, ia) * yj;
-        if (ib < j) yb -= at(j, ib) * yj;
+    for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
+        double fa[kSubAhead], fb[kSubAhead];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = max(j0 - u, 0);
+            fa[u] = at(j, ra);
+            fb[u] = at(j, rb);
+        }
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = j0 - u;
+            if (j < 0) break;
+            const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+            if (ia < j) ya -= fa[u] * yj;
+            if (ib < j) yb -= fb[u] * yj;
+        }
     }
     if (ia < n) b[perm[ia]] = ya;
     if (ib < n) b[perm[ib]] = yb;
@@ -3175,7 +3224,7 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
         (void)hipFuncSetAttribute((const void *)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)solve_smem_bytes(kSolveMaxDim));
     });
-    int rc = timed_launch(c, 5, c->stream, [&] { k_solve<<<c->n_win, 64, smem, c->stream>>>(S); });
+    int rc = timed_launch(c, 5, c->stream, [&] { k_solve<<<c->n_win, kSolveThreads, smem, c->stream>>>(S); });
     if (rc) return rc;
     if (x_out) {
         HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,

@@ -11,6 +11,6 @@ import json; d=json.load(open('gpurun_out/bench_$TAG.json'))
 print('value %.3e res/s  ms/step %.4f' % (d['value'], d['ms_per_step']))
 print('kernels', {k: round(v*1e3,1) for k,v in d['kernel_ms_per_step'].items()})
 print('roofline frac %.3f achieved %.0f GB/s' % (d['roofline']['frac'], d['roofline']['achieved']))
-print('single', d['single_window'], 'ms/solve', d['ms_per_solve'])
+print('single', d['single_window'])
 print('gn batched', d.get('gn_iteration_batched'))
 "
