@@ -92,6 +92,8 @@ def main():
         dist = tdist
     import torch
 
+    # torch's bundled HIP runtime must initialise before the one libldso_ba.so links
+    torch.cuda.set_device(local_rank)
     from ldso_amd import BAContext, synth
 
     B, N, P = args.windows, args.frames, args.points

@@ -18,3 +18,18 @@ def built():
     import __graft_entry__ as g
     g.build_native()
     return True
+
+
+@pytest.fixture(scope="session", autouse=True)
+def torch_hip_first():
+    """torch ships its own HIP/HSA runtime next to the system one libldso_ba.so links; when both
+    live in one process, torch's must initialise first or its device enumeration comes back
+    empty.  Tests that hand torch buffers to the C ABI rely on this ordering."""
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:  # CPU container: nothing to order
+        pass
+    yield
