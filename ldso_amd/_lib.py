@@ -13,7 +13,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libldso_ba.so")
+LIB_PATH = os.environ.get("LDSO_BA_LIB") or os.path.join(LIB_DIR, "libldso_ba.so")  # override: A/B builds only
 SYNTH_PATH = os.path.join(LIB_DIR, "libldso_synth.so")
 
 PATTERN_NUM = 8

@@ -1136,6 +1136,8 @@ struct StitchParams {
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
     int pair_base;  // first global pair of this launch
+    int win_base;   // first window of this launch
+    int n_win;      // windows of this launch: blocks [0, n_win) run their setNewFrameEnergyTH
 };
 
 __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row <= col
@@ -1307,15 +1309,17 @@ __device__ __forceinline__ double g_elem(const float *__restrict__ slab, int n_i
 
 __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     extern __shared__ double sm[];  // sized on the host for the largest window (stitch_smem_bytes)
-    const int pair = P.pair_base + blockIdx.x;
+    if ((int)blockIdx.x < P.n_win) {  // the longest single-block chain goes first in the grid
+        const int w = P.win_base + blockIdx.x;
+        frame_threshold_and_energy(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
+        return;
+    }
+    const int pair = P.pair_base + blockIdx.x - P.n_win;
     const int w = P.pair_win[pair];
     const WinDev &W = P.wins[w];
     const int N = W.N, D = W.D, aidx = pair - W.pair_base, h = aidx % N, t = aidx / N;
     const int tid = threadIdx.x;
-    if (h == t) {
-        if (aidx == 0) frame_threshold_and_energy(P, W, w, reinterpret_cast<unsigned *>(sm));
-        return;
-    }
+    if (h == t) return;
     if (!P.accumulate) return;
     double *sys = P.sys + W.sys_base;
     const long long pl = packed_len(D);
@@ -2957,7 +2961,9 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
             if (rc) return rc;
         }
         Sp.pair_base = p0;
-        rc = timed_launch(c, 2, st, [&] { k_stitch<<<p1 - p0, kStThreads, st_smem, st>>>(Sp); });
+        Sp.win_base = w0;
+        Sp.n_win = w1 - w0;
+        rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + p1 - p0, kStThreads, st_smem, st>>>(Sp); });
         if (rc) return rc;
     }
     if (G > 1) {  // join: the context stream orders everything that follows

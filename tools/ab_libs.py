@@ -1,0 +1,65 @@
+"""A/B whole library builds on the bench workload: each build runs in its own process
+(LDSO_BA_LIB=<path>), k_linearize / per-kernel HIP-event times, rounds interleaved.
+  python tools/ab_libs.py lib1.so lib2.so ... [--windows 64] [--rounds 3]"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import json, os, sys
+sys.path.insert(0, ROOT)
+import torch
+torch.cuda.init()
+from ldso_amd import BAContext, synth
+B = WINDOWS
+ws = [synth.make_window(**synth.S7, seed=1000 + i) for i in range(B)]
+c = BAContext(0)
+c.load(ws)
+for _ in range(3):
+    c.linearize()
+out = {}
+for acc in (True, False):
+    c.linearize(accumulate=acc)
+    c.set_kernel_timing(True)
+    for _ in range(20):
+        c.linearize(accumulate=acc)
+    c.sync()
+    kt = c.kernel_times()
+    c.set_kernel_timing(False)
+    out["acc" if acc else "noacc"] = {k: 1e3 * v[0] / v[1] for k, v in kt.items() if v[1]}
+print("RESULT " + json.dumps(out))
+'''
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--windows", type=int, default=64)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    code = CHILD.replace("ROOT", repr(ROOT)).replace("WINDOWS", str(a.windows))
+    res = {l: [] for l in a.libs}
+    for _ in range(a.rounds):
+        for l in a.libs:
+            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(l))
+            p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+            line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
+            if p.returncode != 0 or not line:
+                print(l, "FAILED", p.returncode, p.stderr[-2000:])
+                sys.exit(1)
+            res[l].append(json.loads(line[0][7:]))
+    for l, rs in res.items():
+        best = {}
+        for r in rs:
+            for mode, kt in r.items():
+                for k, v in kt.items():
+                    best[(mode, k)] = min(best.get((mode, k), 1e9), v)
+        print(os.path.basename(l), " ".join(f"{m}:{k}={v:.1f}us" for (m, k), v in sorted(best.items())))
+
+
+if __name__ == "__main__":
+    main()
