@@ -122,6 +122,27 @@ ABI = [
     ("ldso_ba_stats", C.c_int, [C.c_void_p, i64p, i64p, i64p]),
 ]
 
+f32pp = C.POINTER(f32p)
+
+# (name, restype, argtypes) of every entry point declared in include/ldso_ct.h (coarse tracker)
+CT_ABI = [
+    ("ldso_ct_create", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p), i32p]),
+    ("ldso_ct_destroy", None, [C.c_void_p]),
+    ("ldso_ct_make_k", C.c_int, [C.c_void_p, f32p, f32p]),
+    ("ldso_ct_set_new_frame", C.c_int, [C.c_void_p, f32p, C.c_double, f32p]),
+    ("ldso_ct_get_frame_level", C.c_int, [C.c_void_p, C.c_int32, f32p, f32p]),
+    ("ldso_ct_set_reference", C.c_int,
+     [C.c_void_p, i32p, f32pp, f32pp, f32pp, f32pp, C.c_double, C.c_double, C.c_double]),
+    ("ldso_ct_calc_res", C.c_int, [C.c_void_p, C.c_int32, f64p, C.c_double, C.c_double, C.c_float, f64p]),
+    ("ldso_ct_calc_res_batch", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, f64p, f64p, C.c_float, f64p]),
+    ("ldso_ct_calc_gs", C.c_int, [C.c_void_p, C.c_int32, f64p, C.c_double, C.c_double, f64p, f64p]),
+    ("ldso_ct_get_warped", C.c_int, [C.c_void_p, i32p, f32p, C.c_int32]),
+    ("ldso_ct_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
+    ("ldso_ct_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),
+    ("ldso_ct_kernel_name", C.c_char_p, [C.c_int32]),
+    ("ldso_ct_num_kernels", C.c_int32, []),
+]
+
 _lib = None
 _synth = None
 
@@ -135,7 +156,7 @@ def lib():
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(make -C ldso_amd/csrc). The HIP path has no CPU fallback.")
         L = C.CDLL(LIB_PATH)
-        for name, res, args in ABI:
+        for name, res, args in ABI + CT_ABI:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -57,6 +57,14 @@ int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
 }
+
+}  // namespace
+
+namespace ldso_ba {
+int set_error(int code, const std::string &msg) { return fail(code, msg); }
+}  // namespace ldso_ba
+
+namespace {
 #define HIP_TRY(expr)                                                                              \
     do {                                                                                           \
         hipError_t e_ = (expr);                                                                    \

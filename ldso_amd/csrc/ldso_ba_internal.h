@@ -1,6 +1,8 @@
 // ldso_ba_internal.h -- constants of the hot path (include/Settings.h, src/Setting.cc) and
 // host-side helpers shared by the C ABI translation units.
 #pragma once
+#include <string>
+
 #include "../../include/ldso_ba.h"
 
 #if defined(__HIP__)
@@ -81,6 +83,9 @@ LDSO_HD inline bool gram_inverse_coef7(const double (&G)[7][7], const double (&n
     }
     return true;
 }
+
+// the ldso_ba_last_error() message of this thread; returns code
+int set_error(int code, const std::string &msg);
 
 int frame_precalc(int N, const ldso_ba_frame_state *fr, const float calib[4], float *out);
 int set_adjoints(int N, const ldso_ba_frame_state *fr, double *adH, double *adT, double *cPrior);

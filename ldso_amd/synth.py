@@ -62,3 +62,53 @@ def make_window(n_frames=7, n_points=2000, width=640, height=480, seed=0, outlie
     if finalize:
         w.refresh_frame_terms()
     return w
+
+
+def make_tracker_scene(width=640, height=480, n_points=(8000, 4000, 2000, 1000, 500, 250), seed=0, blobs=64):
+    """A coarse-tracking scene: a smooth textured reference image (sum of
+    Gaussian blobs, [0, 255] float, the same family as §8d's frames) and per-level reference point
+    clouds at integer pixel positions of that level, as CoarseTracker::makeCoarseDepthL0 emits
+    them (CoarseTracker.cc:357-538), with the level's pyramid intensity as pc_color.  The caller
+    supplies the level intensities (``level_images``, e.g. FrameHessian::makeImages' output) so
+    pc_color is exact; idepth ~ U(0.3, 1.5).  Returns (color [h][w], make_pc(level_images))."""
+    rng = np.random.default_rng(0x1D50 + int(seed))
+    yy, xx = np.mgrid[0:height, 0:width].astype(np.float64)
+    img = np.full((height, width), 90.0)
+    for _ in range(int(blobs)):
+        cx, cy = rng.uniform(0, width), rng.uniform(0, height)
+        s = rng.uniform(4, 40) * width / 640
+        a = rng.uniform(20, 120) * rng.choice([-1, 1])
+        img += a * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * s * s))
+    color = np.clip(img, 0, 255).astype(np.float32)
+
+    def make_pc(level_images):
+        pcs = []
+        for l, I in enumerate(level_images):
+            wl, hl = width >> l, height >> l
+            n = min(int(n_points[min(l, len(n_points) - 1)]), (wl - 4) * (hl - 4))
+            idx = rng.choice((wl - 4) * (hl - 4), size=n, replace=False)
+            u = (idx % (wl - 4) + 2).astype(np.float32)
+            v = (idx // (wl - 4) + 2).astype(np.float32)
+            col = np.asarray(I, np.float32).reshape(-1)[(v.astype(np.int64) * wl + u.astype(np.int64))]
+            idepth = rng.uniform(0.3, 1.5, n).astype(np.float32)
+            pcs.append(dict(u=u, v=v, idepth=idepth, color=col))
+        return pcs
+
+    return color, make_pc
+
+
+def se3_matrix(omega, upsilon):
+    """Sophus::SE3::exp((upsilon, omega)).matrix3x4() (se3.hpp: translation first), in double."""
+    w = np.asarray(omega, np.float64)
+    th = np.linalg.norm(w)
+    W = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+    if th < 1e-10:
+        R = np.eye(3) + W
+        V = np.eye(3) + 0.5 * W
+    else:
+        R = np.eye(3) + np.sin(th) / th * W + (1 - np.cos(th)) / th ** 2 * W @ W
+        V = np.eye(3) + (1 - np.cos(th)) / th ** 2 * W + (th - np.sin(th)) / th ** 3 * W @ W
+    T = np.zeros((3, 4))
+    T[:, :3] = R
+    T[:, 3] = V @ np.asarray(upsilon, np.float64)
+    return T

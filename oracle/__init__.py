@@ -60,6 +60,12 @@ def lib():
             "oracle_frame_take_data": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p]),
             "oracle_nullspaces": (C.c_int, [C.c_int, C.c_void_p, f64p]),
             "oracle_time_iterations": (C.c_double, [C.c_void_p, C.c_int]),
+            "oracle_ct_levels": (C.c_int, [C.c_int, C.c_int]),
+            "oracle_ct_make_k": (None, [f32p, C.c_int, C.c_int, C.c_int, f32p]),
+            "oracle_make_images": (None, [f32p, C.c_int, C.c_int, C.c_int, f32p, f32p, f32p]),
+            "oracle_ct_calc_res": (C.c_int, [C.c_int, C.c_int, C.c_int, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p,
+                                             f64p, f64p, C.c_float, f64p, f32p, i32p]),
+            "oracle_ct_calc_gs": (C.c_int, [C.c_int, f32p, C.c_float, C.c_float, f64p, f64p, f64p]),
         }
         for k, (res, args) in sig.items():
             f = getattr(Lb, k)
@@ -198,3 +204,59 @@ def frame_terms(window):
     lib().oracle_nullspaces(N, fr.ctypes.data, _p(ns, f64p))
     return dict(precalc=pre, ad_host=adH, ad_target=adT, c_prior=cp, frame_prior=prior, frame_delta=delta,
                 frame_delta_prior=dprior, nullspaces=ns)
+
+
+# ---- coarse tracker (ldso_oracle_tracker.cpp): the checker of include/ldso_ct.h -------------
+def ct_levels(w, h):
+    return int(lib().oracle_ct_levels(int(w), int(h)))
+
+
+def ct_make_k(calib, w, h):
+    L = ct_levels(w, h)
+    out = np.zeros((L, 13), np.float32)
+    lib().oracle_ct_make_k(_p(np.ascontiguousarray(calib, np.float32), f32p), int(w), int(h), L, _p(out, f32p))
+    return out
+
+
+def make_images(color, w, h, b_response=None):
+    """FrameHessian::makeImages: per level (dI [wl*hl][3], absSquaredGrad [wl*hl])."""
+    L = ct_levels(w, h)
+    tot = sum((w >> l) * (h >> l) for l in range(L))
+    dIp = np.zeros((tot, 3), np.float32)
+    ag = np.zeros(tot, np.float32)
+    B = None if b_response is None else np.ascontiguousarray(b_response, np.float32)
+    lib().oracle_make_images(_p(np.ascontiguousarray(color, np.float32).reshape(-1), f32p), int(w), int(h), L,
+                             _p(B, f32p), _p(dIp, f32p), _p(ag, f32p))
+    out, off = [], 0
+    for l in range(L):
+        n = (w >> l) * (h >> l)
+        out.append((dIp[off:off + n], ag[off:off + n]))
+        off += n
+    return out
+
+
+def ct_calc_res(lvl, wl, hl, kl, dI, pc, T, aff6, cutoff_th):
+    """CoarseTracker::calcRes -> (rs[6], warped [buf_warped_n][8])."""
+    u, v, idp, col = [np.ascontiguousarray(a, np.float32).reshape(-1) for a in pc]
+    n = u.size
+    rs = np.zeros(6, np.float64)
+    warped = np.zeros((n + 4, 8), np.float32)
+    nw = C.c_int32()
+    Tm = np.ascontiguousarray(np.asarray(T, np.float64)[:3, :4])
+    lib().oracle_ct_calc_res(int(lvl), int(wl), int(hl), _p(np.ascontiguousarray(kl, np.float32), f32p),
+                             _p(np.ascontiguousarray(dI, np.float32), f32p), n, _p(u, f32p), _p(v, f32p),
+                             _p(idp, f32p), _p(col, f32p), _p(Tm, f64p),
+                             _p(np.ascontiguousarray(aff6, np.float64), f64p), float(cutoff_th), _p(rs, f64p),
+                             _p(warped, f32p), C.byref(nw))
+    return rs, warped[:nw.value].copy()
+
+
+def ct_calc_gs(warped, fxl, fyl, aff6):
+    """CoarseTracker::calcGSSSE (Accumulator9 in SSE lane order) -> (H 8x8, b 8)."""
+    H = np.zeros((8, 8), np.float64)
+    b = np.zeros(8, np.float64)
+    w = np.ascontiguousarray(warped, np.float32)
+    rc = lib().oracle_ct_calc_gs(int(w.shape[0]), _p(w, f32p), float(fxl), float(fyl),
+                                 _p(np.ascontiguousarray(aff6, np.float64), f64p), _p(H, f64p), _p(b, f64p))
+    assert rc == 0
+    return H, b

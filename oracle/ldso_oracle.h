@@ -74,6 +74,19 @@ int oracle_frame_take_data(int n_frames, const ldso_ba_frame_state *frames, doub
  * out [7][8N+4] in the order orthogonalize() stacks them. */
 int oracle_nullspaces(int n_frames, const ldso_ba_frame_state *frames, double *out);
 
+/* ---- coarse tracker (ldso_oracle_tracker.cpp; the checker of include/ldso_ct.h) ---------- */
+int oracle_ct_levels(int w, int h);
+/* per level 13 floats {fx, fy, cx, cy, Ki[9]} */
+void oracle_ct_make_k(const float calib[4], int w, int h, int levels, float *out);
+/* dIp: all levels concatenated, [wl*hl][3] each; absg: [wl*hl] each; B: response (NULL = none) */
+void oracle_make_images(const float *color, int w, int h, int levels, const float *B, float *dIp, float *absg);
+/* aff6 = {ref exposure, new exposure, ref a, ref b, new a, new b}; T = refToNew 3x4 row-major */
+int oracle_ct_calc_res(int lvl, int wl, int hl, const float *kl, const float *dI, int n, const float *pc_u,
+                       const float *pc_v, const float *pc_idepth, const float *pc_color, const double *T,
+                       const double *aff6, float cutoffTH, double *rs, float *warped_out, int *n_warped);
+int oracle_ct_calc_gs(int n, const float *warped, float fxl, float fyl, const double *aff6, double *H_out,
+                      double *b_out);
+
 /* CPU-baseline timing: run `iters` oracle_iteration passes, return wall seconds. */
 double oracle_time_iterations(oracle_window *ow, int iters);
 

@@ -16,12 +16,13 @@ from ldso_amd import synth
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "ldso_ba.h")
+CT_HEADER = os.path.join(ROOT, "include", "ldso_ct.h")
 
 
-def declared_symbols():
-    txt = open(HEADER).read()
+def declared_symbols(header=HEADER, prefix="ldso_ba_"):
+    txt = open(header).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(ldso_ba_[a-z0-9_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(" + prefix + r"[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exports_every_declared_symbol(built):
@@ -36,6 +37,19 @@ def test_library_exports_every_declared_symbol(built):
     lib = L.lib()
     assert lib.ldso_ba_abi_version() == 1
     assert lib.ldso_ba_num_kernels() >= 3
+
+
+def test_library_exports_every_tracker_symbol(built):
+    syms = declared_symbols(CT_HEADER, "ldso_ct_")
+    assert len(syms) >= 14
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (ldso_ct_\w+)", out))
+    assert not [s for s in syms if s not in exported]
+    assert set(syms) == {name for name, _, _ in L.CT_ABI}
+    lib = L.lib()
+    assert lib.ldso_ct_num_kernels() == 4 and lib.ldso_ct_kernel_name(2) == b"k_ct_calc_res"
+    h = C.c_void_p()
+    assert lib.ldso_ct_create(0, 4, 4, C.byref(h), None) < 0 and b"small" in lib.ldso_ba_last_error()
 
 
 def test_library_is_gfx950_only(built, tmp_path):
