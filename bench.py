@@ -66,6 +66,82 @@ def cpu_baseline(seconds=10.0, threads=6):
                       f"accumulate{{AF,LF,SCF}}+stitch in {el:.1f} s, {threads}-thread IndexThreadReduce"}
 
 
+def tracker_leg(device, reps=50, n_hyp=32, cpu_seconds=2.0, with_cpu=True):
+    """Coarse tracker (include/ldso_ct.h) on a 640x480 frame with the
+    reference point clouds of synth.make_tracker_scene (8000 level-0 points):
+    * lm_iteration: one calcRes + calcGSSSE at level 0, what each LM iteration of
+      CoarseTracker::trackNewestCoarse calls (CoarseTracker.cc:61-310), host clock, results on
+      the host;
+    * hypotheses: calcRes of n_hyp motion hypotheses in one launch (FullSystem::trackNewCoarse's
+      tries, FullSystem.cc:282-386), point-evaluations/s;
+    * k_ct_calc_res roofline: 48 B (4 bilinear taps x 12-B [I, dx, dy]) per point-evaluation
+      + 16 B per point per launch, over its mean HIP-event duration;
+    * cpu: the oracle's calcRes + calcGSSSE (single thread, as the reference's tracker) on the
+      same level-0 cloud."""
+    from ldso_amd import synth
+    from ldso_amd.tracker import CoarseTracker
+
+    w, h = 640, 480
+    calib = np.array([384.0, 432.0, 319.5, 239.5], np.float32)
+    color, make_pc = synth.make_tracker_scene(w, h, seed=0)
+    ct = CoarseTracker(w, h, device)
+    ct.make_k(calib)
+    ct.set_new_frame(color, 1.0)
+    pcs = make_pc([ct.frame_level(l)[0][:, 0] for l in range(ct.levels)])
+    ct.set_reference([(p["u"], p["v"], p["idepth"], p["color"]) for p in pcs], 1.0, (0.02, 3.0))
+    rng = np.random.default_rng(3)
+    Ts = np.stack([synth.se3_matrix(rng.normal(0, 2e-3, 3), rng.normal(0, 1e-2, 3)) for _ in range(n_hyp)])
+    ab = np.tile([0.05, 1.0], (n_hyp, 1))
+    n0 = int(pcs[0]["u"].size)
+    for _ in range(5):
+        ct.calc_res(0, Ts[0], ab[0])
+        ct.calc_gs(0, Ts[0], ab[0])
+        ct.calc_res_batch(0, Ts, ab)
+    t0 = time.perf_counter()
+    for i in range(reps):
+        ct.calc_res(0, Ts[i % n_hyp], ab[0])
+        ct.calc_gs(0, Ts[i % n_hyp], ab[0])
+    lm_ms = 1e3 * (time.perf_counter() - t0) / reps
+    ct.set_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ct.calc_res_batch(0, Ts, ab)
+    hyp_ms = 1e3 * (time.perf_counter() - t0) / reps
+    kt = ct.kernel_times()
+    ct.set_kernel_timing(False)
+    k_ms, k_n = kt["k_ct_calc_res"]
+    k_s = k_ms / max(1, k_n) / 1e3
+    algo = n_hyp * n0 * 48.0 + n0 * 16.0
+    out = {
+        "frame": "640x480, 4 levels", "points_level0": n0,
+        "lm_iteration": {"ms": lm_ms, "calls": "calcRes + calcGSSSE, level 0"},
+        "hypotheses": {"n_hyp": n_hyp, "ms_per_launch_host": hyp_ms,
+                       "point_evals_per_s": n_hyp * n0 / (hyp_ms / 1e3)},
+        "k_ct_calc_res": {"avg_launch_us": k_s * 1e6, "algo_bytes_per_launch": algo,
+                          "achieved_GBps": algo / k_s / 1e9 if k_s > 0 else None,
+                          "frac_of_hbm_peak": algo / k_s / 1e9 / HBM_PEAK_GBS if k_s > 0 else None},
+    }
+    ct.close()
+    if with_cpu:
+        import oracle
+
+        lv = oracle.make_images(color, w, h)
+        K = oracle.ct_make_k(calib, w, h)
+        aff6 = (1.0, 1.0, 0.02, 3.0, 0.05, 1.0)
+        pc = (pcs[0]["u"], pcs[0]["v"], pcs[0]["idepth"], pcs[0]["color"])
+        n, el = 0, 0.0
+        while el < cpu_seconds:
+            t0 = time.perf_counter()
+            rs, warped = oracle.ct_calc_res(0, w, h, K[0], lv[0][0], pc, Ts[n % n_hyp], aff6, 20.0)
+            oracle.ct_calc_gs(warped, K[0, 0], K[0, 1], aff6)
+            el += time.perf_counter() - t0
+            n += 1
+        out["cpu_lm_iteration"] = {"ms": 1e3 * el / n, "cores": 1, "kind": "port",
+                                   "sample": f"{n} oracle calcRes + calcGSSSE at level 0 ({n0} points)"}
+        out["lm_iteration_speedup_vs_cpu"] = out["cpu_lm_iteration"]["ms"] / lm_ms
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,6 +153,7 @@ def main():
     ap.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-tracker", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -230,6 +307,10 @@ def main():
                   "ms_per_gn_iteration_host_solve": ms_solve, "ms_per_gn_iteration_device_solve": ms_solve_dev}
         c1.close()
 
+    tracker = None
+    if rank == 0 and not args.no_tracker:
+        tracker = tracker_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_seconds)
@@ -272,6 +353,7 @@ def main():
             "kernel_ms_per_step": {k: v[0] / max(1, v[1]) for k, v in kall.items() if v[1]},
             "gn_iteration_batched": gn,
             "single_window": single,
+            "tracker": tracker,
             "cpu_baseline": cpu,
         }
         if cpu is not None:
