@@ -140,6 +140,15 @@ int ldso_ba_nullspaces(int32_t n_frames, const ldso_ba_frame_state *frames, doub
  * point).  Returns 0 or a negative code with ldso_ba_last_error() set. */
 int ldso_ba_validate_window(const ldso_ba_window *w);
 
+/* EnergyFunctional::marginalizeFrame (EnergyFunctional.cc:109-191), the dense part: frame idx's
+ * 8 rows/columns of HM, bM (dimension 8N+4, row-major) are moved to the end, its prior
+ * (FrameHessian::prior, delta_prior [8]) added, the block Schur-complemented out after
+ * Jacobi scaling with MatrixInverter::invertPosDef (pseudo-inverse) and the result symmetrised.
+ * Outputs HM_out (8(N-1)+4)^2 and bM_out 8(N-1)+4. */
+int ldso_ba_marginalize_frame(int32_t n_frames, int32_t idx, const double *HM, const double *bM,
+                              const double *prior, const double *delta_prior, double *HM_out,
+                              double *bM_out);
+
 /* ---- device context --------------------------------------------------------------- */
 
 /* Create a context on HIP device `device` with its own non-blocking stream. */
@@ -163,6 +172,23 @@ int ldso_ba_update(ldso_ba_ctx *ctx, int32_t win, const ldso_ba_window *w);
 
 /* PointFrameResidual::resetOOB for every residual of window win (win < 0: all windows). */
 int ldso_ba_reset_oob(ldso_ba_ctx *ctx, int32_t win);
+
+/* Point marginalisation.  `marg` is a context of its own whose single
+ * window holds the points being marginalised (FullSystem::flagPointsForRemoval's MARGINALIZED
+ * points, FullSystem.cc:1384-1404) and their residuals; its frames are window parent_win of
+ * `parent`, whose device images are borrowed (points->dI may be NULL; the parent must stay
+ * loaded while marg is used).  priorF is scaled by setting_idepthFixPriorMargFac at load
+ * (EnergyFunctional.cc:216). */
+int ldso_ba_load_marginalization(ldso_ba_ctx *marg, const ldso_ba_ctx *parent, int32_t parent_win,
+                                 const ldso_ba_window *points);
+/* For every residual: resetOOB, linearize, applyRes(true) and, if active, fixLinearizationF
+ * (FullSystem.cc:1390-1398, Residuals.cc:219-245); then AccumulatedTopHessianSSE::addPoint<2> and
+ * AccumulatedSCHessianSSE::addPoint(p, false) with both stitches (EnergyFunctional.cc:226-243).
+ * ad_ht_delta: EnergyFunctional::adHTdeltaF [N*N][8] (float, index h + N t).  Outputs
+ * H = M - Msc ((8N+4)^2, full symmetric) and b = Mb - Mbsc; the caller adds
+ * setting_margWeightFac * (H, b) to (HM, bM) (EnergyFunctional.cc:254-255).  Residual states and
+ * points of `marg` are readable with get_residuals / get_points as after a pass. */
+int ldso_ba_marginalize_points(ldso_ba_ctx *marg, const float *ad_ht_delta, double *H, double *b);
 
 /* One hot-path pass over all loaded windows, asynchronous on the context stream:
  *   linearizeAll(fix) + applyRes(true) + setNewFrameEnergyTH, and if accumulate != 0

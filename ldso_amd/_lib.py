@@ -120,6 +120,9 @@ ABI = [
     ("ldso_ba_kernel_name", C.c_char_p, [C.c_int32]),
     ("ldso_ba_num_kernels", C.c_int32, []),
     ("ldso_ba_stats", C.c_int, [C.c_void_p, i64p, i64p, i64p]),
+    ("ldso_ba_marginalize_frame", C.c_int, [C.c_int32, C.c_int32, f64p, f64p, f64p, f64p, f64p, f64p]),
+    ("ldso_ba_load_marginalization", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(LdsoBaWindow)]),
+    ("ldso_ba_marginalize_points", C.c_int, [C.c_void_p, f32p, f64p, f64p]),
 ]
 
 f32pp = C.POINTER(f32p)

@@ -49,6 +49,26 @@ class BAContext:
             w._keep = []  # host copies are no longer referenced by the device
         return self
 
+    def load_marginalization(self, parent: "BAContext", parent_win: int, window: Window):
+        """Make this context the marginalisation context of `parent`'s window `parent_win` for the
+        points (and residuals) of `window` (ldso_ba_load_marginalization: images are borrowed)."""
+        self.windows = [window]
+        s = window.c_struct(with_images=False)
+        L.check(self._lib.ldso_ba_load_marginalization(self._h, parent._h, int(parent_win), C.byref(s)))
+        self._structs = s
+        self._parent = parent  # the borrowed images must outlive this context
+        window._keep = []
+        return self
+
+    def marginalize_points(self, ad_ht_delta):
+        """ldso_ba_marginalize_points -> (H, b) = (M - Msc, Mb - Mbsc) (EnergyFunctional.cc:226-243)."""
+        n = self.windows[0].dim
+        H = np.zeros((n, n), np.float64)
+        b = np.zeros(n, np.float64)
+        adh = np.ascontiguousarray(ad_ht_delta, np.float32)
+        L.check(self._lib.ldso_ba_marginalize_points(self._h, L.ptr(adh, L.f32p), L.ptr(H, L.f64p), L.ptr(b, L.f64p)))
+        return H, b
+
     def update(self, win: int, window: Window):
         s = window.c_struct()
         L.check(self._lib.ldso_ba_update(self._h, int(win), C.byref(s)))

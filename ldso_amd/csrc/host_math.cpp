@@ -458,4 +458,123 @@ int solve_system(int N, int iteration, double lambda, const double *HA, const do
     return 0;
 }
 
+namespace {
+// util::MatrixInverter::invertPosDef, non-fast branch (src/util/MatrixInverter.cc:25-51): Jacobi
+// scaling, pseudo-inverse of the scaled symmetric matrix (the SVD of a symmetric matrix has
+// V diag(1/sigma) U^T = sum over non-zero eigenvalues of q q^T / lambda), scaling undone.
+// M is read as selfadjointView<Upper>; the full symmetric inverse is returned.
+void invert_pos_def(int n, const double *M, double *out) {
+    std::vector<double> s(n), A((size_t)n * n), V((size_t)n * n, 0.0);
+    for (int i = 0; i < n; i++) s[i] = 1.0 / std::sqrt(std::fabs(M[(size_t)i * n + i]) + 10);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            const double m = i <= j ? M[(size_t)i * n + j] : M[(size_t)j * n + i];
+            A[(size_t)i * n + j] = s[i] * m * s[j];
+        }
+    for (int i = 0; i < n; i++) V[(size_t)i * n + i] = 1;
+    for (int sweep = 0; sweep < 100; sweep++) {  // cyclic Jacobi
+        double off = 0, diag = 0;
+        for (int p = 0; p < n; p++) {
+            diag += A[(size_t)p * n + p] * A[(size_t)p * n + p];
+            for (int q = p + 1; q < n; q++) off += A[(size_t)p * n + q] * A[(size_t)p * n + q];
+        }
+        if (off <= 1e-32 * diag) break;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) {
+                const double apq = A[(size_t)p * n + q];
+                if (apq == 0) continue;
+                const double th = (A[(size_t)q * n + q] - A[(size_t)p * n + p]) / (2 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1));
+                const double c = 1 / std::sqrt(t * t + 1), sn = t * c;
+                for (int k = 0; k < n; k++) {
+                    const double akp = A[(size_t)k * n + p], akq = A[(size_t)k * n + q];
+                    A[(size_t)k * n + p] = c * akp - sn * akq;
+                    A[(size_t)k * n + q] = sn * akp + c * akq;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double apk = A[(size_t)p * n + k], aqk = A[(size_t)q * n + k];
+                    A[(size_t)p * n + k] = c * apk - sn * aqk;
+                    A[(size_t)q * n + k] = sn * apk + c * aqk;
+                    const double vkp = V[(size_t)k * n + p], vkq = V[(size_t)k * n + q];
+                    V[(size_t)k * n + p] = c * vkp - sn * vkq;
+                    V[(size_t)k * n + q] = sn * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            double acc = 0;
+            for (int e = 0; e < n; e++) {
+                const double lam = A[(size_t)e * n + e];
+                if (lam != 0) acc += V[(size_t)i * n + e] * V[(size_t)j * n + e] / lam;
+            }
+            out[(size_t)i * n + j] = s[i] * acc * s[j];
+        }
+}
+}  // namespace
+
+// EnergyFunctional::marginalizeFrame (EnergyFunctional.cc:109-191), HM / bM part
+int marginalize_frame(int N, int idx, const double *HM, const double *bM, const double *prior,
+                      const double *delta_prior, double *HM_out, double *bM_out) {
+    const int odim = 8 * N + 4, ndim = odim - 8;
+    std::vector<double> H(HM, HM + (size_t)odim * odim), b(bM, bM + odim);
+    if (idx != N - 1) {  // move frame idx's rows and columns to the end, :120-139
+        const int io = idx * 8 + 4;
+        std::vector<int> order;  // new position -> old index
+        for (int i = 0; i < io; i++) order.push_back(i);
+        for (int i = io + 8; i < odim; i++) order.push_back(i);
+        for (int i = io; i < io + 8; i++) order.push_back(i);
+        std::vector<double> H2((size_t)odim * odim), b2(odim);
+        for (int i = 0; i < odim; i++) {
+            b2[i] = b[order[i]];
+            for (int j = 0; j < odim; j++) H2[(size_t)i * odim + j] = H[(size_t)order[i] * odim + order[j]];
+        }
+        H.swap(H2);
+        b.swap(b2);
+    }
+    for (int i = 0; i < 8; i++) {  // the frame's prior, :143-144
+        H[(size_t)(ndim + i) * odim + ndim + i] += prior[i];
+        b[ndim + i] += prior[i] * delta_prior[i];
+    }
+    std::vector<double> sv(odim), svi(odim);
+    for (int i = 0; i < odim; i++) {
+        sv[i] = std::sqrt(std::fabs(H[(size_t)i * odim + i]) + 10);
+        svi[i] = 1.0 / sv[i];
+    }
+    for (int i = 0; i < odim; i++) {
+        b[i] *= svi[i];
+        for (int j = 0; j < odim; j++) H[(size_t)i * odim + j] *= svi[i] * svi[j];
+    }
+    double hp[64], hpi[64];
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 8; j++) hp[i * 8 + j] = H[(size_t)(ndim + i) * odim + ndim + j];
+    invert_pos_def(8, hp, hpi);
+    // bli = H(bottom, 0:ndim)^T hpi; H(0:ndim, 0:ndim) -= bli H(bottom, 0:ndim); b -= bli b_tail
+    std::vector<double> bli((size_t)ndim * 8);
+    for (int i = 0; i < ndim; i++)
+        for (int k = 0; k < 8; k++) {
+            double acc = 0;
+            for (int m = 0; m < 8; m++) acc += H[(size_t)(ndim + m) * odim + i] * hpi[m * 8 + k];
+            bli[(size_t)i * 8 + k] = acc;
+        }
+    for (int i = 0; i < ndim; i++) {
+        for (int j = 0; j < ndim; j++) {
+            double acc = 0;
+            for (int k = 0; k < 8; k++) acc += bli[(size_t)i * 8 + k] * H[(size_t)(ndim + k) * odim + j];
+            H[(size_t)i * odim + j] -= acc;
+        }
+        double acc = 0;
+        for (int k = 0; k < 8; k++) acc += bli[(size_t)i * 8 + k] * b[ndim + k];
+        b[i] -= acc;
+    }
+    for (int i = 0; i < ndim; i++) {  // unscale and symmetrise, :166-171
+        bM_out[i] = sv[i] * b[i];
+        for (int j = 0; j < ndim; j++) H[(size_t)i * odim + j] *= sv[i] * sv[j];
+    }
+    for (int i = 0; i < ndim; i++)
+        for (int j = 0; j < ndim; j++)
+            HM_out[(size_t)i * ndim + j] = 0.5 * (H[(size_t)i * odim + j] + H[(size_t)j * odim + i]);
+    return 0;
+}
+
 }  // namespace ldso_ba

@@ -86,6 +86,7 @@ struct WinDev {
     int width, height;
     float wM3, hM3;
     float calib[4];
+    float cdelta[4];         // EnergyFunctional::cDeltaF (marginalisation pass only)
 };
 
 __host__ __device__ inline long long packed_len(int D) { return (long long)D * (D + 1) / 2; }
@@ -120,6 +121,7 @@ struct LinParams {
     int tiles_per_row;       // 2-wide tiles per tile row
     int fix;
     int accumulate;
+    const float *ad_ht_delta;  // [pair_global][8] EnergyFunctional::adHTdeltaF (marginalisation pass)
 };
 
 struct Geo {
@@ -593,9 +595,14 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// one pattern pixel of Residuals.cc:128-190: the 17 addends, in the reference's expression order
+// one pattern pixel of Residuals.cc:128-190: the 17 addends, in the reference's expression order.
+// kMarg: the JI_r / Jab_r / rr addends use res_toZeroF of fixLinearizationF (Residuals.cc:219-245,
+// resF - JIdx Jp_delta - JabF delta_ab) as AccumulatedTopHessianSSE::addPoint<2> does
+// (AccumulatedTopHessian.cc:44-45, 66-76); jx, jy = Jp_delta_x/y, da, db = adHTdeltaF[6], [7].
+template <bool kMarg>
 __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float color, float weight, float aff0,
-                                            float aff1, float b0, float t[kSums]) {
+                                            float aff1, float b0, float t[kSums], float jx, float jy, float da,
+                                            float db) {
 #pragma clang fp contract(off)
     const float residual = I - (float)(aff0 * color + aff1);
     const float drdA = (color - b0);
@@ -620,16 +627,23 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
     t[10] = drdA * hw * hw;
     t[11] = hw * hw;
     t[1] = hw * hw * (gx * gx + gy * gy);
-    t[12] = resF * gx;
-    t[13] = resF * gy;
-    t[14] = resF * jab0;
-    t[15] = resF * hw;
-    t[16] = resF * resF;
+    float ra = resF;
+    if constexpr (kMarg) {
+        ra = ra - gx * jx;
+        ra = ra - gy * jy;
+        ra = ra - jab0 * da;
+        ra = ra - hw * db;
+    }
+    t[12] = ra * gx;
+    t[13] = ra * gy;
+    t[14] = ra * jab0;
+    t[15] = ra * hw;
+    t[16] = ra * ra;
 }
 
 // kImg: 0 row-major float4 texels, 1 2x4-tiled float4 texels, 2 quad records (see k_tile_image),
 // 3 intensity only in 8x4-float tiles with the gradients recomputed (see k_intensity_image)
-template <int kImg, bool kXcdRemap>
+template <int kImg, bool kXcdRemap, bool kMarg>
 __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
     constexpr bool kTiled = kImg == 1;
     __shared__ float lds_terms[4][8][kSums][8];
@@ -664,6 +678,33 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
     float4 centre = P.rs_center[rq];
     const float4 my_pd0 = *(const float4 *)(P.pt_data + (size_t)my_point * LDSO_BA_POINT_STRIDE);
     if (!valid) my_state = LDSO_BA_RES_OOB;
+    // marginalisation pass: Jp * delta of fixLinearizationF (Residuals.cc:221-232) from the centre
+    // geometry, per residual, before the pattern pixels need it (dot products left to right)
+    float jp_dx = 0.f, jp_dy = 0.f, m_da = 0.f, m_db = 0.f;
+    if constexpr (kMarg) {
+#pragma clang fp contract(off)
+        const float *dp = P.ad_ht_delta + (size_t)it.z * 8;
+        m_da = dp[6];
+        m_db = dp[7];
+        Geo gm;
+        if (centre_projection(pre, my_pd0.x, my_pd0.y, my_pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
+                              wM3, hM3, gm)) {
+            const float dd = P.pt_data[(size_t)my_point * LDSO_BA_POINT_STRIDE + 5];
+            float x6 = 0.f, y6 = 0.f, x4 = 0.f, y4 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                x6 += gm.d_xi_x[i] * dp[i];
+                y6 += gm.d_xi_y[i] * dp[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                x4 += gm.d_C_x[i] * W.cdelta[i];
+                y4 += gm.d_C_y[i] * W.cdelta[i];
+            }
+            jp_dx = x6 + x4 + gm.d_d_x * dd;
+            jp_dy = y6 + y4 + gm.d_d_y * dd;
+        }
+    }
 
     // ---------------- phase A: pattern pixels, 8 residuals per step -------------------------
     // One-step software pipeline: the projection and the 4 tap loads of step k+1 are issued
@@ -685,6 +726,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             float3 t00, t10, t01, t11;  // kImg 0/1: the four taps
             float4 qi, qx, qy;          // kImg 2: I, dx, dy of the quad (00, 10, 01, 11)
             float iv[12];               // kImg 3: I at rows y-1 (x, x+1), y and y+1 (x-1..x+2), y+2 (x, x+1)
+            float jx, jy;               // kMarg: Jp_delta of the residual
             bool gok;
         };
         auto issue = [&](int k, Stage &q) {
@@ -694,6 +736,10 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             const float pu = __shfl(my_pd0.x, j, kWave), pv = __shfl(my_pd0.y, j, kWave),
                         pz = __shfl(my_pd0.z, j, kWave);
             const bool go = j < it.y && st != LDSO_BA_RES_OOB;
+            if constexpr (kMarg) {
+                q.jx = __shfl(jp_dx, j, kWave);
+                q.jy = __shfl(jp_dy, j, kWave);
+            }
             const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
             q.color = pd[8 + sl];
             q.weight = pd[16 + sl];
@@ -771,7 +817,8 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
                 }
                 fin = isfinite(I);
                 float tt[kSums];
-                pixel_terms(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt);
+                pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt, kMarg ? q.jx : 0.f,
+                                   kMarg ? q.jy : 0.f, m_da, m_db);
 #pragma unroll
                 for (int e = 0; e < kSums; e++) T[e * 8 + sl] = tt[e];
             }
@@ -972,6 +1019,7 @@ struct PointParams {
     float *sc_slab;
     int n_items;
     int item_base;
+    int shift_prior;  // AccumulatedSCHessianSSE::addPoint's shiftPriorToZero (false when marginalising)
 };
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
@@ -1039,7 +1087,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
             ih = H;
             HdiF = (float)(1.0 / (double)H);
             bdSum = bd + 0.0f;
-            bdSum += priorF * deltaF;
+            if (P.shift_prior) bdSum += priorF * deltaF;
             row[Kj + 0] = hcd[0] + 0.0f;
             row[Kj + 1] = hcd[1] + 0.0f;
             row[Kj + 2] = hcd[2] + 0.0f;
@@ -2067,24 +2115,29 @@ void launch_lin1(bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t 
     }
 }
 // variant = occupancy target in waves per SIMD (see DESIGN.md for the measured choice)
+template <bool kMarg>
+void launch_sp(int img_mode, bool xcd, int nb, hipStream_t st, const LinParams &L) {
+    if (img_mode == 3) {
+        if (xcd) k_linearize_sp<3, true, kMarg><<<nb, 256, 0, st>>>(L);
+        else k_linearize_sp<3, false, kMarg><<<nb, 256, 0, st>>>(L);
+    } else if (img_mode == 2) {
+        if (xcd) k_linearize_sp<2, true, kMarg><<<nb, 256, 0, st>>>(L);
+        else k_linearize_sp<2, false, kMarg><<<nb, 256, 0, st>>>(L);
+    } else if (img_mode == 1) {
+        if (xcd) k_linearize_sp<1, true, kMarg><<<nb, 256, 0, st>>>(L);
+        else k_linearize_sp<1, false, kMarg><<<nb, 256, 0, st>>>(L);
+    } else {
+        if (xcd) k_linearize_sp<0, true, kMarg><<<nb, 256, 0, st>>>(L);
+        else k_linearize_sp<0, false, kMarg><<<nb, 256, 0, st>>>(L);
+    }
+}
+// marg: the marginalisation pass (addPoint<2> sums; sample-parallel kernel only)
 void launch_linearize(int variant, int img_mode, bool load3, bool xcd, bool cf, int nb, hipStream_t st,
-                      const LinParams &L) {
+                      const LinParams &L, bool marg) {
     const bool tiled = img_mode == 1;
-    if (variant == 3) {
-        if (img_mode == 3) {
-            if (xcd) k_linearize_sp<3, true><<<nb, 256, 0, st>>>(L);
-            else k_linearize_sp<3, false><<<nb, 256, 0, st>>>(L);
-        } else if (img_mode == 2) {
-            if (xcd) k_linearize_sp<2, true><<<nb, 256, 0, st>>>(L);
-            else k_linearize_sp<2, false><<<nb, 256, 0, st>>>(L);
-        } else if (tiled) {
-            if (xcd) k_linearize_sp<1, true><<<nb, 256, 0, st>>>(L);
-            else k_linearize_sp<1, false><<<nb, 256, 0, st>>>(L);
-        } else {
-            if (xcd) k_linearize_sp<0, true><<<nb, 256, 0, st>>>(L);
-            else k_linearize_sp<0, false><<<nb, 256, 0, st>>>(L);
-        }
-    } else if (variant == 2) launch_lin1<4>(tiled, load3, xcd, cf, nb, st, L);
+    if (marg) launch_sp<true>(img_mode, xcd, nb, st, L);
+    else if (variant == 3) launch_sp<false>(img_mode, xcd, nb, st, L);
+    else if (variant == 2) launch_lin1<4>(tiled, load3, xcd, cf, nb, st, L);
     else launch_lin1<1>(tiled, load3, xcd, cf, nb, st, L);
 }
 
@@ -2165,6 +2218,11 @@ struct ldso_ba_ctx {
     DevBuf<float> d_xad;            // [win][kXadStride]
     DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
     DevBuf<int> d_pt_win;
+    // marginalisation context (ldso_ba_load_marginalization): images borrowed from the parent
+    // context's window, addPoint<2> sums, no prior shift in the SC pass
+    bool marg = false;
+    const float4 *img_ext = nullptr;
+    DevBuf<float> d_adhtd;  // [pairs][8] adHTdeltaF
     int vec_total = 0;
     size_t sc_smem_max = 0;
     bool timing = false;
@@ -2234,10 +2292,10 @@ int timed_launch(ldso_ba_ctx *c, int slot, hipStream_t st, F &&launch) {
     return 0;
 }
 
-int check_window(const ldso_ba_window &w) {
+int check_window(const ldso_ba_window &w, bool need_images = true) {
     if (w.n_frames < 2 || w.n_frames > LDSO_BA_MAX_FRAMES) return fail(-1, "n_frames out of range [2,16]");
     if (w.n_points < 0 || w.n_residuals < 0) return fail(-1, "negative counts");
-    if (!w.dI || !w.frame_energy_th || !w.precalc || !w.ad_host || !w.ad_target || !w.c_prior || !w.c_delta ||
+    if ((need_images && !w.dI) || !w.frame_energy_th || !w.precalc || !w.ad_host || !w.ad_target || !w.c_prior || !w.c_delta ||
         !w.frame_prior || !w.frame_delta_prior)
         return fail(-1, "null frame-level pointer");
     if (w.n_points > 0 && (!w.point_host || !w.point_data || !w.point_res_begin))
@@ -2403,6 +2461,14 @@ int ldso_ba_solve_system(int32_t n, int32_t it, double lambda, const double *HA,
     return solve_system(n, it, lambda, HA, bA, HL, bL, HM, bM, Hsc, bsc, ns, nn, x);
 }
 
+int ldso_ba_marginalize_frame(int32_t n, int32_t idx, const double *HM, const double *bM, const double *prior,
+                              const double *delta_prior, double *HM_out, double *bM_out) {
+    if (n < 2 || n > LDSO_BA_MAX_FRAMES || idx < 0 || idx >= n || !HM || !bM || !prior || !delta_prior || !HM_out ||
+        !bM_out)
+        return fail(-1, "bad arguments");
+    return marginalize_frame(n, idx, HM, bM, prior, delta_prior, HM_out, bM_out);
+}
+
 int ldso_ba_validate_window(const ldso_ba_window *w) {
     if (!w) return fail(-1, "null window");
     return check_window(*w);
@@ -2488,12 +2554,17 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
 
 void *ldso_ba_stream(ldso_ba_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
-int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32_t shard_rank,
-                 int32_t shard_count) {
+}  // extern "C"
+
+namespace {
+// parent != nullptr: a marginalisation context over `ws[0]` whose frames are the parent's window
+// parent_win (images borrowed, not uploaded; priorF scaled by setting_idepthFixPriorMargFac)
+int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32_t shard_rank, int32_t shard_count,
+              const ldso_ba_ctx *parent, int parent_win) {
     if (!c || n_windows < 1 || !ws) return fail(-1, "bad arguments");
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(-1, "bad shard");
     for (int w = 0; w < n_windows; w++) {
-        int rc = check_window(ws[w]);
+        int rc = check_window(ws[w], parent == nullptr);
         if (rc) return rc;
         if (ws[w].width != ws[0].width || ws[w].height != ws[0].height)
             return fail(-1, "all windows of a context must share the image size");
@@ -2504,7 +2575,17 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     c->width = ws[0].width;
     c->height = ws[0].height;
     c->npix = c->width * c->height;
-    image_geometry(c);
+    c->marg = parent != nullptr;
+    c->img_ext = nullptr;
+    if (parent) {
+        c->img_mode = parent->img_mode;
+        c->tiles_per_row = parent->tiles_per_row;
+        c->padded_h = parent->padded_h;
+        c->frame_stride = parent->frame_stride;
+        c->img_ext = parent->d_img.p + (size_t)parent->wd[parent_win].frame_base * parent->frame_stride;
+    } else {
+        image_geometry(c);
+    }
     c->groups = c->groups_req ? c->groups_req : 1;
     c->wh.assign(n_windows, WinHost());
     c->wd.assign(n_windows, WinDev());
@@ -2605,6 +2686,8 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
             pt_host.push_back(in.point_host[p]);
             pt_data.insert(pt_data.end(), in.point_data + (size_t)p * LDSO_BA_POINT_STRIDE,
                            in.point_data + (size_t)(p + 1) * LDSO_BA_POINT_STRIDE);
+            if (c->marg)  // marginalizePointsF: p->priorF *= setting_idepthFixPriorMargFac (EnergyFunctional.cc:216)
+                pt_data[pt_data.size() - LDSO_BA_POINT_STRIDE + 4] *= kIdepthFixPriorMargFac;
             const int b = in.point_res_begin[p], e = in.point_res_begin[p + 1];
             pt_nres.push_back(e - b);
             unsigned long long tg = 0;
@@ -2633,6 +2716,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         D.wM3 = (float)(in.width - 3);
         D.hM3 = (float)(in.height - 3);
         for (int i = 0; i < 4; i++) D.calib[i] = in.calib[i];
+        for (int i = 0; i < 4; i++) D.cdelta[i] = in.c_delta[i];
         D.K = 8 * (N - 1) + 5;
         D.KP = (D.K + 3) / 4 * 4;
         const int nt = D.KP / 4;
@@ -2702,7 +2786,9 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         if (rc) return rc;              \
     } while (0)
     ALLOC(c->d_wins, n_windows);
-    ALLOC(c->d_img, (size_t)c->n_frames * c->frame_stride);
+    if (c->marg) c->d_img.release();
+    else ALLOC(c->d_img, (size_t)c->n_frames * c->frame_stride);
+    if (c->marg) ALLOC(c->d_adhtd, (size_t)c->n_pairs * 8);
     ALLOC(c->d_precalc, precalc.size());
     ALLOC(c->d_frame_th, frame_th.size());
     ALLOC(c->d_pt_data, std::max<size_t>(1, pt_data.size()));
@@ -2790,7 +2876,7 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
     // images: per frame through a float3 staging buffer, repacked on the device; the
     // intensity-only layout falls back to 2x4 float4 tiles if the caller's gradients are not
     // makeImages' (then recomputing them would not be exact)
-    {
+    if (!c->marg) {
         int mismatch = 0;
         rc = stage_images(c, ws, n_windows, &mismatch);
         if (rc) return rc;
@@ -2812,6 +2898,25 @@ int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, in
         if (rc) return rc;
     }
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int ldso_ba_load(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32_t shard_rank,
+                 int32_t shard_count) {
+    return load_impl(c, n_windows, ws, shard_rank, shard_count, nullptr, 0);
+}
+
+int ldso_ba_load_marginalization(ldso_ba_ctx *marg, const ldso_ba_ctx *parent, int32_t parent_win,
+                                 const ldso_ba_window *points) {
+    if (!marg || !parent || !points || marg == parent) return fail(-1, "bad arguments");
+    if (parent_win < 0 || parent_win >= parent->n_win) return fail(-1, "parent window out of range");
+    if (marg->device != parent->device) return fail(-1, "contexts on different devices");
+    const WinDev &pw = parent->wd[parent_win];
+    if (points->n_frames != pw.N || points->width != pw.width || points->height != pw.height)
+        return fail(-1, "marginalisation window does not match the parent window's frames");
+    return load_impl(marg, 1, points, 0, 1, parent, parent_win);
 }
 
 int ldso_ba_update(ldso_ba_ctx *c, int32_t win, const ldso_ba_window *w) {
@@ -2871,7 +2976,7 @@ int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
 
 int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
-    if (c->img_mode >= 2 && c->lin_variant != 3)
+    if (c->img_mode >= 2 && c->lin_variant != 3 && !c->marg)
         return fail(-1, "quad / intensity-only image layouts need LIN_VARIANT 3");
     HIP_TRY(hipSetDevice(c->device));
     c->sys_host_valid = false;
@@ -2882,7 +2987,8 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     LinParams L;
     L.items = c->d_top_items.p;
     L.wins = c->d_wins.p;
-    L.img = c->d_img.p;
+    L.img = c->img_ext ? c->img_ext : c->d_img.p;
+    L.ad_ht_delta = c->marg ? c->d_adhtd.p : nullptr;
     L.precalc = c->d_precalc.p;
     L.frame_th = c->d_frame_th.p;
     L.rs_point = c->d_rs_point.p;
@@ -2911,6 +3017,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.pt_rec = c->d_pt_rec.p;
     Pp.pt_out = c->d_pt_out.p;
     Pp.sc_slab = c->d_sc_slab.p;
+    Pp.shift_prior = c->marg ? 0 : 1;
     StitchParams Sp;
     Sp.wins = c->d_wins.p;
     Sp.pair_win = c->d_pair_win.p;
@@ -2954,7 +3061,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
             L.n_blocks = (L.n_items + 3) / 4;
             rc = timed_launch(c, 0, st, [&] {
                 launch_linearize(c->lin_variant, c->img_mode, c->load3, c->xcd_remap, c->centre_first, L.n_blocks, st,
-                                 L);
+                                 L, c->marg);
             });
             if (rc) return rc;
         }
@@ -2978,6 +3085,26 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     }
+    return 0;
+}
+
+int ldso_ba_marginalize_points(ldso_ba_ctx *c, const float *ad_ht_delta, double *H, double *b) {
+    if (!c || !ad_ht_delta || !H || !b) return fail(-1, "bad arguments");
+    if (!c->marg || c->n_win != 1) return fail(-1, "not a marginalisation context (ldso_ba_load_marginalization)");
+    HIP_TRY(hipSetDevice(c->device));
+    const WinDev &D = c->wd[0];
+    HIP_TRY(hipMemcpyAsync(c->d_adhtd.p, ad_ht_delta, (size_t)D.N * D.N * 8 * sizeof(float), hipMemcpyHostToDevice,
+                           c->stream));
+    int rc = ldso_ba_reset_oob(c, 0);
+    if (rc) return rc;
+    rc = ldso_ba_linearize(c, 0, 1);
+    if (rc) return rc;
+    const int n = D.D;
+    std::vector<double> Hsc((size_t)n * n), bsc(n);
+    rc = ldso_ba_get_system(c, 0, H, b, nullptr, nullptr, Hsc.data(), bsc.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < (size_t)n * n; i++) H[i] -= Hsc[i];  // EnergyFunctional.cc:242-243
+    for (int i = 0; i < n; i++) b[i] -= bsc[i];
     return 0;
 }
 

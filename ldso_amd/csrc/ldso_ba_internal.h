@@ -32,6 +32,8 @@ constexpr float kInitialTransPrior = 1e10f;                // :19
 constexpr float kInitialAffBPrior = 1e14f;                 // :20
 constexpr float kInitialAffAPrior = 1e14f;                 // :21
 constexpr double kSolverModeDelta = 0.00001;               // :24
+constexpr float kIdepthFixPriorMargFac = 600.0f * 600.0f;   // :17
+constexpr float kMargWeightFac = 0.5f * 0.5f;               // :45
 
 // Fast path of the nullspace projection (EnergyFunctional::orthogonalize, EnergyFunctional.cc:809-841)
 // for 7 nullspaces: when the Gram matrix G = N^T N of the normalised nullspaces is so well
@@ -94,5 +96,7 @@ int nullspaces(int N, const ldso_ba_frame_state *fr, double *out);
 int solve_system(int N, int iteration, double lambda, const double *HA, const double *bA, const double *HL,
                  const double *bL, const double *HM, const double *bM, const double *Hsc, const double *bsc,
                  const double *ns, int n_null, double *x_out);
+int marginalize_frame(int N, int idx, const double *HM, const double *bM, const double *prior,
+                      const double *delta_prior, double *HM_out, double *bM_out);
 
 }  // namespace ldso_ba

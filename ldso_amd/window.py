@@ -83,11 +83,12 @@ class Window:
         L.check(L.lib().ldso_ba_nullspaces(self.n_frames, fr.ctypes.data, L.ptr(out, L.f64p)))
         return out
 
-    def c_struct(self) -> L.LdsoBaWindow:
+    def c_struct(self, with_images: bool = True) -> L.LdsoBaWindow:
+        """with_images=False leaves dI NULL (a marginalisation window borrows its parent's)."""
         if self.precalc is None:
             self.refresh_frame_terms()
         arrs = dict(
-            dI=np.ascontiguousarray(self.dI, np.float32),
+            dI=np.ascontiguousarray(self.dI, np.float32) if with_images else None,
             frame_energy_th=np.ascontiguousarray(self.frame_energy_th, np.float32),
             precalc=np.ascontiguousarray(self.precalc, np.float32),
             ad_host=np.ascontiguousarray(self.ad_host, np.float64),
@@ -104,7 +105,7 @@ class Window:
             res_energy=np.ascontiguousarray(self.res_energy, np.float32),
             res_flags=np.ascontiguousarray(self.res_flags, np.uint8),
         )
-        self._keep = list(arrs.values())
+        self._keep = [a for a in arrs.values() if a is not None]
         s = L.LdsoBaWindow()
         s.n_frames = self.n_frames
         s.n_points = self.n_points
@@ -114,7 +115,8 @@ class Window:
         s.calib[:] = [float(x) for x in self.calib]
         types = {np.float32: L.f32p, np.float64: L.f64p, np.int32: L.i32p, np.int8: L.i8p, np.uint8: L.u8p}
         for k, a in arrs.items():
-            setattr(s, k, L.ptr(a, types[a.dtype.type]))
+            if a is not None:
+                setattr(s, k, L.ptr(a, types[a.dtype.type]))
         return s
 
     def copy_state(self) -> "Window":

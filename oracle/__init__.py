@@ -60,6 +60,7 @@ def lib():
             "oracle_frame_take_data": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p]),
             "oracle_nullspaces": (C.c_int, [C.c_int, C.c_void_p, f64p]),
             "oracle_time_iterations": (C.c_double, [C.c_void_p, C.c_int]),
+            "oracle_marginalize_points": (C.c_int, [C.c_void_p, C.c_int, i32p, f32p, f64p, f64p]),
             "oracle_ct_levels": (C.c_int, [C.c_int, C.c_int]),
             "oracle_ct_make_k": (None, [f32p, C.c_int, C.c_int, C.c_int, f32p]),
             "oracle_make_images": (None, [f32p, C.c_int, C.c_int, C.c_int, f32p, f32p, f32p]),
@@ -170,6 +171,18 @@ class OracleWindow:
         step = np.zeros(self.window.n_points, np.float32)
         lib().oracle_resubstitute(self._h, _p(np.ascontiguousarray(x, np.float64), f64p), float(lam), _p(step, f32p))
         return step
+
+    def marginalize_points(self, points, ad_ht_delta):
+        """flagPointsForRemoval + marginalizePointsF for `points` -> (H, b) = (M - Msc, Mb - Mbsc)."""
+        n = self.window.dim
+        pts = np.ascontiguousarray(points, np.int32)
+        adh = np.ascontiguousarray(ad_ht_delta, np.float32)
+        H = np.zeros((n, n), np.float64)
+        b = np.zeros(n, np.float64)
+        rc = lib().oracle_marginalize_points(self._h, int(pts.size), _p(pts, i32p), _p(adh, f32p), _p(H, f64p),
+                                             _p(b, f64p))
+        assert rc == 0
+        return H, b
 
     def time_iterations(self, iters: int) -> float:
         return float(lib().oracle_time_iterations(self._h, int(iters)))

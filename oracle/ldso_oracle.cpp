@@ -1819,6 +1819,74 @@ int oracle_nullspaces(int N, const ldso_ba_frame_state *frames, double *out) {
     return 0;
 }
 
+// ---- point marginalisation --------------------------------------
+// FullSystem::flagPointsForRemoval's per-residual part for the MARGINALIZED points
+// (FullSystem.cc:1390-1398) with PointFrameResidual::fixLinearizationF (Residuals.cc:219-245;
+// the Eigen dot products taken left to right), then EnergyFunctional::marginalizePointsF
+// (EnergyFunctional.cc:205-243): priorF *= setting_idepthFixPriorMargFac, addPoint<2>,
+// SC addPoint(p, false), single-threaded stitchDouble of both; H = M - Msc, b = Mb - Mbsc.
+int oracle_marginalize_points(oracle_window *ow, int n, const int *pts, const float *adHTdeltaF, double *H,
+                              double *b) {
+    if (!ow || n < 0 || (n > 0 && !pts) || !adHTdeltaF || !H || !b) return -1;
+    const int N = ow->N, D = dimH(N);
+    for (int k = 0; k < n; k++)
+        if (pts[k] < 0 || pts[k] >= (int)ow->points.size()) return -1;
+    for (int k = 0; k < n; k++) {
+        PointH &p = ow->points[pts[k]];
+        for (int ri : p.residuals) {
+            Residual &r = ow->res[ri];
+            r.resetOOB();
+            linearize(ow, r);
+            r.isLinearized = false;
+            r.applyRes(true);
+            if (!r.isActive()) continue;
+            // fixLinearizationF
+            const RawResidualJacobian &J = r.J;
+            const float *dp = adHTdeltaF + (size_t)(r.hostIDX + N * r.targetIDX) * 8;
+            float x6 = 0, y6 = 0, x4 = 0, y4 = 0;
+            for (int i = 0; i < 6; i++) {
+                x6 += J.Jpdxi[0][i] * dp[i];
+                y6 += J.Jpdxi[1][i] * dp[i];
+            }
+            for (int i = 0; i < 4; i++) {
+                x4 += J.Jpdc[0][i] * ow->cDeltaF[i];
+                y4 += J.Jpdc[1][i] * ow->cDeltaF[i];
+            }
+            const float Jp_delta_x = x6 + x4 + J.Jpdd[0] * p.deltaF;
+            const float Jp_delta_y = y6 + y4 + J.Jpdd[1] * p.deltaF;
+            const float delta_a = dp[6], delta_b = dp[7];
+            for (int i = 0; i < patternNum; i++) {
+                float rtz = J.resF[i];
+                rtz = rtz - J.JIdx[0][i] * Jp_delta_x;
+                rtz = rtz - J.JIdx[1][i] * Jp_delta_y;
+                rtz = rtz - J.JabF[0][i] * delta_a;
+                rtz = rtz - J.JabF[1][i] * delta_b;
+                r.res_toZeroF[i] = rtz;
+            }
+            r.isLinearized = true;
+        }
+    }
+    ensure_pool(ow);
+    for (int k = 0; k < n; k++) ow->points[pts[k]].priorF *= 600.0f * 600.0f;  // setting_idepthFixPriorMargFac
+    for (auto &a : ow->accTop[0]) a.initialize();
+    ow->nres[0] = 0;
+    ow->accHcc[0].initialize();
+    ow->accbc[0].initialize();
+    for (auto &a : ow->accE[0]) a.initialize();
+    for (auto &a : ow->accEB[0]) a.initialize();
+    for (auto &a : ow->accD[0]) a.initialize();
+    for (int k = 0; k < n; k++) {
+        topAddPoint<2>(ow, ow->points[pts[k]], 0);
+        scAddPoint(ow, ow->points[pts[k]], false, 0);
+    }
+    std::vector<double> M, Mb, Msc, Mbsc;
+    topStitchMT(ow, M, Mb, false, false);
+    scStitchMT(ow, Msc, Mbsc, false);
+    for (size_t i = 0; i < (size_t)D * D; i++) H[i] = M[i] - Msc[i];
+    for (int i = 0; i < D; i++) b[i] = Mb[i] - Mbsc[i];
+    return 0;
+}
+
 double oracle_time_iterations(oracle_window *ow, int iters) {
     ensure_pool(ow);
     auto t0 = std::chrono::steady_clock::now();

@@ -74,6 +74,13 @@ int oracle_frame_take_data(int n_frames, const ldso_ba_frame_state *frames, doub
  * out [7][8N+4] in the order orthogonalize() stacks them. */
 int oracle_nullspaces(int n_frames, const ldso_ba_frame_state *frames, double *out);
 
+/* Point marginalisation of the points pts[n] (flagPointsForRemoval's relinearisation +
+ * fixLinearizationF, then marginalizePointsF's addPoint<2> / SC addPoint(p, false) / stitch):
+ * H = M - Msc [(8N+4)^2], b = Mb - Mbsc.  adHTdeltaF [N*N][8].  Mutates the points' residuals and
+ * priorF as the reference does. */
+int oracle_marginalize_points(oracle_window *ow, int n, const int *pts, const float *adHTdeltaF, double *H,
+                              double *b);
+
 /* ---- coarse tracker (ldso_oracle_tracker.cpp; the checker of include/ldso_ct.h) ---------- */
 int oracle_ct_levels(int w, int h);
 /* per level 13 floats {fx, fy, cx, cy, Ki[9]} */
