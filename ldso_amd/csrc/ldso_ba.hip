@@ -741,8 +741,14 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
                 q.jy = __shfl(jp_dy, j, kWave);
             }
             const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+#if LDSO_EXP_NO_PT
+            q.color = 100.f + sl + (p & 7);
+            q.weight = 0.5f;
+            (void)pd;
+#else
             q.color = pd[8 + sl];
             q.weight = pd[16 + sl];
+#endif
             const float up = pu + px, vp = pv + py;
             float ptp[3];
 #pragma unroll
@@ -758,7 +764,12 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             if constexpr (kImg == 3) {
                 const float *imf = reinterpret_cast<const float *>(img);
                 auto at = [&](int x, int y) {
+#if LDSO_EXP_NO_TEX
+                    (void)imf;
+                    return (float)((x * 7 + y * 13) & 255);
+#else
                     return imf[(((y >> 2) * tpr2 + (x >> 3)) << 5) + ((y & 3) << 3) + (x & 7)];
+#endif
                 };
                 q.iv[0] = at(ix, iy - 1);
                 q.iv[1] = at(ix + 1, iy - 1);
@@ -933,7 +944,9 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             active = (new_state == LDSO_BA_RES_IN);
             flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
             state_energy = new_energy;
+#if !LDSO_EXP_NO_REC
             write_record(P.pt_rec + (size_t)my_slot * 4, active, g, s);
+#endif
             if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
 #pragma clang fp contract(off)
                 float pi[3], pr[3];
@@ -1194,6 +1207,7 @@ struct StitchParams {
     int pair_base;  // first global pair of this launch
     int win_base;   // first window of this launch
     int n_win;      // windows of this launch: blocks [0, n_win) run their setNewFrameEnergyTH
+    int part;       // 0: Top and SC halves; 1: Top half (+ the setNewFrameEnergyTH blocks); 2: SC half
 };
 
 __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row <= col
@@ -1384,6 +1398,9 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 
     // All global loads of both halves are issued first (one round trip for the block): the
     // Top bucket partial sums and pair adjoints, and the SC rows of G_i with the host's adjoints.
+    // part 1 / 2 (two launches on two streams, the Top half overlapping k_point_sc) skip the
+    // other half's loads and work; the branches are block-uniform.
+    const bool do_top = P.part != 2, do_sc = P.part != 1;
     double *acc = sm, *A = acc + 96, *AH = A + 169, *AT = AH + 64, *TH = AT + 64, *TT = TH + 64;  // 521
     const int i = h, j = t, KP = W.KP, nt = KP / 4, per = W.ntiles * 16, Kc = 8 * (N - 1);
     const int sj = j < i ? j : j - 1;
@@ -1397,6 +1414,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     {
         const int2 pi = P.pair_items[pair];
         if (tid < kTopVals) {
+            if (do_top) {
             const float *src = P.top_slab + (size_t)pi.x * kTopVals + tid;
             double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
             int k = 0;
@@ -1408,6 +1426,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
             }
             for (; k < pi.y; k++) s0 += (double)src[(size_t)k * kTopVals];
             acc[tid] = (s0 + s1) + (s2 + s3);
+            }
         } else if (tid < kTopVals + 64) {
             AH[tid - kTopVals] = P.adH[(size_t)pair * 64 + tid - kTopVals];
         } else if (tid < kTopVals + 128) {
@@ -1415,15 +1434,15 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
         }
         const int2 hi = P.host_items[W.frame_base + i];
         const float *slab = P.sc_slab + W.sc_slab_base + (size_t)(hi.x - W.sc_item_base) * per;
-        for (int e = tid; e < 8 * KP; e += kStThreads) {
+        for (int e = do_sc ? tid : 8 * KP; e < 8 * KP; e += kStThreads) {
             const int r = e / KP, col = e % KP;
             Gj[e] = col < Kc + 5 ? g_elem(slab, hi.y, per, nt, 8 * sj + r, col) : 0.0;
         }
-        if (sj == 0 && tid < 20) {  // accHcc / accbc once per host (AccumulatedSCHessian.cc:105-113)
+        if (do_sc && sj == 0 && tid < 20) {  // accHcc / accbc once per host (AccumulatedSCHessian.cc:105-113)
             const int r = tid / 5, c = tid % 5;
             Cc[tid] = g_elem(slab, hi.y, per, nt, Kc + r, Kc + c);
         }
-        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
+        for (int e = do_sc ? tid : (N - 1) * 64; e < (N - 1) * 64; e += kStThreads) {
             const int s = e >> 6, k = s + (s >= i), pik = W.pair_base + i + N * k;
             AHk[e] = P.adH[(size_t)pik * 64 + (e & 63)];
             ATk[e] = P.adT[(size_t)pik * 64 + (e & 63)];
@@ -1432,7 +1451,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     __syncthreads();
 
     // ---------------- Top: bucket (h, t) ------------------------------------------------
-    {
+    if (do_top) {
         if (tid < 169) A[tid] = acc[top_slot(tid / 13, tid % 13)];
         __syncthreads();
         if (tid < 128) {
@@ -1479,7 +1498,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     }
 
     // ---------------- SC: host i = h, target j = t ---------------------------------------
-    {
+    if (do_sc) {
         // per k != i: X_k = AT_ij D_jk, S_k = D_jk AH_ik^T
         for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
             const int s = e >> 6, r = (e >> 3) & 7, c = e & 7;
@@ -2195,6 +2214,10 @@ struct ldso_ba_ctx {
     hipEvent_t ev_fork = nullptr, ev_lin0 = nullptr, ev_join = nullptr;
     int groups_req = 0;             // LDSO_BA_TUNE_PIPELINE_GROUPS (0 = automatic)
     int groups = 1;                 // pipelined window groups per pass
+#ifndef LDSO_STITCH_SPLIT_DEFAULT
+#define LDSO_STITCH_SPLIT_DEFAULT 0
+#endif
+    bool stitch_split = LDSO_STITCH_SPLIT_DEFAULT;  // Top half of k_stitch on stream2, overlapping k_point_sc (LDSO_BA_TUNE_STITCH_SPLIT)
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
     std::vector<WinDev> wd;
@@ -3069,17 +3092,35 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
             HIP_TRY(hipEventRecord(c->ev_lin0, c->stream));
             HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_lin0, 0));
         }
+        Sp.pair_base = p0;
+        Sp.win_base = w0;
+        Sp.n_win = w1 - w0;
+        Sp.part = 0;
+        // One group: k_stitch's Top half and setNewFrameEnergyTH need only k_linearize, so they run
+        // on stream 2 beside k_point_sc; the SC half follows k_point_sc on the context stream.
+        const bool split = G == 1 && accumulate && c->stitch_split;
+        if (split) {
+            HIP_TRY(hipEventRecord(c->ev_lin0, st));
+            HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_lin0, 0));
+            Sp.part = 1;
+            rc = timed_launch(c, 2, c->stream2,
+                              [&] { k_stitch<<<Sp.n_win + p1 - p0, kStThreads, st_smem, c->stream2>>>(Sp); });
+            if (rc) return rc;
+            Sp.part = 2;
+            Sp.n_win = 0;
+        }
         if (accumulate && si1 > si0) {
             Pp.item_base = si0;
             Pp.n_items = si1 - si0;
             rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
             if (rc) return rc;
         }
-        Sp.pair_base = p0;
-        Sp.win_base = w0;
-        Sp.n_win = w1 - w0;
         rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + p1 - p0, kStThreads, st_smem, st>>>(Sp); });
         if (rc) return rc;
+        if (split) {  // join
+            HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
+            HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
+        }
     }
     if (G > 1) {  // join: the context stream orders everything that follows
         HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
@@ -3509,6 +3550,10 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
         if (value < 0 || value > 64) return fail(-1, "groups must be in [0, 64]");
         c->groups_req = value;
         c->groups = value ? value : 1;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_STITCH_SPLIT) {
+        c->stitch_split = value != 0;
         return 0;
     }
     if (key == LDSO_BA_TUNE_TIMING_MASK) {

@@ -31,6 +31,15 @@ for acc in (True, False):
     kt = c.kernel_times()
     c.set_kernel_timing(False)
     out["acc" if acc else "noacc"] = {k: 1e3 * v[0] / v[1] for k, v in kt.items() if v[1]}
+import time
+for _ in range(5):
+    c.linearize()
+c.sync()
+t0 = time.perf_counter()
+for _ in range(50):
+    c.linearize()
+c.sync()
+out["wall"] = {"pass": 1e6 * (time.perf_counter() - t0) / 50}
 print("RESULT " + json.dumps(out))
 '''
 
