@@ -292,7 +292,9 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              0 = default 1 (measured: 2/4/8 groups are 15-60% slower)
  *   LDSO_BA_TUNE_STITCH_SPLIT  1: with one group, k_stitch's Top half and the frame threshold run
  *                              on a second stream beside k_point_sc; 0 (default; measured: the
- *                              split pass is 3% slower, 188 vs 182 us on 64 x S7): one k_stitch */
+ *                              split pass is 3% slower, 188 vs 182 us on 64 x S7): one k_stitch
+ *   LDSO_BA_TUNE_ITEM_ORDER    k_linearize chunk order: 0 (default) target-major, 1 host-major;
+ *                              set before ldso_ba_load */
 #define LDSO_BA_TUNE_LIN_VARIANT 1
 #define LDSO_BA_TUNE_TILED_IMAGES 2
 #define LDSO_BA_TUNE_LOAD3 3
@@ -302,6 +304,7 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
 #define LDSO_BA_TUNE_TIMING_MASK 7
 #define LDSO_BA_TUNE_PIPELINE_GROUPS 8
 #define LDSO_BA_TUNE_STITCH_SPLIT 9
+#define LDSO_BA_TUNE_ITEM_ORDER 10
 int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);

@@ -2217,7 +2217,11 @@ struct ldso_ba_ctx {
 #ifndef LDSO_STITCH_SPLIT_DEFAULT
 #define LDSO_STITCH_SPLIT_DEFAULT 0
 #endif
-    bool stitch_split = LDSO_STITCH_SPLIT_DEFAULT;  // Top half of k_stitch on stream2, overlapping k_point_sc (LDSO_BA_TUNE_STITCH_SPLIT)
+    bool stitch_split = LDSO_STITCH_SPLIT_DEFAULT;
+#ifndef LDSO_ITEM_ORDER_DEFAULT
+#define LDSO_ITEM_ORDER_DEFAULT 0
+#endif
+    int item_order = LDSO_ITEM_ORDER_DEFAULT;  // k_linearize chunk order: 0 target-major, 1 host-major  // Top half of k_stitch on stream2, overlapping k_point_sc (LDSO_BA_TUNE_STITCH_SPLIT)
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
     std::vector<WinDev> wd;
@@ -2747,13 +2751,18 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         smem_max = std::max(smem_max, sc_smem_bytes(D.KP));
         // top items: chunks of `chunk` residuals of one bucket (one wave each)
         D.top_item_base = (int)top_items.size();
-        for (int b = 0; b < N * N; b++) {
+        const size_t pi0 = pair_items.size();
+        pair_items.resize(pi0 + (size_t)N * N);
+        for (int bb = 0; bb < N * N; bb++) {
+            // bucket b = h + N t; chunks in target-major order (the N-1 buckets reading one target
+            // image run together) or host-major (the buckets of one host's points run together)
+            const int b = c->item_order ? (bb / N) + N * (bb % N) : bb;
             const int first = (int)top_items.size();
             for (int s = bucket_start[b]; s < bucket_start[b + 1]; s += chunk)
                 top_items.push_back(make_int4(res_base + s, std::min(chunk, bucket_start[b + 1] - s), pair_base + b, w));
-            pair_items.push_back(make_int2(first, (int)top_items.size() - first));
-            pair_win.push_back(w);
+            pair_items[pi0 + b] = make_int2(first, (int)top_items.size() - first);
         }
+        for (int b = 0; b < N * N; b++) pair_win.push_back(w);
         D.n_top_items = (int)top_items.size() - D.top_item_base;
         // sc items: chunks of 64 points of one host
         D.sc_item_base = (int)sc_items.size();
@@ -3550,6 +3559,11 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
         if (value < 0 || value > 64) return fail(-1, "groups must be in [0, 64]");
         c->groups_req = value;
         c->groups = value ? value : 1;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_ITEM_ORDER) {
+        if (c->n_win) return fail(-1, "item order must be chosen before ldso_ba_load");
+        c->item_order = value != 0;
         return 0;
     }
     if (key == LDSO_BA_TUNE_STITCH_SPLIT) {
