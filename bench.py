@@ -66,6 +66,40 @@ def cpu_baseline(seconds=10.0, threads=6):
                       f"accumulate{{AF,LF,SCF}}+stitch in {el:.1f} s, {threads}-thread IndexThreadReduce"}
 
 
+def secondary_s11(device, windows=8, steps=20):
+    """BASELINE config[3]'s window shape (11 keyframes, 8000 points, 640x480) on ONE GPU, batched
+    like the headline (a parity/scaling case in BASELINE.json, reported beside the headline, not
+    as `value`): denser windows share more texel lines between residuals."""
+    from ldso_amd import BAContext, synth
+
+    ws = [synth.make_window(**synth.S11, seed=5000 + i) for i in range(windows)]
+    ctx = BAContext(device)
+    ctx.load(ws)
+    for w in ws:
+        w.dI = None
+    R = ctx.stats()["residuals"]
+    for _ in range(3):
+        ctx.linearize()
+    ctx.sync()
+    n_gather = sum(int((ctx.residuals(i)["state"] != 1).sum()) for i in range(len(ws)))
+    ctx.set_tuning(7, 1)
+    ctx.set_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.linearize()
+    ctx.sync()
+    el = time.perf_counter() - t0
+    kt = ctx.kernel_times()
+    ctx.set_kernel_timing(False)
+    ctx.close()
+    k_ms, k_n = kt["k_linearize"]
+    k_s = k_ms / max(1, k_n) / 1e3
+    ach = n_gather * algo_bytes_per_residual(11) / k_s / 1e9
+    return {"workload": f"{windows} x S11 synthetic windows (11 KF, 8000 pts, 640x480)", "residuals_per_step": R,
+            "ms_per_step": 1e3 * el / steps, "point_residuals_per_s": R * steps / el,
+            "k_linearize_us": k_s * 1e6, "roofline_frac": ach / HBM_PEAK_GBS, "achieved_GBps": ach}
+
+
 def tracker_leg(device, reps=50, n_hyp=32, cpu_seconds=2.0, with_cpu=True):
     """Coarse tracker (include/ldso_ct.h) on a 640x480 frame with the
     reference point clouds of synth.make_tracker_scene (8000 level-0 points):
@@ -102,6 +136,12 @@ def tracker_leg(device, reps=50, n_hyp=32, cpu_seconds=2.0, with_cpu=True):
         ct.calc_res(0, Ts[i % n_hyp], ab[0])
         ct.calc_gs(0, Ts[i % n_hyp], ab[0])
     lm_ms = 1e3 * (time.perf_counter() - t0) / reps
+    for _ in range(5):
+        ct.calc_res_gs(0, Ts[0], ab[0])
+    t0 = time.perf_counter()
+    for i in range(reps):
+        ct.calc_res_gs(0, Ts[i % n_hyp], ab[0])
+    lm_fused_ms = 1e3 * (time.perf_counter() - t0) / reps
     ct.set_kernel_timing(True)
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -114,7 +154,8 @@ def tracker_leg(device, reps=50, n_hyp=32, cpu_seconds=2.0, with_cpu=True):
     algo = n_hyp * n0 * 48.0 + n0 * 16.0
     out = {
         "frame": "640x480, 4 levels", "points_level0": n0,
-        "lm_iteration": {"ms": lm_ms, "calls": "calcRes + calcGSSSE, level 0"},
+        "lm_iteration": {"ms": lm_fused_ms, "calls": "calcRes + calcGSSSE, level 0, one round trip (ldso_ct_calc_res_gs)",
+                         "ms_two_calls": lm_ms},
         "hypotheses": {"n_hyp": n_hyp, "ms_per_launch_host": hyp_ms,
                        "point_evals_per_s": n_hyp * n0 / (hyp_ms / 1e3)},
         "k_ct_calc_res": {"avg_launch_us": k_s * 1e6, "algo_bytes_per_launch": algo,
@@ -138,7 +179,7 @@ def tracker_leg(device, reps=50, n_hyp=32, cpu_seconds=2.0, with_cpu=True):
             n += 1
         out["cpu_lm_iteration"] = {"ms": 1e3 * el / n, "cores": 1, "kind": "port",
                                    "sample": f"{n} oracle calcRes + calcGSSSE at level 0 ({n0} points)"}
-        out["lm_iteration_speedup_vs_cpu"] = out["cpu_lm_iteration"]["ms"] / lm_ms
+        out["lm_iteration_speedup_vs_cpu"] = out["cpu_lm_iteration"]["ms"] / lm_fused_ms
     return out
 
 
@@ -154,6 +195,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the S11 line")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -307,13 +349,19 @@ def main():
                   "ms_per_gn_iteration_host_solve": ms_solve, "ms_per_gn_iteration_device_solve": ms_solve_dev}
         c1.close()
 
+    s11 = None
+    if rank == 0 and args.mode == "replicas" and not args.no_secondary:
+        s11 = secondary_s11(local_rank)
+
     tracker = None
     if rank == 0 and not args.no_tracker:
         tracker = tracker_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
 
-    cpu = None
+    cpu = cpu16 = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds)  # the reference's own IndexThreadReduce (NUM_THREADS = 6)
+        # every core this job may use on the GPU box's host (16 per GPU there)
+        cpu16 = cpu_baseline(args.cpu_seconds, threads=min(16, os.cpu_count() or 16))
 
     if rank == 0:
         out = {
@@ -353,11 +401,15 @@ def main():
             "kernel_ms_per_step": {k: v[0] / max(1, v[1]) for k, v in kall.items() if v[1]},
             "gn_iteration_batched": gn,
             "single_window": single,
+            "s11": s11,
             "tracker": tracker,
             "cpu_baseline": cpu,
+            "cpu_baseline_all_job_cores": cpu16,
         }
         if cpu is not None:
             out["speedup_vs_cpu"] = value / cpu["value"]
+        if cpu16 is not None:
+            out["speedup_vs_cpu_all_job_cores"] = value / cpu16["value"]
         print(json.dumps(out))
     ctx.close()
     if dist is not None:

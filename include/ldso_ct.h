@@ -76,6 +76,12 @@ int ldso_ct_calc_res_batch(ldso_ct_ctx *ctx, int32_t lvl, int32_t n_hyp, const d
  * ldso_ct_calc_res at this level.  H_out [8][8], b_out [8]. */
 int ldso_ct_calc_gs(ldso_ct_ctx *ctx, int32_t lvl, const double ref_to_new[12], double aff_a, double aff_b,
                     double *H_out, double *b_out);
+/* calcRes followed by calcGSSSE at the same pose (what trackNewestCoarse does at the start of
+ * each level and for every LM step, CoarseTracker.cc:90-105, 218-245; a rejected step simply
+ * ignores H and b): both launches
+ * back to back on the context stream and one round trip; results equal the two separate calls. */
+int ldso_ct_calc_res_gs(ldso_ct_ctx *ctx, int32_t lvl, const double ref_to_new[12], double aff_a, double aff_b,
+                        float cutoff_th, double rs_out[6], double *H_out, double *b_out);
 /* the warped buffers of the last calcRes, compacted in point order and zero-padded to a multiple
  * of 4 exactly as buf_warped_* / buf_warped_n: out [n][8] = {idepth, u, v, dx, dy, residual,
  * weight, refColor}; *n_out = buf_warped_n.  out may be NULL to query n. */

@@ -139,6 +139,8 @@ CT_ABI = [
     ("ldso_ct_calc_res", C.c_int, [C.c_void_p, C.c_int32, f64p, C.c_double, C.c_double, C.c_float, f64p]),
     ("ldso_ct_calc_res_batch", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, f64p, f64p, C.c_float, f64p]),
     ("ldso_ct_calc_gs", C.c_int, [C.c_void_p, C.c_int32, f64p, C.c_double, C.c_double, f64p, f64p]),
+    ("ldso_ct_calc_res_gs", C.c_int,
+     [C.c_void_p, C.c_int32, f64p, C.c_double, C.c_double, C.c_float, f64p, f64p, f64p]),
     ("ldso_ct_get_warped", C.c_int, [C.c_void_p, i32p, f32p, C.c_int32]),
     ("ldso_ct_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("ldso_ct_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),

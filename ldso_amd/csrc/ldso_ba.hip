@@ -798,6 +798,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
         auto consume = [&](int k, const Stage &q) {
             const int j = 8 * k + g;
             bool fin = false;
+            float tt[kSums];
             if (q.gok) {
                 const int ix = (int)q.Ku, iy = (int)q.Kv;
                 const float dx = q.Ku - ix, dy = q.Kv - iy, dxdy = dx * dy;
@@ -827,7 +828,6 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
                     gy = w11 * q.t11.z + w01 * q.t01.z + w10 * q.t10.z + w00 * q.t00.z;
                 }
                 fin = isfinite(I);
-                float tt[kSums];
                 pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt, kMarg ? q.jx : 0.f,
                                    kMarg ? q.jy : 0.f, m_da, m_db);
 #pragma unroll

@@ -373,11 +373,11 @@ int check_level(const ldso_ct_ctx *c, int lvl) {
     return 0;
 }
 
-// launch calcRes for n_hyp poses already staged in h_poses; rs_out [n_hyp][6]
-int run_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_warp, double *rs_out) {
+// launch calcRes for n_hyp poses already staged in h_poses (partials to d_parts[0, n_hyp*nb*8))
+int launch_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_warp, size_t extra_parts) {
     const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
     const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
-    int rc = ensure_parts(c, (size_t)n_hyp * nb * kResParts);
+    int rc = ensure_parts(c, (size_t)n_hyp * nb * kResParts + extra_parts);
     if (rc) return rc;
     CT_TRY(hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n_hyp * sizeof(CtPose), hipMemcpyHostToDevice, c->stream));
     CtResParams P;
@@ -400,11 +400,13 @@ int run_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_
     P.cutoffTH = cutoffTH;
     P.maxEnergy = 2 * kHuberTH * cutoffTH - kHuberTH * kHuberTH;  // CoarseTracker.cc:565-566
     for (int k = 0; k < 9; k++) P.Ki[k] = c->Ki[lvl][k];
-    rc = ct_launch(c, 2, [&] { k_ct_calc_res<<<dim3(nb, n_hyp), kCtThreads, 0, c->stream>>>(P); });
-    if (rc) return rc;
-    CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (size_t)n_hyp * nb * kResParts * sizeof(double),
-                          hipMemcpyDeviceToHost, c->stream));
-    CT_TRY(hipStreamSynchronize(c->stream));
+    return ct_launch(c, 2, [&] { k_ct_calc_res<<<dim3(nb, n_hyp), kCtThreads, 0, c->stream>>>(P); });
+}
+
+// the Vec6 of every hypothesis from the block partials already on the host
+void finish_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, bool write_warp, double *rs_out) {
+    const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
+    const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
     for (int hI = 0; hI < n_hyp; hI++) {
         double s[kResParts] = {0};
         const double *p = c->h_parts + (size_t)hI * nb * kResParts;
@@ -422,7 +424,57 @@ int run_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_
         rs[5] = nSat / (float)nE;
         if (write_warp && hI == 0) c->last_warped = (int)s[6];
     }
+}
+
+int run_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_warp, double *rs_out) {
+    int rc = launch_calc_res(c, lvl, n_hyp, cutoffTH, write_warp, 0);
+    if (rc) return rc;
+    const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
+    const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
+    CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (size_t)n_hyp * nb * kResParts * sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+    CT_TRY(hipStreamSynchronize(c->stream));
+    finish_calc_res(c, lvl, n_hyp, write_warp, rs_out);
     return 0;
+}
+
+// calcGSSSE launch over the warped buffers, partials at d_parts + off
+int launch_calc_gs(ldso_ct_ctx *c, int lvl, double aff_a, double aff_b, size_t off) {
+    const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
+    const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
+    float aLL, bLL;
+    affine_from_to(c->ref_exposure, c->new_exposure, c->ref_a, c->ref_b, (float)aff_a, (float)aff_b, aLL, bLL);
+    CtGsParams P;
+    P.state = c->d_state;
+    P.warp = c->d_warp;
+    P.parts = c->d_parts + off;
+    P.n = n;
+    P.fxl = c->fx[lvl];
+    P.fyl = c->fy[lvl];
+    P.a = (float)(double)aLL;
+    P.b0 = c->ref_b;
+    return ct_launch(c, 3, [&] { k_ct_calc_gs<<<nb, kCtThreads, 0, c->stream>>>(P); });
+}
+
+// Accumulator9::finish + CoarseTracker.cc:725-740 from the GS block partials on the host
+void finish_calc_gs(ldso_ct_ctx *c, int lvl, const double *parts, double *H_out, double *b_out) {
+    const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
+    const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
+    double s[kGsParts] = {0};
+    for (int b = 0; b < nb; b++)
+        for (int k = 0; k < kGsParts; k++) s[k] += parts[(size_t)b * kGsParts + k];
+    float H[9][9];
+    int k = 0;
+    for (int r = 0; r < 9; r++)
+        for (int cc = r; cc < 9; cc++, k++) H[r][cc] = H[cc][r] = (float)s[k];
+    const int nw = (c->last_warped + 3) / 4 * 4;  // buf_warped_n (padded to a multiple of 4)
+    const double inv_n = (double)(1.0f / nw);
+    const float scale[8] = {kScaleXiTrans, kScaleXiTrans, kScaleXiTrans, kScaleXiRot,
+                            kScaleXiRot,   kScaleXiRot,   kScaleA,       kScaleB};
+    for (int r = 0; r < 8; r++) {
+        for (int cc = 0; cc < 8; cc++) H_out[8 * r + cc] = (double)H[r][cc] * inv_n * scale[cc] * scale[r];
+        b_out[r] = (double)H[r][8] * inv_n * scale[r];
+    }
 }
 
 }  // namespace
@@ -660,38 +712,35 @@ int ldso_ct_calc_gs(ldso_ct_ctx *c, int32_t lvl, const double ref_to_new[12], do
     const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
     rc = ensure_parts(c, (size_t)nb * kGsParts);
     if (rc) return rc;
-    float aLL, bLL;
-    affine_from_to(c->ref_exposure, c->new_exposure, c->ref_a, c->ref_b, (float)aff_a, (float)aff_b, aLL, bLL);
-    CtGsParams P;
-    P.state = c->d_state;
-    P.warp = c->d_warp;
-    P.parts = c->d_parts;
-    P.n = n;
-    P.fxl = c->fx[lvl];
-    P.fyl = c->fy[lvl];
-    P.a = (float)(double)aLL;
-    P.b0 = c->ref_b;
-    rc = ct_launch(c, 3, [&] { k_ct_calc_gs<<<nb, kCtThreads, 0, c->stream>>>(P); });
+    rc = launch_calc_gs(c, lvl, aff_a, aff_b, 0);
     if (rc) return rc;
     CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (size_t)nb * kGsParts * sizeof(double), hipMemcpyDeviceToHost,
                           c->stream));
     CT_TRY(hipStreamSynchronize(c->stream));
-    double s[kGsParts] = {0};
-    for (int b = 0; b < nb; b++)
-        for (int k = 0; k < kGsParts; k++) s[k] += c->h_parts[(size_t)b * kGsParts + k];
-    // Accumulator9::finish -> float H (MatrixAccumulators.h:1121-1135), then CoarseTracker.cc:725-740
-    float H[9][9];
-    int k = 0;
-    for (int r = 0; r < 9; r++)
-        for (int cc = r; cc < 9; cc++, k++) H[r][cc] = H[cc][r] = (float)s[k];
-    const int nw = (c->last_warped + 3) / 4 * 4;  // buf_warped_n (padded to a multiple of 4)
-    const double inv_n = (double)(1.0f / nw);
-    const float scale[8] = {kScaleXiTrans, kScaleXiTrans, kScaleXiTrans, kScaleXiRot,
-                            kScaleXiRot,   kScaleXiRot,   kScaleA,       kScaleB};
-    for (int r = 0; r < 8; r++) {
-        for (int cc = 0; cc < 8; cc++) H_out[8 * r + cc] = (double)H[r][cc] * inv_n * scale[cc] * scale[r];
-        b_out[r] = (double)H[r][8] * inv_n * scale[r];
-    }
+    finish_calc_gs(c, lvl, c->h_parts, H_out, b_out);
+    return 0;
+}
+
+int ldso_ct_calc_res_gs(ldso_ct_ctx *c, int32_t lvl, const double ref_to_new[12], double aff_a, double aff_b,
+                        float cutoff_th, double rs_out[6], double *H_out, double *b_out) {
+    int rc = check_level(c, lvl);
+    if (rc) return rc;
+    if (!ref_to_new || !rs_out || !H_out || !b_out) return set_error(-1, "null argument");
+    CT_TRY(hipSetDevice(c->device));
+    const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
+    const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
+    const size_t res_parts = (size_t)nb * kResParts;
+    make_pose(c, lvl, ref_to_new, (float)aff_a, (float)aff_b, c->h_poses[0]);
+    rc = launch_calc_res(c, lvl, 1, cutoff_th, true, (size_t)nb * kGsParts);
+    if (rc) return rc;
+    rc = launch_calc_gs(c, lvl, aff_a, aff_b, res_parts);  // same stream: reads the warped buffers just written
+    if (rc) return rc;
+    CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (res_parts + (size_t)nb * kGsParts) * sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+    CT_TRY(hipStreamSynchronize(c->stream));
+    finish_calc_res(c, lvl, 1, true, rs_out);
+    c->last_lvl = lvl;
+    finish_calc_gs(c, lvl, c->h_parts + res_parts, H_out, b_out);
     return 0;
 }
 

@@ -8,6 +8,7 @@ Mirrors the reference class (src/frontend/CoarseTracker.cc) for the parts that r
     setCoarseTrackingRef's pc_* outputs   -> set_reference(levels, ...)        CoarseTracker.cc:357-538
     calcRes(lvl, refToNew, aff, cutoff)   -> calc_res(lvl, T, aff, cutoff)     CoarseTracker.cc:540-673
     calcGSSSE(lvl, H, b, refToNew, aff)   -> calc_gs(lvl, T, aff)              CoarseTracker.cc:675-741
+    calcRes + calcGSSSE at one pose       -> calc_res_gs(lvl, T, aff, cutoff)  CoarseTracker.cc:90-105, 218-245
 
 No numerical work happens here; every call goes to libldso_ba.so (no fallback).
 """
@@ -104,6 +105,16 @@ class CoarseTracker:
         L.check(L.lib().ldso_ct_calc_gs(self._h, int(lvl), L.ptr(T, L.f64p), float(aff_ab[0]), float(aff_ab[1]),
                                         L.ptr(H, L.f64p), L.ptr(b, L.f64p)))
         return H, b
+
+    def calc_res_gs(self, lvl: int, ref_to_new, aff_ab=(0.0, 0.0), cutoff_th: float = 20.0):
+        """calcRes + calcGSSSE at the same pose in one round trip -> (rs[6], H 8x8, b 8)."""
+        T = np.ascontiguousarray(np.asarray(ref_to_new, np.float64)[:3, :4])
+        rs = np.zeros(6, np.float64)
+        H = np.zeros((8, 8), np.float64)
+        b = np.zeros(8, np.float64)
+        L.check(L.lib().ldso_ct_calc_res_gs(self._h, int(lvl), L.ptr(T, L.f64p), float(aff_ab[0]), float(aff_ab[1]),
+                                            float(cutoff_th), L.ptr(rs, L.f64p), L.ptr(H, L.f64p), L.ptr(b, L.f64p)))
+        return rs, H, b
 
     def warped(self) -> np.ndarray:
         """buf_warped_* of the last calc_res as [n][8] {idepth, u, v, dx, dy, residual, weight, refColor}."""

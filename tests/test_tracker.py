@@ -249,6 +249,23 @@ def test_gpu_calc_res_batch_equals_single_calls(built):
 
 
 @pytest.mark.gpu
+def test_gpu_fused_res_gs_equals_separate_calls(built):
+    w, h = 640, 480
+    color, levels, pcs, calib, K = scene(w, h, 3)
+    ct = _tracker(w, h, color, pcs, calib)
+    for l in range(ct.levels):
+        for i in range(3):
+            T = pose(10 + i, 2.0 ** l)
+            rs, H, b = ct.calc_res_gs(l, T, AFF6[4:6], 20.0)
+            rs2 = ct.calc_res(l, T, AFF6[4:6], 20.0)
+            H2, b2 = ct.calc_gs(l, T, AFF6[4:6])
+            np.testing.assert_array_equal(rs, rs2)
+            np.testing.assert_array_equal(H, H2)
+            np.testing.assert_array_equal(b, b2)
+    ct.close()
+
+
+@pytest.mark.gpu
 def test_gpu_tracker_edge_cases(built):
     from ldso_amd.tracker import CoarseTracker
 
