@@ -641,6 +641,54 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
     t[16] = ra * ra;
 }
 
+// G += U^T diag(Wt) U over the upper 4x4 tiles of the (KP x KP) block of one point chunk
+// (AccumulatedSCHessianSSE::addPoint's accD/accE/accEB/accHcc/accbc updates, summed by point):
+// 16 products per point as 8 packed FMAs on diagonal pairs (after 2 packed weight multiplies),
+// e.g. {acc00, acc11} += {ua.x, ua.y} * {ub.x, ub.y} and {acc01, acc10} += {ua.x, ua.y} *
+// {ub.y, ub.x}: both operands are natural register pairs (or a swapped one), no broadcast moves.
+__device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int KP, int nt, int ntiles, int cnt,
+                                           float *slab, int tid, int nthreads) {
+    for (int tile = tid; tile < ntiles; tile += nthreads) {
+        int a = 0, rem = tile;
+        while (rem >= nt - a) {
+            rem -= nt - a;
+            a++;
+        }
+        const int bb = a + rem;
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 c[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) c[i] = f2{0.f, 0.f};
+        const float *pa = U + 4 * a, *pb = U + 4 * bb;
+#pragma unroll 4
+        for (int p = 0; p < cnt; p++, pa += KP, pb += KP) {
+            const float w = Wt[p];
+            const float4 ua = *(const float4 *)pa;
+            const float4 ub = *(const float4 *)pb;
+            const f2 a01 = f2{ua.x, ua.y} * w, a23 = f2{ua.z, ua.w} * w;
+            const f2 b01 = {ub.x, ub.y}, b10 = {ub.y, ub.x}, b23 = {ub.z, ub.w}, b32 = {ub.w, ub.z};
+            c[0] += a01 * b01;  // (0,0) (1,1)
+            c[1] += a01 * b10;  // (0,1) (1,0)
+            c[2] += a01 * b23;  // (0,2) (1,3)
+            c[3] += a01 * b32;  // (0,3) (1,2)
+            c[4] += a23 * b01;  // (2,0) (3,1)
+            c[5] += a23 * b10;  // (2,1) (3,0)
+            c[6] += a23 * b23;  // (2,2) (3,3)
+            c[7] += a23 * b32;  // (2,3) (3,2)
+        }
+        float acc[16];
+        acc[0] = c[0].x, acc[5] = c[0].y, acc[1] = c[1].x, acc[4] = c[1].y;
+        acc[2] = c[2].x, acc[7] = c[2].y, acc[3] = c[3].x, acc[6] = c[3].y;
+        acc[8] = c[4].x, acc[13] = c[4].y, acc[9] = c[5].x, acc[12] = c[5].y;
+        acc[10] = c[6].x, acc[15] = c[6].y, acc[11] = c[7].x, acc[14] = c[7].y;
+        float4 *o = (float4 *)(slab + (size_t)tile * 16);
+        o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+        o[2] = make_float4(acc[8], acc[9], acc[10], acc[11]);
+        o[3] = make_float4(acc[12], acc[13], acc[14], acc[15]);
+    }
+}
+
 // kImg: 0 row-major float4 texels, 1 2x4-tiled float4 texels, 2 quad records (see k_tile_image),
 // 3 intensity only in 8x4-float tiles with the gradients recomputed (see k_intensity_image)
 template <int kImg, bool kXcdRemap, bool kMarg>
@@ -1122,51 +1170,8 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     }
     __syncthreads();
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
-    const int cnt = it.y;
-    float *slab = P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16;
-    for (int tile = tid; tile < ntiles; tile += blockDim.x) {
-        int a = 0, rem = tile;
-        while (rem >= nt - a) {
-            rem -= nt - a;
-            a++;
-        }
-        const int bb = a + rem;
-        // G += U^T diag(HdiF) U on 4x4 tiles: 16 products per point as 8 packed FMAs on
-        // diagonal pairs (after 2 packed weight multiplies), e.g. {acc00, acc11} +=
-        // {ua.x, ua.y} * {ub.x, ub.y} and {acc01, acc10} += {ua.x, ua.y} * {ub.y, ub.x}: both
-        // operands are natural register pairs (or a swapped one), so no broadcast moves
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 c[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) c[i] = f2{0.f, 0.f};
-        const float *pa = U + 4 * a, *pb = U + 4 * bb;
-#pragma unroll 4
-        for (int p = 0; p < cnt; p++, pa += KP, pb += KP) {
-            const float w = Wt[p];
-            const float4 ua = *(const float4 *)pa;
-            const float4 ub = *(const float4 *)pb;
-            const f2 a01 = f2{ua.x, ua.y} * w, a23 = f2{ua.z, ua.w} * w;
-            const f2 b01 = {ub.x, ub.y}, b10 = {ub.y, ub.x}, b23 = {ub.z, ub.w}, b32 = {ub.w, ub.z};
-            c[0] += a01 * b01;  // (0,0) (1,1)
-            c[1] += a01 * b10;  // (0,1) (1,0)
-            c[2] += a01 * b23;  // (0,2) (1,3)
-            c[3] += a01 * b32;  // (0,3) (1,2)
-            c[4] += a23 * b01;  // (2,0) (3,1)
-            c[5] += a23 * b10;  // (2,1) (3,0)
-            c[6] += a23 * b23;  // (2,2) (3,3)
-            c[7] += a23 * b32;  // (2,3) (3,2)
-        }
-        float acc[16];
-        acc[0] = c[0].x, acc[5] = c[0].y, acc[1] = c[1].x, acc[4] = c[1].y;
-        acc[2] = c[2].x, acc[7] = c[2].y, acc[3] = c[3].x, acc[6] = c[3].y;
-        acc[8] = c[4].x, acc[13] = c[4].y, acc[9] = c[5].x, acc[12] = c[5].y;
-        acc[10] = c[6].x, acc[15] = c[6].y, acc[11] = c[7].x, acc[14] = c[7].y;
-        float4 *o = (float4 *)(slab + (size_t)tile * 16);
-        o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-        o[2] = make_float4(acc[8], acc[9], acc[10], acc[11]);
-        o[3] = make_float4(acc[12], acc[13], acc[14], acc[15]);
-    }
+    syrk_tiles(U, Wt, KP, nt, ntiles, it.y,
+               P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16, tid, blockDim.x);
 }
 
 // ============================================================================================
