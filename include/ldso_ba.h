@@ -294,7 +294,11 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              on a second stream beside k_point_sc; 0 (default; measured: the
  *                              split pass is 3% slower, 188 vs 182 us on 64 x S7): one k_stitch
  *   LDSO_BA_TUNE_ITEM_ORDER    k_linearize chunk order: 0 (default) target-major, 1 host-major;
- *                              set before ldso_ba_load */
+ *                              set before ldso_ba_load
+ *   LDSO_BA_TUNE_FUSED         1: point-major k_linearize that also runs the point's Schur term
+ *                              (k_point_sc folded in, records kept in LDS); 0 (default; measured:
+ *                              the fused pass is 4% slower, 189 vs 182 us on 64 x S7): chunk-major
+ *                              k_linearize + k_point_sc; set before ldso_ba_load */
 #define LDSO_BA_TUNE_LIN_VARIANT 1
 #define LDSO_BA_TUNE_TILED_IMAGES 2
 #define LDSO_BA_TUNE_LOAD3 3
@@ -305,6 +309,7 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
 #define LDSO_BA_TUNE_PIPELINE_GROUPS 8
 #define LDSO_BA_TUNE_STITCH_SPLIT 9
 #define LDSO_BA_TUNE_ITEM_ORDER 10
+#define LDSO_BA_TUNE_FUSED 11
 int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);

@@ -122,7 +122,16 @@ struct LinParams {
     int fix;
     int accumulate;
     const float *ad_ht_delta;  // [pair_global][8] EnergyFunctional::adHTdeltaF (marginalisation pass)
+    // fused (point-major) pass: one workgroup per 32-point block of one host, wave w holding the
+    // block's residuals to target slots 2w and 2w+1; the SC half of k_point_sc runs in the block
+    const int4 *__restrict__ pblocks;  // {first point (global), points, first half, window}
+    const int *__restrict__ pt_nres;
+    const unsigned long long *__restrict__ pt_tgt;
+    float *pt_out;                     // [P][12]
+    float *sc_slab;
+    int shift_prior;                   // AccumulatedSCHessianSSE::addPoint's shiftPriorToZero
 };
+constexpr int kFusedPts = 32;  // points per fused workgroup (two target slots per wavefront)
 
 struct Geo {
     float Ku, Kv, new_idepth;
@@ -317,6 +326,29 @@ __device__ __forceinline__ void write_record(float4 *rec, bool active, const Geo
     }
 }
 
+// Fused pass: the full record goes to LDS for the block's SC phase; global memory keeps what
+// k_resubstitute and ldso_ba_get_residuals read (JpJdF and the active marker).
+__device__ __forceinline__ void write_record_fused(float4 *grec, float4 *lrec, bool active, const Geo &g,
+                                                   const PhotoSums &s) {
+    if (active) {
+        float jp[8], hc[4], hdd, bd;
+        point_terms(g, s, jp, hc, hdd, bd);
+        const float4 r0 = make_float4(jp[0], jp[1], jp[2], jp[3]), r1 = make_float4(jp[4], jp[5], jp[6], jp[7]);
+        const float4 r3 = make_float4(hdd, bd, 1.f, 0.f);
+        grec[0] = r0;
+        grec[1] = r1;
+        grec[3] = r3;
+        lrec[0] = r0;
+        lrec[1] = r1;
+        lrec[2] = make_float4(hc[0], hc[1], hc[2], hc[3]);
+        lrec[3] = r3;
+    } else {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        grec[3] = z;
+        lrec[3] = z;
+    }
+}
+
 // Recursive-halving wavefront reduction of 96 floats: 96 shuffles instead of 6*96.  On return
 // lane l (all 64) holds the full sums of elements base(l) + {0,1,2}, base = 48 b0 + 24 b1 +
 // 12 b2 + 6 b3 + 3 b4 (b = bits of the lane id).
@@ -395,8 +427,10 @@ __device__ __forceinline__ void first_halve24(const TopIn &t, float *v, bool upp
         first_halve24<Off, I + 1>(t, v, upper);
     }
 }
-template <int Off>
-__device__ __forceinline__ void reduce_top_pass(const TopIn &t, int lane, float *slab_item) {
+// kHalves: lanes 0-31 and 32-63 are reduced separately (two pairs per wavefront, fused pass);
+// each half's lanes 0-15 (and 32-47) write their own slab item (write_ok per half).
+template <int Off, bool kHalves = false>
+__device__ __forceinline__ void reduce_top_pass(const TopIn &t, int lane, float *slab_item, bool write_ok = true) {
     float v[24];
     first_halve24<Off, 0>(t, v, (lane & 1) != 0);
     halve<24, 2>(v, lane);
@@ -405,9 +439,9 @@ __device__ __forceinline__ void reduce_top_pass(const TopIn &t, int lane, float 
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         v[i] += __shfl_xor(v[i], 16, kWave);
-        v[i] += __shfl_xor(v[i], 32, kWave);
+        if (!kHalves) v[i] += __shfl_xor(v[i], 32, kWave);
     }
-    if (lane < 16) {
+    if (kHalves ? ((lane & 31) < 16 && write_ok) : lane < 16) {
         const int base = Off + 24 * (lane & 1) + 12 * ((lane >> 1) & 1) + 6 * ((lane >> 2) & 1) + 3 * ((lane >> 3) & 1);
         slab_item[base] = v[0];
         slab_item[base + 1] = v[1];
@@ -691,32 +725,90 @@ __device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int 
 
 // kImg: 0 row-major float4 texels, 1 2x4-tiled float4 texels, 2 quad records (see k_tile_image),
 // 3 intensity only in 8x4-float tiles with the gradients recomputed (see k_intensity_image)
-template <int kImg, bool kXcdRemap, bool kMarg>
-__global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
+// Per wavefront LDS: the per-pixel addends [8 residuals][kSums][8 pixels] and the per-residual
+// sums [64][kSumStride] (dynamic shared memory: 4 waves in the chunk-major pass, (N-1)/2 rounded
+// up in the fused one).  In the fused pass the addend region of wave w then holds the records
+// of target slots 2w, 2w+1 and the sums regions the block's SYRK rows.
+constexpr int kTermsPerWave = 8 * kSums * 8;
+constexpr int kSumsPerWave = 64 * kSumStride;
+// + the block's SYRK weights and its points' {nres, targets lo/hi, priorF, deltaF} (fused)
+__host__ __device__ constexpr size_t lin_lds_bytes(int waves) {
+    return ((size_t)waves * (kTermsPerWave + kSumsPerWave) + 6 * kFusedPts) * sizeof(float);
+}
+#ifndef LDSO_EXP_FUSED_NO_SC
+#define LDSO_EXP_FUSED_NO_SC 0
+#endif
+#ifndef LDSO_EXP_FUSED_NO_SYRK
+#define LDSO_EXP_FUSED_NO_SYRK 0
+#endif
+#ifndef LDSO_EXP_FUSED_PREFETCH
+#define LDSO_EXP_FUSED_PREFETCH 1
+#endif
+template <int kImg, bool kXcdRemap, bool kMarg, bool kFused>
+__global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParams P) {
     constexpr bool kTiled = kImg == 1;
-    __shared__ float lds_terms[4][8][kSums][8];
-    __shared__ __attribute__((aligned(16))) float lds_sums[4][64][kSumStride];
+    extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwaves = blockDim.x >> 6;
+    float *lds_terms_w = lds_dyn + wave * kTermsPerWave;
+    float *lds_sums_w = lds_dyn + nwaves * kTermsPerWave + wave * kSumsPerWave;
     const int nb = P.n_blocks, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
     const int lblock = kXcdRemap ? xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3) : (int)blockIdx.x;
-    if (lblock * 4 + wave >= P.n_items) return;
-    const int item = P.item_base + lblock * 4 + wave;  // global chunk index
-    const int4 it = P.items[item];
-    const WinDev &W = P.wins[it.w];
+    // chunk-major: wave = one chunk of <= 64 residuals of one pair.  fused: lanes 0-31 / 32-63
+    // hold the block's residuals to target slot 2w / 2w+1 (one pair each).
+    int4 it, bd = make_int4(0, 0, 0, 0);
+    int itemL, pairA, pairB, jlimit, half_slot = 0;
+    bool valid;
+    if constexpr (kFused) {
+        if (lblock >= P.n_items) return;  // whole blocks only: the SC phase synchronises the block
+        bd = P.pblocks[P.item_base + lblock];
+        const int nhalf = P.wins[bd.w].N - 1;
+        half_slot = 2 * wave + (lane >> 5);
+        const bool hv = half_slot < nhalf;
+        it = P.items[bd.z + min(half_slot, nhalf - 1)];  // {res_begin, count, pair, slab item}
+        itemL = it.w;
+        valid = hv && (lane & 31) < it.y;
+        pairA = __builtin_amdgcn_readfirstlane(it.z);
+        pairB = __shfl(it.z, 32, kWave);
+        pairB = __builtin_amdgcn_readfirstlane(pairB);
+        jlimit = 64;
+        if (LDSO_EXP_FUSED_PREFETCH && (int)threadIdx.x < bd.y) {
+            // the SC tail's per-point inputs, fetched now so their latency hides under phase A
+            const int p = bd.x + threadIdx.x;
+            int *side = reinterpret_cast<int *>(lds_dyn + nwaves * (kTermsPerWave + kSumsPerWave) + kFusedPts);
+            const unsigned long long tg = P.pt_tgt[p];
+            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+            side[threadIdx.x] = P.pt_nres[p];
+            side[kFusedPts + threadIdx.x] = (int)(unsigned)tg;
+            side[2 * kFusedPts + threadIdx.x] = (int)(unsigned)(tg >> 32);
+            side[3 * kFusedPts + threadIdx.x] = __float_as_int(pd[4]);
+            side[4 * kFusedPts + threadIdx.x] = __float_as_int(pd[5]);
+        }
+    } else {
+        if (lblock * 4 + wave >= P.n_items) return;
+        itemL = P.item_base + lblock * 4 + wave;  // global chunk index
+        it = P.items[itemL];
+        valid = lane < it.y;
+        pairA = pairB = it.z;
+        jlimit = it.y;
+    }
+    const WinDev &W = P.wins[kFused ? bd.w : it.w];
     const int N = W.N;
-    const int aidx = it.z - W.pair_base;
-    const int h = aidx % N, t = aidx / N;
-    const float *pre = P.precalc + (size_t)it.z * LDSO_BA_PRECALC_STRIDE;
-    const float4 *img = P.img + (size_t)(W.frame_base + t) * P.frame_stride;
-    const float th = fmaxf(P.frame_th[W.frame_base + h], P.frame_th[W.frame_base + t]);
+    const int h = (pairA - W.pair_base) % N, tA = (pairA - W.pair_base) / N, tB = (pairB - W.pair_base) / N;
+    const float *preA = P.precalc + (size_t)pairA * LDSO_BA_PRECALC_STRIDE;
+    const float *preB = P.precalc + (size_t)pairB * LDSO_BA_PRECALC_STRIDE;
+    const float4 *imgA = P.img + (size_t)(W.frame_base + tA) * P.frame_stride;
+    const float4 *imgB = P.img + (size_t)(W.frame_base + tB) * P.frame_stride;
+    const bool upper = kFused && lane >= 32;
+    const float *pre = upper ? preB : preA;  // this lane's residual's pair
+    const float th = fmaxf(P.frame_th[W.frame_base + h], P.frame_th[W.frame_base + (upper ? tB : tA)]);
     const float wM3 = W.wM3, hM3 = W.hM3;
 
-    const bool valid = lane < it.y;
-    const int r = it.x + lane;
+    const int r = it.x + (kFused ? (lane & 31) : lane);
     // Everything phase B needs is loaded up front (unconditionally, from a clamped index: a load
     // inside a divergent branch is waited for at the branch's end) so it lands during phase A.
-    const int rq = valid ? r : it.x;
+    const int rq = valid ? r : 0;
     int my_state = P.rs_state[rq];
     const int my_point = P.rs_point[rq];
     const int my_slot = P.rs_slot[rq];
@@ -728,12 +820,14 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
     if (!valid) my_state = LDSO_BA_RES_OOB;
     // marginalisation pass: Jp * delta of fixLinearizationF (Residuals.cc:221-232) from the centre
     // geometry, per residual, before the pattern pixels need it (dot products left to right)
-    float jp_dx = 0.f, jp_dy = 0.f, m_da = 0.f, m_db = 0.f;
+    float jp_dx = 0.f, jp_dy = 0.f, daA = 0.f, dbA = 0.f, daB = 0.f, dbB = 0.f;
     if constexpr (kMarg) {
 #pragma clang fp contract(off)
-        const float *dp = P.ad_ht_delta + (size_t)it.z * 8;
-        m_da = dp[6];
-        m_db = dp[7];
+        const float *dp = P.ad_ht_delta + (size_t)(upper ? pairB : pairA) * 8;
+        daA = P.ad_ht_delta[(size_t)pairA * 8 + 6];  // delta_a, delta_b of each step's pair
+        dbA = P.ad_ht_delta[(size_t)pairA * 8 + 7];
+        daB = P.ad_ht_delta[(size_t)pairB * 8 + 6];
+        dbB = P.ad_ht_delta[(size_t)pairB * 8 + 7];
         Geo gm;
         if (centre_projection(pre, my_pd0.x, my_pd0.y, my_pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
                               wM3, hM3, gm)) {
@@ -763,10 +857,15 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
         // staticPattern[8] (Setting.cc:275) offset of this lane's pixel
         const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
         const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
-        const float aff0 = pre[24], aff1 = pre[25], b0 = pre[26];
-        float *T = &lds_terms[wave][g][0][0];
-        float *S = &lds_sums[wave][0][0];
-        const int nsteps = (it.y + 7) >> 3;
+        // a step's 8 residuals share one pair (the fused pass switches pair at step 4)
+        const float aff0A = preA[24], aff1A = preA[25], b0A = preA[26];
+        const float aff0B = preB[24], aff1B = preB[25], b0B = preB[26];
+        float *T = lds_terms_w + g * (kSums * 8);
+        float *S = lds_sums_w;
+        int nsteps = (jlimit + 7) >> 3;
+        if constexpr (kFused) {  // skip the upper half's steps when this wave has no slot 2w+1
+            if (2 * wave + 1 >= N - 1) nsteps = 4;
+        }
         const int tpr2 = P.tiles_per_row;
 
         struct Stage {
@@ -779,11 +878,13 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
         };
         auto issue = [&](int k, Stage &q) {
             const int j = 8 * k + g;
+            const float *pre = (kFused && k >= 4) ? preB : preA;  // the step's pair (uniform)
+            const float4 *img = (kFused && k >= 4) ? imgB : imgA;
             const int st = __shfl(my_state, j, kWave);
             const int p = __shfl(my_point, j, kWave);
             const float pu = __shfl(my_pd0.x, j, kWave), pv = __shfl(my_pd0.y, j, kWave),
                         pz = __shfl(my_pd0.z, j, kWave);
-            const bool go = j < it.y && st != LDSO_BA_RES_OOB;
+            const bool go = j < jlimit && st != LDSO_BA_RES_OOB;
             if constexpr (kMarg) {
                 q.jx = __shfl(jp_dx, j, kWave);
                 q.jy = __shfl(jp_dy, j, kWave);
@@ -876,8 +977,10 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
                     gy = w11 * q.t11.z + w01 * q.t01.z + w10 * q.t10.z + w00 * q.t00.z;
                 }
                 fin = isfinite(I);
-                pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt, kMarg ? q.jx : 0.f,
-                                   kMarg ? q.jy : 0.f, m_da, m_db);
+                const bool hb = kFused && k >= 4;
+                pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, hb ? aff0B : aff0A, hb ? aff1B : aff1A,
+                                   hb ? b0B : b0A, tt, kMarg ? q.jx : 0.f, kMarg ? q.jy : 0.f, hb ? daB : daA,
+                                   hb ? dbB : dbA);
 #pragma unroll
                 for (int e = 0; e < kSums; e++) T[e * 8 + sl] = tt[e];
             }
@@ -903,7 +1006,7 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
                     }
                 }
             }
-            if (sl == 0 && j < it.y) S[j * kSumStride + kSums] = rok ? 1.0f : 0.0f;
+            if (sl == 0 && j < jlimit) S[j * kSumStride + kSums] = rok ? 1.0f : 0.0f;
             wave_lds_sync();
         };
         // ping-pong stages, loads issued unconditionally (a step past the item's end has no valid
@@ -944,9 +1047,12 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
         if (old_state == LDSO_BA_RES_OOB) {
             energy = state_energy;
             P.pt_rec[(size_t)my_slot * 4 + 3] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
+            if constexpr (kFused)
+                reinterpret_cast<float4 *>(lds_terms_w)[((lane >> 5) * kFusedPts + (my_point - bd.x)) * 4 + 3] =
+                    make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
             const float4 pd0 = my_pd0;
-            const float *Sr = &lds_sums[wave][lane][0];
+            const float *Sr = lds_sums_w + lane * kSumStride;
             const float4 s0 = *(const float4 *)(Sr), s1 = *(const float4 *)(Sr + 4), s2 = *(const float4 *)(Sr + 8),
                          s3 = *(const float4 *)(Sr + 12), s4 = *(const float4 *)(Sr + 16);
             s.energy = s0.x;
@@ -993,7 +1099,13 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
             flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
             state_energy = new_energy;
 #if !LDSO_EXP_NO_REC
-            write_record(P.pt_rec + (size_t)my_slot * 4, active, g, s);
+            if constexpr (kFused)
+                write_record_fused(P.pt_rec + (size_t)my_slot * 4,
+                                   reinterpret_cast<float4 *>(lds_terms_w) +
+                                       ((lane >> 5) * kFusedPts + (my_point - bd.x)) * 4,
+                                   active, g, s);
+            else
+                write_record(P.pt_rec + (size_t)my_slot * 4, active, g, s);
 #endif
             if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
 #pragma clang fp contract(off)
@@ -1019,11 +1131,13 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
 
     double esum = energy;
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
+    for (int m = kFused ? 16 : 32; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
     const unsigned long long inmask = __ballot(isIN);
-    if (lane == 0) {
-        P.item_energy[2 * item] = esum;
-        P.item_energy[2 * item + 1] = (double)__popcll(inmask);
+    const bool half_ok = !kFused || half_slot < N - 1;  // this lane's half has a target slot
+    if ((kFused ? (lane & 31) : lane) == 0 && half_ok) {
+        P.item_energy[2 * itemL] = esum;
+        P.item_energy[2 * itemL + 1] =
+            (double)__popcll(kFused ? (upper ? inmask >> 32 : inmask & 0xFFFFFFFFull) : inmask);
     }
     if (!P.accumulate) return;
 
@@ -1061,9 +1175,87 @@ __global__ __launch_bounds__(256, 4) void k_linearize_sp(LinParams P) {
 #pragma unroll
         for (int i = 0; i < 6; i++) tin.tr[i] = tin.br[i] = 0;
     }
-    float *slab_item = P.top_slab + (size_t)item * kTopVals;
-    reduce_top_pass<0>(tin, lane, slab_item);
-    reduce_top_pass<48>(tin, lane, slab_item);
+    float *slab_item = P.top_slab + (size_t)itemL * kTopVals;
+    reduce_top_pass<0, kFused>(tin, lane, slab_item, half_ok);
+    reduce_top_pass<48, kFused>(tin, lane, slab_item, half_ok);
+
+    if constexpr (kFused && !LDSO_EXP_FUSED_NO_SC) {
+        // ---- the block's SC half (k_point_sc for its 32 points), records read from LDS ----
+        __syncthreads();  // every record of the block is in LDS; the sums regions are free
+        const int npts = bd.y, KP = W.KP, nt = KP / 4, ntiles = W.ntiles, Kj = 8 * (N - 1);
+        float *U = lds_dyn + nwaves * kTermsPerWave;  // [32][KP] over the sums regions
+        float *Wt = lds_dyn + nwaves * (kTermsPerWave + kSumsPerWave);
+        for (int i = threadIdx.x; i < kFusedPts * KP; i += blockDim.x) U[i] = 0;
+        __syncthreads();
+        const int tq = threadIdx.x;
+        if (tq < npts) {
+#pragma clang fp contract(off)
+            const int p = bd.x + tq;
+            const int *side = reinterpret_cast<const int *>(Wt + kFusedPts);
+            const int nres = LDSO_EXP_FUSED_PREFETCH ? side[tq] : P.pt_nres[p];
+            const unsigned long long tgs =
+                LDSO_EXP_FUSED_PREFETCH ? (unsigned long long)(unsigned)side[kFusedPts + tq] |
+                                              ((unsigned long long)(unsigned)side[2 * kFusedPts + tq] << 32)
+                                        : P.pt_tgt[p];
+            float hdd = 0, bsum = 0, hcd[4] = {0, 0, 0, 0};
+            int ngood = 0;
+            float *row = U + tq * KP;
+            // sums in the point's residual order (AccumulatedTopHessian.cc:94-116)
+            for (int k = 0; k < nres; k++) {
+                const int tg = (int)((tgs >> (4 * k)) & 15ull);
+                const int slot = tg < h ? tg : tg - 1;
+                const float4 *rl = reinterpret_cast<const float4 *>(lds_dyn + (slot >> 1) * kTermsPerWave) +
+                                   ((slot & 1) * kFusedPts + tq) * 4;
+                const float4 hb = rl[3];
+                if (hb.z == 0.0f) continue;
+                ngood++;
+                const float4 j0 = rl[0], j1 = rl[1], hc = rl[2];
+                bsum += hb.y;
+                hdd += hb.x;
+                hcd[0] += hc.x;
+                hcd[1] += hc.y;
+                hcd[2] += hc.z;
+                hcd[3] += hc.w;
+                *(float4 *)(row + 8 * slot) = j0;
+                *(float4 *)(row + 8 * slot + 4) = j1;
+            }
+            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+            const float priorF = LDSO_EXP_FUSED_PREFETCH ? __int_as_float(side[3 * kFusedPts + tq]) : pd[4];
+            const float deltaF = LDSO_EXP_FUSED_PREFETCH ? __int_as_float(side[4 * kFusedPts + tq]) : pd[5];
+            float HdiF = 0, bdSum = 0, ih = 0;
+            if (ngood > 0) {
+                // AccumulatedSCHessian.cc:24-33 (Hdd_accLF = bd_accLF = Hcd_accLF = 0 in the hot path)
+                float H = hdd + 0.0f + priorF;
+                if (H < 1e-10f) H = 1e-10f;
+                ih = H;
+                HdiF = (float)(1.0 / (double)H);
+                bdSum = bsum + 0.0f;
+                if (P.shift_prior) bdSum += priorF * deltaF;
+                row[Kj + 0] = hcd[0] + 0.0f;
+                row[Kj + 1] = hcd[1] + 0.0f;
+                row[Kj + 2] = hcd[2] + 0.0f;
+                row[Kj + 3] = hcd[3] + 0.0f;
+                row[Kj + 4] = bdSum;
+            }
+            Wt[tq] = HdiF;
+            float *o = P.pt_out + (size_t)p * 12;
+            o[0] = HdiF;
+            o[1] = bdSum;
+            o[2] = ih;
+            o[3] = hdd;
+            o[4] = bsum;
+            o[5] = hcd[0];
+            o[6] = hcd[1];
+            o[7] = hcd[2];
+            o[8] = hcd[3];
+            o[9] = (float)ngood;
+        }
+        __syncthreads();
+        const int sc_item = P.item_base + lblock;  // point blocks and SC items share one order
+        if (!LDSO_EXP_FUSED_NO_SYRK)
+            syrk_tiles(U, Wt, KP, nt, ntiles, npts,
+                       P.sc_slab + W.sc_slab_base + (size_t)(sc_item - W.sc_item_base) * ntiles * 16, tq, blockDim.x);
+    }
 }
 
 // ============================================================================================
@@ -2141,25 +2333,50 @@ void launch_lin1(bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t 
 // variant = occupancy target in waves per SIMD (see DESIGN.md for the measured choice)
 template <bool kMarg>
 void launch_sp(int img_mode, bool xcd, int nb, hipStream_t st, const LinParams &L) {
+    const size_t lds = lin_lds_bytes(4);
     if (img_mode == 3) {
-        if (xcd) k_linearize_sp<3, true, kMarg><<<nb, 256, 0, st>>>(L);
-        else k_linearize_sp<3, false, kMarg><<<nb, 256, 0, st>>>(L);
+        if (xcd) k_linearize_sp<3, true, kMarg, false><<<nb, 256, lds, st>>>(L);
+        else k_linearize_sp<3, false, kMarg, false><<<nb, 256, lds, st>>>(L);
     } else if (img_mode == 2) {
-        if (xcd) k_linearize_sp<2, true, kMarg><<<nb, 256, 0, st>>>(L);
-        else k_linearize_sp<2, false, kMarg><<<nb, 256, 0, st>>>(L);
+        if (xcd) k_linearize_sp<2, true, kMarg, false><<<nb, 256, lds, st>>>(L);
+        else k_linearize_sp<2, false, kMarg, false><<<nb, 256, lds, st>>>(L);
     } else if (img_mode == 1) {
-        if (xcd) k_linearize_sp<1, true, kMarg><<<nb, 256, 0, st>>>(L);
-        else k_linearize_sp<1, false, kMarg><<<nb, 256, 0, st>>>(L);
+        if (xcd) k_linearize_sp<1, true, kMarg, false><<<nb, 256, lds, st>>>(L);
+        else k_linearize_sp<1, false, kMarg, false><<<nb, 256, lds, st>>>(L);
     } else {
-        if (xcd) k_linearize_sp<0, true, kMarg><<<nb, 256, 0, st>>>(L);
-        else k_linearize_sp<0, false, kMarg><<<nb, 256, 0, st>>>(L);
+        if (xcd) k_linearize_sp<0, true, kMarg, false><<<nb, 256, lds, st>>>(L);
+        else k_linearize_sp<0, false, kMarg, false><<<nb, 256, lds, st>>>(L);
     }
+}
+// the fused (point-major) pass: one workgroup of `waves` wavefronts per 32-point block
+template <bool kMarg>
+void launch_fused(int img_mode, int waves, int nb, hipStream_t st, const LinParams &L) {
+    const size_t lds = lin_lds_bytes(waves);
+    const int th = 64 * waves;
+    if (img_mode == 3) k_linearize_sp<3, true, kMarg, true><<<nb, th, lds, st>>>(L);
+    else if (img_mode == 2) k_linearize_sp<2, true, kMarg, true><<<nb, th, lds, st>>>(L);
+    else if (img_mode == 1) k_linearize_sp<1, true, kMarg, true><<<nb, th, lds, st>>>(L);
+    else k_linearize_sp<0, true, kMarg, true><<<nb, th, lds, st>>>(L);
+}
+int allow_fused_lds(size_t bytes) {
+    if (bytes <= 64 * 1024) return 0;
+    const void *fns[] = {(const void *)k_linearize_sp<3, true, false, true>, (const void *)k_linearize_sp<2, true, false, true>,
+                         (const void *)k_linearize_sp<1, true, false, true>, (const void *)k_linearize_sp<0, true, false, true>,
+                         (const void *)k_linearize_sp<3, true, true, true>,  (const void *)k_linearize_sp<2, true, true, true>,
+                         (const void *)k_linearize_sp<1, true, true, true>,  (const void *)k_linearize_sp<0, true, true, true>};
+    for (const void *f : fns)
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+            return fail(-2, "hipFuncSetAttribute (fused k_linearize LDS)");
+    return 0;
 }
 // marg: the marginalisation pass (addPoint<2> sums; sample-parallel kernel only)
 void launch_linearize(int variant, int img_mode, bool load3, bool xcd, bool cf, int nb, hipStream_t st,
-                      const LinParams &L, bool marg) {
+                      const LinParams &L, bool marg, int fused_waves) {
     const bool tiled = img_mode == 1;
-    if (marg) launch_sp<true>(img_mode, xcd, nb, st, L);
+    if (fused_waves > 0) {
+        if (marg) launch_fused<true>(img_mode, fused_waves, nb, st, L);
+        else launch_fused<false>(img_mode, fused_waves, nb, st, L);
+    } else if (marg) launch_sp<true>(img_mode, xcd, nb, st, L);
     else if (variant == 3) launch_sp<false>(img_mode, xcd, nb, st, L);
     else if (variant == 2) launch_lin1<4>(tiled, load3, xcd, cf, nb, st, L);
     else launch_lin1<1>(tiled, load3, xcd, cf, nb, st, L);
@@ -2226,7 +2443,13 @@ struct ldso_ba_ctx {
 #ifndef LDSO_ITEM_ORDER_DEFAULT
 #define LDSO_ITEM_ORDER_DEFAULT 0
 #endif
-    int item_order = LDSO_ITEM_ORDER_DEFAULT;  // k_linearize chunk order: 0 target-major, 1 host-major  // Top half of k_stitch on stream2, overlapping k_point_sc (LDSO_BA_TUNE_STITCH_SPLIT)
+    int item_order = LDSO_ITEM_ORDER_DEFAULT;  // k_linearize chunk order: 0 target-major, 1 host-major
+#ifndef LDSO_FUSED_DEFAULT
+#define LDSO_FUSED_DEFAULT 0
+#endif
+    bool fused_req = LDSO_FUSED_DEFAULT;  // point-major fused pass (LDSO_BA_TUNE_FUSED), chosen at load
+    int fused_waves = 0;                  // > 0: the loaded layout is the fused one
+    DevBuf<int4> d_pblocks;  // Top half of k_stitch on stream2, overlapping k_point_sc (LDSO_BA_TUNE_STITCH_SPLIT)
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
     std::vector<WinDev> wd;
@@ -2572,6 +2795,8 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_pt_rec.release();
     c->d_top_items.release();
     c->d_sc_items.release();
+    c->d_pblocks.release();
+    c->d_adhtd.release();
     c->d_pair_items.release();
     c->d_host_items.release();
     c->d_top_slab.release();
@@ -2625,7 +2850,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     c->energy_valid = false;
 
     // host-side layout
-    std::vector<int4> top_items, sc_items;
+    std::vector<int4> top_items, sc_items, pblocks;
     std::vector<int2> pair_items, host_items;
     std::vector<int> pair_win, frame_win, rs_point, rs_slot, pt_nres, pt_host;
     std::vector<unsigned long long> pt_tgt;
@@ -2754,6 +2979,63 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         const int nt = D.KP / 4;
         D.ntiles = nt * (nt + 1) / 2;
         smem_max = std::max(smem_max, sc_smem_bytes(D.KP));
+        if (c->fused_req) {
+            // Fused pass: point blocks of <= 32 points of one host (host order; they are also the
+            // SC items).  Each block has one "half" per target slot: the block's residuals to that
+            // target, contiguous in bucket (h, t).  Top slab items are numbered pair-major (a
+            // pair's items, one per block of its host, are contiguous for k_stitch); a half
+            // records its slab item.
+            D.top_item_base = (int)top_items.size();
+            std::vector<int> nblk(N, 0), hq0(N + 1, 0);
+            {
+                int q = 0;
+                for (int f = 0; f < N; f++) {
+                    hq0[f] = q;
+                    while (q < P && H.pt_host[q] == f) q++;
+                    nblk[f] = (q - hq0[f] + kFusedPts - 1) / kFusedPts;
+                }
+                hq0[N] = q;
+            }
+            std::vector<int> pair_first(N * N, 0);
+            int nslab = 0;
+            for (int b = 0; b < N * N; b++) {
+                const int hh = b % N, tt = b / N;
+                pair_first[b] = nslab;
+                if (hh != tt) nslab += nblk[hh];
+                pair_items.push_back(make_int2(D.top_item_base + pair_first[b], hh != tt ? nblk[hh] : 0));
+                pair_win.push_back(w);
+            }
+            D.sc_item_base = (int)sc_items.size();
+            std::vector<int> first_pos(N), cnt(N);
+            for (int f = 0; f < N; f++) {
+                const int first_sc = (int)sc_items.size();
+                for (int k = 0; k < nblk[f]; k++) {
+                    const int qs = hq0[f] + k * kFusedPts, npts = std::min(kFusedPts, hq0[f + 1] - qs);
+                    sc_items.push_back(make_int4(point_base + qs, npts, f, w));
+                    pblocks.push_back(make_int4(point_base + qs, npts, (int)top_items.size(), w));
+                    std::fill(first_pos.begin(), first_pos.end(), -1);
+                    std::fill(cnt.begin(), cnt.end(), 0);
+                    for (int q = qs; q < qs + npts; q++) {
+                        const int p = H.pt_orig[q];
+                        for (int kk = in.point_res_begin[p]; kk < in.point_res_begin[p + 1]; kk++) {
+                            const int tg = in.res_target[kk], pos = res_pos_of[kk];
+                            if (first_pos[tg] < 0 || pos < first_pos[tg]) first_pos[tg] = pos;
+                            cnt[tg]++;
+                        }
+                    }
+                    for (int sl = 0; sl < N - 1; sl++) {
+                        const int tg = sl < f ? sl : sl + 1;
+                        top_items.push_back(make_int4(res_base + (cnt[tg] ? first_pos[tg] : 0), cnt[tg],
+                                                      pair_base + f + N * tg,
+                                                      D.top_item_base + pair_first[f + N * tg] + k));
+                    }
+                }
+                host_items.push_back(make_int2(first_sc, (int)sc_items.size() - first_sc));
+                frame_win.push_back(w);
+            }
+            D.n_top_items = (int)top_items.size() - D.top_item_base;
+            D.n_sc_items = (int)sc_items.size() - D.sc_item_base;
+        } else {
         // top items: chunks of `chunk` residuals of one bucket (one wave each)
         D.top_item_base = (int)top_items.size();
         const size_t pi0 = pair_items.size();
@@ -2784,6 +3066,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
             }
         }
         D.n_sc_items = (int)sc_items.size() - D.sc_item_base;
+        }
         D.sc_slab_base = sc_slab_total;
         sc_slab_total += (long long)D.n_sc_items * D.ntiles * 16;
         D.sys_base = sys_total;
@@ -2817,6 +3100,12 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     c->sc_smem_max = smem_max;
 
     int rc = 0;
+    // fused pass: ceil((N-1)/2) waves, one target per half-wave
+    c->fused_waves = c->fused_req ? c->max_frames / 2 : 0;
+    if (c->fused_waves) {
+        rc = allow_fused_lds(lin_lds_bytes(c->fused_waves));
+        if (rc) return rc;
+    }
 #define ALLOC(buf, n)                   \
     do {                                \
         rc = (buf).alloc(n);            \
@@ -2851,6 +3140,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_pt_rec, std::max<size_t>(1, (size_t)rec_base * 4));
     ALLOC(c->d_top_items, std::max<size_t>(1, top_items.size()));
     ALLOC(c->d_sc_items, std::max<size_t>(1, sc_items.size()));
+    ALLOC(c->d_pblocks, std::max<size_t>(1, pblocks.size()));
     ALLOC(c->d_pair_items, pair_items.size());
     ALLOC(c->d_host_items, host_items.size());
     ALLOC(c->d_top_slab, std::max<size_t>(1, top_items.size() * kTopVals));
@@ -2895,6 +3185,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     UP(c->d_rs_newenergy, rs_energy);
     UP(c->d_top_items, top_items);
     UP(c->d_sc_items, sc_items);
+    UP(c->d_pblocks, pblocks);
     UP(c->d_pair_items, pair_items);
     UP(c->d_host_items, host_items);
 #undef UP
@@ -3045,6 +3336,12 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     L.tiles_per_row = c->tiles_per_row;
     L.fix = fix;
     L.accumulate = accumulate;
+    L.pblocks = c->d_pblocks.p;
+    L.pt_nres = c->d_pt_nres.p;
+    L.pt_tgt = c->d_pt_tgt.p;
+    L.pt_out = c->d_pt_out.p;
+    L.sc_slab = c->d_sc_slab.p;
+    L.shift_prior = c->marg ? 0 : 1;
     PointParams Pp;
     Pp.items = c->d_sc_items.p;
     Pp.wins = c->d_wins.p;
@@ -3092,13 +3389,15 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         const int ti0 = A.top_item_base, ti1 = B.top_item_base + B.n_top_items;
         const int si0 = A.sc_item_base, si1 = B.sc_item_base + B.n_sc_items;
         const int p0 = A.pair_base, p1 = B.pair_base + B.N * B.N;
-        if (ti1 > ti0) {
-            L.item_base = ti0;
-            L.n_items = ti1 - ti0;
-            L.n_blocks = (L.n_items + 3) / 4;
+        const bool fused = c->fused_waves > 0;
+        if (fused ? si1 > si0 : ti1 > ti0) {
+            // fused: one workgroup per point block (= SC item); else 4 chunks per workgroup
+            L.item_base = fused ? si0 : ti0;
+            L.n_items = fused ? si1 - si0 : ti1 - ti0;
+            L.n_blocks = fused ? L.n_items : (L.n_items + 3) / 4;
             rc = timed_launch(c, 0, st, [&] {
                 launch_linearize(c->lin_variant, c->img_mode, c->load3, c->xcd_remap, c->centre_first, L.n_blocks, st,
-                                 L, c->marg);
+                                 L, c->marg, c->fused_waves);
             });
             if (rc) return rc;
         }
@@ -3123,7 +3422,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
             Sp.part = 2;
             Sp.n_win = 0;
         }
-        if (accumulate && si1 > si0) {
+        if (accumulate && si1 > si0 && !fused) {
             Pp.item_base = si0;
             Pp.n_items = si1 - si0;
             rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
@@ -3569,6 +3868,11 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
     if (key == LDSO_BA_TUNE_ITEM_ORDER) {
         if (c->n_win) return fail(-1, "item order must be chosen before ldso_ba_load");
         c->item_order = value != 0;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_FUSED) {
+        if (c->n_win) return fail(-1, "fused pass must be chosen before ldso_ba_load");
+        c->fused_req = value != 0;
         return 0;
     }
     if (key == LDSO_BA_TUNE_STITCH_SPLIT) {

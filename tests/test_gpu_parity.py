@@ -313,6 +313,34 @@ def test_chunk_sizes_agree(built, chunk):
     c.close()
 
 
+@pytest.mark.parametrize("fused", [0, 1])
+@pytest.mark.parametrize("cfg", [dict(n_frames=2, n_points=90, seed=81), dict(n_frames=3, n_points=33, seed=82),
+                                 dict(n_frames=8, n_points=700, seed=83), dict(n_frames=16, n_points=300, seed=84)])
+def test_fused_and_chunk_major_passes_agree(built, cfg, fused):
+    """The point-major pass (k_linearize + the point's Schur term in one kernel, LDSO_BA_TUNE_FUSED
+    = 1) and the chunk-major pass (k_linearize then k_point_sc, the default) both match the oracle:
+    per-residual and per-point outputs bit for bit, the system within BLOCK_TOL. Window sizes
+    cover one wave with an idle upper half-slot (N = 2, 3), an odd target count (N = 8) and the
+    widest block (N = 16, 8 waves)."""
+    c = BAContext(0)
+    c.set_tuning(11, fused)  # LDSO_BA_TUNE_FUSED, before load
+    c.load([synth.make_window(**cfg)])
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    for _ in range(2):
+        c.linearize()
+        e_cpu, s_cpu = ow.iteration()
+        compare_pass(c, ow, 0, e_cpu, s_cpu)
+    c.close()
+
+
+def test_fused_knob_must_precede_load(built):
+    c = BAContext(0)
+    c.load([synth.make_window(n_frames=3, n_points=20, seed=2)])
+    with pytest.raises(RuntimeError, match="before"):
+        c.set_tuning(11, 0)
+    c.close()
+
+
 @pytest.mark.parametrize("groups", [1, 2, 3])
 def test_pipelined_groups_agree(built, groups):
     """Window groups pipelined over two streams give the same per-window results."""
