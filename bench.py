@@ -183,6 +183,62 @@ def tracker_leg(device, reps=50, n_hyp=32, cpu_seconds=2.0, with_cpu=True):
     return out
 
 
+def trace_leg(device, reps=50, cpu_seconds=2.0, with_cpu=True):
+    """traceNewCoarse (SURVEY.md §8f row 4; ldso_ct_trace): ImmaturePoint::traceOn of 7 hosts x
+    1500 immature points (setting_desiredImmatureDensity) against a 640x480 new frame, records
+    resident on the device.  Reported: host-clock ms per traceNewCoarse (launch + counters + one
+    round trip), the k_ct_trace kernel's mean HIP-event duration and point traces/s, and the
+    oracle's single-thread traceNewCoarse (the reference runs it on one thread under mapMutex,
+    FullSystem.cc:1157-1194) on the same records.  The 4.9 MB level-0 frame stays in L2 / MALL:
+    the kernel is latency bound (dependent bilinear taps), not an HBM stream."""
+    from ldso_amd import synth
+    from ldso_amd.tracker import CoarseTracker
+
+    w, h = 640, 480
+    host, new, uv, krki, kt, aff = synth.make_trace_scene(w, h)
+    n_hosts, per = uv.shape[0], uv.shape[1]
+    ct = CoarseTracker(w, h, device)
+    ct.set_new_frame(host, 1.0)
+    pts = np.concatenate([ct.make_immature(uv[i], 1.0, i) for i in range(n_hosts)])
+    ct.set_new_frame(new, 1.0)
+    for _ in range(3):
+        ct.immature_upload(pts)
+        ct.trace(krki, kt, aff)
+    ct.set_kernel_timing(True)
+    total = 0.0
+    counts = None
+    for _ in range(reps):
+        ct.immature_upload(pts)  # every rep traces the same freshly created records
+        t0 = time.perf_counter()
+        counts = ct.trace(krki, kt, aff)
+        total += time.perf_counter() - t0
+    kt_ = ct.kernel_times()
+    ct.close()
+    k_ms, k_n = kt_["k_ct_trace"]
+    k_us = 1e3 * k_ms / max(1, k_n)
+    n = pts.size
+    out = {"points": int(n), "hosts": int(n_hosts), "frame": f"{w}x{h}",
+           "status_counts": dict(zip(("good", "oob", "outlier", "skipped", "badcondition", "uninitialized"),
+                                     [int(x) for x in counts])),
+           "ms_per_trace_new_coarse": 1e3 * total / reps, "k_ct_trace_us": k_us,
+           "point_traces_per_s": n / (k_us / 1e6) if k_us > 0 else None}
+    if with_cpu:
+        import oracle
+
+        dN = oracle.make_images(new, w, h)[0][0]
+        m, el = 0, 0.0
+        while el < cpu_seconds:
+            ref = pts.copy()
+            t0 = time.perf_counter()
+            oracle.ip_trace(dN, w, h, krki, kt, aff, ref)
+            el += time.perf_counter() - t0
+            m += 1
+        out["cpu_trace_new_coarse"] = {"ms": 1e3 * el / m, "cores": 1, "kind": "port",
+                                       "sample": f"{m} oracle traceNewCoarse calls over the same {n} records"}
+        out["kernel_speedup_vs_cpu"] = out["cpu_trace_new_coarse"]["ms"] / (k_us / 1e3) if k_us > 0 else None
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -356,6 +412,7 @@ def main():
     tracker = None
     if rank == 0 and not args.no_tracker:
         tracker = tracker_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
+        tracker["trace_new_coarse"] = trace_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
 
     cpu = cpu16 = None
     if rank == 0 and world == 1 and not args.no_cpu:

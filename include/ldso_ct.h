@@ -29,6 +29,7 @@
 #define LDSO_CT_H_
 
 #include <stdint.h>
+#include <stddef.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -86,6 +87,59 @@ int ldso_ct_calc_res_gs(ldso_ct_ctx *ctx, int32_t lvl, const double ref_to_new[1
  * of 4 exactly as buf_warped_* / buf_warped_n: out [n][8] = {idepth, u, v, dx, dy, residual,
  * weight, refColor}; *n_out = buf_warped_n.  out may be NULL to query n. */
 int ldso_ct_get_warped(ldso_ct_ctx *ctx, int32_t *n_out, float *out, int32_t capacity);
+
+/* ---- immature points: point creation and epipolar tracing ----------
+ *
+ *   ImmaturePoint::ImmaturePoint        src/internal/ImmaturePoint.cc:14-39   -> ldso_ct_make_immature
+ *   ImmaturePoint::traceOn over all     src/internal/ImmaturePoint.cc:47-317  -> ldso_ct_trace
+ *     immature points of all frames,    (FullSystem::traceNewCoarse,
+ *     with the new frame                 src/frontend/FullSystem.cc:1157-1194)
+ *
+ * One record per ImmaturePoint (ImmaturePoint.h:101-121), 128 bytes.  `host` indexes the per-host
+ * tables of ldso_ct_trace (traceNewCoarse's per-frame KRKi, Kt, aff).  The traced frame is the
+ * context's new frame (ldso_ct_set_new_frame, level 0); ldso_ct_make_immature samples the same
+ * frame, as makeNewTraces creates the points of the keyframe that was just made
+ * (FullSystem.cc:1425-1475).  Where the reference would read outside the image (a rotated
+ * pattern tap past the border: undefined behaviour there), both this path and the oracle clamp
+ * the tap to the last interpolable texel. */
+typedef struct ldso_ct_immature {
+    float u, v;                  /* feature->uv */
+    float idepth_min, idepth_max;
+    float quality;
+    float energy_th;             /* energyTH (NaN: a pattern colour was not finite) */
+    float color[8];              /* pattern order: staticPattern[8], Setting.cc:275 */
+    float weights[8];
+    float grad_h[4];             /* gradH, row-major 2x2 */
+    int32_t host;                /* index into ldso_ct_trace's host tables */
+    int32_t last_status;         /* ImmaturePointStatus: GOOD 0, OOB 1, OUTLIER 2, SKIPPED 3,
+                                    BADCONDITION 4, UNINITIALIZED 5 */
+    float last_uv[2];            /* lastTraceUV */
+    float last_interval;         /* lastTracePixelInterval */
+    float type;                  /* my_type */
+} ldso_ct_immature;
+
+#define LDSO_CT_IPS_GOOD 0
+#define LDSO_CT_IPS_OOB 1
+#define LDSO_CT_IPS_OUTLIER 2
+#define LDSO_CT_IPS_SKIPPED 3
+#define LDSO_CT_IPS_BADCONDITION 4
+#define LDSO_CT_IPS_UNINITIALIZED 5
+
+/* new ImmaturePoint(newFrame, feat, type, HCalib) for n features at uv [n][2] on the context's
+ * new frame: colour, weights, gradH and energyTH; idepth_min 0, idepth_max NaN, quality 10000,
+ * status UNINITIALIZED, host = `host` for all n.  out: host memory [n]. */
+int ldso_ct_make_immature(ldso_ct_ctx *ctx, int32_t n, const float *uv, float type, int32_t host,
+                          ldso_ct_immature *out);
+/* make the n records resident on the device (replaces the previous set) / read them back */
+int ldso_ct_immature_upload(ldso_ct_ctx *ctx, int32_t n, const ldso_ct_immature *pts);
+int ldso_ct_immature_download(ldso_ct_ctx *ctx, int32_t n, ldso_ct_immature *pts);
+/* traceNewCoarse: traceOn of every resident record with the context's new frame.
+ * krki [n_hosts][9] row-major, kt [n_hosts][3], aff [n_hosts][2] (AffLight::fromToVecExposure
+ * host -> new frame), as traceNewCoarse builds them per host frame.
+ * counts_out (may be NULL): [6] records per lastTraceStatus after the call (trace_good,
+ * trace_oob, trace_out, trace_skip, trace_badcondition, trace_uninitialized). */
+int ldso_ct_trace(ldso_ct_ctx *ctx, int32_t n_hosts, const float *krki, const float *kt, const float *aff,
+                  int32_t *counts_out);
 
 /* kernel timing of the tracker's launches (same slots mechanism as ldso_ba) */
 int ldso_ct_set_kernel_timing(ldso_ct_ctx *ctx, int32_t enable);

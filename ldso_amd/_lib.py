@@ -127,6 +127,15 @@ ABI = [
 
 f32pp = C.POINTER(f32p)
 
+# ldso_ct_immature (include/ldso_ct.h): one ImmaturePoint, 128 bytes
+IMMATURE_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("idepth_min", "<f4"), ("idepth_max", "<f4"),
+                           ("quality", "<f4"), ("energy_th", "<f4"), ("color", "<f4", (8,)),
+                           ("weights", "<f4", (8,)), ("grad_h", "<f4", (4,)), ("host", "<i4"),
+                           ("last_status", "<i4"), ("last_uv", "<f4", (2,)), ("last_interval", "<f4"),
+                           ("type", "<f4")])
+assert IMMATURE_DTYPE.itemsize == 128
+IPS_NAMES = ("GOOD", "OOB", "OUTLIER", "SKIPPED", "BADCONDITION", "UNINITIALIZED")  # ImmaturePoint.h:31-38
+
 # (name, restype, argtypes) of every entry point declared in include/ldso_ct.h (coarse tracker)
 CT_ABI = [
     ("ldso_ct_create", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p), i32p]),
@@ -142,6 +151,10 @@ CT_ABI = [
     ("ldso_ct_calc_res_gs", C.c_int,
      [C.c_void_p, C.c_int32, f64p, C.c_double, C.c_double, C.c_float, f64p, f64p, f64p]),
     ("ldso_ct_get_warped", C.c_int, [C.c_void_p, i32p, f32p, C.c_int32]),
+    ("ldso_ct_make_immature", C.c_int, [C.c_void_p, C.c_int32, f32p, C.c_float, C.c_int32, C.c_void_p]),
+    ("ldso_ct_immature_upload", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
+    ("ldso_ct_immature_download", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
+    ("ldso_ct_trace", C.c_int, [C.c_void_p, C.c_int32, f32p, f32p, f32p, i32p]),
     ("ldso_ct_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("ldso_ct_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),
     ("ldso_ct_kernel_name", C.c_char_p, [C.c_int32]),

@@ -18,6 +18,17 @@
 //   k_ct_calc_gs    thread per point with state "warped": the 8 Jacobian entries + residual of
 //                   calcGSSSE and the 45 weighted outer-product terms of Accumulator9, reduced over
 //                   the wavefront and the block into 45 partials per block.
+// Immature points (ImmaturePoint.cc:14-39, 47-317; FullSystem::traceNewCoarse):
+//   k_ct_make_immature  thread per new point: 8 bilinear pattern samples of the new frame.
+//   k_ct_trace          wavefront per immature point: the scalar preamble (epipolar segment,
+//                       bounds, error bound) runs uniformly on all lanes; lane i evaluates
+//                       discrete search step i (and i + 64), its position reproduced by the
+//                       reference's sequential ptx += dx; argmin (first index of the minimum)
+//                       and the second best outside +-2 steps are wave reductions; each GN
+//                       iteration samples the 8 pattern taps on lanes 0-7 and every lane sums
+//                       them in pattern order.  Statuses and intervals are bit-identical to the
+//                       CPU restatement.
+//   k_ct_ip_count       one block: the traceNewCoarse status counters.
 // The per-point arithmetic is compiled with contraction off in the reference's statement order
 // (states, warped records bit-identical to the CPU restatement); E and the H/b sums are
 // reassociated (the reference sums them sequentially in float) and tolerance-checked.
@@ -44,8 +55,9 @@ constexpr int kCtThreads = 256;
 constexpr int kResParts = 8;   // E, nE, nSat, shiftT, shiftRT, shiftNum, nWarped, pad
 constexpr int kGsParts = 45;   // upper 9x9 of Accumulator9
 constexpr int kMaxHyp = 256;
-constexpr int kNumCtKernels = 4;
-const char *kCtKernelNames[kNumCtKernels] = {"k_ct_pyr_down", "k_ct_pyr_grad", "k_ct_calc_res", "k_ct_calc_gs"};
+constexpr int kNumCtKernels = 7;
+const char *kCtKernelNames[kNumCtKernels] = {"k_ct_pyr_down",      "k_ct_pyr_grad", "k_ct_calc_res", "k_ct_calc_gs",
+                                             "k_ct_make_immature", "k_ct_trace",    "k_ct_ip_count"};
 constexpr float kHuberTH = ldso_ba::kHuberTH;  // setting_huberTH, Setting.cc:76
 constexpr float kScaleXiRot = 1.0f, kScaleXiTrans = 0.5f, kScaleA = 10.0f, kScaleB = 1000.0f;  // Settings.h:29-35
 
@@ -275,6 +287,366 @@ __global__ __launch_bounds__(kCtThreads) void k_ct_calc_gs(CtGsParams P) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// immature points: ImmaturePoint::ImmaturePoint and ::traceOn (ImmaturePoint.cc:14-39, 47-317)
+// ---------------------------------------------------------------------------------------------
+constexpr int kPatX[8] = {0, -1, 1, -2, 0, 2, -1, 0}, kPatY[8] = {-2, -1, -1, 0, 0, 0, 1, 2};  // Setting.cc:275
+constexpr float kOutlierTHSumComponent = ldso_ba::kOutlierTHSumComponent;  // Setting.cc:41
+constexpr float kOutlierTH = 12 * 12;                    // Setting.cc:39
+constexpr float kOverallEnergyTHWeight = ldso_ba::kOverallEnergyTHWeight;
+constexpr float kMaxPixSearch = 0.027f;                  // Setting.cc:28
+constexpr int kMinTraceTestRadius = 2;                   // Setting.cc:52
+constexpr float kTraceStepsize = 1.0f;                   // Setting.cc:89
+constexpr int kTraceGNIterations = 3;                    // Setting.cc:90
+constexpr float kTraceGNThreshold = 0.1f;                // Setting.cc:91
+constexpr float kTraceExtraSlackOnTH = 1.2f;             // Setting.cc:92
+constexpr float kTraceSlackInterval = 1.5f;              // Setting.cc:93
+constexpr float kTraceMinImprovementFactor = 2;          // Setting.cc:94
+constexpr int kHostStride = 16;                          // KRKi[9], Kt[3], aff[2], pad[2]
+
+// top-left texel of a bilinear tap, clamped into [0, w-2] x [0, h-2] (the reference would read
+// past the image there; the oracle clamps the same way)
+__device__ __forceinline__ int ip_base(float x, float y, int w, int h, float &fx, float &fy) {
+    const int ix = (int)x, iy = (int)y;
+    fx = x - ix;
+    fy = y - iy;
+    return min(max(ix, 0), w - 2) + min(max(iy, 0), h - 2) * w;
+}
+
+struct IpRec {  // ldso_ct_immature viewed as 32 words
+    float u, v, idepth_min, idepth_max, quality, energy_th, color[8], weights[8], grad_h[4];
+    int host, last_status;
+    float last_uv[2], last_interval, type;
+};
+static_assert(sizeof(IpRec) == sizeof(ldso_ct_immature), "record layout");
+
+// new ImmaturePoint(newFrame, feat, type, HCalib): getInterpolatedElement33BiLin (GlobalFuncs.h:186-207)
+__global__ __launch_bounds__(kCtThreads) void k_ct_make_immature(const float4 *__restrict__ dI, int w, int h, int n,
+                                                                 const float2 *__restrict__ uv, float type, int host,
+                                                                 IpRec *__restrict__ out) {
+    const int k = blockIdx.x * kCtThreads + threadIdx.x;
+    if (k >= n) return;
+    IpRec p;
+    p.u = uv[k].x;
+    p.v = uv[k].y;
+    p.idepth_min = 0;
+    p.idepth_max = __builtin_nanf("");
+    p.quality = 10000;
+    p.type = type;
+    p.host = host;
+    p.last_status = LDSO_CT_IPS_UNINITIALIZED;
+    p.last_uv[0] = p.last_uv[1] = 0;
+    p.last_interval = 0;
+    float G0 = 0, G1 = 0, G2 = 0, G3 = 0;
+    bool ok = true;
+#pragma unroll
+    for (int idx = 0; idx < 8; idx++) p.color[idx] = p.weights[idx] = 0;
+#pragma unroll
+    for (int idx = 0; idx < 8; idx++) {
+        if (!ok) break;
+        float dx, dy;
+        const int b = ip_base(p.u + kPatX[idx], p.v + kPatY[idx], w, h, dx, dy);
+        const float tl = dI[b].x, tr = dI[b + 1].x, bl = dI[b + w].x, br = dI[b + w + 1].x;
+        const float topInt = dx * tr + (1 - dx) * tl;
+        const float botInt = dx * br + (1 - dx) * bl;
+        const float leftInt = dy * bl + (1 - dy) * tl;
+        const float rightInt = dy * br + (1 - dy) * tr;
+        const float c0 = dx * rightInt + (1 - dx) * leftInt, g0 = rightInt - leftInt, g1 = botInt - topInt;
+        p.color[idx] = c0;
+        if (!isfinite(c0)) {
+            ok = false;
+            break;
+        }
+        G0 += g0 * g0;
+        G1 += g0 * g1;
+        G2 += g1 * g0;
+        G3 += g1 * g1;
+        p.weights[idx] = sqrtf(kOutlierTHSumComponent / (kOutlierTHSumComponent + (g0 * g0 + g1 * g1)));
+    }
+    p.grad_h[0] = G0;
+    p.grad_h[1] = G1;
+    p.grad_h[2] = G2;
+    p.grad_h[3] = G3;
+    float e = 8 * kOutlierTH;
+    e *= kOverallEnergyTHWeight * kOverallEnergyTHWeight;
+    p.energy_th = ok ? e : __builtin_nanf("");
+    out[k] = p;
+}
+
+struct TraceParams {
+    const float4 *__restrict__ dI;  // level 0 [I, dx, dy, |g|^2]
+    const float *__restrict__ hosts;  // [n_hosts][kHostStride]
+    IpRec *pts;
+    int n, w, h;
+};
+
+__device__ __forceinline__ void ip_finish(IpRec *q, int status, float u, float v, float interval) {
+    if (threadIdx.x % kWave == 0) {
+        q->last_status = status;
+        q->last_uv[0] = u;
+        q->last_uv[1] = v;
+        q->last_interval = interval;
+    }
+}
+
+// getInterpolatedElement31 (GlobalFuncs.h:146-159)
+__device__ __forceinline__ float interp31(const float4 *__restrict__ dI, float x, float y, int w, int h) {
+    float dx, dy;
+    const int b = ip_base(x, y, w, h, dx, dy);
+    const float dxdy = dx * dy;
+    return dxdy * dI[b + 1 + w].x + (dy - dxdy) * dI[b + w].x + (dx - dxdy) * dI[b + 1].x +
+           (1 - dx - dy + dxdy) * dI[b].x;
+}
+
+// one wavefront per immature point; every branch before the search is wave-uniform
+__global__ __launch_bounds__(kCtThreads) void k_ct_trace(TraceParams P) {
+    const int lane = threadIdx.x % kWave;
+    const int k = __builtin_amdgcn_readfirstlane(blockIdx.x * (kCtThreads / kWave) + threadIdx.x / kWave);
+    if (k >= P.n) return;
+    IpRec *q = P.pts + k;
+    const int last = q->last_status;
+    if (last == LDSO_CT_IPS_OOB) return;
+    const int w = P.w, h = P.h;
+    const float *H = P.hosts + (size_t)q->host * kHostStride;
+    const float KR[9] = {H[0], H[1], H[2], H[3], H[4], H[5], H[6], H[7], H[8]};
+    const float Kt[3] = {H[9], H[10], H[11]}, aff0 = H[12], aff1 = H[13];
+    const float u = q->u, v = q->v, idepth_min = q->idepth_min, idepth_max = q->idepth_max;
+    const float maxPixSearch = (w + h) * kMaxPixSearch;
+    float pr[3], ptpMin[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) pr[i] = KR[3 * i] * u + KR[3 * i + 1] * v + KR[3 * i + 2] * 1.0f;
+#pragma unroll
+    for (int i = 0; i < 3; i++) ptpMin[i] = pr[i] + Kt[i] * idepth_min;
+    const float uMin = ptpMin[0] / ptpMin[2], vMin = ptpMin[1] / ptpMin[2];
+    if (!(uMin > 4 && vMin > 4 && uMin < w - 5 && vMin < h - 5)) return ip_finish(q, LDSO_CT_IPS_OOB, -1, -1, 0);
+    const bool finite_max = isfinite(idepth_max);
+    float dist, uMax, vMax;
+    if (finite_max) {
+        float ptpMax[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) ptpMax[i] = pr[i] + Kt[i] * idepth_max;
+        uMax = ptpMax[0] / ptpMax[2];
+        vMax = ptpMax[1] / ptpMax[2];
+        if (!(uMax > 4 && vMax > 4 && uMax < w - 5 && vMax < h - 5)) return ip_finish(q, LDSO_CT_IPS_OOB, -1, -1, 0);
+        dist = (uMin - uMax) * (uMin - uMax) + (vMin - vMax) * (vMin - vMax);
+        dist = sqrtf(dist);
+        if (dist < kTraceSlackInterval)
+            return ip_finish(q, LDSO_CT_IPS_SKIPPED, (uMax + uMin) * 0.5f, (vMax + vMin) * 0.5f, dist);
+    } else {
+        dist = maxPixSearch;
+        float ptpMax[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) ptpMax[i] = pr[i] + Kt[i] * 0.01f;
+        uMax = ptpMax[0] / ptpMax[2];
+        vMax = ptpMax[1] / ptpMax[2];
+        const float dx = uMax - uMin, dy = vMax - vMin;
+        const float d = 1.0f / sqrtf(dx * dx + dy * dy);
+        uMax = uMin + dist * dx * d;
+        vMax = vMin + dist * dy * d;
+        if (!(uMax > 4 && vMax > 4 && uMax < w - 5 && vMax < h - 5)) return ip_finish(q, LDSO_CT_IPS_OOB, -1, -1, 0);
+    }
+    if (!(idepth_min < 0 || (ptpMin[2] > 0.75f && ptpMin[2] < 1.5f))) return ip_finish(q, LDSO_CT_IPS_OOB, -1, -1, 0);
+
+    float dx = kTraceStepsize * (uMax - uMin);
+    float dy = kTraceStepsize * (vMax - vMin);
+    const float G0 = q->grad_h[0], G1 = q->grad_h[1], G2 = q->grad_h[2], G3 = q->grad_h[3];
+    const float a = (dx * G0 + dy * G2) * dx + (dx * G1 + dy * G3) * dy;
+    const float b = (dy * G0 + -dx * G2) * dy + (dy * G1 + -dx * G3) * -dx;
+    float errorInPixel = 0.2f + 0.2f * (a + b) / a;
+    if (errorInPixel * kTraceMinImprovementFactor > dist && finite_max)
+        return ip_finish(q, LDSO_CT_IPS_BADCONDITION, (uMax + uMin) * 0.5f, (vMax + vMin) * 0.5f, dist);
+    if (errorInPixel > 10) errorInPixel = 10;
+    dx /= dist;
+    dy /= dist;
+    if (dist > maxPixSearch) dist = maxPixSearch;  // (uMax, vMax are not used past this point)
+    int numSteps = 1.9999f + dist / kTraceStepsize;
+    const float randShift = uMin * 1000 - floorf(uMin * 1000);
+    const float ptx0 = uMin - randShift * dx, pty0 = vMin - randShift * dy;
+    float rpx[8], rpy[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        rpx[i] = KR[0] * (float)kPatX[i] + KR[1] * (float)kPatY[i];
+        rpy[i] = KR[3] * (float)kPatX[i] + KR[4] * (float)kPatY[i];
+    }
+    if (!isfinite(dx) || !isfinite(dy)) return ip_finish(q, LDSO_CT_IPS_OOB, -1, -1, 0);
+    if (numSteps >= 100) numSteps = 99;
+    float col[8], wts[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        col[i] = q->color[i];
+        wts[i] = q->weights[i];
+    }
+
+    // ---- discrete search: lane i takes step i and step i + 64 ----
+    float x0 = 0, y0 = 0, x1 = 0, y1 = 0;  // ptx, pty of the lane's steps (sequential sums)
+    {
+        float px = ptx0, py = pty0;
+        for (int i = 0; i < numSteps; i++) {
+            if (i == lane) {
+                x0 = px;
+                y0 = py;
+            }
+            if (i == lane + kWave) {
+                x1 = px;
+                y1 = py;
+            }
+            px += dx;
+            py += dy;
+        }
+    }
+    auto step_energy = [&](float ptx, float pty) {
+        float energy = 0;
+#pragma unroll
+        for (int idx = 0; idx < 8; idx++) {
+            const float hitColor = interp31(P.dI, (float)(ptx + rpx[idx]), (float)(pty + rpy[idx]), w, h);
+            if (!isfinite(hitColor)) {
+                energy += 1e5f;
+                continue;
+            }
+            const float residual = hitColor - (float)(aff0 * col[idx] + aff1);
+            const float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
+            energy += hw * residual * residual * (2 - hw);
+        }
+        return energy;
+    };
+    const bool has0 = lane < numSteps, has1 = lane + kWave < numSteps;
+    const float e0 = has0 ? step_energy(x0, y0) : 0.f;
+    const float e1 = has1 ? step_energy(x1, y1) : 0.f;
+    // first index of the minimum among energies < 1e10 (energies are >= 0 or NaN)
+    auto key = [](bool has, float e, int i) -> unsigned long long {
+        return (has && e < 1e10f) ? ((unsigned long long)__float_as_uint(e) << 32) | (unsigned)i : ~0ull;
+    };
+    unsigned long long kmin = min(key(has0, e0, lane), key(has1, e1, lane + kWave));
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) kmin = min(kmin, (unsigned long long)__shfl_xor(kmin, m, kWave));
+    int bestIdx = -1;
+    float bestEnergy = 1e10f, bestU = 0, bestV = 0;
+    if (kmin != ~0ull) {
+        bestIdx = (int)(unsigned)kmin;
+        bestEnergy = __uint_as_float((unsigned)(kmin >> 32));
+        const int src = bestIdx & (kWave - 1);
+        const float bx0 = __shfl(x0, src, kWave), by0 = __shfl(y0, src, kWave);
+        const float bx1 = __shfl(x1, src, kWave), by1 = __shfl(y1, src, kWave);
+        bestU = bestIdx < kWave ? bx0 : bx1;
+        bestV = bestIdx < kWave ? by0 : by1;
+    }
+    auto outside = [&](int i) { return i < bestIdx - kMinTraceTestRadius || i > bestIdx + kMinTraceTestRadius; };
+    float sb = 1e10f;
+    if (has0 && outside(lane) && e0 < sb) sb = e0;
+    if (has1 && outside(lane + kWave) && e1 < sb) sb = e1;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) sb = fminf(sb, __shfl_xor(sb, m, kWave));
+    const float newQuality = sb / bestEnergy;
+    float quality = q->quality;
+    if (newQuality < quality || numSteps > 10) quality = newQuality;
+
+    // ---- GN refinement: taps on lanes 0-7, sums in pattern order on every lane ----
+    float uBak = bestU, vBak = bestV, gnstepsize = 1, stepBack = 0;
+    if (kTraceGNIterations > 0) bestEnergy = 1e5f;
+    for (int it = 0; it < kTraceGNIterations; it++) {
+        const int idx = lane & 7;
+        float rpxi = rpx[0], rpyi = rpy[0], ci = col[0], wi = wts[0];
+#pragma unroll
+        for (int i = 1; i < 8; i++)
+            if (idx == i) {
+                rpxi = rpx[i];
+                rpyi = rpy[i];
+                ci = col[i];
+                wi = wts[i];
+            }
+        float fx, fy;
+        const int bb = ip_base((float)(bestU + rpxi), (float)(bestV + rpyi), w, h, fx, fy);
+        const float4 t00 = P.dI[bb], t10 = P.dI[bb + 1], t01 = P.dI[bb + w], t11 = P.dI[bb + w + 1];
+        const float dxdy = fx * fy;
+        const float w11 = dxdy, w01 = fy - dxdy, w10 = fx - dxdy, w00 = 1 - fx - fy + dxdy;
+        const float hc0 = w11 * t11.x + w01 * t01.x + w10 * t10.x + w00 * t00.x;
+        const float hc1 = w11 * t11.y + w01 * t01.y + w10 * t10.y + w00 * t00.y;
+        const float hc2 = w11 * t11.z + w01 * t01.z + w10 * t10.z + w00 * t00.z;
+        const bool fin = isfinite(hc0);
+        const float residual = hc0 - (aff0 * ci + aff1);
+        const float dResdDist = dx * hc1 + dy * hc2;
+        const float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
+        const float tH = hw * dResdDist * dResdDist;
+        const float tb = hw * residual * dResdDist;
+        const float tE = wi * wi * hw * residual * residual * (2 - hw);
+        float Hs = 1, bs = 0, energy = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const bool f = __shfl(fin ? 1 : 0, i, kWave) != 0;
+            const float h_ = __shfl(tH, i, kWave), b_ = __shfl(tb, i, kWave), e_ = __shfl(tE, i, kWave);
+            if (!f) {
+                energy += 1e5f;
+                continue;
+            }
+            Hs += h_;
+            bs += b_;
+            energy += e_;
+        }
+        if (energy > bestEnergy) {
+            stepBack *= 0.5f;
+            bestU = uBak + stepBack * dx;
+            bestV = vBak + stepBack * dy;
+        } else {
+            float step = -gnstepsize * bs / Hs;
+            if (step < -0.5f) step = -0.5f;
+            else if (step > 0.5f) step = 0.5f;
+            if (!isfinite(step)) step = 0;
+            uBak = bestU;
+            vBak = bestV;
+            stepBack = step;
+            bestU += step * dx;
+            bestV += step * dy;
+            bestEnergy = energy;
+        }
+        if (fabsf(stepBack) < kTraceGNThreshold) break;
+    }
+    if (lane == 0) q->quality = quality;
+
+    if (!(bestEnergy < q->energy_th * kTraceExtraSlackOnTH))
+        return ip_finish(q, last == LDSO_CT_IPS_OUTLIER ? LDSO_CT_IPS_OOB : LDSO_CT_IPS_OUTLIER, -1, -1, 0);
+    float imin, imax;
+    if (dx * dx > dy * dy) {
+        imin = (pr[2] * (bestU - errorInPixel * dx) - pr[0]) / (Kt[0] - Kt[2] * (bestU - errorInPixel * dx));
+        imax = (pr[2] * (bestU + errorInPixel * dx) - pr[0]) / (Kt[0] - Kt[2] * (bestU + errorInPixel * dx));
+    } else {
+        imin = (pr[2] * (bestV - errorInPixel * dy) - pr[1]) / (Kt[1] - Kt[2] * (bestV - errorInPixel * dy));
+        imax = (pr[2] * (bestV + errorInPixel * dy) - pr[1]) / (Kt[1] - Kt[2] * (bestV + errorInPixel * dy));
+    }
+    if (imin > imax) {
+        const float t = imin;
+        imin = imax;
+        imax = t;
+    }
+    if (lane == 0) {
+        q->idepth_min = imin;
+        q->idepth_max = imax;
+    }
+    if (!isfinite(imin) || !isfinite(imax) || (imax < 0)) return ip_finish(q, LDSO_CT_IPS_OUTLIER, -1, -1, 0);
+    ip_finish(q, LDSO_CT_IPS_GOOD, bestU, bestV, 2 * errorInPixel);
+}
+
+// traceNewCoarse's counters (FullSystem.cc:1184-1190): one block
+__global__ __launch_bounds__(1024) void k_ct_ip_count(const IpRec *__restrict__ pts, int n, int *__restrict__ counts) {
+    __shared__ int c[8];
+    if (threadIdx.x < 8) c[threadIdx.x] = 0;
+    __syncthreads();
+    int loc[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int s = pts[k].last_status;
+#pragma unroll
+        for (int j = 0; j < 6; j++) loc[j] += s == j;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        int x = loc[j];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, kWave);
+        if (threadIdx.x % kWave == 0 && x) atomicAdd(&c[j], x);
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) counts[threadIdx.x] = c[threadIdx.x];
+}
+
+// ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
 void affine_from_to(float expF, float expT, float aF, float bF, float aT, float bT, float &a, float &b) {
@@ -308,6 +680,15 @@ struct ldso_ct_ctx {
     CtPose *h_poses = nullptr, *d_poses = nullptr;
     double *h_parts = nullptr, *d_parts = nullptr;
     size_t parts_cap = 0;
+    // immature points (resident records, per-host tables, make staging, counters)
+    IpRec *d_ip = nullptr;
+    int ip_n = 0, ip_cap = 0, ip_max_host = -1;
+    float *d_hosts = nullptr, *h_hosts = nullptr;
+    int hosts_cap = 0;
+    float2 *d_uv = nullptr;
+    IpRec *d_mk = nullptr;
+    int mk_cap = 0;
+    int *d_counts = nullptr, *h_counts = nullptr;
     // kernel timing
     bool timing = false;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -520,6 +901,8 @@ int ldso_ct_create(int32_t device, int32_t width, int32_t height, ldso_ct_ctx **
     if (e == hipSuccess) e = hipMalloc(&c->d_B, 256 * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&c->d_poses, kMaxHyp * sizeof(CtPose));
     if (e == hipSuccess) e = hipHostMalloc(&c->h_poses, kMaxHyp * sizeof(CtPose), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&c->d_counts, 8 * sizeof(int));
+    if (e == hipSuccess) e = hipHostMalloc(&c->h_counts, 8 * sizeof(int), hipHostMallocDefault);
     if (e != hipSuccess) {
         ldso_ct_destroy(c);
         return set_error(-3, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -537,10 +920,13 @@ void ldso_ct_destroy(ldso_ct_ctx *c) {
         (void)hipEventDestroy(p.second.first);
         (void)hipEventDestroy(p.second.second);
     }
-    void *dev[] = {c->d_color, c->d_inten, c->d_B, c->d_dIp, c->d_pc, c->d_state, c->d_warp, c->d_poses, c->d_parts};
+    void *dev[] = {c->d_color, c->d_inten, c->d_B,  c->d_dIp, c->d_pc,  c->d_state,  c->d_warp,
+                   c->d_poses, c->d_parts, c->d_ip, c->d_hosts, c->d_uv, c->d_mk, c->d_counts};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_poses) (void)hipHostFree(c->h_poses);
+    if (c->h_hosts) (void)hipHostFree(c->h_hosts);
+    if (c->h_counts) (void)hipHostFree(c->h_counts);
     if (c->h_parts) (void)hipHostFree(c->h_parts);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -769,6 +1155,116 @@ int ldso_ct_get_warped(ldso_ct_ctx *c, int32_t *n_out, float *out, int32_t capac
         k++;
     }
     for (; k < nw; k++) std::memset(out + 8 * (size_t)k, 0, 8 * sizeof(float));
+    return 0;
+}
+
+int ldso_ct_make_immature(ldso_ct_ctx *c, int32_t n, const float *uv, float type, int32_t host,
+                          ldso_ct_immature *out) {
+    if (!c) return set_error(-1, "null context");
+    if (n < 0 || (n > 0 && (!uv || !out))) return set_error(-1, "bad point arguments");
+    if (!c->have_frame) return set_error(-1, "ldso_ct_set_new_frame has not been called");
+    if (n == 0) return 0;
+    CT_TRY(hipSetDevice(c->device));
+    if (n > c->mk_cap) {
+        if (c->d_uv) CT_TRY(hipFree(c->d_uv));
+        if (c->d_mk) CT_TRY(hipFree(c->d_mk));
+        c->d_uv = nullptr;
+        c->d_mk = nullptr;
+        c->mk_cap = 0;
+        CT_TRY(hipMalloc(&c->d_uv, (size_t)n * sizeof(float2)));
+        CT_TRY(hipMalloc(&c->d_mk, (size_t)n * sizeof(IpRec)));
+        c->mk_cap = n;
+    }
+    CT_TRY(hipMemcpyAsync(c->d_uv, uv, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, c->stream));
+    const int w = c->pyr.w, h = c->pyr.h;
+    int rc = ct_launch(c, 4, [&] {
+        k_ct_make_immature<<<(n + kCtThreads - 1) / kCtThreads, kCtThreads, 0, c->stream>>>(
+            c->d_dIp, w, h, n, c->d_uv, type, host, c->d_mk);
+    });
+    if (rc) return rc;
+    CT_TRY(hipMemcpyAsync(out, c->d_mk, (size_t)n * sizeof(IpRec), hipMemcpyDeviceToHost, c->stream));
+    CT_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int ldso_ct_immature_upload(ldso_ct_ctx *c, int32_t n, const ldso_ct_immature *pts) {
+    if (!c) return set_error(-1, "null context");
+    if (n < 0 || (n > 0 && !pts)) return set_error(-1, "bad point arguments");
+    int max_host = -1;
+    for (int k = 0; k < n; k++) {
+        if (pts[k].host < 0) return set_error(-1, "immature point with a negative host index");
+        if (pts[k].last_status < 0 || pts[k].last_status > LDSO_CT_IPS_UNINITIALIZED)
+            return set_error(-1, "immature point with an invalid status");
+        max_host = std::max(max_host, (int)pts[k].host);
+    }
+    CT_TRY(hipSetDevice(c->device));
+    if (n > c->ip_cap) {
+        if (c->d_ip) CT_TRY(hipFree(c->d_ip));
+        c->d_ip = nullptr;
+        c->ip_cap = 0;
+        CT_TRY(hipMalloc(&c->d_ip, (size_t)n * sizeof(IpRec)));
+        c->ip_cap = n;
+    }
+    if (n) CT_TRY(hipMemcpyAsync(c->d_ip, pts, (size_t)n * sizeof(IpRec), hipMemcpyHostToDevice, c->stream));
+    CT_TRY(hipStreamSynchronize(c->stream));
+    c->ip_n = n;
+    c->ip_max_host = max_host;
+    return 0;
+}
+
+int ldso_ct_immature_download(ldso_ct_ctx *c, int32_t n, ldso_ct_immature *pts) {
+    if (!c) return set_error(-1, "null context");
+    if (n != c->ip_n) return set_error(-1, "count differs from the resident immature points");
+    if (n == 0) return 0;
+    if (!pts) return set_error(-1, "null output");
+    CT_TRY(hipSetDevice(c->device));
+    CT_TRY(hipMemcpyAsync(pts, c->d_ip, (size_t)n * sizeof(IpRec), hipMemcpyDeviceToHost, c->stream));
+    CT_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int ldso_ct_trace(ldso_ct_ctx *c, int32_t n_hosts, const float *krki, const float *kt, const float *aff,
+                  int32_t *counts_out) {
+    if (!c) return set_error(-1, "null context");
+    if (!c->have_frame) return set_error(-1, "ldso_ct_set_new_frame has not been called");
+    if (n_hosts <= c->ip_max_host) return set_error(-1, "an immature point's host index is >= n_hosts");
+    if (n_hosts > 0 && (!krki || !kt || !aff)) return set_error(-1, "null host tables");
+    CT_TRY(hipSetDevice(c->device));
+    if (n_hosts > c->hosts_cap) {
+        if (c->d_hosts) CT_TRY(hipFree(c->d_hosts));
+        if (c->h_hosts) CT_TRY(hipHostFree(c->h_hosts));
+        c->d_hosts = c->h_hosts = nullptr;
+        c->hosts_cap = 0;
+        CT_TRY(hipMalloc(&c->d_hosts, (size_t)n_hosts * kHostStride * sizeof(float)));
+        CT_TRY(hipHostMalloc(&c->h_hosts, (size_t)n_hosts * kHostStride * sizeof(float), hipHostMallocDefault));
+        c->hosts_cap = n_hosts;
+    }
+    CT_TRY(hipStreamSynchronize(c->stream));  // the staging buffer may still feed a previous copy
+    for (int i = 0; i < n_hosts; i++) {
+        float *o = c->h_hosts + (size_t)i * kHostStride;
+        std::memcpy(o, krki + 9 * (size_t)i, 9 * sizeof(float));
+        std::memcpy(o + 9, kt + 3 * (size_t)i, 3 * sizeof(float));
+        o[12] = aff[2 * (size_t)i];
+        o[13] = aff[2 * (size_t)i + 1];
+        o[14] = o[15] = 0;
+    }
+    if (n_hosts)
+        CT_TRY(hipMemcpyAsync(c->d_hosts, c->h_hosts, (size_t)n_hosts * kHostStride * sizeof(float),
+                              hipMemcpyHostToDevice, c->stream));
+    const int n = c->ip_n;
+    if (n > 0) {
+        TraceParams P{c->d_dIp, c->d_hosts, c->d_ip, n, c->pyr.w, c->pyr.h};
+        const int per = kCtThreads / kWave;
+        int rc = ct_launch(c, 5, [&] { k_ct_trace<<<(n + per - 1) / per, kCtThreads, 0, c->stream>>>(P); });
+        if (rc) return rc;
+    }
+    if (counts_out) {
+        int rc = ct_launch(c, 6, [&] { k_ct_ip_count<<<1, 1024, 0, c->stream>>>(c->d_ip, n, c->d_counts); });
+        if (rc) return rc;
+        CT_TRY(hipMemcpyAsync(c->h_counts, c->d_counts, 6 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    }
+    CT_TRY(hipStreamSynchronize(c->stream));
+    if (counts_out) std::memcpy(counts_out, c->h_counts, 6 * sizeof(int));
     return 0;
 }
 

@@ -112,3 +112,32 @@ def se3_matrix(omega, upsilon):
     T[:, :3] = R
     T[:, 3] = V @ np.asarray(upsilon, np.float64)
     return T
+
+
+def make_trace_scene(width=640, height=480, n_hosts=7, points_per_host=1500, shift=8.0, seed=0):
+    """traceNewCoarse workload: a blob-textured fronto-parallel plane at
+    inverse depth 0.5 seen by n_hosts host keyframes translated along x, and the new frame.
+    Host i sees the plane shifted by shift * (1 + i / n_hosts) pixels in the new frame.
+    Returns (host_image, new_image, uv [n_hosts][points_per_host][2], krki [n][9], kt [n][3],
+    aff [n][2]).  points_per_host defaults to setting_desiredImmatureDensity (Setting.cc)."""
+    rng = np.random.default_rng(0x7ACE + int(seed))
+    yy, xx = np.mgrid[0:height, 0:width].astype(np.float64)
+    blobs = [(rng.uniform(0, width), rng.uniform(0, height), rng.uniform(2.0, 8.0),
+              rng.uniform(20, 80) * rng.choice([-1, 1])) for _ in range(int(width * height / 2000))]
+
+    def render(dx, a=1.0, b=0.0):
+        img = np.full((height, width), 90.0)
+        for cx, cy, s, A in blobs:
+            img += A * np.exp(-((xx - dx - cx) ** 2 + (yy - cy) ** 2) / (2 * s * s))
+        return (a * img + b).astype(np.float32)
+
+    host, new = render(0.0), render(shift, 1.1, -5.0)
+    fx, rho = 0.6 * width, 0.5
+    krki = np.tile(np.eye(3, dtype=np.float32).reshape(1, 9), (n_hosts, 1))
+    kt = np.zeros((n_hosts, 3), np.float32)
+    kt[:, 0] = [shift * (1 + i / n_hosts) / rho for i in range(n_hosts)]
+    aff = np.tile(np.array([1.1, -5.0], np.float32), (n_hosts, 1))
+    uv = np.stack([rng.uniform(10, width - 50, (n_hosts, points_per_host)),
+                   rng.uniform(10, height - 10, (n_hosts, points_per_host))], -1).astype(np.float32)
+    del fx
+    return host, new, uv, krki, kt, aff

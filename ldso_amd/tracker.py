@@ -9,6 +9,11 @@ Mirrors the reference class (src/frontend/CoarseTracker.cc) for the parts that r
     calcRes(lvl, refToNew, aff, cutoff)   -> calc_res(lvl, T, aff, cutoff)     CoarseTracker.cc:540-673
     calcGSSSE(lvl, H, b, refToNew, aff)   -> calc_gs(lvl, T, aff)              CoarseTracker.cc:675-741
     calcRes + calcGSSSE at one pose       -> calc_res_gs(lvl, T, aff, cutoff)  CoarseTracker.cc:90-105, 218-245
+    new ImmaturePoint(newFrame, feat, ..) -> make_immature(uv, type, host)     ImmaturePoint.cc:14-39
+    traceNewCoarse -> ImmaturePoint::traceOn
+                                          -> trace(krki, kt, aff)              FullSystem.cc:1157-1194,
+                                             (records resident: immature_upload / immature_download)
+                                                                               ImmaturePoint.cc:47-317
 
 No numerical work happens here; every call goes to libldso_ba.so (no fallback).
 """
@@ -135,3 +140,34 @@ class CoarseTracker:
         cnt = np.zeros(k, np.int64)
         L.check(lib.ldso_ct_get_kernel_times(self._h, L.ptr(ms, L.f64p), L.ptr(cnt, L.i64p), int(k)))
         return {lib.ldso_ct_kernel_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(k)}
+
+    # ---- immature points ----
+    def make_immature(self, uv, type_: float = 1.0, host: int = 0) -> np.ndarray:
+        """ImmaturePoint(newFrame, feat, type) for features uv [n][2] on the new frame -> records."""
+        uv = _f32(uv).reshape(-1, 2)
+        out = np.zeros(uv.shape[0], L.IMMATURE_DTYPE)
+        L.check(L.lib().ldso_ct_make_immature(self._h, int(uv.shape[0]), L.ptr(uv, L.f32p), float(type_), int(host),
+                                              out.ctypes.data))
+        return out
+
+    def immature_upload(self, pts: np.ndarray):
+        assert pts.dtype == L.IMMATURE_DTYPE and pts.flags.c_contiguous
+        L.check(L.lib().ldso_ct_immature_upload(self._h, int(pts.size), pts.ctypes.data))
+        self._ip_n = int(pts.size)
+
+    def immature_download(self) -> np.ndarray:
+        out = np.zeros(getattr(self, "_ip_n", 0), L.IMMATURE_DTYPE)
+        L.check(L.lib().ldso_ct_immature_download(self._h, int(out.size), out.ctypes.data))
+        return out
+
+    def trace(self, krki, kt, aff, counts: bool = True):
+        """traceNewCoarse over the resident records: per host KRKi [9], Kt [3], aff [2] -> counts [6]
+        (GOOD, OOB, OUTLIER, SKIPPED, BADCONDITION, UNINITIALIZED) or None."""
+        krki = _f32(krki).reshape(-1, 9)
+        kt = _f32(kt).reshape(-1, 3)
+        aff = _f32(aff).reshape(-1, 2)
+        assert krki.shape[0] == kt.shape[0] == aff.shape[0]
+        c = np.zeros(6, np.int32) if counts else None
+        L.check(L.lib().ldso_ct_trace(self._h, int(krki.shape[0]), L.ptr(krki, L.f32p), L.ptr(kt, L.f32p),
+                                      L.ptr(aff, L.f32p), L.ptr(c, L.i32p)))
+        return c

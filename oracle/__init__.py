@@ -67,6 +67,8 @@ def lib():
             "oracle_ct_calc_res": (C.c_int, [C.c_int, C.c_int, C.c_int, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p,
                                              f64p, f64p, C.c_float, f64p, f32p, i32p]),
             "oracle_ct_calc_gs": (C.c_int, [C.c_int, f32p, C.c_float, C.c_float, f64p, f64p, f64p]),
+            "oracle_ip_make": (None, [f32p, C.c_int, C.c_int, C.c_int, f32p, C.c_float, C.c_int, C.c_void_p]),
+            "oracle_ip_trace": (None, [f32p, C.c_int, C.c_int, f32p, f32p, f32p, C.c_int, C.c_void_p, i32p]),
         }
         for k, (res, args) in sig.items():
             f = getattr(Lb, k)
@@ -273,3 +275,34 @@ def ct_calc_gs(warped, fxl, fyl, aff6):
                                  _p(np.ascontiguousarray(aff6, np.float64), f64p), _p(H, f64p), _p(b, f64p))
     assert rc == 0
     return H, b
+
+
+# ---- immature points (ldso_oracle_tracker.cpp): the checker of ldso_ct_make_immature / _trace --
+# ldso_ct_immature (include/ldso_ct.h), 128 bytes
+IMMATURE_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("idepth_min", "<f4"), ("idepth_max", "<f4"),
+                           ("quality", "<f4"), ("energy_th", "<f4"), ("color", "<f4", (8,)),
+                           ("weights", "<f4", (8,)), ("grad_h", "<f4", (4,)), ("host", "<i4"),
+                           ("last_status", "<i4"), ("last_uv", "<f4", (2,)), ("last_interval", "<f4"),
+                           ("type", "<f4")])
+assert IMMATURE_DTYPE.itemsize == 128
+
+
+def ip_make(dI0, w, h, uv, type_=1.0, host=0):
+    """new ImmaturePoint(frame, feat, type, HCalib) for features uv [n][2] on level-0 dI [w*h][3]."""
+    uv = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+    out = np.zeros(uv.shape[0], IMMATURE_DTYPE)
+    lib().oracle_ip_make(_p(np.ascontiguousarray(dI0, np.float32), f32p), int(w), int(h), int(uv.shape[0]),
+                         _p(uv, f32p), float(type_), int(host), out.ctypes.data)
+    return out
+
+
+def ip_trace(dI0, w, h, krki, kt, aff, pts):
+    """traceNewCoarse over the records pts (updated in place) -> status counts [6]."""
+    assert pts.dtype == IMMATURE_DTYPE and pts.flags.c_contiguous
+    counts = np.zeros(6, np.int32)
+    lib().oracle_ip_trace(_p(np.ascontiguousarray(dI0, np.float32), f32p), int(w), int(h),
+                          _p(np.ascontiguousarray(krki, np.float32), f32p),
+                          _p(np.ascontiguousarray(kt, np.float32), f32p),
+                          _p(np.ascontiguousarray(aff, np.float32), f32p), int(pts.size), pts.ctypes.data,
+                          _p(counts, i32p))
+    return counts

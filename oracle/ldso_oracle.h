@@ -18,6 +18,7 @@
 #define LDSO_ORACLE_H_
 
 #include "../include/ldso_ba.h"
+#include "../include/ldso_ct.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -93,6 +94,13 @@ int oracle_ct_calc_res(int lvl, int wl, int hl, const float *kl, const float *dI
                        const double *aff6, float cutoffTH, double *rs, float *warped_out, int *n_warped);
 int oracle_ct_calc_gs(int n, const float *warped, float fxl, float fyl, const double *aff6, double *H_out,
                       double *b_out);
+
+/* ImmaturePoint constructor over n features uv [n][2] of the level-0 frame dI [w*h][3] */
+void oracle_ip_make(const float *dI, int w, int h, int n, const float *uv, float type, int host,
+                    ldso_ct_immature *out);
+/* traceNewCoarse: traceOn of every record against dI with its host's krki/kt/aff; counts [6] */
+void oracle_ip_trace(const float *dI, int w, int h, const float *krki, const float *kt, const float *aff, int n,
+                     ldso_ct_immature *pts, int *counts);
 
 /* CPU-baseline timing: run `iters` oracle_iteration passes, return wall seconds. */
 double oracle_time_iterations(oracle_window *ow, int iters);

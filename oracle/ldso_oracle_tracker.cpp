@@ -12,6 +12,10 @@
 //                        with Accumulator9 (4 SSE lanes, 1k/1M blocked flush, finish)
 //                                                            MatrixAccumulators.h:1104-1643
 //   affine               AffLight::fromToVecExposure         include/AffLight.h:27-35
+//   oracle_ip_make       ImmaturePoint::ImmaturePoint        src/internal/ImmaturePoint.cc:14-39
+//   oracle_ip_trace      traceNewCoarse -> traceOn           src/frontend/FullSystem.cc:1157-1194
+//                                                            src/internal/ImmaturePoint.cc:47-317
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -314,6 +318,282 @@ int oracle_ct_calc_gs(int n, const float *warped, float fxl_, float fyl_, const 
         for (int c = 0; c < 8; c++) H_out[8 * r + c] *= scale[r];
     for (int r = 0; r < 8; r++) b_out[r] *= scale[r];
     return 0;
+}
+
+}  // extern "C"
+
+// ============================================================================================
+// Immature points: ImmaturePoint::ImmaturePoint and ImmaturePoint::traceOn
+// (src/internal/ImmaturePoint.cc:14-39, 47-317) over FullSystem::traceNewCoarse's loop
+// (src/frontend/FullSystem.cc:1157-1194).  dI: the traced / sampled frame's level-0 [w*h][3].
+// Taps are clamped to the last interpolable texel (the reference reads past the image there).
+// ============================================================================================
+namespace {
+
+constexpr int kPat[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};  // Setting.cc:275
+constexpr float kOutlierTHSumComponent = 50.0f * 50.0f;  // Setting.cc:41
+constexpr float kOutlierTH = 12 * 12;                    // Setting.cc:39
+constexpr float kOverallEnergyTHWeight = 1.0f;           // Setting.cc:82
+constexpr float kMaxPixSearch = 0.027f;                  // Setting.cc:28
+constexpr int kMinTraceTestRadius = 2;                   // Setting.cc:52
+constexpr float kTraceStepsize = 1.0f;                   // Setting.cc:89
+constexpr int kTraceGNIterations = 3;                    // Setting.cc:90
+constexpr float kTraceGNThreshold = 0.1f;                // Setting.cc:91
+constexpr float kTraceExtraSlackOnTH = 1.2f;             // Setting.cc:92
+constexpr float kTraceSlackInterval = 1.5f;              // Setting.cc:93
+constexpr float kTraceMinImprovementFactor = 2;          // Setting.cc:94
+
+// index of the top-left texel of a bilinear tap, clamped into [0, w-2] x [0, h-2]
+inline long ip_base(float x, float y, int w, int h, float &fx, float &fy) {
+    long ix = (long)(int)x, iy = (long)(int)y;
+    fx = x - (int)x;
+    fy = y - (int)y;
+    ix = ix < 0 ? 0 : ix > w - 2 ? w - 2 : ix;
+    iy = iy < 0 ? 0 : iy > h - 2 ? h - 2 : iy;
+    return ix + iy * (long)w;
+}
+
+// getInterpolatedElement31 (GlobalFuncs.h:146-159)
+inline float interp31(const float *dI, float x, float y, int w, int h) {
+    float dx, dy;
+    const float *bp = dI + 3 * ip_base(x, y, w, h, dx, dy);
+    const float dxdy = dx * dy;
+    return dxdy * bp[3 * (1 + w)] + (dy - dxdy) * bp[3 * w] + (dx - dxdy) * bp[3] + (1 - dx - dy + dxdy) * bp[0];
+}
+
+// getInterpolatedElement33 (GlobalFuncs.h:90-103), component by component
+inline void interp33(const float *dI, float x, float y, int w, int h, float out[3]) {
+    float dx, dy;
+    const float *bp = dI + 3 * ip_base(x, y, w, h, dx, dy);
+    const float dxdy = dx * dy;
+    for (int c = 0; c < 3; c++)
+        out[c] = dxdy * bp[3 * (1 + w) + c] + (dy - dxdy) * bp[3 * w + c] + (dx - dxdy) * bp[3 + c] +
+                 (1 - dx - dy + dxdy) * bp[c];
+}
+
+// getInterpolatedElement33BiLin (GlobalFuncs.h:186-207)
+inline void interp33_bilin(const float *dI, float x, float y, int w, int h, float out[3]) {
+    float dx, dy;
+    const float *bp = dI + 3 * ip_base(x, y, w, h, dx, dy);
+    const float tl = bp[0], tr = bp[3], bl = bp[3 * w], br = bp[3 * w + 3];
+    const float topInt = dx * tr + (1 - dx) * tl;
+    const float botInt = dx * br + (1 - dx) * bl;
+    const float leftInt = dy * bl + (1 - dy) * tl;
+    const float rightInt = dy * br + (1 - dy) * tr;
+    out[0] = dx * rightInt + (1 - dx) * leftInt;
+    out[1] = rightInt - leftInt;
+    out[2] = botInt - topInt;
+}
+
+int set_status(ldso_ct_immature &p, int s, float u, float v, float interval) {
+    p.last_uv[0] = u;
+    p.last_uv[1] = v;
+    p.last_interval = interval;
+    return p.last_status = s;
+}
+
+// ImmaturePoint::traceOn (ImmaturePoint.cc:47-317)
+int trace_on(ldso_ct_immature &p, const float *dI, int w, int h, const float *KRKi, const float *Kt,
+             const float *aff) {
+    if (p.last_status == LDSO_CT_IPS_OOB) return p.last_status;
+    const float maxPixSearch = (w + h) * kMaxPixSearch;
+    float pr[3];
+    for (int i = 0; i < 3; i++) pr[i] = KRKi[3 * i] * p.u + KRKi[3 * i + 1] * p.v + KRKi[3 * i + 2] * 1.0f;
+    float ptpMin[3];
+    for (int i = 0; i < 3; i++) ptpMin[i] = pr[i] + Kt[i] * p.idepth_min;
+    const float uMin = ptpMin[0] / ptpMin[2], vMin = ptpMin[1] / ptpMin[2];
+    if (!(uMin > 4 && vMin > 4 && uMin < w - 5 && vMin < h - 5)) return set_status(p, LDSO_CT_IPS_OOB, -1, -1, 0);
+
+    float dist, uMax, vMax, ptpMax[3];
+    if (std::isfinite(p.idepth_max)) {
+        for (int i = 0; i < 3; i++) ptpMax[i] = pr[i] + Kt[i] * p.idepth_max;
+        uMax = ptpMax[0] / ptpMax[2];
+        vMax = ptpMax[1] / ptpMax[2];
+        if (!(uMax > 4 && vMax > 4 && uMax < w - 5 && vMax < h - 5)) return set_status(p, LDSO_CT_IPS_OOB, -1, -1, 0);
+        dist = (uMin - uMax) * (uMin - uMax) + (vMin - vMax) * (vMin - vMax);
+        dist = std::sqrt(dist);
+        if (dist < kTraceSlackInterval)
+            return set_status(p, LDSO_CT_IPS_SKIPPED, (uMax + uMin) * 0.5f, (vMax + vMin) * 0.5f, dist);
+    } else {
+        dist = maxPixSearch;
+        for (int i = 0; i < 3; i++) ptpMax[i] = pr[i] + Kt[i] * 0.01f;  // Eigen casts the double 0.01 to float
+        uMax = ptpMax[0] / ptpMax[2];
+        vMax = ptpMax[1] / ptpMax[2];
+        const float dx = uMax - uMin, dy = vMax - vMin;
+        const float d = 1.0f / std::sqrt(dx * dx + dy * dy);
+        uMax = uMin + dist * dx * d;
+        vMax = vMin + dist * dy * d;
+        if (!(uMax > 4 && vMax > 4 && uMax < w - 5 && vMax < h - 5)) return set_status(p, LDSO_CT_IPS_OOB, -1, -1, 0);
+    }
+    if (!(p.idepth_min < 0 || (ptpMin[2] > 0.75f && ptpMin[2] < 1.5f))) return set_status(p, LDSO_CT_IPS_OOB, -1, -1, 0);
+
+    float dx = kTraceStepsize * (uMax - uMin);
+    float dy = kTraceStepsize * (vMax - vMin);
+    const float *G = p.grad_h;
+    const float a = (dx * G[0] + dy * G[2]) * dx + (dx * G[1] + dy * G[3]) * dy;       // (v^T G) v
+    const float b = (dy * G[0] + -dx * G[2]) * dy + (dy * G[1] + -dx * G[3]) * -dx;  // v = (dy, -dx)
+    float errorInPixel = 0.2f + 0.2f * (a + b) / a;
+    if (errorInPixel * kTraceMinImprovementFactor > dist && std::isfinite(p.idepth_max))
+        return set_status(p, LDSO_CT_IPS_BADCONDITION, (uMax + uMin) * 0.5f, (vMax + vMin) * 0.5f, dist);
+    if (errorInPixel > 10) errorInPixel = 10;
+
+    dx /= dist;
+    dy /= dist;
+    if (dist > maxPixSearch) {
+        uMax = uMin + maxPixSearch * dx;
+        vMax = vMin + maxPixSearch * dy;
+        dist = maxPixSearch;
+    }
+    int numSteps = 1.9999f + dist / kTraceStepsize;
+    const float R00 = KRKi[0], R01 = KRKi[1], R10 = KRKi[3], R11 = KRKi[4];  // Rplane = topLeftCorner<2,2>
+    const float randShift = uMin * 1000 - std::floor(uMin * 1000);
+    float ptx = uMin - randShift * dx;
+    float pty = vMin - randShift * dy;
+    float rp[8][2];
+    for (int i = 0; i < 8; i++) {
+        rp[i][0] = R00 * (float)kPat[i][0] + R01 * (float)kPat[i][1];
+        rp[i][1] = R10 * (float)kPat[i][0] + R11 * (float)kPat[i][1];
+    }
+    if (!std::isfinite(dx) || !std::isfinite(dy)) return set_status(p, LDSO_CT_IPS_OOB, -1, -1, 0);
+
+    float errors[100];
+    float bestU = 0, bestV = 0, bestEnergy = 1e10f;
+    int bestIdx = -1;
+    if (numSteps >= 100) numSteps = 99;
+    for (int i = 0; i < numSteps; i++) {
+        float energy = 0;
+        for (int idx = 0; idx < 8; idx++) {
+            const float hitColor = interp31(dI, (float)(ptx + rp[idx][0]), (float)(pty + rp[idx][1]), w, h);
+            if (!std::isfinite(hitColor)) {
+                energy += 1e5f;
+                continue;
+            }
+            const float residual = hitColor - (float)(aff[0] * p.color[idx] + aff[1]);
+            const float hw = std::fabs(residual) < kHuberTH ? 1 : kHuberTH / std::fabs(residual);
+            energy += hw * residual * residual * (2 - hw);
+        }
+        errors[i] = energy;
+        if (energy < bestEnergy) {
+            bestU = ptx;
+            bestV = pty;
+            bestEnergy = energy;
+            bestIdx = i;
+        }
+        ptx += dx;
+        pty += dy;
+    }
+    float secondBest = 1e10f;
+    for (int i = 0; i < numSteps; i++)
+        if ((i < bestIdx - kMinTraceTestRadius || i > bestIdx + kMinTraceTestRadius) && errors[i] < secondBest)
+            secondBest = errors[i];
+    const float newQuality = secondBest / bestEnergy;
+    if (newQuality < p.quality || numSteps > 10) p.quality = newQuality;
+
+    float uBak = bestU, vBak = bestV, gnstepsize = 1, stepBack = 0;
+    if (kTraceGNIterations > 0) bestEnergy = 1e5f;
+    for (int it = 0; it < kTraceGNIterations; it++) {
+        float H = 1, bb = 0, energy = 0;
+        for (int idx = 0; idx < 8; idx++) {
+            float hc[3];
+            interp33(dI, (float)(bestU + rp[idx][0]), (float)(bestV + rp[idx][1]), w, h, hc);
+            if (!std::isfinite(hc[0])) {
+                energy += 1e5f;
+                continue;
+            }
+            const float residual = hc[0] - (aff[0] * p.color[idx] + aff[1]);
+            const float dResdDist = dx * hc[1] + dy * hc[2];
+            const float hw = std::fabs(residual) < kHuberTH ? 1 : kHuberTH / std::fabs(residual);
+            H += hw * dResdDist * dResdDist;
+            bb += hw * residual * dResdDist;
+            energy += p.weights[idx] * p.weights[idx] * hw * residual * residual * (2 - hw);
+        }
+        if (energy > bestEnergy) {
+            stepBack *= 0.5f;
+            bestU = uBak + stepBack * dx;
+            bestV = vBak + stepBack * dy;
+        } else {
+            float step = -gnstepsize * bb / H;
+            if (step < -0.5f) step = -0.5f;
+            else if (step > 0.5f) step = 0.5f;
+            if (!std::isfinite(step)) step = 0;
+            uBak = bestU;
+            vBak = bestV;
+            stepBack = step;
+            bestU += step * dx;
+            bestV += step * dy;
+            bestEnergy = energy;
+        }
+        if (std::fabs(stepBack) < kTraceGNThreshold) break;
+    }
+
+    if (!(bestEnergy < p.energy_th * kTraceExtraSlackOnTH))
+        return set_status(p, p.last_status == LDSO_CT_IPS_OUTLIER ? LDSO_CT_IPS_OOB : LDSO_CT_IPS_OUTLIER, -1, -1, 0);
+
+    if (dx * dx > dy * dy) {
+        p.idepth_min = (pr[2] * (bestU - errorInPixel * dx) - pr[0]) / (Kt[0] - Kt[2] * (bestU - errorInPixel * dx));
+        p.idepth_max = (pr[2] * (bestU + errorInPixel * dx) - pr[0]) / (Kt[0] - Kt[2] * (bestU + errorInPixel * dx));
+    } else {
+        p.idepth_min = (pr[2] * (bestV - errorInPixel * dy) - pr[1]) / (Kt[1] - Kt[2] * (bestV - errorInPixel * dy));
+        p.idepth_max = (pr[2] * (bestV + errorInPixel * dy) - pr[1]) / (Kt[1] - Kt[2] * (bestV + errorInPixel * dy));
+    }
+    if (p.idepth_min > p.idepth_max) std::swap(p.idepth_min, p.idepth_max);
+    if (!std::isfinite(p.idepth_min) || !std::isfinite(p.idepth_max) || (p.idepth_max < 0))
+        return set_status(p, LDSO_CT_IPS_OUTLIER, -1, -1, 0);
+    return set_status(p, LDSO_CT_IPS_GOOD, bestU, bestV, 2 * errorInPixel);
+}
+
+}  // namespace
+
+extern "C" {
+
+void oracle_ip_make(const float *dI, int w, int h, int n, const float *uv, float type, int host,
+                    ldso_ct_immature *out) {
+    for (int k = 0; k < n; k++) {
+        ldso_ct_immature &p = out[k];
+        std::memset(&p, 0, sizeof(p));
+        p.u = uv[2 * k];
+        p.v = uv[2 * k + 1];
+        p.idepth_min = 0;
+        p.idepth_max = NAN;
+        p.quality = 10000;
+        p.type = type;
+        p.host = host;
+        p.last_status = LDSO_CT_IPS_UNINITIALIZED;
+        float G[4] = {0, 0, 0, 0};
+        bool ok = true;
+        for (int idx = 0; idx < 8; idx++) {
+            float ptc[3];
+            interp33_bilin(dI, p.u + kPat[idx][0], p.v + kPat[idx][1], w, h, ptc);
+            p.color[idx] = ptc[0];
+            if (!std::isfinite(p.color[idx])) {
+                ok = false;
+                break;
+            }
+            G[0] += ptc[1] * ptc[1];
+            G[1] += ptc[1] * ptc[2];
+            G[2] += ptc[2] * ptc[1];
+            G[3] += ptc[2] * ptc[2];
+            p.weights[idx] = std::sqrt(kOutlierTHSumComponent / (kOutlierTHSumComponent + (ptc[1] * ptc[1] + ptc[2] * ptc[2])));
+        }
+        for (int i = 0; i < 4; i++) p.grad_h[i] = G[i];
+        if (!ok) {
+            p.energy_th = NAN;
+            continue;
+        }
+        float e = 8 * kOutlierTH;
+        e *= kOverallEnergyTHWeight * kOverallEnergyTHWeight;
+        p.energy_th = e;
+    }
+}
+
+void oracle_ip_trace(const float *dI, int w, int h, const float *krki, const float *kt, const float *aff, int n,
+                     ldso_ct_immature *pts, int *counts) {
+    for (int s = 0; s < 6; s++) counts[s] = 0;
+    for (int k = 0; k < n; k++) {
+        const int hh = pts[k].host;
+        trace_on(pts[k], dI, w, h, krki + 9 * hh, kt + 3 * hh, aff + 2 * hh);
+        counts[pts[k].last_status]++;
+    }
 }
 
 }  // extern "C"

@@ -47,7 +47,8 @@ def test_library_exports_every_tracker_symbol(built):
     assert not [s for s in syms if s not in exported]
     assert set(syms) == {name for name, _, _ in L.CT_ABI}
     lib = L.lib()
-    assert lib.ldso_ct_num_kernels() == 4 and lib.ldso_ct_kernel_name(2) == b"k_ct_calc_res"
+    assert lib.ldso_ct_num_kernels() == 7 and lib.ldso_ct_kernel_name(2) == b"k_ct_calc_res"
+    assert lib.ldso_ct_kernel_name(5) == b"k_ct_trace"
     h = C.c_void_p()
     assert lib.ldso_ct_create(0, 4, 4, C.byref(h), None) < 0 and b"small" in lib.ldso_ba_last_error()
 
