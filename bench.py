@@ -183,6 +183,47 @@ def tracker_leg(device, reps=50, n_hyp=32, cpu_seconds=2.0, with_cpu=True):
     return out
 
 
+def activation_leg(device, reps=20, cpu_seconds=2.0, with_cpu=True):
+    """Point activation (ldso_ba_activate_points): optimizeImmaturePoint for
+    the 2000 points of an S7 window (inverse-depth interval +-10 %), against every other frame
+    (6 residuals x 8 pixels x 4 evaluations per point).  Host-clock ms per call (upload, k_activate,
+    download), k_activate's mean HIP-event duration, and the oracle's single-thread loop (the
+    reference's activatePointsMT runs on 6 threads; its per-point work is this loop)."""
+    from ldso_amd import BAContext, synth
+
+    w = synth.make_window(**synth.S7, seed=1)
+    pts = synth.immature_from_window(w)
+    ctx = BAContext(device).load([w])
+    for _ in range(3):
+        ctx.activate_points(0, pts)
+    ctx.set_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = ctx.activate_points(0, pts)
+    ms = 1e3 * (time.perf_counter() - t0) / reps
+    kt = ctx.kernel_times()
+    ctx.close()
+    k_ms, k_n = kt["k_activate"]
+    k_us = 1e3 * k_ms / max(1, k_n)
+    res = {"points": int(pts.size), "window": "S7 (7 KF, 640x480)", "activated": int((out["status"] == 0).sum()),
+           "ms_per_call": ms, "k_activate_us": k_us,
+           "point_activations_per_s": pts.size / (k_us / 1e6) if k_us > 0 else None}
+    if with_cpu:
+        import oracle
+
+        ow = oracle.OracleWindow(synth.make_window(**synth.S7, seed=1), threads=0)
+        m, el = 0, 0.0
+        while el < cpu_seconds:
+            t0 = time.perf_counter()
+            ow.activate_points(pts)
+            el += time.perf_counter() - t0
+            m += 1
+        ow.close()
+        res["cpu"] = {"ms": 1e3 * el / m, "cores": 1, "kind": "port", "sample": f"{m} oracle calls over {pts.size} points"}
+        res["kernel_speedup_vs_cpu"] = res["cpu"]["ms"] / (k_us / 1e3) if k_us > 0 else None
+    return res
+
+
 def trace_leg(device, reps=50, cpu_seconds=2.0, with_cpu=True):
     """traceNewCoarse (SURVEY.md §8f row 4; ldso_ct_trace): ImmaturePoint::traceOn of 7 hosts x
     1500 immature points (setting_desiredImmatureDensity) against a 640x480 new frame, records
@@ -413,6 +454,7 @@ def main():
     if rank == 0 and not args.no_tracker:
         tracker = tracker_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
         tracker["trace_new_coarse"] = trace_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
+        tracker["activate_points"] = activation_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
 
     cpu = cpu16 = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -14,6 +14,8 @@
  *                                                            src/internal/OptimizationBackend/EnergyFunctional.cc:280-471, 611-749
  *   FrameFramePrecalc::Set, EnergyFunctional::setAdjointsF  src/internal/FrameFramePrecalc.cc:6-35,
  *                                                            src/internal/OptimizationBackend/EnergyFunctional.cc:551-609
+ *   FullSystem::optimizeImmaturePoint with                   src/frontend/FullSystem.cc:1035-1156,
+ *     ImmaturePoint::linearizeResidual (point activation)    src/internal/ImmaturePoint.cc:319-389
  *
  * Conventions (mirroring the reference):
  *   - frame-pair index            pair = h + N*t      (AccumulatedTopHessian.cc:38)
@@ -189,6 +191,27 @@ int ldso_ba_load_marginalization(ldso_ba_ctx *marg, const ldso_ba_ctx *parent, i
  * setting_margWeightFac * (H, b) to (HM, bM) (EnergyFunctional.cc:254-255).  Residual states and
  * points of `marg` are readable with get_residuals / get_points as after a pass. */
 int ldso_ba_marginalize_points(ldso_ba_ctx *marg, const float *ad_ht_delta, double *H, double *b);
+
+/* ---- point activation ----
+ * FullSystem::optimizeImmaturePoint(point, min_obs, residuals) (FullSystem.cc:1035-1156) for n
+ * immature points of window `win`: ImmaturePoint::linearizeResidual (ImmaturePoint.cc:319-389)
+ * against every other frame of the window in window order, from idepth (min + max) / 2, then
+ * setting_GNItsOnPointActivation LM steps on the inverse depth.  pts: ldso_ct_immature records
+ * (include/ldso_ct.h; u, v, idepth_min/max, energy_th, color, weights, host = frame index in the
+ * window).  Uses the context's images, FrameFramePrecalc (PRE_RTll, PRE_tTll, PRE_aff_mode) and
+ * calibration as last loaded / set.  activatePointsMT calls it with min_obs = 1. */
+struct ldso_ct_immature;
+typedef struct ldso_ba_activation {
+    float idepth;      /* currentIdepth at return                                              */
+    int32_t status;    /* 0: a PointHessian is created (setIdepth(idepth)); 1: nullptr (idepth not
+                          finite, or fewer than min_obs IN residuals); 2: 0 (energy not finite or
+                          Hdd < setting_minIdepthH_act)                                        */
+    uint32_t in_mask;  /* status 0: bit f set = the residual to window frame f is IN and moves
+                          into the new point (lastResiduals follow from frames N-1, N-2)       */
+    float energy;      /* lastEnergy at return                                                 */
+} ldso_ba_activation;
+int ldso_ba_activate_points(ldso_ba_ctx *ctx, int32_t win, int32_t n, const struct ldso_ct_immature *pts,
+                            int32_t min_obs, ldso_ba_activation *out);
 
 /* One hot-path pass over all loaded windows, asynchronous on the context stream:
  *   linearizeAll(fix) + applyRes(true) + setNewFrameEnergyTH, and if accumulate != 0

@@ -123,6 +123,7 @@ ABI = [
     ("ldso_ba_marginalize_frame", C.c_int, [C.c_int32, C.c_int32, f64p, f64p, f64p, f64p, f64p, f64p]),
     ("ldso_ba_load_marginalization", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(LdsoBaWindow)]),
     ("ldso_ba_marginalize_points", C.c_int, [C.c_void_p, f32p, f64p, f64p]),
+    ("ldso_ba_activate_points", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]),
 ]
 
 f32pp = C.POINTER(f32p)
@@ -134,6 +135,8 @@ IMMATURE_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("idepth_min", "<f4"), ("
                            ("last_status", "<i4"), ("last_uv", "<f4", (2,)), ("last_interval", "<f4"),
                            ("type", "<f4")])
 assert IMMATURE_DTYPE.itemsize == 128
+# ldso_ba_activation (include/ldso_ba.h)
+ACTIVATION_DTYPE = np.dtype([("idepth", "<f4"), ("status", "<i4"), ("in_mask", "<u4"), ("energy", "<f4")])
 IPS_NAMES = ("GOOD", "OOB", "OUTLIER", "SKIPPED", "BADCONDITION", "UNINITIALIZED")  # ImmaturePoint.h:31-38
 
 # (name, restype, argtypes) of every entry point declared in include/ldso_ct.h (coarse tracker)

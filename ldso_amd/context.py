@@ -73,6 +73,15 @@ class BAContext:
         s = window.c_struct()
         L.check(self._lib.ldso_ba_update(self._h, int(win), C.byref(s)))
 
+    def activate_points(self, win: int, pts: np.ndarray, min_obs: int = 1) -> np.ndarray:
+        """FullSystem::optimizeImmaturePoint for ldso_ct_immature records hosted in window `win`
+        (FullSystem.cc:1035-1156) -> ldso_ba_activation records {idepth, status, in_mask, energy}."""
+        assert pts.dtype == L.IMMATURE_DTYPE and pts.flags.c_contiguous
+        out = np.zeros(pts.size, L.ACTIVATION_DTYPE)
+        L.check(self._lib.ldso_ba_activate_points(self._h, int(win), int(pts.size), pts.ctypes.data, int(min_obs),
+                                                  out.ctypes.data))
+        return out
+
     def reset_oob(self, win: int = -1):
         L.check(self._lib.ldso_ba_reset_oob(self._h, int(win)))
 

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../include/ldso_ba.h"
+#include "../../include/ldso_ct.h"
 #include "ldso_ba_internal.h"
 
 using namespace ldso_ba;
@@ -48,9 +49,9 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kTopVals = 96;    // 55 + 30 + 6 AccumulatorApprox entries, padded to 96
 constexpr int kMaxRes = LDSO_BA_MAX_FRAMES - 1;
-constexpr int kNumKernels = 6;
+constexpr int kNumKernels = 7;
 const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch", "k_resubstitute", "k_frame_th",
-                                         "k_solve"};
+                                         "k_solve",     "k_activate"};
 
 thread_local std::string g_err;
 int fail(int code, const std::string &msg) {
@@ -2218,6 +2219,242 @@ __global__ __launch_bounds__(256) void k_xad(const WinDev *__restrict__ wins, co
     if (threadIdx.x < 4) o[(size_t)N * N * 8 + threadIdx.x] = (float)xw[threadIdx.x];
 }
 
+// ============================================================================================
+// k_activate: FullSystem::optimizeImmaturePoint (FullSystem.cc:1035-1156) with
+// ImmaturePoint::linearizeResidual (ImmaturePoint.cc:319-389), SURVEY §8f row 4.
+// One wavefront per immature point; lane r owns the temporary residual to the r-th other frame
+// (window order) and evaluates its 8 pattern pixels; the point's Hdd, bd and energy are then
+// summed on every lane in the reference's order (residual by residual, pixel by pixel, with the
+// pixels before an OOB pixel still counted), so the LM steps are wave-uniform and bit-identical
+// to the CPU restatement.
+// ============================================================================================
+struct ActParams {
+    const WinDev *__restrict__ wins;
+    const float4 *__restrict__ img;
+    const float *__restrict__ precalc;
+    const ldso_ct_immature *__restrict__ pts;
+    ldso_ba_activation *out;
+    long long frame_stride;
+    int tpr, img_mode, win, n, min_obs;
+};
+
+// getInterpolatedElement33 (GlobalFuncs.h:89-103) of a resident frame in any image layout
+__device__ inline float3 sample33(const float4 *__restrict__ img, int mode, int tpr, int width, float x, float y) {
+#pragma clang fp contract(off)
+    const int ix = (int)x, iy = (int)y;
+    const float dx = x - ix, dy = y - iy, dxdy = dx * dy;
+    const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+    float3 t00, t10, t01, t11;
+    if (mode == 3) {
+        const float *imf = reinterpret_cast<const float *>(img);
+        auto at = [&](int xx, int yy) { return imf[(((yy >> 2) * tpr + (xx >> 3)) << 5) + ((yy & 3) << 3) + (xx & 7)]; };
+        auto grad = [](float a, float b) {
+            const float d = 0.5f * (a - b);
+            return (isnan(d) || fabsf(d) > 255.0f) ? 0.0f : d;
+        };
+        float v[12];
+        v[0] = at(ix, iy - 1);
+        v[1] = at(ix + 1, iy - 1);
+        v[2] = at(ix - 1, iy);
+        v[3] = at(ix, iy);
+        v[4] = at(ix + 1, iy);
+        v[5] = at(ix + 2, iy);
+        v[6] = at(ix - 1, iy + 1);
+        v[7] = at(ix, iy + 1);
+        v[8] = at(ix + 1, iy + 1);
+        v[9] = at(ix + 2, iy + 1);
+        v[10] = at(ix, iy + 2);
+        v[11] = at(ix + 1, iy + 2);
+        t00 = make_float3(v[3], grad(v[4], v[2]), grad(v[7], v[0]));
+        t10 = make_float3(v[4], grad(v[5], v[3]), grad(v[8], v[1]));
+        t01 = make_float3(v[7], grad(v[8], v[6]), grad(v[10], v[3]));
+        t11 = make_float3(v[8], grad(v[9], v[7]), grad(v[11], v[4]));
+    } else if (mode == 2) {
+        const float4 *rec = img + ((size_t)iy * width + ix) * 4;
+        const float4 qi = rec[0], qx = rec[1], qy = rec[2];
+        t00 = make_float3(qi.x, qx.x, qy.x);
+        t10 = make_float3(qi.y, qx.y, qy.y);
+        t01 = make_float3(qi.z, qx.z, qy.z);
+        t11 = make_float3(qi.w, qx.w, qy.w);
+    } else if (mode == 1) {
+        t00 = tex<true, false>(img, tpr, ix, iy);
+        t10 = tex<true, false>(img, tpr, ix + 1, iy);
+        t01 = tex<true, false>(img, tpr, ix, iy + 1);
+        t11 = tex<true, false>(img, tpr, ix + 1, iy + 1);
+    } else {
+        t00 = tex<false, false>(img, tpr, ix, iy);
+        t10 = tex<false, false>(img, tpr, ix + 1, iy);
+        t01 = tex<false, false>(img, tpr, ix, iy + 1);
+        t11 = tex<false, false>(img, tpr, ix + 1, iy + 1);
+    }
+    return make_float3(w11 * t11.x + w01 * t01.x + w10 * t10.x + w00 * t00.x,
+                       w11 * t11.y + w01 * t01.y + w10 * t10.y + w00 * t00.y,
+                       w11 * t11.z + w01 * t01.z + w10 * t10.z + w00 * t00.z);
+}
+
+__global__ __launch_bounds__(256) void k_activate(ActParams P) {
+#pragma clang fp contract(off)
+    constexpr int pat[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};
+    constexpr float kMinIdepthHAct = 100;  // setting_minIdepthH_act, Setting.cc:25
+    constexpr int kGNItsOnPointActivation = 3;  // Setting.cc:47
+    const int lane = threadIdx.x & 63;
+    const int k = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (k >= P.n) return;
+    const WinDev &W = P.wins[P.win];
+    const ldso_ct_immature &ip = P.pts[k];
+    const int N = W.N, host = ip.host, nres = N - 1;
+    const float fxl = W.calib[0], fyl = W.calib[1], cxl = W.calib[2], cyl = W.calib[3];
+    const float fxli = 1.0f / fxl, fyli = 1.0f / fyl;
+    const float u0 = ip.u, v0 = ip.v, eth = ip.energy_th;
+    // this lane's temporary residual (ImmaturePointTemporaryResidual, ImmaturePoint.h:18-26)
+    const bool mine = lane < nres;
+    const int tgt = mine ? lane + (lane >= host) : host;
+    int st_state = LDSO_BA_RES_IN, st_new = LDSO_BA_RES_OUTLIER;
+    float st_energy = 0, st_newenergy = 0;  // doubles in the reference holding float values
+    const float *pre = P.precalc + (size_t)(W.pair_base + host + N * tgt) * LDSO_BA_PRECALC_STRIDE;
+    const float4 *img = P.img + (size_t)(W.frame_base + tgt) * P.frame_stride;
+    float R[9], t[3];
+#pragma unroll
+    for (int i = 0; i < 9; i++) R[i] = pre[12 + i];
+#pragma unroll
+    for (int i = 0; i < 3; i++) t[i] = pre[21 + i];
+    const float aff0 = pre[24], aff1 = pre[25];
+    float col[8], wsq[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        col[i] = ip.color[i];
+        wsq[i] = ip.weights[i] * ip.weights[i];
+    }
+
+    // linearizeResidual(HCalib, slack, tmpRes, Hdd, bd, idepth) of every residual, then the
+    // point's sums in the reference's order -> (energy, Hdd, bd), identical on every lane
+    auto evaluate = [&](float slack, float idepth, float &E, float &Hdd, float &bd) {
+        float tH[8], tb[8];
+        int nvalid = 0;
+        float ret = st_energy;
+        if (mine) {
+            if (st_state == LDSO_BA_RES_OOB) {
+                st_new = LDSO_BA_RES_OOB;
+            } else {
+                float energyLeft = 0;
+                bool oob = false;
+#pragma unroll
+                for (int idx = 0; idx < 8; idx++) {
+                    tH[idx] = tb[idx] = 0;
+                    if (oob) continue;
+                    const float K0 = (u0 + pat[idx][0] - cxl) * fxli, K1 = (v0 + pat[idx][1] - cyl) * fyli;
+                    float ptp[3];
+#pragma unroll
+                    for (int i = 0; i < 3; i++) ptp[i] = (R[3 * i] * K0 + R[3 * i + 1] * K1 + R[3 * i + 2] * 1.0f) + t[i] * idepth;
+                    const float drescale = 1.0f / ptp[2];
+                    const float uu = ptp[0] * drescale, vv = ptp[1] * drescale;
+                    const float Ku = uu * fxl + cxl, Kv = vv * fyl + cyl;
+                    if (!(drescale > 0) || !(Ku > 1.1f && Kv > 1.1f && Ku < W.wM3 && Kv < W.hM3)) {
+                        oob = true;
+                        continue;
+                    }
+                    const float3 hc = sample33(img, P.img_mode, P.tpr, W.width, Ku, Kv);
+                    if (!isfinite(hc.x)) {
+                        oob = true;
+                        continue;
+                    }
+                    const float residual = hc.x - (aff0 * col[idx] + aff1);
+                    float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
+                    energyLeft += wsq[idx] * hw * residual * residual * (2 - hw);
+                    const float dxInterp = hc.y * fxl, dyInterp = hc.z * fyl;
+                    const float d_idepth =
+                        (dxInterp * drescale * (t[0] - t[2] * uu) + dyInterp * drescale * (t[1] - t[2] * vv)) * kScaleIdepth;
+                    hw *= wsq[idx];
+                    tH[idx] = (hw * d_idepth) * d_idepth;
+                    tb[idx] = (hw * residual) * d_idepth;
+                    nvalid = idx + 1;
+                }
+                if (oob) {
+                    st_new = LDSO_BA_RES_OOB;
+                } else {
+                    if (energyLeft > eth * slack) {
+                        energyLeft = eth * slack;
+                        st_new = LDSO_BA_RES_OUTLIER;
+                    } else {
+                        st_new = LDSO_BA_RES_IN;
+                    }
+                    st_newenergy = energyLeft;
+                    ret = energyLeft;
+                }
+            }
+        }
+        for (int r = 0; r < nres; r++) {
+            const int nv = __shfl(nvalid, r, 64);
+#pragma unroll
+            for (int idx = 0; idx < 8; idx++) {
+                const float h_ = __shfl(tH[idx], r, 64), b_ = __shfl(tb[idx], r, 64);
+                if (idx < nv) {
+                    Hdd += h_;
+                    bd += b_;
+                }
+            }
+            E = (float)((double)E + (double)__shfl(ret, r, 64));
+        }
+    };
+    auto commit = [&]() {
+        st_state = st_new;
+        st_energy = st_newenergy;
+    };
+
+    float lastEnergy = 0, lastHdd = 0, lastbd = 0;
+    float currentIdepth = (ip.idepth_max + ip.idepth_min) * 0.5f;
+    evaluate(1000.f, currentIdepth, lastEnergy, lastHdd, lastbd);
+    commit();
+    int status = 0;
+    if (!isfinite(lastEnergy) || lastHdd < kMinIdepthHAct) {
+        status = 2;
+    } else {
+        float lambda = 0.1f;
+        for (int iteration = 0; iteration < kGNItsOnPointActivation; iteration++) {
+            float H = lastHdd;
+            H *= 1 + lambda;
+            const float step = (float)((1.0 / (double)H) * (double)lastbd);
+            const float newIdepth = currentIdepth - step;
+            float newHdd = 0, newbd = 0, newEnergy = 0;
+            evaluate(1.f, newIdepth, newEnergy, newHdd, newbd);
+            if (!isfinite(lastEnergy) || newHdd < kMinIdepthHAct) {
+                status = 2;
+                break;
+            }
+            if (newEnergy < lastEnergy) {
+                currentIdepth = newIdepth;
+                lastHdd = newHdd;
+                lastbd = newbd;
+                lastEnergy = newEnergy;
+                commit();
+                lambda *= 0.5f;
+            } else {
+                lambda = (float)((double)lambda * 5.0);
+            }
+            if ((double)fabsf(step) < 0.0001 * (double)currentIdepth) break;
+        }
+        if (status == 0 && !isfinite(currentIdepth)) status = 1;
+    }
+    unsigned mask = 0;
+    if (status == 0) {
+        const unsigned long long in = __ballot(mine && st_state == LDSO_BA_RES_IN);
+        if (__popcll(in) < P.min_obs) {
+            status = 1;
+        } else {
+            for (int r = 0; r < nres; r++)
+                if ((in >> r) & 1ull) mask |= 1u << (r + (r >= host));
+        }
+    }
+    if (lane == 0) {
+        ldso_ba_activation o;
+        o.idepth = currentIdepth;
+        o.status = status;
+        o.in_mask = mask;
+        o.energy = lastEnergy;
+        P.out[k] = o;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
 #pragma clang fp contract(off)
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2456,6 +2693,8 @@ struct ldso_ba_ctx {
     int n_top_items = 0, n_sc_items = 0, n_pairs = 0, n_frames = 0, P_tot = 0, R_tot = 0, max_frames = 0;
     DevBuf<WinDev> d_wins;
     DevBuf<float4> d_img;
+    DevBuf<ldso_ct_immature> d_act_in;  // point activation staging (ldso_ba_activate_points)
+    DevBuf<ldso_ba_activation> d_act_out;
     int tiles_per_row = 0, padded_h = 0;
     long long frame_stride = 0;
     DevBuf<float> d_precalc, d_frame_th, d_pt_data, d_pt_out, d_pt_step;
@@ -2770,6 +3009,8 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (c->pin_step) (void)hipHostFree(c->pin_step);
     c->d_wins.release();
     c->d_img.release();
+    c->d_act_in.release();
+    c->d_act_out.release();
     c->d_precalc.release();
     c->d_frame_th.release();
     c->d_pt_data.release();
@@ -3439,6 +3680,40 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     }
+    return 0;
+}
+
+int ldso_ba_activate_points(ldso_ba_ctx *c, int32_t win, int32_t n, const ldso_ct_immature *pts, int32_t min_obs,
+                            ldso_ba_activation *out) {
+    if (!c || win < 0 || win >= c->n_win || n < 0 || (n > 0 && (!pts || !out))) return fail(-1, "bad arguments");
+    const int N = c->wh[win].N;
+    for (int k = 0; k < n; k++)
+        if (pts[k].host < 0 || pts[k].host >= N) return fail(-1, "immature point host index outside the window");
+    if (n == 0) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    if ((size_t)n > c->d_act_in.n) {
+        int rc = c->d_act_in.alloc(n);
+        if (!rc) rc = c->d_act_out.alloc(n);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_act_in.p, pts, (size_t)n * sizeof(ldso_ct_immature), hipMemcpyHostToDevice, c->stream));
+    ActParams A;
+    A.wins = c->d_wins.p;
+    A.img = c->img_ext ? c->img_ext : c->d_img.p;
+    A.precalc = c->d_precalc.p;
+    A.pts = c->d_act_in.p;
+    A.out = c->d_act_out.p;
+    A.frame_stride = c->frame_stride;
+    A.tpr = c->tiles_per_row;
+    A.img_mode = c->img_mode;
+    A.win = win;
+    A.n = n;
+    A.min_obs = min_obs;
+    int rc = timed_launch(c, 6, c->stream, [&] { k_activate<<<(n + 3) / 4, 256, 0, c->stream>>>(A); });
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->d_act_out.p, (size_t)n * sizeof(ldso_ba_activation), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
 }
 

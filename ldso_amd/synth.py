@@ -141,3 +141,24 @@ def make_trace_scene(width=640, height=480, n_hosts=7, points_per_host=1500, shi
                    rng.uniform(10, height - 10, (n_hosts, points_per_host))], -1).astype(np.float32)
     del fx
     return host, new, uv, krki, kt, aff
+
+
+def immature_from_window(w, spread=0.1, seed=0):
+    """Point-activation workload: the window's points as ImmaturePoint
+    records (include/ldso_ct.h) with the window's host, pixel, colour and weights and an
+    inverse-depth interval of +-spread (jittered 3 %) around the stored inverse depth."""
+    rng = np.random.default_rng(seed)
+    P = w.point_data.shape[0]
+    pts = np.zeros(P, L.IMMATURE_DTYPE)
+    pd = w.point_data
+    pts["u"], pts["v"] = pd[:, 0], pd[:, 1]
+    idp = pd[:, 2]
+    jitter = rng.uniform(-0.03, 0.03, P).astype(np.float32)
+    pts["idepth_min"] = idp * np.float32(1 - spread) * (1 + jitter)
+    pts["idepth_max"] = idp * np.float32(1 + spread) * (1 + jitter)
+    pts["energy_th"] = np.float32(8 * 144)
+    pts["color"] = pd[:, 8:16]
+    pts["weights"] = pd[:, 16:24]
+    pts["host"] = w.point_host
+    pts["quality"] = 10000
+    return pts

@@ -67,6 +67,7 @@ def lib():
             "oracle_ct_calc_res": (C.c_int, [C.c_int, C.c_int, C.c_int, f32p, f32p, C.c_int, f32p, f32p, f32p, f32p,
                                              f64p, f64p, C.c_float, f64p, f32p, i32p]),
             "oracle_ct_calc_gs": (C.c_int, [C.c_int, f32p, C.c_float, C.c_float, f64p, f64p, f64p]),
+            "oracle_activate_points": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]),
             "oracle_ip_make": (None, [f32p, C.c_int, C.c_int, C.c_int, f32p, C.c_float, C.c_int, C.c_void_p]),
             "oracle_ip_trace": (None, [f32p, C.c_int, C.c_int, f32p, f32p, f32p, C.c_int, C.c_void_p, i32p]),
         }
@@ -186,6 +187,14 @@ class OracleWindow:
         assert rc == 0
         return H, b
 
+    def activate_points(self, pts, min_obs=1):
+        """FullSystem::optimizeImmaturePoint for immature-point records of this window."""
+        assert pts.dtype == IMMATURE_DTYPE and pts.flags.c_contiguous
+        out = np.zeros(pts.size, ACTIVATION_DTYPE)
+        rc = lib().oracle_activate_points(self._h, int(pts.size), pts.ctypes.data, int(min_obs), out.ctypes.data)
+        assert rc == 0
+        return out
+
     def time_iterations(self, iters: int) -> float:
         return float(lib().oracle_time_iterations(self._h, int(iters)))
 
@@ -285,6 +294,7 @@ IMMATURE_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("idepth_min", "<f4"), ("
                            ("last_status", "<i4"), ("last_uv", "<f4", (2,)), ("last_interval", "<f4"),
                            ("type", "<f4")])
 assert IMMATURE_DTYPE.itemsize == 128
+ACTIVATION_DTYPE = np.dtype([("idepth", "<f4"), ("status", "<i4"), ("in_mask", "<u4"), ("energy", "<f4")])
 
 
 def ip_make(dI0, w, h, uv, type_=1.0, host=0):

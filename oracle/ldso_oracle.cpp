@@ -1896,4 +1896,154 @@ double oracle_time_iterations(oracle_window *ow, int iters) {
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+
+// ---- point activation ------------------------------------------------
+// ImmaturePoint::linearizeResidual (ImmaturePoint.cc:319-389) with projectPoint / derive_idepth
+// (ResidualProjections.h:12-18, 57-84), inside FullSystem::optimizeImmaturePoint
+// (FullSystem.cc:1035-1156): residuals to every other frame in window order.
+namespace {
+struct IpTmpRes {  // ImmaturePointTemporaryResidual (ImmaturePoint.h:18-26)
+    int state_state;
+    double state_energy;
+    int state_NewState;
+    double state_NewEnergy;
+    int target;
+};
+double ip_linearize_residual(const oracle_window *ow, const ldso_ct_immature &ip, int host, float outlierTHSlack,
+                             IpTmpRes &r, float &Hdd, float &bd, float idepth) {
+    if (r.state_state == OOB) {
+        r.state_NewState = OOB;
+        return r.state_energy;
+    }
+    const int N = ow->N;
+    const float *pre = ow->precalc.data() + (size_t)(host + N * r.target) * LDSO_BA_PRECALC_STRIDE;
+    const float *R = pre + 12, *t = pre + 21;  // PRE_RTll, PRE_tTll
+    const float aff0 = pre[24], aff1 = pre[25];  // PRE_aff_mode
+    const float *dIl = ow->dI.data() + (size_t)r.target * ow->w * ow->h * 3;
+    float energyLeft = 0;
+    for (int idx = 0; idx < patternNum; idx++) {
+        const int dx = patternP[idx][0], dy = patternP[idx][1];
+        const float K0 = (ip.u + dx - ow->cxl()) * ow->fxli(), K1 = (ip.v + dy - ow->cyl()) * ow->fyli();
+        float ptp[3];
+        for (int i = 0; i < 3; i++) ptp[i] = (R[3 * i] * K0 + R[3 * i + 1] * K1 + R[3 * i + 2] * 1.0f) + t[i] * idepth;
+        const float drescale = 1.0f / ptp[2];
+        if (!(drescale > 0)) {
+            r.state_NewState = OOB;
+            return r.state_energy;
+        }
+        const float u = ptp[0] * drescale, v = ptp[1] * drescale;
+        const float Ku = u * ow->fxl() + ow->cxl(), Kv = v * ow->fyl() + ow->cyl();
+        if (!(Ku > 1.1f && Kv > 1.1f && Ku < ow->wM3G && Kv < ow->hM3G)) {
+            r.state_NewState = OOB;
+            return r.state_energy;
+        }
+        float hitColor[3];
+        interp33(dIl, Ku, Kv, ow->w, hitColor);
+        if (!std::isfinite(hitColor[0])) {
+            r.state_NewState = OOB;
+            return r.state_energy;
+        }
+        const float residual = hitColor[0] - (aff0 * ip.color[idx] + aff1);
+        float hw = std::fabs(residual) < setting_huberTH ? 1 : setting_huberTH / std::fabs(residual);
+        energyLeft += ip.weights[idx] * ip.weights[idx] * hw * residual * residual * (2 - hw);
+        const float dxInterp = hitColor[1] * ow->fxl();
+        const float dyInterp = hitColor[2] * ow->fyl();
+        const float d_idepth = (dxInterp * drescale * (t[0] - t[2] * u) + dyInterp * drescale * (t[1] - t[2] * v)) * 1.0f;
+        hw *= ip.weights[idx] * ip.weights[idx];
+        Hdd += (hw * d_idepth) * d_idepth;
+        bd += (hw * residual) * d_idepth;
+    }
+    if (energyLeft > ip.energy_th * outlierTHSlack) {
+        energyLeft = ip.energy_th * outlierTHSlack;
+        r.state_NewState = OUTLIER;
+    } else {
+        r.state_NewState = IN;
+    }
+    r.state_NewEnergy = energyLeft;
+    return energyLeft;
+}
+}  // namespace
+
+int oracle_activate_points(oracle_window *ow, int n, const ldso_ct_immature *pts, int min_obs,
+                           ldso_ba_activation *out) {
+    constexpr float setting_minIdepthH_act = 100;    // Setting.cc:25
+    constexpr int setting_GNItsOnPointActivation = 3;  // Setting.cc:47
+    const int N = ow->N;
+    for (int k = 0; k < n; k++) {
+        const ldso_ct_immature &ip = pts[k];
+        ldso_ba_activation &o = out[k];
+        const int host = ip.host;
+        if (host < 0 || host >= N) return -1;
+        IpTmpRes res[LDSO_BA_MAX_FRAMES];
+        int nres = 0;
+        for (int f = 0; f < N; f++)
+            if (f != host) res[nres++] = IpTmpRes{IN, 0.0, OUTLIER, 0.0, f};
+        float lastEnergy = 0, lastHdd = 0, lastbd = 0;
+        float currentIdepth = (ip.idepth_max + ip.idepth_min) * 0.5f;
+        o.status = 0;
+        o.in_mask = 0;
+        for (int i = 0; i < nres; i++) {
+            lastEnergy += ip_linearize_residual(ow, ip, host, 1000, res[i], lastHdd, lastbd, currentIdepth);
+            res[i].state_state = res[i].state_NewState;
+            res[i].state_energy = res[i].state_NewEnergy;
+        }
+        o.energy = lastEnergy;
+        o.idepth = currentIdepth;
+        if (!std::isfinite(lastEnergy) || lastHdd < setting_minIdepthH_act) {
+            o.status = 2;
+            continue;
+        }
+        float lambda = 0.1f;
+        bool zero = false;
+        for (int iteration = 0; iteration < setting_GNItsOnPointActivation; iteration++) {
+            float H = lastHdd;
+            H *= 1 + lambda;
+            const float step = (1.0 / H) * lastbd;
+            const float newIdepth = currentIdepth - step;
+            float newHdd = 0, newbd = 0, newEnergy = 0;
+            for (int i = 0; i < nres; i++)
+                newEnergy += ip_linearize_residual(ow, ip, host, 1, res[i], newHdd, newbd, newIdepth);
+            if (!std::isfinite(lastEnergy) || newHdd < setting_minIdepthH_act) {
+                zero = true;
+                break;
+            }
+            if (newEnergy < lastEnergy) {
+                currentIdepth = newIdepth;
+                lastHdd = newHdd;
+                lastbd = newbd;
+                lastEnergy = newEnergy;
+                for (int i = 0; i < nres; i++) {
+                    res[i].state_state = res[i].state_NewState;
+                    res[i].state_energy = res[i].state_NewEnergy;
+                }
+                lambda *= 0.5;
+            } else {
+                lambda *= 5;
+            }
+            if (std::fabs(step) < 0.0001 * currentIdepth) break;
+        }
+        o.energy = lastEnergy;
+        o.idepth = currentIdepth;
+        if (zero) {
+            o.status = 2;
+            continue;
+        }
+        if (!std::isfinite(currentIdepth)) {
+            o.status = 1;
+            continue;
+        }
+        int numGoodRes = 0;
+        for (int i = 0; i < nres; i++)
+            if (res[i].state_state == IN) {
+                numGoodRes++;
+                o.in_mask |= 1u << res[i].target;
+            }
+        if (numGoodRes < min_obs) {
+            o.status = 1;
+            o.in_mask = 0;
+        }
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -102,6 +102,10 @@ void oracle_ip_make(const float *dI, int w, int h, int n, const float *uv, float
 void oracle_ip_trace(const float *dI, int w, int h, const float *krki, const float *kt, const float *aff, int n,
                      ldso_ct_immature *pts, int *counts);
 
+/* FullSystem::optimizeImmaturePoint for n immature points hosted in the window (pts[k].host) */
+int oracle_activate_points(oracle_window *ow, int n, const ldso_ct_immature *pts, int min_obs,
+                           ldso_ba_activation *out);
+
 /* CPU-baseline timing: run `iters` oracle_iteration passes, return wall seconds. */
 double oracle_time_iterations(oracle_window *ow, int iters);
 
