@@ -373,7 +373,8 @@ __global__ __launch_bounds__(kCtThreads) void k_ct_make_immature(const float4 *_
 }
 
 struct TraceParams {
-    const float4 *__restrict__ dI;  // level 0 [I, dx, dy, |g|^2]
+    const float4 *__restrict__ dI;  // level 0 [I, dx, dy, |g|^2] (GN taps)
+    const float *__restrict__ inten;  // level 0 intensities, = dI[].x (discrete-search taps: 4 B, not 16)
     const float *__restrict__ hosts;  // [n_hosts][kHostStride]
     IpRec *pts;
     int n, w, h;
@@ -389,12 +390,11 @@ __device__ __forceinline__ void ip_finish(IpRec *q, int status, float u, float v
 }
 
 // getInterpolatedElement31 (GlobalFuncs.h:146-159)
-__device__ __forceinline__ float interp31(const float4 *__restrict__ dI, float x, float y, int w, int h) {
+__device__ __forceinline__ float interp31(const float *__restrict__ I, float x, float y, int w, int h) {
     float dx, dy;
     const int b = ip_base(x, y, w, h, dx, dy);
     const float dxdy = dx * dy;
-    return dxdy * dI[b + 1 + w].x + (dy - dxdy) * dI[b + w].x + (dx - dxdy) * dI[b + 1].x +
-           (1 - dx - dy + dxdy) * dI[b].x;
+    return dxdy * I[b + 1 + w] + (dy - dxdy) * I[b + w] + (dx - dxdy) * I[b + 1] + (1 - dx - dy + dxdy) * I[b];
 }
 
 // one wavefront per immature point; every branch before the search is wave-uniform
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(kCtThreads) void k_ct_trace(TraceParams P) {
         float energy = 0;
 #pragma unroll
         for (int idx = 0; idx < 8; idx++) {
-            const float hitColor = interp31(P.dI, (float)(ptx + rpx[idx]), (float)(pty + rpy[idx]), w, h);
+            const float hitColor = interp31(P.inten, (float)(ptx + rpx[idx]), (float)(pty + rpy[idx]), w, h);
             if (!isfinite(hitColor)) {
                 energy += 1e5f;
                 continue;
@@ -1253,7 +1253,7 @@ int ldso_ct_trace(ldso_ct_ctx *c, int32_t n_hosts, const float *krki, const floa
                               hipMemcpyHostToDevice, c->stream));
     const int n = c->ip_n;
     if (n > 0) {
-        TraceParams P{c->d_dIp, c->d_hosts, c->d_ip, n, c->pyr.w, c->pyr.h};
+        TraceParams P{c->d_dIp, c->d_inten, c->d_hosts, c->d_ip, n, c->pyr.w, c->pyr.h};
         const int per = kCtThreads / kWave;
         int rc = ct_launch(c, 5, [&] { k_ct_trace<<<(n + per - 1) / per, kCtThreads, 0, c->stream>>>(P); });
         if (rc) return rc;
