@@ -39,12 +39,12 @@
 extern "C" {
 #endif
 
-#define LDSO_BA_ABI_VERSION 1
+#define LDSO_BA_ABI_VERSION 2
 
 #define LDSO_BA_PATTERN_NUM 8      /* patternNum, Settings.h:225 (staticPattern[8])     */
 #define LDSO_BA_CPARS 4            /* CPARS, NumTypes.h:25                              */
 #define LDSO_BA_MAX_FRAMES 16      /* window size supported by one context              */
-#define LDSO_BA_PRECALC_STRIDE 32  /* floats per FrameFramePrecalc record (see below)   */
+#define LDSO_BA_PRECALC_STRIDE 48  /* floats per FrameFramePrecalc record (see below)   */
 #define LDSO_BA_POINT_STRIDE 24    /* floats per PointHessian record (see below)        */
 
 /* Residual states, Residuals.h:33 */
@@ -60,7 +60,11 @@ extern "C" {
  * FrameFramePrecalc record (FrameFramePrecalc.h:35-44), LDSO_BA_PRECALC_STRIDE floats:
  *   [0..8]  PRE_KRKiTll (3x3 row-major)   [9..11]  PRE_KtTll
  *   [12..20] PRE_RTll_0 (3x3 row-major)   [21..23] PRE_tTll_0
- *   [24..25] PRE_aff_mode                 [26]     PRE_b0_mode      [27..31] unused
+ *   [24..25] PRE_aff_mode                 [26]     PRE_b0_mode
+ *   [27..35] PRE_RTll (3x3 row-major)     [36..38] PRE_tTll        [39..47] unused
+ * PRE_RTll_0 / PRE_tTll_0 come from the evaluation points (worldToCam_evalPT) and feed the FEJ
+ * Jacobians of PointFrameResidual::linearize; PRE_RTll / PRE_tTll come from the current poses
+ * (PRE_worldToCam) and feed ImmaturePoint::linearizeResidual (ImmaturePoint.cc:336-337).
  *
  * PointHessian record (PointHessian.h:83-131), LDSO_BA_POINT_STRIDE floats:
  *   [0] u  [1] v  [2] idepth_scaled  [3] idepth_zero_scaled  [4] priorF  [5] deltaF

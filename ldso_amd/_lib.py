@@ -19,7 +19,7 @@ SYNTH_PATH = os.path.join(LIB_DIR, "libldso_synth.so")
 PATTERN_NUM = 8
 CPARS = 4
 MAX_FRAMES = 16
-PRECALC_STRIDE = 32
+PRECALC_STRIDE = 48
 POINT_STRIDE = 24
 RES_IN, RES_OOB, RES_OUTLIER = 0, 1, 2
 FLAG_ACTIVE, FLAG_NEW = 1, 2

@@ -163,12 +163,12 @@ int frame_precalc(int N, const ldso_ba_frame_state *fr, const float calib[4], fl
             const Pose l = cur[t] * curInvH;  // leftToLeft
             float R[9], tt[3];
             for (int k = 0; k < 9; k++) {
-                o[12 + k] = (float)l0.R.m[k];
-                R[k] = (float)l.R.m[k];
+                o[12 + k] = (float)l0.R.m[k];  // PRE_RTll_0
+                o[27 + k] = R[k] = (float)l.R.m[k];  // PRE_RTll
             }
             for (int k = 0; k < 3; k++) {
-                o[21 + k] = (float)l0.t[k];
-                tt[k] = (float)l.t[k];
+                o[21 + k] = (float)l0.t[k];  // PRE_tTll_0
+                o[36 + k] = tt[k] = (float)l.t[k];  // PRE_tTll
             }
             float KR[9];
             for (int r = 0; r < 3; r++)

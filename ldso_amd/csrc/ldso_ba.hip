@@ -2315,9 +2315,9 @@ __global__ __launch_bounds__(256) void k_activate(ActParams P) {
     const float4 *img = P.img + (size_t)(W.frame_base + tgt) * P.frame_stride;
     float R[9], t[3];
 #pragma unroll
-    for (int i = 0; i < 9; i++) R[i] = pre[12 + i];
+    for (int i = 0; i < 9; i++) R[i] = pre[27 + i];  // PRE_RTll (current poses, ImmaturePoint.cc:336-337)
 #pragma unroll
-    for (int i = 0; i < 3; i++) t[i] = pre[21 + i];
+    for (int i = 0; i < 3; i++) t[i] = pre[36 + i];  // PRE_tTll
     const float aff0 = pre[24], aff1 = pre[25];
     float col[8], wsq[8];
 #pragma unroll
@@ -2629,13 +2629,14 @@ struct DevBuf {
     int alloc(size_t count) {
         if (p) (void)hipFree(p);
         p = nullptr;
-        n = count;
+        n = 0;
         if (count == 0) return 0;
         hipError_t e = hipMalloc(&p, count * sizeof(T));
         if (e != hipSuccess) {
             p = nullptr;
             return fail(-3, std::string("hipMalloc failed: ") + hipGetErrorString(e));
         }
+        n = count;  // only a successful allocation counts as capacity
         return 0;
     }
     void release() {
@@ -3691,7 +3692,7 @@ int ldso_ba_activate_points(ldso_ba_ctx *c, int32_t win, int32_t n, const ldso_c
         if (pts[k].host < 0 || pts[k].host >= N) return fail(-1, "immature point host index outside the window");
     if (n == 0) return 0;
     HIP_TRY(hipSetDevice(c->device));
-    if ((size_t)n > c->d_act_in.n) {
+    if ((size_t)n > c->d_act_in.n || (size_t)n > c->d_act_out.n || !c->d_act_in.p || !c->d_act_out.p) {
         int rc = c->d_act_in.alloc(n);
         if (!rc) rc = c->d_act_out.alloc(n);
         if (rc) return rc;

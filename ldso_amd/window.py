@@ -33,7 +33,7 @@ class Window:
     res_state: np.ndarray             # i8[R]
     res_energy: np.ndarray            # f32[R]
     res_flags: np.ndarray             # u8[R]
-    precalc: np.ndarray = None        # f32[N*N, 32]
+    precalc: np.ndarray = None        # f32[N*N, LDSO_BA_PRECALC_STRIDE]
     ad_host: np.ndarray = None        # f64[N*N, 64]
     ad_target: np.ndarray = None      # f64[N*N, 64]
     c_prior: np.ndarray = None        # f64[4]

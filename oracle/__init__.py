@@ -214,7 +214,7 @@ def frame_terms(window):
     """Oracle restatement of FrameFramePrecalc::Set / setAdjointsF / takeData / nullspaces."""
     N = window.n_frames
     fr = np.ascontiguousarray(window.frames)
-    pre = np.zeros((N * N, 32), np.float32)
+    pre = np.zeros((N * N, 48), np.float32)  # LDSO_BA_PRECALC_STRIDE
     lib().oracle_frame_precalc(N, fr.ctypes.data, _p(np.ascontiguousarray(window.calib, np.float32), f32p), _p(pre, f32p))
     adH = np.zeros((N * N, 64))
     adT = np.zeros((N * N, 64))

@@ -1674,12 +1674,12 @@ int oracle_frame_precalc(int N, const ldso_ba_frame_state *frames, const float c
             SE3d l2l = se3_mul(frame_pre_w2c(frames[t]), se3_inv(frame_pre_w2c(frames[h])));
             float RTll[9], tTll[3];
             for (int i = 0; i < 9; i++) {
-                o[12 + i] = (float)l2l0.R[i];
-                RTll[i] = (float)l2l.R[i];
+                o[12 + i] = (float)l2l0.R[i];          // PRE_RTll_0
+                o[27 + i] = RTll[i] = (float)l2l.R[i];  // PRE_RTll
             }
             for (int i = 0; i < 3; i++) {
-                o[21 + i] = (float)l2l0.t[i];
-                tTll[i] = (float)l2l.t[i];
+                o[21 + i] = (float)l2l0.t[i];          // PRE_tTll_0
+                o[36 + i] = tTll[i] = (float)l2l.t[i];  // PRE_tTll
             }
             float K[9] = {calib[0], 0, calib[2], 0, calib[1], calib[3], 0, 0, 1};
             // K.inverse(): Eigen's 3x3 cofactor inverse (Eigen/src/LU/InverseImpl.h,
@@ -1917,7 +1917,7 @@ double ip_linearize_residual(const oracle_window *ow, const ldso_ct_immature &ip
     }
     const int N = ow->N;
     const float *pre = ow->precalc.data() + (size_t)(host + N * r.target) * LDSO_BA_PRECALC_STRIDE;
-    const float *R = pre + 12, *t = pre + 21;  // PRE_RTll, PRE_tTll
+    const float *R = pre + 27, *t = pre + 36;  // PRE_RTll, PRE_tTll (current poses, ImmaturePoint.cc:336-337)
     const float aff0 = pre[24], aff1 = pre[25];  // PRE_aff_mode
     const float *dIl = ow->dI.data() + (size_t)r.target * ow->w * ow->h * 3;
     float energyLeft = 0;

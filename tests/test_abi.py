@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(built):
     bound = {name for name, _, _ in L.ABI}
     assert set(syms) == bound, set(syms) ^ bound
     lib = L.lib()
-    assert lib.ldso_ba_abi_version() == 1
+    assert lib.ldso_ba_abi_version() == 2
     assert lib.ldso_ba_num_kernels() >= 3
 
 
@@ -198,3 +198,41 @@ def test_product_solver_projection_known_answer(built, degenerate):
     xr = x0 - Nm @ (np.linalg.pinv(Nm, rcond=1e-10) @ x0)
     assert np.linalg.norm(x2 - xr) <= 1e-9 * np.linalg.norm(x0)
     assert np.abs(Nm.T @ x2).max() <= 1e-9 * np.linalg.norm(x0)
+
+
+def test_precalc_current_pose_rotation_known_answer(built):
+    """FrameFramePrecalc::Set (FrameFramePrecalc.cc:12-19): PRE_RTll / PRE_tTll (record slots
+    27..38) come from the CURRENT poses PRE_worldToCam = exp(scaled state) * evalPT, while
+    PRE_RTll_0 / PRE_tTll_0 (slots 12..23) come from the evaluation points.  A non-newest frame
+    is moved away from its state_zero and the record is checked against the relative poses
+    rebuilt here in numpy (ImmaturePoint::linearizeResidual reads slots 27..38)."""
+    from ldso_amd.synth import se3_matrix
+
+    w = synth.make_window(n_frames=5, n_points=50, width=160, height=120, seed=4)
+    fr = w.frames
+    fr["state"][2, :6] = [0.02, -0.01, 0.03, 0.004, -0.006, 0.002]  # frame 2 is not the newest
+    w.refresh_frame_terms()
+    N = w.n_frames
+
+    def pose(f, current):
+        T = np.eye(4)
+        T[:3, :3] = fr["world_to_cam_evalpt"][f][:9].reshape(3, 3)
+        T[:3, 3] = fr["world_to_cam_evalpt"][f][9:]
+        if current:
+            s = fr["state"][f]
+            E = np.eye(4)
+            E[:3] = se3_matrix(s[3:6] * 1.0, s[0:3] * 0.5)  # SCALE_XI_ROT = 1, SCALE_XI_TRANS = 0.5
+            T = E @ T
+        return T
+
+    for h in range(N):
+        for t in range(N):
+            rec = w.precalc[h + N * t]
+            for current, (ro, to) in ((True, (27, 36)), (False, (12, 21))):
+                L2L = pose(t, current) @ np.linalg.inv(pose(h, current))
+                np.testing.assert_allclose(rec[ro:ro + 9], L2L[:3, :3].ravel(), rtol=0, atol=1e-6)
+                np.testing.assert_allclose(rec[to:to + 3], L2L[:3, 3], rtol=0, atol=1e-6)
+    # the moved frame's pairs differ between the two pose sets, frame 0 <-> 1 (both at their
+    # evaluation points) does not
+    assert not np.array_equal(w.precalc[2 + N * 0][27:36], w.precalc[2 + N * 0][12:21])
+    np.testing.assert_array_equal(w.precalc[0 + N * 1][27:39], w.precalc[0 + N * 1][12:24])
