@@ -300,43 +300,23 @@ int ldso_ba_iterate(ldso_ba_ctx *ctx, int32_t iteration, double lambda, const do
 int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
 
 /* Tuning knobs (defaults are the measured best):
- *   LDSO_BA_TUNE_LIN_VARIANT   k_linearize form: 1 or 2 = lane per residual (occupancy target in
- *                              waves per SIMD), 3 = sample-parallel (8 lanes per residual)
- *   LDSO_BA_TUNE_TILED_IMAGES  frame layout: 0 row-major [I,dx,dy,0] texels, 1 2x4-texel tiles,
- *                              2 one 64-B bilinear quad record per pixel (needs LIN_VARIANT 3);
- *                              set before ldso_ba_load
- *   LDSO_BA_TUNE_LOAD3         texel loads as dwordx3 (1) or dwordx4 (0)
- *   LDSO_BA_TUNE_XCD_REMAP     XCD-contiguous block->chunk mapping in k_linearize (1) or not
- *   LDSO_BA_TUNE_CENTRE_FIRST  centre projection before the pattern gathers (1, reference order)
- *                              or after them (0)
+ *   LDSO_BA_TUNE_TILED_IMAGES  frame layout: 3 (default) intensity only, band-interleaved, the
+ *                              gradients recomputed with makeImages' rule (falls back to 1 when the
+ *                              caller's dI gradients are not makeImages'); 1 [I, dx, dy, 0]
+ *                              texels in 2x4 tiles; set before ldso_ba_load
  *   LDSO_BA_TUNE_TOP_CHUNK     residuals per k_linearize wavefront: 16, 32, 64, or 0 = automatic
  *                              (64 for large batches, shorter for a single window); set before
  *                              ldso_ba_load
  *   LDSO_BA_TUNE_TIMING_MASK   bit i: bracket kernel slot i with events when timing is enabled
  *                              (default all; each event pair costs the stream a few us)
- *   LDSO_BA_TUNE_PIPELINE_GROUPS  window groups pipelined over two streams in a pass (one group's
- *                              k_point_sc/k_stitch overlap the next group's k_linearize);
- *                              0 = default 1 (measured: 2/4/8 groups are 15-60% slower)
- *   LDSO_BA_TUNE_STITCH_SPLIT  1: with one group, k_stitch's Top half and the frame threshold run
- *                              on a second stream beside k_point_sc; 0 (default; measured: the
- *                              split pass is 3% slower, 188 vs 182 us on 64 x S7): one k_stitch
  *   LDSO_BA_TUNE_ITEM_ORDER    k_linearize chunk order: 0 (default) target-major, 1 host-major;
  *                              set before ldso_ba_load
- *   LDSO_BA_TUNE_FUSED         1: point-major k_linearize that also runs the point's Schur term
- *                              (k_point_sc folded in, records kept in LDS); 0 (default; measured:
- *                              the fused pass is 4% slower, 189 vs 182 us on 64 x S7): chunk-major
- *                              k_linearize + k_point_sc; set before ldso_ba_load */
-#define LDSO_BA_TUNE_LIN_VARIANT 1
+ * Keys 1, 3, 4, 5, 8, 9 and 11 named experiment variants that measured slower and were removed
+ * (DESIGN.md §5 keeps their numbers); setting them returns -1. */
 #define LDSO_BA_TUNE_TILED_IMAGES 2
-#define LDSO_BA_TUNE_LOAD3 3
-#define LDSO_BA_TUNE_XCD_REMAP 4
-#define LDSO_BA_TUNE_CENTRE_FIRST 5
 #define LDSO_BA_TUNE_TOP_CHUNK 6
 #define LDSO_BA_TUNE_TIMING_MASK 7
-#define LDSO_BA_TUNE_PIPELINE_GROUPS 8
-#define LDSO_BA_TUNE_STITCH_SPLIT 9
 #define LDSO_BA_TUNE_ITEM_ORDER 10
-#define LDSO_BA_TUNE_FUSED 11
 int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);

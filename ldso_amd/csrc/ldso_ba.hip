@@ -3,14 +3,14 @@
 // One Gauss-Newton pass over every loaded window (ldso_ba_linearize) is three stream-ordered
 // launches plus a memset of the packed systems:
 //
-//   k_linearize   lane per PointFrameResidual, one wavefront per 64-residual chunk of one
-//                 (host,target) bucket.  linearize (Residuals.cc:15-217) + applyRes
-//                 (Residuals.h:70-88) + the per-residual AccumulatorApprox terms
-//                 (AccumulatedTopHessian.cc:66-99, MatrixAccumulators.h:893-1045) reduced across
-//                 the wavefront into a 96-float partial per chunk.  The pair precalc, frame
-//                 thresholds and image base are wave-uniform (scalar loads); the vector traffic is
-//                 the point record and the 32 bilinear taps per residual into 2x4-texel tiled
-//                 [I, dx, dy, 0] frames.
+//   k_linearize   one wavefront per <= 64-residual chunk of one (host,target) bucket: linearize
+//                 (Residuals.cc:15-217) with 8 lanes per residual (one per pattern pixel),
+//                 applyRes (Residuals.h:70-88) with a lane per residual, and the chunk's
+//                 AccumulatorApprox block (AccumulatedTopHessian.cc:66-99,
+//                 MatrixAccumulators.h:893-1045) as 32 fp32 MFMAs into a 96-float partial.  The
+//                 pair precalc, frame thresholds and image base are wave-uniform (scalar loads);
+//                 the vector traffic is the point record and 12 intensity taps per pattern pixel
+//                 from band-interleaved frames (band_offset) via buffer loads.
 //   k_point_sc    per point: Hdd/bd/Hcd sums (AccumulatedTopHessian.cc:94-116), HdiF
 //                 (AccumulatedSCHessian.cc:24-33); then the Schur terms of a 64-point chunk of one
 //                 host as one symmetric rank-64 update G += U^T diag(HdiF) U staged in LDS (the
@@ -99,7 +99,7 @@ __host__ __device__ inline long long sys_len(int D) { return 2 * (packed_len(D) 
 struct LinParams {
     const int4 *__restrict__ items;  // {res_begin, count, pair_global, win}
     const WinDev *__restrict__ wins;
-    const float4 *__restrict__ img;  // [I, dx, dy, 0] texels, 2x4-texel tiles (see tex())
+    const float4 *__restrict__ img;  // frames: layout 3 (band_offset) or layout 1 (tex())
     const float *__restrict__ precalc;
     const float *__restrict__ frame_th;
     const int *__restrict__ rs_point;
@@ -118,21 +118,12 @@ struct LinParams {
     int n_items;             // chunks of this launch: [item_base, item_base + n_items)
     int item_base;
     int n_blocks;
-    long long frame_stride;  // texels per tiled frame
-    int tiles_per_row;       // 2-wide tiles per tile row
+    long long frame_stride;  // float4 units per frame
+    int tiles_per_row;       // layout 3: 8-pixel tiles per row; layout 1: 2-texel tiles per row
     int fix;
     int accumulate;
     const float *ad_ht_delta;  // [pair_global][8] EnergyFunctional::adHTdeltaF (marginalisation pass)
-    // fused (point-major) pass: one workgroup per 32-point block of one host, wave w holding the
-    // block's residuals to target slots 2w and 2w+1; the SC half of k_point_sc runs in the block
-    const int4 *__restrict__ pblocks;  // {first point (global), points, first half, window}
-    const int *__restrict__ pt_nres;
-    const unsigned long long *__restrict__ pt_tgt;
-    float *pt_out;                     // [P][12]
-    float *sc_slab;
-    int shift_prior;                   // AccumulatedSCHessianSSE::addPoint's shiftPriorToZero
 };
-constexpr int kFusedPts = 32;  // points per fused workgroup (two target slots per wavefront)
 
 struct Geo {
     float Ku, Kv, new_idepth;
@@ -199,99 +190,67 @@ struct PhotoSums {
     float JI_r0, JI_r1, Jab_r0, Jab_r1, rr;  // AccumulatedTopHessian.cc:69-77 (mode 0: resApprox = resF)
 };
 
-// Image texel fetch.  Frames live in HBM as FrameHessian::dI texels [I, dx, dy, 0] (16 B),
-// tiled 2 (x) by 4 (y) texels per 128-byte line: the 8-pixel pattern's 32 bilinear taps then
-// touch ~6.3 lines per residual instead of ~8.1 for row-major (tools/ measurements).
-template <bool kTiled, bool kLoad3>
+// Image layout 1 texel fetch: FrameHessian::dI texels [I, dx, dy, 0] (16 B) tiled 2 (x) by 4 (y)
+// per 128-byte line.  Used when the caller's gradients are not makeImages' (layout 3 would then
+// not reproduce them) and by k_activate on such frames.
 __device__ inline float3 tex(const float4 *__restrict__ img, int tpr2, int x, int y) {
-    const int idx = kTiled ? (((y >> 2) * tpr2 + (x >> 1)) << 3) + ((y & 3) << 1) + (x & 1) : y * (tpr2 * 2) + x;
-    if constexpr (kLoad3) {
-        return *reinterpret_cast<const float3 *>(img + idx);  // dwordx3: pad never loaded
-    } else {
-        const float4 v = img[idx];
-        return make_float3(v.x, v.y, v.z);
-    }
+    const float4 v = img[(((y >> 2) * tpr2 + (x >> 1)) << 3) + ((y & 3) << 1) + (x & 1)];
+    return make_float3(v.x, v.y, v.z);
 }
 
-// Pattern loop of Residuals.cc:128-190 with getInterpolatedElement33 (GlobalFuncs.h:89-103).
-// The JI_r / Jab_r / rr sums of the Top accumulation are folded into the same loop (same
-// order, so identical rounding to summing the stored J afterwards).
-template <bool kTiled, bool kLoad3>
-__device__ inline bool pattern_loop(const float *__restrict__ pre, const float4 *__restrict__ img, int tpr2,
-                                    float wM3, float hM3, float u, float v, float ids,
-                                    const float *__restrict__ color, const float *__restrict__ weights,
-                                    PhotoSums &s) {
+// Image layout 3 (default): the intensity channel only, in bands of 4 rows stored column by
+// column, i.e. byte offset (y >> 2) * band + 16 x + 4 (y & 3) with band = 16 * padded width.
+// A 128-byte line is an 8 x 4 pixel tile, and the four taps of one row of a pixel's
+// neighbourhood are 16 B apart, so one row offset serves all of them (immediate offsets).
+__device__ __forceinline__ unsigned band_offset(int x, int y, unsigned band) {
+    return ((unsigned)y >> 2) * band + ((unsigned)x << 4) + (((unsigned)y & 3u) << 2);
+}
+__device__ __forceinline__ float ldb(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const float *base, long long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// makeImages' gradient rule (FrameHessian.cc:96-101): 0.5 (a - b), zeroed when NaN or |d| > 255
+// (one compare: NaN fails it too)
+__device__ __forceinline__ float make_grad(float a, float b) {
 #pragma clang fp contract(off)
-    constexpr int pat[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};
-    const float aff0 = pre[24], aff1 = pre[25], b0 = pre[26];
-    s.energy = s.wJI2 = 0;
-    s.JIdx2_00 = s.JIdx2_10 = s.JIdx2_11 = 0;
-    s.JabJIdx_00 = s.JabJIdx_01 = s.JabJIdx_10 = s.JabJIdx_11 = 0;
-    s.Jab2_00 = s.Jab2_01 = s.Jab2_11 = 0;
-    s.JI_r0 = s.JI_r1 = s.Jab_r0 = s.Jab_r1 = s.rr = 0;
-    // all eight projections first: any OOB pattern pixel makes the residual OOB
-    float Kus[8], Kvs[8];
-    bool ok = true;
-#pragma unroll
-    for (int idx = 0; idx < 8; idx++) {
-        const float up = u + pat[idx][0], vp = v + pat[idx][1];
-        float ptp[3];
-#pragma unroll
-        for (int i = 0; i < 3; i++) ptp[i] = (pre[3 * i] * up + pre[3 * i + 1] * vp + pre[3 * i + 2] * 1.0f) + pre[9 + i] * ids;
-        Kus[idx] = ptp[0] / ptp[2];
-        Kvs[idx] = ptp[1] / ptp[2];
-        ok = ok && (Kus[idx] > 1.1f && Kvs[idx] > 1.1f && Kus[idx] < wM3 && Kvs[idx] < hM3);
-    }
-    if (!ok) return false;
-    float3 t00[8], t10[8], t01[8], t11[8];
-#pragma unroll
-    for (int idx = 0; idx < 8; idx++) {  // issue all 32 texel loads before any use
-        const int ix = (int)Kus[idx], iy = (int)Kvs[idx];
-        t00[idx] = tex<kTiled, kLoad3>(img, tpr2, ix, iy);
-        t10[idx] = tex<kTiled, kLoad3>(img, tpr2, ix + 1, iy);
-        t01[idx] = tex<kTiled, kLoad3>(img, tpr2, ix, iy + 1);
-        t11[idx] = tex<kTiled, kLoad3>(img, tpr2, ix + 1, iy + 1);
-    }
-#pragma unroll
-    for (int idx = 0; idx < 8; idx++) {
-        const int ix = (int)Kus[idx], iy = (int)Kvs[idx];
-        const float dx = Kus[idx] - ix, dy = Kvs[idx] - iy, dxdy = dx * dy;
-        const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
-        const float I = w11 * t11[idx].x + w01 * t01[idx].x + w10 * t10[idx].x + w00 * t00[idx].x;
-        float gx = w11 * t11[idx].y + w01 * t01[idx].y + w10 * t10[idx].y + w00 * t00[idx].y;
-        float gy = w11 * t11[idx].z + w01 * t01[idx].z + w10 * t10[idx].z + w00 * t00[idx].z;
-        const float residual = I - (float)(aff0 * color[idx] + aff1);
-        const float drdA = (color[idx] - b0);
-        if (!isfinite(I)) return false;
-        float wg = sqrtf(kOutlierTHSumComponent / (kOutlierTHSumComponent + (gx * gx + gy * gy)));
-        wg = 0.5f * (wg + weights[idx]);
-        float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
-        s.energy += wg * wg * hw * residual * residual * (2 - hw);
-        if (hw < 1) hw = sqrtf(hw);
-        hw = hw * wg;
-        gx *= hw;
-        gy *= hw;
-        const float resF = residual * hw;
-        const float jab0 = drdA * hw;
-        s.JIdx2_00 += gx * gx;
-        s.JIdx2_11 += gy * gy;
-        s.JIdx2_10 += gx * gy;
-        s.JabJIdx_00 += drdA * hw * gx;
-        s.JabJIdx_01 += drdA * hw * gy;
-        s.JabJIdx_10 += hw * gx;
-        s.JabJIdx_11 += hw * gy;
-        s.Jab2_00 += drdA * drdA * hw * hw;
-        s.Jab2_01 += drdA * hw * hw;
-        s.Jab2_11 += hw * hw;
-        s.wJI2 += hw * hw * (gx * gx + gy * gy);
-        // setting_affineOptModeA/B >= 0 (Setting.cc:65-66): JabF stays as computed
-        s.JI_r0 += resF * gx;
-        s.JI_r1 += resF * gy;
-        s.Jab_r0 += resF * jab0;
-        s.Jab_r1 += resF * hw;
-        s.rr += resF * resF;
-    }
-    return true;
+    const float d = 0.5f * (a - b);
+    return fabsf(d) <= 255.0f ? d : 0.0f;
+}
+
+// The 12 intensities a bilinear [I, dx, dy] sample at (ix + dx, iy + dy) needs, layout 3:
+// rows iy-1 (ix, ix+1), iy and iy+1 (ix-1 .. ix+2), iy+2 (ix, ix+1).
+__device__ __forceinline__ void load12(__amdgpu_buffer_rsrc_t r, unsigned band, int ix, int iy, float *iv) {
+    const unsigned o0 = band_offset(ix - 1, iy - 1, band), o1 = band_offset(ix - 1, iy, band),
+                   o2 = band_offset(ix - 1, iy + 1, band), o3 = band_offset(ix - 1, iy + 2, band);
+    iv[0] = ldb(r, o0 + 16);
+    iv[1] = ldb(r, o0 + 32);
+    iv[2] = ldb(r, o1);
+    iv[3] = ldb(r, o1 + 16);
+    iv[4] = ldb(r, o1 + 32);
+    iv[5] = ldb(r, o1 + 48);
+    iv[6] = ldb(r, o2);
+    iv[7] = ldb(r, o2 + 16);
+    iv[8] = ldb(r, o2 + 32);
+    iv[9] = ldb(r, o2 + 48);
+    iv[10] = ldb(r, o3 + 16);
+    iv[11] = ldb(r, o3 + 32);
+}
+// getInterpolatedElement33 (GlobalFuncs.h:89-103) from those 12 values with the gradients
+// recomputed; bit-identical to sampling the caller's dI when dI's gradients are makeImages'.
+__device__ __forceinline__ float3 bilin12(const float *v, float dx, float dy) {
+#pragma clang fp contract(off)
+    const float dxdy = dx * dy;
+    const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+    const float3 t00 = make_float3(v[3], make_grad(v[4], v[2]), make_grad(v[7], v[0]));
+    const float3 t10 = make_float3(v[4], make_grad(v[5], v[3]), make_grad(v[8], v[1]));
+    const float3 t01 = make_float3(v[7], make_grad(v[8], v[6]), make_grad(v[10], v[3]));
+    const float3 t11 = make_float3(v[8], make_grad(v[9], v[7]), make_grad(v[11], v[4]));
+    return make_float3(w11 * t11.x + w01 * t01.x + w10 * t10.x + w00 * t00.x,
+                       w11 * t11.y + w01 * t01.y + w10 * t10.y + w00 * t00.y,
+                       w11 * t11.z + w01 * t01.z + w10 * t10.z + w00 * t00.z);
 }
 
 // Point-side terms of AccumulatedTopHessian.cc:94-97 and takeData (Residuals.h:120-129).
@@ -326,303 +285,8 @@ __device__ __forceinline__ void write_record(float4 *rec, bool active, const Geo
         rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
-
-// Fused pass: the full record goes to LDS for the block's SC phase; global memory keeps what
-// k_resubstitute and ldso_ba_get_residuals read (JpJdF and the active marker).
-__device__ __forceinline__ void write_record_fused(float4 *grec, float4 *lrec, bool active, const Geo &g,
-                                                   const PhotoSums &s) {
-    if (active) {
-        float jp[8], hc[4], hdd, bd;
-        point_terms(g, s, jp, hc, hdd, bd);
-        const float4 r0 = make_float4(jp[0], jp[1], jp[2], jp[3]), r1 = make_float4(jp[4], jp[5], jp[6], jp[7]);
-        const float4 r3 = make_float4(hdd, bd, 1.f, 0.f);
-        grec[0] = r0;
-        grec[1] = r1;
-        grec[3] = r3;
-        lrec[0] = r0;
-        lrec[1] = r1;
-        lrec[2] = make_float4(hc[0], hc[1], hc[2], hc[3]);
-        lrec[3] = r3;
-    } else {
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        grec[3] = z;
-        lrec[3] = z;
-    }
-}
-
-// Recursive-halving wavefront reduction of 96 floats: 96 shuffles instead of 6*96.  On return
-// lane l (all 64) holds the full sums of elements base(l) + {0,1,2}, base = 48 b0 + 24 b1 +
-// 12 b2 + 6 b3 + 3 b4 (b = bits of the lane id).
-template <int L, int M>
-__device__ inline void halve(float *v, int lane) {
-    constexpr int H = L / 2;
-    const bool upper = (lane & M) != 0;
-#pragma unroll
-    for (int i = 0; i < H; i++) {
-        const float send = upper ? v[i] : v[i + H];
-        const float keep = upper ? v[i + H] : v[i];
-        v[i] = keep + __shfl_xor(send, M, kWave);
-    }
-}
-
-// Inputs of one residual's AccumulatorApprox contribution (x = [Jpdc0, Jpdxi0], y = [Jpdc1,
-// Jpdxi1]; a, b, c = JIdx2; tr = JabJIdx and JI_r; br = Jab2, Jab_r, rr).
-struct TopIn {
-    float x[10], y[10];
-    float a, b, c;
-    float tr[6], br[6];
-};
-// Element K of the 96-slot layout: [0,55) upper-triangular 10x10 row-major (Data[]),
-// [55,85) TopRight 10x3, [85,91) BotRight, [91,96) zero.  All index arithmetic is constexpr.
-constexpr int tri_row(int k) {
-    int r = 0;
-    while (k >= 10 - r) {
-        k -= 10 - r;
-        r++;
-    }
-    return r;
-}
-constexpr int tri_col(int k) {
-    int r = 0;
-    while (k >= 10 - r) {
-        k -= 10 - r;
-        r++;
-    }
-    return r + k;
-}
-template <int K>
-__device__ __forceinline__ float topval(const TopIn &t) {
-    if constexpr (K < 55) {
-        constexpr int r = tri_row(K), cc = tri_col(K);
-        return t.a * t.x[cc] * t.x[r] + t.c * t.y[cc] * t.y[r] + t.b * (t.x[cc] * t.y[r] + t.y[cc] * t.x[r]);
-    } else if constexpr (K < 85) {
-        constexpr int r = (K - 55) / 3, j = (K - 55) % 3;
-        return t.x[r] * t.tr[2 * j] + t.y[r] * t.tr[2 * j + 1];
-    } else if constexpr (K < 91) {
-        return t.br[K - 85];
-    } else {
-        return 0.0f;
-    }
-}
-// first recursive-halving step (lane mask 1) with the 96 terms generated on the fly
-template <int I>
-__device__ __forceinline__ void first_halve(const TopIn &t, float *v, bool upper) {
-    if constexpr (I < 48) {
-        const float lo = topval<I>(t), hi = topval<I + 48>(t);
-        const float send = upper ? lo : hi;
-        const float keep = upper ? hi : lo;
-        v[I] = keep + __shfl_xor(send, 1, kWave);
-        first_halve<I + 1>(t, v, upper);
-    }
-}
-
-// Two-pass form of the same reduction (48 slots per pass): only 24 partial sums are live
-// next to the TopIn operands, which keeps the kernel under 128 VGPRs.
-template <int Off, int I>
-__device__ __forceinline__ void first_halve24(const TopIn &t, float *v, bool upper) {
-    if constexpr (I < 24) {
-        const float lo = topval<Off + I>(t), hi = topval<Off + I + 24>(t);
-        const float send = upper ? lo : hi;
-        const float keep = upper ? hi : lo;
-        v[I] = keep + __shfl_xor(send, 1, kWave);
-        first_halve24<Off, I + 1>(t, v, upper);
-    }
-}
-// kHalves: lanes 0-31 and 32-63 are reduced separately (two pairs per wavefront, fused pass);
-// each half's lanes 0-15 (and 32-47) write their own slab item (write_ok per half).
-template <int Off, bool kHalves = false>
-__device__ __forceinline__ void reduce_top_pass(const TopIn &t, int lane, float *slab_item, bool write_ok = true) {
-    float v[24];
-    first_halve24<Off, 0>(t, v, (lane & 1) != 0);
-    halve<24, 2>(v, lane);
-    halve<12, 4>(v, lane);
-    halve<6, 8>(v, lane);
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        v[i] += __shfl_xor(v[i], 16, kWave);
-        if (!kHalves) v[i] += __shfl_xor(v[i], 32, kWave);
-    }
-    if (kHalves ? ((lane & 31) < 16 && write_ok) : lane < 16) {
-        const int base = Off + 24 * (lane & 1) + 12 * ((lane >> 1) & 1) + 6 * ((lane >> 2) & 1) + 3 * ((lane >> 3) & 1);
-        slab_item[base] = v[0];
-        slab_item[base + 1] = v[1];
-        slab_item[base + 2] = v[2];
-    }
-}
-
-template <int kMinWavesPerSimd, bool kTiled, bool kLoad3, bool kXcdRemap, bool kCentreFirst>
-__global__ __launch_bounds__(256, kMinWavesPerSimd) void k_linearize(LinParams P) {
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // XCD-aware mapping: blocks b, b+8, b+16, ... share an XCD (round-robin dispatch), so give
-    // each XCD one contiguous range of items.  Items are ordered by (window, target, host):
-    // all chunks reading one target frame then run on one XCD and share its L2.
-    const int nb = P.n_blocks, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
-    const int lblock = kXcdRemap ? xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3) : (int)blockIdx.x;
-    if (lblock * 4 + wave >= P.n_items) return;
-    const int item = P.item_base + lblock * 4 + wave;  // global chunk index
-    const int4 it = P.items[item];
-    const WinDev &W = P.wins[it.w];
-    const int N = W.N;
-    const int aidx = it.z - W.pair_base;
-    const int h = aidx % N, t = aidx / N;
-    const float *pre = P.precalc + (size_t)it.z * LDSO_BA_PRECALC_STRIDE;
-    const float4 *img = P.img + (size_t)(W.frame_base + t) * P.frame_stride;
-    const float th = fmaxf(P.frame_th[W.frame_base + h], P.frame_th[W.frame_base + t]);
-
-    const bool valid = lane < it.y;
-    const int r = it.x + lane;
-    double energy = 0;
-    bool isIN = false, active = false;
-    Geo g;
-    PhotoSums s;
-    if (valid) {
-        const int8_t old_state = P.rs_state[r];
-        uint8_t flags = P.rs_flags[r];
-        float state_energy = P.rs_energy[r];
-        float new_energy = P.rs_newenergy[r];
-        int8_t new_state = LDSO_BA_RES_OOB;
-        float e_wo = -1;
-        float4 centre = P.rs_center[r];
-        if (old_state == LDSO_BA_RES_OOB) {
-            energy = state_energy;  // linearize returns state_energy; applyRes returns early
-            P.pt_rec[(size_t)P.rs_slot[r] * 4 + 3] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
-        } else {
-            const int p = P.rs_point[r];
-            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-            const float4 pd0 = *(const float4 *)pd;
-            bool ok;
-            if constexpr (kCentreFirst) {  // the reference's order (Residuals.cc:59-140)
-                float cw[16];
-#pragma unroll
-                for (int i = 0; i < 4; i++) *(float4 *)&cw[4 * i] = *(const float4 *)(pd + 8 + 4 * i);
-                ok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
-                                       W.wM3, W.hM3, g);
-                if (ok) {
-                    centre.x = g.Ku;
-                    centre.y = g.Kv;
-                    centre.z = g.new_idepth;
-                    ok = pattern_loop<kTiled, kLoad3>(pre, img, P.tiles_per_row, W.wM3, W.hM3, pd0.x, pd0.y, pd0.z,
-                                                      cw, cw + 8, s);
-                }
-            } else {
-                // gathers first, geometry after (not live across the 32 loads); same outcome: any
-                // failure -> OOB, centerProjectedTo set iff the centre projection succeeds
-                ok = pattern_loop<kTiled, kLoad3>(pre, img, P.tiles_per_row, W.wM3, W.hM3, pd0.x, pd0.y, pd0.z, pd + 8,
-                                                  pd + 16, s);
-                const bool cok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2],
-                                                   W.calib[3], W.wM3, W.hM3, g);
-                if (cok) {
-                    centre.x = g.Ku;
-                    centre.y = g.Kv;
-                    centre.z = g.new_idepth;
-                }
-                ok = ok && cok;
-            }
-            if (!ok) {
-                energy = state_energy;  // OOB: return state_energy, NewEnergy untouched
-            } else {
-                e_wo = s.energy;
-                float el = s.energy;
-                if (el > th || s.wJI2 < 2) {
-                    el = th;
-                    new_state = LDSO_BA_RES_OUTLIER;
-                } else {
-                    new_state = LDSO_BA_RES_IN;
-                }
-                new_energy = el;
-                energy = el;
-            }
-            // applyRes(true), Residuals.h:70-88 (state_state != OOB here)
-            active = (new_state == LDSO_BA_RES_IN);
-            flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
-            state_energy = new_energy;
-            write_record(P.pt_rec + (size_t)P.rs_slot[r] * 4, active, g, s);
-            if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
-                // linearizeAll_Reductor relBS (FullSystem.cc:1800-1812)
-#pragma clang fp contract(off)
-                float pi[3], pr[3];
-#pragma unroll
-                for (int i = 0; i < 3; i++) {
-                    pi[i] = pre[3 * i] * pd0.x + pre[3 * i + 1] * pd0.y + pre[3 * i + 2] * 1.0f;
-                    pr[i] = pi[i] + pre[9 + i] * pd0.z;
-                }
-                const float dx = pi[0] / pi[2] - pr[0] / pr[2], dy = pi[1] / pi[2] - pr[1] / pr[2];
-                centre.w = 0.01f * sqrtf(dx * dx + dy * dy);
-            }
-            P.rs_state[r] = new_state;
-            P.rs_flags[r] = flags;
-            P.rs_energy[r] = state_energy;
-            P.rs_newenergy[r] = new_energy;
-            P.rs_center[r] = centre;
-        }
-        isIN = (new_state == LDSO_BA_RES_IN);
-        P.rs_newstate[r] = new_state;
-        P.rs_energy_wo[r] = e_wo;
-    }
-
-    // linearizeAll stats: sum of returned energies (double) and #IN, per chunk
-    double esum = energy;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
-    const unsigned long long inmask = __ballot(isIN);
-    if (lane == 0) {
-        P.item_energy[2 * item] = esum;
-        P.item_energy[2 * item + 1] = (double)__popcll(inmask);
-    }
-    if (!P.accumulate) return;
-
-    // AccumulatorApprox::update / updateTopRight / updateBotRight terms (mode 0), generated on
-    // the fly inside the first halving step so that only 48 partial sums are ever live.
-    TopIn tin;
-    if (active) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            tin.x[i] = g.d_C_x[i];
-            tin.y[i] = g.d_C_y[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            tin.x[4 + i] = g.d_xi_x[i];
-            tin.y[4 + i] = g.d_xi_y[i];
-        }
-        tin.a = s.JIdx2_00;
-        tin.b = s.JIdx2_10;
-        tin.c = s.JIdx2_11;
-        tin.tr[0] = s.JabJIdx_00;
-        tin.tr[1] = s.JabJIdx_01;
-        tin.tr[2] = s.JabJIdx_10;
-        tin.tr[3] = s.JabJIdx_11;
-        tin.tr[4] = s.JI_r0;
-        tin.tr[5] = s.JI_r1;
-        tin.br[0] = s.Jab2_00;
-        tin.br[1] = s.Jab2_01;
-        tin.br[2] = s.Jab_r0;
-        tin.br[3] = s.Jab2_11;
-        tin.br[4] = s.Jab_r1;
-        tin.br[5] = s.rr;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 10; i++) tin.x[i] = tin.y[i] = 0;
-        tin.a = tin.b = tin.c = 0;
-#pragma unroll
-        for (int i = 0; i < 6; i++) tin.tr[i] = tin.br[i] = 0;
-    }
-    float *slab_item = P.top_slab + (size_t)item * kTopVals;
-    reduce_top_pass<0>(tin, lane, slab_item);
-    reduce_top_pass<48>(tin, lane, slab_item);
-}
-
-// ============================================================================================
-// k_linearize_sp: sample-parallel variant.  Phase A: 8 lanes per residual, one per pattern
-// pixel, so one wave-instruction's 64 taps belong to 8 residuals and coalesce into far fewer
-// cache lines, and only 4 taps per lane are live.  The 17 per-pixel sums of
-// Residuals.cc:128-190 are transposed through LDS and added in pattern order by one lane per
-// sum (same rounding as the sequential loop).  Phase B: lane per residual again (state,
-// applyRes, point terms, AccumulatorApprox terms and wave reduction, as k_linearize).
-// ============================================================================================
 constexpr int kSums = 17;      // energy, wJI2, JIdx2 (3), JabJIdx (4), Jab2 (3), JI_r (2), Jab_r (2), rr
-constexpr int kSumStride = 20; // floats per residual in the sums buffer ([17] = pattern ok flag)
+constexpr int kSumStride = kSums;  // floats per residual in the sums buffer (energy < 0: pattern not ok)
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -724,89 +388,136 @@ __device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int 
     }
 }
 
-// kImg: 0 row-major float4 texels, 1 2x4-tiled float4 texels, 2 quad records (see k_tile_image),
-// 3 intensity only in 8x4-float tiles with the gradients recomputed (see k_intensity_image)
-// Per wavefront LDS: the per-pixel addends [8 residuals][kSums][8 pixels] and the per-residual
-// sums [64][kSumStride] (dynamic shared memory: 4 waves in the chunk-major pass, (N-1)/2 rounded
-// up in the fused one).  In the fused pass the addend region of wave w then holds the records
-// of target slots 2w, 2w+1 and the sums regions the block's SYRK rows.
-constexpr int kTermsPerWave = 8 * kSums * 8;
-constexpr int kSumsPerWave = 64 * kSumStride;
-// + the block's SYRK weights and its points' {nres, targets lo/hi, priorF, deltaF} (fused)
-__host__ __device__ constexpr size_t lin_lds_bytes(int waves) {
-    return ((size_t)waves * (kTermsPerWave + kSumsPerWave) + 6 * kFusedPts) * sizeof(float);
+// ---------------------------------------------------------------------------------------------
+// AccumulatorApprox of one chunk on the matrix cores.  The chunk's Top block (13x13, index layout
+// [0:4 intrinsics, 4:10 xi, 10 a, 11 b, 12 r]) is
+//   [0:10, 0:10]  sum_r Jp^T JIdx2 Jp                 (update, MatrixAccumulators.h:893-979)
+//   [0:10, 10:13] sum_r Jp^T [JabJIdx | JI_r]          (updateTopRight, :982-1030)
+//   [10:13,10:13] sum_r [Jab2, Jab_r; ., rr]           (updateBotRight, :1032-1045)
+// with Jp = [x; y] = [Jpdc | Jpdxi] (2x10).  As one GEMM over K = 2 x 64 (residual, row of Jp):
+//   D = A B,  A[i][(r,c)] = Jp_r[c][i],  B[(r,0)][j] = (a x + b y)_j,  B[(r,1)][j] = (b x + c y)_j
+//   for j < 10, and B[(r,c)][10 + m] = column m of [JabJIdx | JI_r] row c.
+// Rows 13 / 14 of A are the indicators of c = 0 / c = 1 and columns 13..15 of B carry the six
+// BotRight terms, so D[13][13..15] and D[14][13..15] are their sums.  32 v_mfma_f32_16x16x4f32
+// per wavefront, operands staged through the wave's LDS (36 floats per residual, two halves of 32
+// residuals).  fp32 products accumulated in fp32 like the blocked AccumulatorApprox sums
+// (tolerance-checked).
+// ---------------------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kTopRow = 36;
+constexpr int kTermQ = 9;                      // quantities per transposition round (17 = 9 + 8)
+constexpr int kTermsPerWave = 8 * kTermQ * 8;   // per-pixel addends of one round [8 residuals][9][8]
+constexpr int kSumsPerWave = 64 * kSumStride;   // per-residual sums [64][17]
+
+__device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, const Geo &g, const PhotoSums &s,
+                                         float *slab_item) {
+    float4 v[9];
+    if (active) {
+        v[0] = make_float4(g.d_C_x[0], g.d_C_y[0], g.d_C_x[1], g.d_C_y[1]);
+        v[1] = make_float4(g.d_C_x[2], g.d_C_y[2], g.d_C_x[3], g.d_C_y[3]);
+        v[2] = make_float4(g.d_xi_x[0], g.d_xi_y[0], g.d_xi_x[1], g.d_xi_y[1]);
+        v[3] = make_float4(g.d_xi_x[2], g.d_xi_y[2], g.d_xi_x[3], g.d_xi_y[3]);
+        v[4] = make_float4(g.d_xi_x[4], g.d_xi_y[4], g.d_xi_x[5], g.d_xi_y[5]);
+        v[5] = make_float4(s.JabJIdx_00, s.JabJIdx_01, s.JabJIdx_10, s.JabJIdx_11);
+        v[6] = make_float4(s.JI_r0, s.JI_r1, s.Jab2_00, s.Jab2_11);
+        v[7] = make_float4(s.Jab2_01, s.Jab_r1, s.Jab_r0, s.rr);
+        v[8] = make_float4(s.JIdx2_00, s.JIdx2_10, s.JIdx2_11, 0.f);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; k++) v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int i = lane & 15, kk = lane >> 4;
+    const bool geo = i < 10, ind = i >= 13;
+    const float a0c = i == 13 ? 1.f : 0.f, a1c = i == 14 ? 1.f : 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        if ((lane >> 5) == half) {
+            float4 *row = reinterpret_cast<float4 *>(tab + (lane & 31) * kTopRow);
+#pragma unroll
+            for (int k = 0; k < 9; k++) row[k] = v[k];
+        }
+        wave_lds_sync();
+        const float *base = tab + kk * 8 * kTopRow;  // K rows (residual kk*8 + m, c)
+#pragma unroll 4
+        for (int m = 0; m < 8; m++) {
+            const float *rr = base + m * kTopRow;
+            const float2 p = *reinterpret_cast<const float2 *>(rr + 2 * i);
+            const float4 q = *reinterpret_cast<const float4 *>(rr + 32);
+            const float A0 = ind ? a0c : p.x, A1 = ind ? a1c : p.y;
+            const float B0 = geo ? q.x * p.x + q.y * p.y : p.x;
+            const float B1 = geo ? q.y * p.x + q.z * p.y : p.y;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A0, B0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A1, B1, acc, 0, 0, 0);
+        }
+        wave_lds_sync();
+    }
+    // lane holds D[4 kk + v][i]; scatter into the 96-slot partial layout read by k_stitch
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const int r = 4 * kk + v, c = i;
+        int slot = -1;
+        if (r < 10 && c < 10 && c >= r) slot = r * 10 - r * (r - 1) / 2 + (c - r);
+        else if (r < 10 && c >= 10 && c < 13) slot = 55 + 3 * r + (c - 10);
+        else if (r == 13 && c >= 13) slot = 85 + (c - 13);
+        else if (r == 14 && c >= 13) slot = 88 + (c - 13);
+        if (slot >= 0) slab_item[slot] = acc[v];
+        else if (r == 15 && c < 5) slab_item[91 + c] = 0.f;
+    }
 }
-#ifndef LDSO_EXP_FUSED_NO_SC
-#define LDSO_EXP_FUSED_NO_SC 0
+
+// ============================================================================================
+// k_linearize: one wavefront per chunk of <= 64 residuals of one (host, target) bucket, 4 per
+// workgroup, XCD-contiguous chunk ranges.
+//   phase A  8 lanes per residual (lane = pattern pixel), 8 residuals per step, a one-step
+//            software pipeline: the projection and the 12 intensity taps (layout 3) or 4 texels
+//            (layout 1) of step k+1 are issued before step k's arithmetic.  The 17 per-pixel
+//            addends of Residuals.cc:128-190 go through LDS and are summed in pattern order.
+//   phase B  lane per residual: centre projection (FEJ Jacobians), state / energy
+//            (Residuals.cc:192-217), applyRes + the takeData record, relBS on the fix pass.
+//   Top      the chunk's AccumulatorApprox block on the matrix cores (top_mfma).
+// kMarg: the marginalisation pass (addPoint<2> sums with fixLinearizationF's res_toZeroF).
+// ============================================================================================
+constexpr int kWaveLds = kTermsPerWave + kSumsPerWave;  // floats of LDS per wavefront (6.5 KB: 6 waves/SIMD)
+static_assert(32 * kTopRow <= kWaveLds, "the Top operand table (one half) reuses the wave's LDS");
+// LDS requested per 4-wave workgroup: sets the resident workgroups per CU (= waves per SIMD).
+// 160 KB / 32 KB = 5: measured fastest (64 x S7: 121.6 us; 4 blocks 125.7, 3 blocks 143.5; 6
+// waves/SIMD need <= 80 VGPRs and spill, 145 us).
+#ifndef LDSO_LIN_BLOCKS_PER_CU
+#define LDSO_LIN_BLOCKS_PER_CU 5
 #endif
-#ifndef LDSO_EXP_FUSED_NO_SYRK
-#define LDSO_EXP_FUSED_NO_SYRK 0
-#endif
-#ifndef LDSO_EXP_FUSED_PREFETCH
-#define LDSO_EXP_FUSED_PREFETCH 1
-#endif
-template <int kImg, bool kXcdRemap, bool kMarg, bool kFused>
-__global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParams P) {
-    constexpr bool kTiled = kImg == 1;
+constexpr size_t kLinLdsBytes = (160 * 1024 / LDSO_LIN_BLOCKS_PER_CU) & ~(size_t)511;
+static_assert(kLinLdsBytes >= 4 * kWaveLds * sizeof(float), "k_linearize LDS");
+
+template <int kImg, bool kMarg>
+__global__ __launch_bounds__(256, 4) void k_linearize(LinParams P) {
+    static_assert(kImg == 1 || kImg == 3, "image layouts 1 and 3");
     extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwaves = blockDim.x >> 6;
-    float *lds_terms_w = lds_dyn + wave * kTermsPerWave;
-    float *lds_sums_w = lds_dyn + nwaves * kTermsPerWave + wave * kSumsPerWave;
+    float *lds_terms_w = lds_dyn + wave * kWaveLds;
+    float *lds_sums_w = lds_terms_w + kTermsPerWave;
+    // XCD-aware mapping: blocks b, b+8, b+16, ... share an XCD (round-robin dispatch), so each XCD
+    // gets one contiguous range of chunks; chunks are ordered (window, target, host), so the
+    // chunks reading one target frame run on one XCD and share its L2.
     const int nb = P.n_blocks, xcd = blockIdx.x & 7, q8 = nb >> 3, r8 = nb & 7;
-    const int lblock = kXcdRemap ? xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3) : (int)blockIdx.x;
-    // chunk-major: wave = one chunk of <= 64 residuals of one pair.  fused: lanes 0-31 / 32-63
-    // hold the block's residuals to target slot 2w / 2w+1 (one pair each).
-    int4 it, bd = make_int4(0, 0, 0, 0);
-    int itemL, pairA, pairB, jlimit, half_slot = 0;
-    bool valid;
-    if constexpr (kFused) {
-        if (lblock >= P.n_items) return;  // whole blocks only: the SC phase synchronises the block
-        bd = P.pblocks[P.item_base + lblock];
-        const int nhalf = P.wins[bd.w].N - 1;
-        half_slot = 2 * wave + (lane >> 5);
-        const bool hv = half_slot < nhalf;
-        it = P.items[bd.z + min(half_slot, nhalf - 1)];  // {res_begin, count, pair, slab item}
-        itemL = it.w;
-        valid = hv && (lane & 31) < it.y;
-        pairA = __builtin_amdgcn_readfirstlane(it.z);
-        pairB = __shfl(it.z, 32, kWave);
-        pairB = __builtin_amdgcn_readfirstlane(pairB);
-        jlimit = 64;
-        if (LDSO_EXP_FUSED_PREFETCH && (int)threadIdx.x < bd.y) {
-            // the SC tail's per-point inputs, fetched now so their latency hides under phase A
-            const int p = bd.x + threadIdx.x;
-            int *side = reinterpret_cast<int *>(lds_dyn + nwaves * (kTermsPerWave + kSumsPerWave) + kFusedPts);
-            const unsigned long long tg = P.pt_tgt[p];
-            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-            side[threadIdx.x] = P.pt_nres[p];
-            side[kFusedPts + threadIdx.x] = (int)(unsigned)tg;
-            side[2 * kFusedPts + threadIdx.x] = (int)(unsigned)(tg >> 32);
-            side[3 * kFusedPts + threadIdx.x] = __float_as_int(pd[4]);
-            side[4 * kFusedPts + threadIdx.x] = __float_as_int(pd[5]);
-        }
-    } else {
-        if (lblock * 4 + wave >= P.n_items) return;
-        itemL = P.item_base + lblock * 4 + wave;  // global chunk index
-        it = P.items[itemL];
-        valid = lane < it.y;
-        pairA = pairB = it.z;
-        jlimit = it.y;
-    }
-    const WinDev &W = P.wins[kFused ? bd.w : it.w];
+    const int lblock = xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3);
+    if (lblock * 4 + wave >= P.n_items) return;
+    const int itemL = P.item_base + lblock * 4 + wave;  // global chunk index
+    const int4 it = P.items[itemL];                     // {res_begin, count, pair_global, win}
+    const bool valid = lane < it.y;
+    const int pair = __builtin_amdgcn_readfirstlane(it.z), jlimit = __builtin_amdgcn_readfirstlane(it.y);
+    const WinDev &W = P.wins[__builtin_amdgcn_readfirstlane(it.w)];
     const int N = W.N;
-    const int h = (pairA - W.pair_base) % N, tA = (pairA - W.pair_base) / N, tB = (pairB - W.pair_base) / N;
-    const float *preA = P.precalc + (size_t)pairA * LDSO_BA_PRECALC_STRIDE;
-    const float *preB = P.precalc + (size_t)pairB * LDSO_BA_PRECALC_STRIDE;
-    const float4 *imgA = P.img + (size_t)(W.frame_base + tA) * P.frame_stride;
-    const float4 *imgB = P.img + (size_t)(W.frame_base + tB) * P.frame_stride;
-    const bool upper = kFused && lane >= 32;
-    const float *pre = upper ? preB : preA;  // this lane's residual's pair
-    const float th = fmaxf(P.frame_th[W.frame_base + h], P.frame_th[W.frame_base + (upper ? tB : tA)]);
+    const int h = (pair - W.pair_base) % N, t = (pair - W.pair_base) / N;
+    const float *pre = P.precalc + (size_t)pair * LDSO_BA_PRECALC_STRIDE;
+    const float th = fmaxf(P.frame_th[W.frame_base + h], P.frame_th[W.frame_base + t]);
     const float wM3 = W.wM3, hM3 = W.hM3;
+    const float4 *img = P.img + (size_t)(W.frame_base + t) * P.frame_stride;
+    const __amdgpu_buffer_rsrc_t rsrc = frame_rsrc(reinterpret_cast<const float *>(img), P.frame_stride * 16);
+    const unsigned band = (unsigned)P.tiles_per_row * 8u * 16u;
 
-    const int r = it.x + (kFused ? (lane & 31) : lane);
+    const int r = it.x + lane;
     // Everything phase B needs is loaded up front (unconditionally, from a clamped index: a load
     // inside a divergent branch is waited for at the branch's end) so it lands during phase A.
     const int rq = valid ? r : 0;
@@ -821,14 +532,12 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
     if (!valid) my_state = LDSO_BA_RES_OOB;
     // marginalisation pass: Jp * delta of fixLinearizationF (Residuals.cc:221-232) from the centre
     // geometry, per residual, before the pattern pixels need it (dot products left to right)
-    float jp_dx = 0.f, jp_dy = 0.f, daA = 0.f, dbA = 0.f, daB = 0.f, dbB = 0.f;
+    float jp_dx = 0.f, jp_dy = 0.f, da = 0.f, db = 0.f;
     if constexpr (kMarg) {
 #pragma clang fp contract(off)
-        const float *dp = P.ad_ht_delta + (size_t)(upper ? pairB : pairA) * 8;
-        daA = P.ad_ht_delta[(size_t)pairA * 8 + 6];  // delta_a, delta_b of each step's pair
-        dbA = P.ad_ht_delta[(size_t)pairA * 8 + 7];
-        daB = P.ad_ht_delta[(size_t)pairB * 8 + 6];
-        dbB = P.ad_ht_delta[(size_t)pairB * 8 + 7];
+        const float *dp = P.ad_ht_delta + (size_t)pair * 8;
+        da = dp[6];  // delta_a, delta_b of the pair (adHTdeltaF[6], [7])
+        db = dp[7];
         Geo gm;
         if (centre_projection(pre, my_pd0.x, my_pd0.y, my_pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
                               wM3, hM3, gm)) {
@@ -850,37 +559,27 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
     }
 
     // ---------------- phase A: pattern pixels, 8 residuals per step -------------------------
-    // One-step software pipeline: the projection and the 4 tap loads of step k+1 are issued
-    // before the arithmetic of step k.
     {
 #pragma clang fp contract(off)
         const int g = lane >> 3, sl = lane & 7;
         // staticPattern[8] (Setting.cc:275) offset of this lane's pixel
         const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
         const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
-        // a step's 8 residuals share one pair (the fused pass switches pair at step 4)
-        const float aff0A = preA[24], aff1A = preA[25], b0A = preA[26];
-        const float aff0B = preB[24], aff1B = preB[25], b0B = preB[26];
-        float *T = lds_terms_w + g * (kSums * 8);
+        const float aff0 = pre[24], aff1 = pre[25], b0 = pre[26];
+        float *T = lds_terms_w + g * (kTermQ * 8);
         float *S = lds_sums_w;
-        int nsteps = (jlimit + 7) >> 3;
-        if constexpr (kFused) {  // skip the upper half's steps when this wave has no slot 2w+1
-            if (2 * wave + 1 >= N - 1) nsteps = 4;
-        }
+        const int nsteps = (jlimit + 7) >> 3;
         const int tpr2 = P.tiles_per_row;
 
         struct Stage {
             float Ku, Kv, color, weight;
-            float3 t00, t10, t01, t11;  // kImg 0/1: the four taps
-            float4 qi, qx, qy;          // kImg 2: I, dx, dy of the quad (00, 10, 01, 11)
-            float iv[12];               // kImg 3: I at rows y-1 (x, x+1), y and y+1 (x-1..x+2), y+2 (x, x+1)
+            float iv[12];               // layout 3: the 12 intensities (load12)
+            float3 t00, t10, t01, t11;  // layout 1: the four texels
             float jx, jy;               // kMarg: Jp_delta of the residual
             bool gok;
         };
         auto issue = [&](int k, Stage &q) {
             const int j = 8 * k + g;
-            const float *pre = (kFused && k >= 4) ? preB : preA;  // the step's pair (uniform)
-            const float4 *img = (kFused && k >= 4) ? imgB : imgA;
             const int st = __shfl(my_state, j, kWave);
             const int p = __shfl(my_point, j, kWave);
             const float pu = __shfl(my_pd0.x, j, kWave), pv = __shfl(my_pd0.y, j, kWave),
@@ -891,14 +590,8 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
                 q.jy = __shfl(jp_dy, j, kWave);
             }
             const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-#if LDSO_EXP_NO_PT
-            q.color = 100.f + sl + (p & 7);
-            q.weight = 0.5f;
-            (void)pd;
-#else
             q.color = pd[8 + sl];
             q.weight = pd[16 + sl];
-#endif
             const float up = pu + px, vp = pv + py;
             float ptp[3];
 #pragma unroll
@@ -909,40 +602,15 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
             const bool pok = go && q.Ku > 1.1f && q.Kv > 1.1f && q.Ku < wM3 && q.Kv < hM3;
             const unsigned long long m1 = __ballot(pok);
             q.gok = ((m1 >> (8 * g)) & 0xFFull) == 0xFFull;
-            // taps of an in-bounds pixel are always addressable; others read texel (1, 1)
+            // taps of an in-bounds pixel are always addressable; others read around texel (1, 1)
             const int ix = pok ? (int)q.Ku : 1, iy = pok ? (int)q.Kv : 1;
             if constexpr (kImg == 3) {
-                const float *imf = reinterpret_cast<const float *>(img);
-                auto at = [&](int x, int y) {
-#if LDSO_EXP_NO_TEX
-                    (void)imf;
-                    return (float)((x * 7 + y * 13) & 255);
-#else
-                    return imf[(((y >> 2) * tpr2 + (x >> 3)) << 5) + ((y & 3) << 3) + (x & 7)];
-#endif
-                };
-                q.iv[0] = at(ix, iy - 1);
-                q.iv[1] = at(ix + 1, iy - 1);
-                q.iv[2] = at(ix - 1, iy);
-                q.iv[3] = at(ix, iy);
-                q.iv[4] = at(ix + 1, iy);
-                q.iv[5] = at(ix + 2, iy);
-                q.iv[6] = at(ix - 1, iy + 1);
-                q.iv[7] = at(ix, iy + 1);
-                q.iv[8] = at(ix + 1, iy + 1);
-                q.iv[9] = at(ix + 2, iy + 1);
-                q.iv[10] = at(ix, iy + 2);
-                q.iv[11] = at(ix + 1, iy + 2);
-            } else if constexpr (kImg == 2) {  // one 64-byte record holds the whole 2x2 footprint
-                const float4 *rec = img + ((size_t)iy * W.width + ix) * 4;
-                q.qi = rec[0];
-                q.qx = rec[1];
-                q.qy = rec[2];
+                load12(rsrc, band, ix, iy, q.iv);
             } else {
-                q.t00 = tex<kTiled, false>(img, tpr2, ix, iy);
-                q.t10 = tex<kTiled, false>(img, tpr2, ix + 1, iy);
-                q.t01 = tex<kTiled, false>(img, tpr2, ix, iy + 1);
-                q.t11 = tex<kTiled, false>(img, tpr2, ix + 1, iy + 1);
+                q.t00 = tex(img, tpr2, ix, iy);
+                q.t10 = tex(img, tpr2, ix + 1, iy);
+                q.t01 = tex(img, tpr2, ix, iy + 1);
+                q.t11 = tex(img, tpr2, ix + 1, iy + 1);
             }
         };
         auto consume = [&](int k, const Stage &q) {
@@ -951,80 +619,63 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
             float tt[kSums];
             if (q.gok) {
                 const int ix = (int)q.Ku, iy = (int)q.Kv;
-                const float dx = q.Ku - ix, dy = q.Kv - iy, dxdy = dx * dy;
-                const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+                const float dx = q.Ku - ix, dy = q.Kv - iy;
                 float I, gx, gy;
                 if constexpr (kImg == 3) {
-                    // FrameHessian::makeImages gradients (FrameHessian.cc:96-101), recomputed
-                    auto grad = [](float a, float b) {
-                        const float d = 0.5f * (a - b);
-                        return (isnan(d) || fabsf(d) > 255.0f) ? 0.0f : d;
-                    };
-                    const float *v = q.iv;
-                    const float3 t00 = make_float3(v[3], grad(v[4], v[2]), grad(v[7], v[0]));
-                    const float3 t10 = make_float3(v[4], grad(v[5], v[3]), grad(v[8], v[1]));
-                    const float3 t01 = make_float3(v[7], grad(v[8], v[6]), grad(v[10], v[3]));
-                    const float3 t11 = make_float3(v[8], grad(v[9], v[7]), grad(v[11], v[4]));
-                    I = w11 * t11.x + w01 * t01.x + w10 * t10.x + w00 * t00.x;
-                    gx = w11 * t11.y + w01 * t01.y + w10 * t10.y + w00 * t00.y;
-                    gy = w11 * t11.z + w01 * t01.z + w10 * t10.z + w00 * t00.z;
-                } else if constexpr (kImg == 2) {
-                    I = w11 * q.qi.w + w01 * q.qi.z + w10 * q.qi.y + w00 * q.qi.x;
-                    gx = w11 * q.qx.w + w01 * q.qx.z + w10 * q.qx.y + w00 * q.qx.x;
-                    gy = w11 * q.qy.w + w01 * q.qy.z + w10 * q.qy.y + w00 * q.qy.x;
+                    const float3 s3 = bilin12(q.iv, dx, dy);
+                    I = s3.x;
+                    gx = s3.y;
+                    gy = s3.z;
                 } else {
+                    const float dxdy = dx * dy;
+                    const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
                     I = w11 * q.t11.x + w01 * q.t01.x + w10 * q.t10.x + w00 * q.t00.x;
                     gx = w11 * q.t11.y + w01 * q.t01.y + w10 * q.t10.y + w00 * q.t00.y;
                     gy = w11 * q.t11.z + w01 * q.t01.z + w10 * q.t10.z + w00 * q.t00.z;
                 }
                 fin = isfinite(I);
-                const bool hb = kFused && k >= 4;
-                pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, hb ? aff0B : aff0A, hb ? aff1B : aff1A,
-                                   hb ? b0B : b0A, tt, kMarg ? q.jx : 0.f, kMarg ? q.jy : 0.f, hb ? daB : daA,
-                                   hb ? dbB : dbA);
-#pragma unroll
-                for (int e = 0; e < kSums; e++) T[e * 8 + sl] = tt[e];
+                pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt, kMarg ? q.jx : 0.f,
+                                   kMarg ? q.jy : 0.f, da, db);
             }
             const unsigned long long m2 = __ballot(fin);
             const bool rok = q.gok && ((m2 >> (8 * g)) & 0xFFull) == 0xFFull;
-            wave_lds_sync();
-            if (rok) {  // lane sl adds sums sl, sl+8 (and 16) over the 8 pixels in pattern order
+            // two transposition rounds (quantities 0-8, then 9-16): lane sl adds quantity q0 + sl
+            // (lane 0 also quantity 8) over the 8 pixels in pattern order
+            auto sum8 = [&](int qq, int e) {
+                const float4 a = *(const float4 *)&T[e * 8], b = *(const float4 *)&T[e * 8 + 4];
+                float sum = 0.0f;
+                sum += a.x;
+                sum += a.y;
+                sum += a.z;
+                sum += a.w;
+                sum += b.x;
+                sum += b.y;
+                sum += b.z;
+                sum += b.w;
+                S[j * kSumStride + qq] = sum;
+            };
+            if (q.gok) {
 #pragma unroll
-                for (int e = 0; e < 3; e++) {
-                    const int qq = sl + 8 * e;
-                    if (qq < kSums) {
-                        const float4 a = *(const float4 *)&T[qq * 8], b = *(const float4 *)&T[qq * 8 + 4];
-                        float sum = 0.0f;
-                        sum += a.x;
-                        sum += a.y;
-                        sum += a.z;
-                        sum += a.w;
-                        sum += b.x;
-                        sum += b.y;
-                        sum += b.z;
-                        sum += b.w;
-                        S[j * kSumStride + qq] = sum;
-                    }
-                }
+                for (int e = 0; e < kTermQ; e++) T[e * 8 + sl] = tt[e];
             }
-            if (sl == 0 && j < jlimit) S[j * kSumStride + kSums] = rok ? 1.0f : 0.0f;
+            wave_lds_sync();
+            if (rok) {
+                sum8(sl, sl);
+                if (sl == 0) sum8(8, 8);
+            } else if (sl == 0 && j < jlimit) {
+                S[j * kSumStride] = -1.0f;  // energy slot: pattern not ok
+            }
+            wave_lds_sync();
+            if (q.gok) {
+#pragma unroll
+                for (int e = 0; e < kSums - kTermQ; e++) T[e * 8 + sl] = tt[kTermQ + e];
+            }
+            wave_lds_sync();
+            if (rok) sum8(kTermQ + sl, sl);
             wave_lds_sync();
         };
-        // ping-pong stages, loads issued unconditionally (a step past the item's end has no valid
-        // group and reads texel (0, 0)), so no load result crosses a branch join
-#if LDSO_LIN_PIPE3
-        Stage A, B, C;
-        issue(0, A);
-        issue(1, B);
-        for (int k = 0; k < nsteps; k += 3) {
-            issue(k + 2, C);
-            consume(k, A);
-            issue(k + 3, A);
-            consume(k + 1, B);
-            issue(k + 4, B);
-            consume(k + 2, C);
-        }
-#else
+        // ping-pong stages, loads issued unconditionally (a step past the chunk's end has no valid
+        // group and reads around texel (1, 1)), so no load result crosses a branch join
         Stage A, B;
         issue(0, A);
         for (int k = 0; k < nsteps; k += 2) {
@@ -1033,7 +684,6 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
             issue(k + 2, A);
             consume(k + 1, B);
         }
-#endif
     }
 
     // ---------------- phase B: lane per residual ---------------------------------------------
@@ -1046,34 +696,29 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
         int8_t new_state = LDSO_BA_RES_OOB;
         float e_wo = -1;
         if (old_state == LDSO_BA_RES_OOB) {
-            energy = state_energy;
+            energy = state_energy;  // linearize returns state_energy; applyRes returns early
             P.pt_rec[(size_t)my_slot * 4 + 3] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
-            if constexpr (kFused)
-                reinterpret_cast<float4 *>(lds_terms_w)[((lane >> 5) * kFusedPts + (my_point - bd.x)) * 4 + 3] =
-                    make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
             const float4 pd0 = my_pd0;
             const float *Sr = lds_sums_w + lane * kSumStride;
-            const float4 s0 = *(const float4 *)(Sr), s1 = *(const float4 *)(Sr + 4), s2 = *(const float4 *)(Sr + 8),
-                         s3 = *(const float4 *)(Sr + 12), s4 = *(const float4 *)(Sr + 16);
-            s.energy = s0.x;
-            s.wJI2 = s0.y;
-            s.JIdx2_00 = s0.z;
-            s.JIdx2_10 = s0.w;
-            s.JIdx2_11 = s1.x;
-            s.JabJIdx_00 = s1.y;
-            s.JabJIdx_01 = s1.z;
-            s.JabJIdx_10 = s1.w;
-            s.JabJIdx_11 = s2.x;
-            s.Jab2_00 = s2.y;
-            s.Jab2_01 = s2.z;
-            s.Jab2_11 = s2.w;
-            s.JI_r0 = s3.x;
-            s.JI_r1 = s3.y;
-            s.Jab_r0 = s3.z;
-            s.Jab_r1 = s3.w;
-            s.rr = s4.x;
-            const bool pat_ok = s4.y != 0.0f;
+            s.energy = Sr[0];
+            s.wJI2 = Sr[1];
+            s.JIdx2_00 = Sr[2];
+            s.JIdx2_10 = Sr[3];
+            s.JIdx2_11 = Sr[4];
+            s.JabJIdx_00 = Sr[5];
+            s.JabJIdx_01 = Sr[6];
+            s.JabJIdx_10 = Sr[7];
+            s.JabJIdx_11 = Sr[8];
+            s.Jab2_00 = Sr[9];
+            s.Jab2_01 = Sr[10];
+            s.Jab2_11 = Sr[11];
+            s.JI_r0 = Sr[12];
+            s.JI_r1 = Sr[13];
+            s.Jab_r0 = Sr[14];
+            s.Jab_r1 = Sr[15];
+            s.rr = Sr[16];
+            const bool pat_ok = !(s.energy < 0.0f);
             bool ok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
                                         wM3, hM3, g);
             if (ok) {
@@ -1083,7 +728,7 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
             }
             ok = ok && pat_ok;
             if (!ok) {
-                energy = state_energy;
+                energy = state_energy;  // OOB: return state_energy, NewEnergy untouched
             } else {
                 e_wo = s.energy;
                 float el = s.energy;
@@ -1096,19 +741,13 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
                 new_energy = el;
                 energy = el;
             }
+            // applyRes(true), Residuals.h:70-88 (state_state != OOB here)
             active = (new_state == LDSO_BA_RES_IN);
             flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
             state_energy = new_energy;
-#if !LDSO_EXP_NO_REC
-            if constexpr (kFused)
-                write_record_fused(P.pt_rec + (size_t)my_slot * 4,
-                                   reinterpret_cast<float4 *>(lds_terms_w) +
-                                       ((lane >> 5) * kFusedPts + (my_point - bd.x)) * 4,
-                                   active, g, s);
-            else
-                write_record(P.pt_rec + (size_t)my_slot * 4, active, g, s);
-#endif
+            write_record(P.pt_rec + (size_t)my_slot * 4, active, g, s);
             if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
+                // linearizeAll_Reductor relBS (FullSystem.cc:1800-1812)
 #pragma clang fp contract(off)
                 float pi[3], pr[3];
 #pragma unroll
@@ -1130,133 +769,18 @@ __global__ __launch_bounds__(kFused ? 512 : 256, 4) void k_linearize_sp(LinParam
         P.rs_energy_wo[r] = e_wo;
     }
 
+    // linearizeAll stats: sum of returned energies (double) and #IN, per chunk
     double esum = energy;
 #pragma unroll
-    for (int m = kFused ? 16 : 32; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
+    for (int m = 32; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
     const unsigned long long inmask = __ballot(isIN);
-    const bool half_ok = !kFused || half_slot < N - 1;  // this lane's half has a target slot
-    if ((kFused ? (lane & 31) : lane) == 0 && half_ok) {
+    if (lane == 0) {
         P.item_energy[2 * itemL] = esum;
-        P.item_energy[2 * itemL + 1] =
-            (double)__popcll(kFused ? (upper ? inmask >> 32 : inmask & 0xFFFFFFFFull) : inmask);
+        P.item_energy[2 * itemL + 1] = (double)__popcll(inmask);
     }
     if (!P.accumulate) return;
-
-    TopIn tin;
-    if (active) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            tin.x[i] = g.d_C_x[i];
-            tin.y[i] = g.d_C_y[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            tin.x[4 + i] = g.d_xi_x[i];
-            tin.y[4 + i] = g.d_xi_y[i];
-        }
-        tin.a = s.JIdx2_00;
-        tin.b = s.JIdx2_10;
-        tin.c = s.JIdx2_11;
-        tin.tr[0] = s.JabJIdx_00;
-        tin.tr[1] = s.JabJIdx_01;
-        tin.tr[2] = s.JabJIdx_10;
-        tin.tr[3] = s.JabJIdx_11;
-        tin.tr[4] = s.JI_r0;
-        tin.tr[5] = s.JI_r1;
-        tin.br[0] = s.Jab2_00;
-        tin.br[1] = s.Jab2_01;
-        tin.br[2] = s.Jab_r0;
-        tin.br[3] = s.Jab2_11;
-        tin.br[4] = s.Jab_r1;
-        tin.br[5] = s.rr;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 10; i++) tin.x[i] = tin.y[i] = 0;
-        tin.a = tin.b = tin.c = 0;
-#pragma unroll
-        for (int i = 0; i < 6; i++) tin.tr[i] = tin.br[i] = 0;
-    }
-    float *slab_item = P.top_slab + (size_t)itemL * kTopVals;
-    reduce_top_pass<0, kFused>(tin, lane, slab_item, half_ok);
-    reduce_top_pass<48, kFused>(tin, lane, slab_item, half_ok);
-
-    if constexpr (kFused && !LDSO_EXP_FUSED_NO_SC) {
-        // ---- the block's SC half (k_point_sc for its 32 points), records read from LDS ----
-        __syncthreads();  // every record of the block is in LDS; the sums regions are free
-        const int npts = bd.y, KP = W.KP, nt = KP / 4, ntiles = W.ntiles, Kj = 8 * (N - 1);
-        float *U = lds_dyn + nwaves * kTermsPerWave;  // [32][KP] over the sums regions
-        float *Wt = lds_dyn + nwaves * (kTermsPerWave + kSumsPerWave);
-        for (int i = threadIdx.x; i < kFusedPts * KP; i += blockDim.x) U[i] = 0;
-        __syncthreads();
-        const int tq = threadIdx.x;
-        if (tq < npts) {
-#pragma clang fp contract(off)
-            const int p = bd.x + tq;
-            const int *side = reinterpret_cast<const int *>(Wt + kFusedPts);
-            const int nres = LDSO_EXP_FUSED_PREFETCH ? side[tq] : P.pt_nres[p];
-            const unsigned long long tgs =
-                LDSO_EXP_FUSED_PREFETCH ? (unsigned long long)(unsigned)side[kFusedPts + tq] |
-                                              ((unsigned long long)(unsigned)side[2 * kFusedPts + tq] << 32)
-                                        : P.pt_tgt[p];
-            float hdd = 0, bsum = 0, hcd[4] = {0, 0, 0, 0};
-            int ngood = 0;
-            float *row = U + tq * KP;
-            // sums in the point's residual order (AccumulatedTopHessian.cc:94-116)
-            for (int k = 0; k < nres; k++) {
-                const int tg = (int)((tgs >> (4 * k)) & 15ull);
-                const int slot = tg < h ? tg : tg - 1;
-                const float4 *rl = reinterpret_cast<const float4 *>(lds_dyn + (slot >> 1) * kTermsPerWave) +
-                                   ((slot & 1) * kFusedPts + tq) * 4;
-                const float4 hb = rl[3];
-                if (hb.z == 0.0f) continue;
-                ngood++;
-                const float4 j0 = rl[0], j1 = rl[1], hc = rl[2];
-                bsum += hb.y;
-                hdd += hb.x;
-                hcd[0] += hc.x;
-                hcd[1] += hc.y;
-                hcd[2] += hc.z;
-                hcd[3] += hc.w;
-                *(float4 *)(row + 8 * slot) = j0;
-                *(float4 *)(row + 8 * slot + 4) = j1;
-            }
-            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-            const float priorF = LDSO_EXP_FUSED_PREFETCH ? __int_as_float(side[3 * kFusedPts + tq]) : pd[4];
-            const float deltaF = LDSO_EXP_FUSED_PREFETCH ? __int_as_float(side[4 * kFusedPts + tq]) : pd[5];
-            float HdiF = 0, bdSum = 0, ih = 0;
-            if (ngood > 0) {
-                // AccumulatedSCHessian.cc:24-33 (Hdd_accLF = bd_accLF = Hcd_accLF = 0 in the hot path)
-                float H = hdd + 0.0f + priorF;
-                if (H < 1e-10f) H = 1e-10f;
-                ih = H;
-                HdiF = (float)(1.0 / (double)H);
-                bdSum = bsum + 0.0f;
-                if (P.shift_prior) bdSum += priorF * deltaF;
-                row[Kj + 0] = hcd[0] + 0.0f;
-                row[Kj + 1] = hcd[1] + 0.0f;
-                row[Kj + 2] = hcd[2] + 0.0f;
-                row[Kj + 3] = hcd[3] + 0.0f;
-                row[Kj + 4] = bdSum;
-            }
-            Wt[tq] = HdiF;
-            float *o = P.pt_out + (size_t)p * 12;
-            o[0] = HdiF;
-            o[1] = bdSum;
-            o[2] = ih;
-            o[3] = hdd;
-            o[4] = bsum;
-            o[5] = hcd[0];
-            o[6] = hcd[1];
-            o[7] = hcd[2];
-            o[8] = hcd[3];
-            o[9] = (float)ngood;
-        }
-        __syncthreads();
-        const int sc_item = P.item_base + lblock;  // point blocks and SC items share one order
-        if (!LDSO_EXP_FUSED_NO_SYRK)
-            syrk_tiles(U, Wt, KP, nt, ntiles, npts,
-                       P.sc_slab + W.sc_slab_base + (size_t)(sc_item - W.sc_item_base) * ntiles * 16, tq, blockDim.x);
-    }
+    wave_lds_sync();  // every lane has read its sums: the wave's LDS becomes the operand table
+    top_mfma(lds_terms_w, lane, active, g, s, P.top_slab + (size_t)itemL * kTopVals);
 }
 
 // ============================================================================================
@@ -1405,7 +929,6 @@ struct StitchParams {
     int pair_base;  // first global pair of this launch
     int win_base;   // first window of this launch
     int n_win;      // windows of this launch: blocks [0, n_win) run their setNewFrameEnergyTH
-    int part;       // 0: Top and SC halves; 1: Top half (+ the setNewFrameEnergyTH blocks); 2: SC half
 };
 
 __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row <= col
@@ -1596,9 +1119,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 
     // All global loads of both halves are issued first (one round trip for the block): the
     // Top bucket partial sums and pair adjoints, and the SC rows of G_i with the host's adjoints.
-    // part 1 / 2 (two launches on two streams, the Top half overlapping k_point_sc) skip the
-    // other half's loads and work; the branches are block-uniform.
-    const bool do_top = P.part != 2, do_sc = P.part != 1;
+    const bool do_top = true, do_sc = true;
     double *acc = sm, *A = acc + 96, *AH = A + 169, *AT = AH + 64, *TH = AT + 64, *TT = TH + 64;  // 521
     const int i = h, j = t, KP = W.KP, nt = KP / 4, per = W.ntiles * 16, Kc = 8 * (N - 1);
     const int sj = j < i ? j : j - 1;
@@ -2238,55 +1759,21 @@ struct ActParams {
     int tpr, img_mode, win, n, min_obs;
 };
 
-// getInterpolatedElement33 (GlobalFuncs.h:89-103) of a resident frame in any image layout
-__device__ inline float3 sample33(const float4 *__restrict__ img, int mode, int tpr, int width, float x, float y) {
+// getInterpolatedElement33 (GlobalFuncs.h:89-103) of a resident frame (layout 3 or 1)
+__device__ inline float3 sample33(const float4 *__restrict__ img, int mode, int tpr, long long frame_stride, float x,
+                                  float y) {
 #pragma clang fp contract(off)
     const int ix = (int)x, iy = (int)y;
-    const float dx = x - ix, dy = y - iy, dxdy = dx * dy;
-    const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
-    float3 t00, t10, t01, t11;
+    const float dx = x - ix, dy = y - iy;
     if (mode == 3) {
-        const float *imf = reinterpret_cast<const float *>(img);
-        auto at = [&](int xx, int yy) { return imf[(((yy >> 2) * tpr + (xx >> 3)) << 5) + ((yy & 3) << 3) + (xx & 7)]; };
-        auto grad = [](float a, float b) {
-            const float d = 0.5f * (a - b);
-            return (isnan(d) || fabsf(d) > 255.0f) ? 0.0f : d;
-        };
         float v[12];
-        v[0] = at(ix, iy - 1);
-        v[1] = at(ix + 1, iy - 1);
-        v[2] = at(ix - 1, iy);
-        v[3] = at(ix, iy);
-        v[4] = at(ix + 1, iy);
-        v[5] = at(ix + 2, iy);
-        v[6] = at(ix - 1, iy + 1);
-        v[7] = at(ix, iy + 1);
-        v[8] = at(ix + 1, iy + 1);
-        v[9] = at(ix + 2, iy + 1);
-        v[10] = at(ix, iy + 2);
-        v[11] = at(ix + 1, iy + 2);
-        t00 = make_float3(v[3], grad(v[4], v[2]), grad(v[7], v[0]));
-        t10 = make_float3(v[4], grad(v[5], v[3]), grad(v[8], v[1]));
-        t01 = make_float3(v[7], grad(v[8], v[6]), grad(v[10], v[3]));
-        t11 = make_float3(v[8], grad(v[9], v[7]), grad(v[11], v[4]));
-    } else if (mode == 2) {
-        const float4 *rec = img + ((size_t)iy * width + ix) * 4;
-        const float4 qi = rec[0], qx = rec[1], qy = rec[2];
-        t00 = make_float3(qi.x, qx.x, qy.x);
-        t10 = make_float3(qi.y, qx.y, qy.y);
-        t01 = make_float3(qi.z, qx.z, qy.z);
-        t11 = make_float3(qi.w, qx.w, qy.w);
-    } else if (mode == 1) {
-        t00 = tex<true, false>(img, tpr, ix, iy);
-        t10 = tex<true, false>(img, tpr, ix + 1, iy);
-        t01 = tex<true, false>(img, tpr, ix, iy + 1);
-        t11 = tex<true, false>(img, tpr, ix + 1, iy + 1);
-    } else {
-        t00 = tex<false, false>(img, tpr, ix, iy);
-        t10 = tex<false, false>(img, tpr, ix + 1, iy);
-        t01 = tex<false, false>(img, tpr, ix, iy + 1);
-        t11 = tex<false, false>(img, tpr, ix + 1, iy + 1);
+        load12(frame_rsrc(reinterpret_cast<const float *>(img), frame_stride * 16), (unsigned)tpr * 128u, ix, iy, v);
+        return bilin12(v, dx, dy);
     }
+    const float dxdy = dx * dy;
+    const float w11 = dxdy, w01 = dy - dxdy, w10 = dx - dxdy, w00 = 1 - dx - dy + dxdy;
+    const float3 t00 = tex(img, tpr, ix, iy), t10 = tex(img, tpr, ix + 1, iy), t01 = tex(img, tpr, ix, iy + 1),
+                 t11 = tex(img, tpr, ix + 1, iy + 1);
     return make_float3(w11 * t11.x + w01 * t01.x + w10 * t10.x + w00 * t00.x,
                        w11 * t11.y + w01 * t01.y + w10 * t10.y + w00 * t00.y,
                        w11 * t11.z + w01 * t01.z + w10 * t10.z + w00 * t00.z);
@@ -2353,7 +1840,7 @@ __global__ __launch_bounds__(256) void k_activate(ActParams P) {
                         oob = true;
                         continue;
                     }
-                    const float3 hc = sample33(img, P.img_mode, P.tpr, W.width, Ku, Kv);
+                    const float3 hc = sample33(img, P.img_mode, P.tpr, P.frame_stride, Ku, Kv);
                     if (!isfinite(hc.x)) {
                         oob = true;
                         continue;
@@ -2489,29 +1976,11 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
     P.pt_step[p] = -b * po[0] / (1 + P.lambda);
 }
 
-// image ingest: FrameHessian::dI (AoS [I, dx, dy]) -> [I, dx, dy, 0] texels in 2x4 tiles
-// (tiled = 1), row-major (0), or (2) one 64-byte quad record per pixel (x, y) holding the
-// bilinear footprint {(x,y), (x+1,y), (x,y+1), (x+1,y+1)} as [I x4][dx x4][dy x4][pad]: every
-// pattern pixel's four taps then come from one record (3 dwordx4 loads in one 64-byte sector)
-// instead of up to four cache lines.  4x the bytes of dI, resident once per keyframe.
-__global__ void k_quad_image(const float *__restrict__ src, float4 *dst, int w, int h) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= w * h) return;
-    const int x = i % w, y = i / w;
-    const int x1 = min(x + 1, w - 1), y1 = min(y + 1, h - 1);
-    const float *a = src + 3 * ((size_t)y * w + x), *b = src + 3 * ((size_t)y * w + x1),
-                *c = src + 3 * ((size_t)y1 * w + x), *d = src + 3 * ((size_t)y1 * w + x1);
-    float4 *o = dst + (size_t)i * 4;
-    o[0] = make_float4(a[0], b[0], c[0], d[0]);
-    o[1] = make_float4(a[1], b[1], c[1], d[1]);
-    o[2] = make_float4(a[2], b[2], c[2], d[2]);
-    o[3] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-// image layout 3: the intensity channel only, in 8x4-float tiles (one 128-byte line each, 1/4
-// of the float4 texel bytes); k_linearize_sp recomputes the gradients with makeImages' rule.
-// That is exact only if the caller's gradients ARE makeImages' (FrameHessian.cc:96-101): every
-// pixel the taps can reach (x in [1, w-2], y in [1, h-2]) is checked and *mismatch is set if not.
+// image layout 3 (default): the intensity channel only, band-interleaved (band_offset: an 8x4
+// pixel tile per 128-byte line, 1/4 of the float4 texel bytes); k_linearize recomputes the
+// gradients with makeImages' rule.  That is exact only if the caller's gradients ARE makeImages'
+// (FrameHessian.cc:96-101): every pixel the taps can reach (x in [1, w-2], y in [1, h-2]) is
+// checked and *mismatch is set if not (the context then falls back to layout 1).
 __global__ void k_intensity_image(const float *__restrict__ src, float *dst, int w, int h, int tpr8, int hp,
                                   int *mismatch) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2523,18 +1992,16 @@ __global__ void k_intensity_image(const float *__restrict__ src, float *dst, int
         const float *p = src + 3 * ((size_t)y * w + x);
         v = p[0];
         if (x >= 1 && x <= w - 2 && y >= 1 && y <= h - 2) {
-            float dx = 0.5f * (p[3] - p[-3]);
-            float dy = 0.5f * (p[3 * w] - p[-3 * w]);
-            if (isnan(dx) || fabsf(dx) > 255.0f) dx = 0;
-            if (isnan(dy) || fabsf(dy) > 255.0f) dy = 0;
+            const float dx = make_grad(p[3], p[-3]), dy = make_grad(p[3 * w], p[-3 * w]);
             if (__float_as_uint(dx) != __float_as_uint(p[1]) || __float_as_uint(dy) != __float_as_uint(p[2]))
                 atomicOr(mismatch, 1);
         }
     }
-    dst[(((y >> 2) * tpr8 + (x >> 3)) << 5) + ((y & 3) << 3) + (x & 7)] = v;
+    dst[band_offset(x, y, (unsigned)wp * 16u) >> 2] = v;
 }
 
-__global__ void k_tile_image(const float *__restrict__ src, float4 *dst, int w, int h, int tpr2, int hp, int tiled) {
+// image layout 1: FrameHessian::dI (AoS [I, dx, dy]) -> [I, dx, dy, 0] texels in 2x4 tiles
+__global__ void k_tile_image(const float *__restrict__ src, float4 *dst, int w, int h, int tpr2, int hp) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int wp = tpr2 * 2;
     if (i >= wp * hp) return;
@@ -2544,79 +2011,13 @@ __global__ void k_tile_image(const float *__restrict__ src, float4 *dst, int w, 
         const float *p = src + 3 * ((size_t)y * w + x);
         v = make_float4(p[0], p[1], p[2], 0.f);
     }
-    dst[tiled ? (((y >> 2) * tpr2 + (x >> 1)) << 3) + ((y & 3) << 1) + (x & 1) : y * wp + x] = v;
+    dst[(((y >> 2) * tpr2 + (x >> 1)) << 3) + ((y & 3) << 1) + (x & 1)] = v;
 }
 
-template <int W, bool T, bool L3>
-void launch_lin2(bool xcd, bool cf, int nb, hipStream_t st, const LinParams &L) {
-    if (xcd) {
-        if (cf) k_linearize<W, T, L3, true, true><<<nb, 256, 0, st>>>(L);
-        else k_linearize<W, T, L3, true, false><<<nb, 256, 0, st>>>(L);
-    } else {
-        if (cf) k_linearize<W, T, L3, false, true><<<nb, 256, 0, st>>>(L);
-        else k_linearize<W, T, L3, false, false><<<nb, 256, 0, st>>>(L);
-    }
-}
-template <int W>
-void launch_lin1(bool tiled, bool load3, bool xcd, bool cf, int nb, hipStream_t st, const LinParams &L) {
-    if (tiled) {
-        if (load3) launch_lin2<W, true, true>(xcd, cf, nb, st, L);
-        else launch_lin2<W, true, false>(xcd, cf, nb, st, L);
-    } else {
-        if (load3) launch_lin2<W, false, true>(xcd, cf, nb, st, L);
-        else launch_lin2<W, false, false>(xcd, cf, nb, st, L);
-    }
-}
-// variant = occupancy target in waves per SIMD (see DESIGN.md for the measured choice)
 template <bool kMarg>
-void launch_sp(int img_mode, bool xcd, int nb, hipStream_t st, const LinParams &L) {
-    const size_t lds = lin_lds_bytes(4);
-    if (img_mode == 3) {
-        if (xcd) k_linearize_sp<3, true, kMarg, false><<<nb, 256, lds, st>>>(L);
-        else k_linearize_sp<3, false, kMarg, false><<<nb, 256, lds, st>>>(L);
-    } else if (img_mode == 2) {
-        if (xcd) k_linearize_sp<2, true, kMarg, false><<<nb, 256, lds, st>>>(L);
-        else k_linearize_sp<2, false, kMarg, false><<<nb, 256, lds, st>>>(L);
-    } else if (img_mode == 1) {
-        if (xcd) k_linearize_sp<1, true, kMarg, false><<<nb, 256, lds, st>>>(L);
-        else k_linearize_sp<1, false, kMarg, false><<<nb, 256, lds, st>>>(L);
-    } else {
-        if (xcd) k_linearize_sp<0, true, kMarg, false><<<nb, 256, lds, st>>>(L);
-        else k_linearize_sp<0, false, kMarg, false><<<nb, 256, lds, st>>>(L);
-    }
-}
-// the fused (point-major) pass: one workgroup of `waves` wavefronts per 32-point block
-template <bool kMarg>
-void launch_fused(int img_mode, int waves, int nb, hipStream_t st, const LinParams &L) {
-    const size_t lds = lin_lds_bytes(waves);
-    const int th = 64 * waves;
-    if (img_mode == 3) k_linearize_sp<3, true, kMarg, true><<<nb, th, lds, st>>>(L);
-    else if (img_mode == 2) k_linearize_sp<2, true, kMarg, true><<<nb, th, lds, st>>>(L);
-    else if (img_mode == 1) k_linearize_sp<1, true, kMarg, true><<<nb, th, lds, st>>>(L);
-    else k_linearize_sp<0, true, kMarg, true><<<nb, th, lds, st>>>(L);
-}
-int allow_fused_lds(size_t bytes) {
-    if (bytes <= 64 * 1024) return 0;
-    const void *fns[] = {(const void *)k_linearize_sp<3, true, false, true>, (const void *)k_linearize_sp<2, true, false, true>,
-                         (const void *)k_linearize_sp<1, true, false, true>, (const void *)k_linearize_sp<0, true, false, true>,
-                         (const void *)k_linearize_sp<3, true, true, true>,  (const void *)k_linearize_sp<2, true, true, true>,
-                         (const void *)k_linearize_sp<1, true, true, true>,  (const void *)k_linearize_sp<0, true, true, true>};
-    for (const void *f : fns)
-        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
-            return fail(-2, "hipFuncSetAttribute (fused k_linearize LDS)");
-    return 0;
-}
-// marg: the marginalisation pass (addPoint<2> sums; sample-parallel kernel only)
-void launch_linearize(int variant, int img_mode, bool load3, bool xcd, bool cf, int nb, hipStream_t st,
-                      const LinParams &L, bool marg, int fused_waves) {
-    const bool tiled = img_mode == 1;
-    if (fused_waves > 0) {
-        if (marg) launch_fused<true>(img_mode, fused_waves, nb, st, L);
-        else launch_fused<false>(img_mode, fused_waves, nb, st, L);
-    } else if (marg) launch_sp<true>(img_mode, xcd, nb, st, L);
-    else if (variant == 3) launch_sp<false>(img_mode, xcd, nb, st, L);
-    else if (variant == 2) launch_lin1<4>(tiled, load3, xcd, cf, nb, st, L);
-    else launch_lin1<1>(tiled, load3, xcd, cf, nb, st, L);
+void launch_linearize(int img_mode, int nb, hipStream_t st, const LinParams &L) {
+    if (img_mode == 3) k_linearize<3, kMarg><<<nb, 256, kLinLdsBytes, st>>>(L);
+    else k_linearize<1, kMarg><<<nb, 256, kLinLdsBytes, st>>>(L);
 }
 
 // ============================================================================================
@@ -2670,24 +2071,7 @@ struct PendingEv {
 struct ldso_ba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;  // second stream of the pipelined window groups
-    hipEvent_t ev_fork = nullptr, ev_lin0 = nullptr, ev_join = nullptr;
-    int groups_req = 0;             // LDSO_BA_TUNE_PIPELINE_GROUPS (0 = automatic)
-    int groups = 1;                 // pipelined window groups per pass
-#ifndef LDSO_STITCH_SPLIT_DEFAULT
-#define LDSO_STITCH_SPLIT_DEFAULT 0
-#endif
-    bool stitch_split = LDSO_STITCH_SPLIT_DEFAULT;
-#ifndef LDSO_ITEM_ORDER_DEFAULT
-#define LDSO_ITEM_ORDER_DEFAULT 0
-#endif
-    int item_order = LDSO_ITEM_ORDER_DEFAULT;  // k_linearize chunk order: 0 target-major, 1 host-major
-#ifndef LDSO_FUSED_DEFAULT
-#define LDSO_FUSED_DEFAULT 0
-#endif
-    bool fused_req = LDSO_FUSED_DEFAULT;  // point-major fused pass (LDSO_BA_TUNE_FUSED), chosen at load
-    int fused_waves = 0;                  // > 0: the loaded layout is the fused one
-    DevBuf<int4> d_pblocks;  // Top half of k_stitch on stream2, overlapping k_point_sc (LDSO_BA_TUNE_STITCH_SPLIT)
+    int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
     std::vector<WinDev> wd;
@@ -2722,10 +2106,8 @@ struct ldso_ba_ctx {
     size_t sc_smem_max = 0;
     bool timing = false;
     unsigned timing_mask = ~0u;  // kernel slots bracketed by events when timing is on
-    int lin_variant = 3;
     int top_chunk = 0;  // residuals per k_linearize wave (0 = automatic); LDSO_BA_TUNE_TOP_CHUNK
-    int img_mode = 3;  // 0 row-major, 1 2x4 tiles, 2 quad records, 3 intensity only (LDSO_BA_TUNE_TILED_IMAGES)
-    bool load3 = false, xcd_remap = true, centre_first = true;  // measured best
+    int img_mode = 3;   // 3 intensity only (band_offset), 1 [I, dx, dy, 0] 2x4 tiles (LDSO_BA_TUNE_TILED_IMAGES)
     std::vector<PendingEv> pending;
     std::vector<hipEvent_t> ev_pool;
     double kms[kNumKernels] = {0};
@@ -2824,9 +2206,6 @@ void image_geometry(ldso_ba_ctx *c) {
     if (c->img_mode == 3) {
         c->tiles_per_row = (c->width + 7) / 8;
         c->frame_stride = (long long)c->tiles_per_row * 8 * c->padded_h / 4;
-    } else if (c->img_mode == 2) {
-        c->tiles_per_row = (c->width + 1) / 2;
-        c->frame_stride = (long long)c->npix * 4;
     } else {
         c->tiles_per_row = (c->width + 1) / 2;
         c->frame_stride = (long long)c->tiles_per_row * 2 * c->padded_h;
@@ -2853,11 +2232,9 @@ int stage_images(ldso_ba_ctx *c, const ldso_ba_window *ws, int n_windows, int *m
                 const long long n = (long long)c->tiles_per_row * 8 * c->padded_h;
                 k_intensity_image<<<(int)((n + 255) / 256), 256, 0, c->stream>>>(
                     stage, reinterpret_cast<float *>(dst), c->width, c->height, c->tiles_per_row, c->padded_h, flag);
-            } else if (c->img_mode == 2) {
-                k_quad_image<<<(c->npix + 255) / 256, 256, 0, c->stream>>>(stage, dst, c->width, c->height);
             } else {
                 k_tile_image<<<(int)((c->frame_stride + 255) / 256), 256, 0, c->stream>>>(
-                    stage, dst, c->width, c->height, c->tiles_per_row, c->padded_h, c->img_mode);
+                    stage, dst, c->width, c->height, c->tiles_per_row, c->padded_h);
             }
             e = hipGetLastError();
         }
@@ -2979,18 +2356,10 @@ int ldso_ba_create(int32_t device, ldso_ba_ctx **out) {
     ldso_ba_ctx *c = new ldso_ba_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_lin0, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e != hipSuccess) {
-        if (c->stream) (void)hipStreamDestroy(c->stream);
-        if (c->stream2) (void)hipStreamDestroy(c->stream2);
         delete c;
         return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
-    if (const char *v = getenv("LDSO_BA_LIN_VARIANT")) c->lin_variant = atoi(v);
-    if (const char *v = getenv("LDSO_BA_TILED")) c->img_mode = atoi(v);
     *out = c;
     return 0;
 }
@@ -2999,12 +2368,8 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     drain_events(c);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {c->ev_fork, c->ev_lin0, c->ev_join})
-        if (e) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->pin_sys) (void)hipHostFree(c->pin_sys);
     if (c->pin_xad) (void)hipHostFree(c->pin_xad);
     if (c->pin_step) (void)hipHostFree(c->pin_step);
@@ -3037,7 +2402,6 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_pt_rec.release();
     c->d_top_items.release();
     c->d_sc_items.release();
-    c->d_pblocks.release();
     c->d_adhtd.release();
     c->d_pair_items.release();
     c->d_host_items.release();
@@ -3085,14 +2449,13 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     } else {
         image_geometry(c);
     }
-    c->groups = c->groups_req ? c->groups_req : 1;
     c->wh.assign(n_windows, WinHost());
     c->wd.assign(n_windows, WinDev());
     c->sys_host_valid = false;
     c->energy_valid = false;
 
     // host-side layout
-    std::vector<int4> top_items, sc_items, pblocks;
+    std::vector<int4> top_items, sc_items;
     std::vector<int2> pair_items, host_items;
     std::vector<int> pair_win, frame_win, rs_point, rs_slot, pt_nres, pt_host;
     std::vector<unsigned long long> pt_tgt;
@@ -3221,63 +2584,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         const int nt = D.KP / 4;
         D.ntiles = nt * (nt + 1) / 2;
         smem_max = std::max(smem_max, sc_smem_bytes(D.KP));
-        if (c->fused_req) {
-            // Fused pass: point blocks of <= 32 points of one host (host order; they are also the
-            // SC items).  Each block has one "half" per target slot: the block's residuals to that
-            // target, contiguous in bucket (h, t).  Top slab items are numbered pair-major (a
-            // pair's items, one per block of its host, are contiguous for k_stitch); a half
-            // records its slab item.
-            D.top_item_base = (int)top_items.size();
-            std::vector<int> nblk(N, 0), hq0(N + 1, 0);
-            {
-                int q = 0;
-                for (int f = 0; f < N; f++) {
-                    hq0[f] = q;
-                    while (q < P && H.pt_host[q] == f) q++;
-                    nblk[f] = (q - hq0[f] + kFusedPts - 1) / kFusedPts;
-                }
-                hq0[N] = q;
-            }
-            std::vector<int> pair_first(N * N, 0);
-            int nslab = 0;
-            for (int b = 0; b < N * N; b++) {
-                const int hh = b % N, tt = b / N;
-                pair_first[b] = nslab;
-                if (hh != tt) nslab += nblk[hh];
-                pair_items.push_back(make_int2(D.top_item_base + pair_first[b], hh != tt ? nblk[hh] : 0));
-                pair_win.push_back(w);
-            }
-            D.sc_item_base = (int)sc_items.size();
-            std::vector<int> first_pos(N), cnt(N);
-            for (int f = 0; f < N; f++) {
-                const int first_sc = (int)sc_items.size();
-                for (int k = 0; k < nblk[f]; k++) {
-                    const int qs = hq0[f] + k * kFusedPts, npts = std::min(kFusedPts, hq0[f + 1] - qs);
-                    sc_items.push_back(make_int4(point_base + qs, npts, f, w));
-                    pblocks.push_back(make_int4(point_base + qs, npts, (int)top_items.size(), w));
-                    std::fill(first_pos.begin(), first_pos.end(), -1);
-                    std::fill(cnt.begin(), cnt.end(), 0);
-                    for (int q = qs; q < qs + npts; q++) {
-                        const int p = H.pt_orig[q];
-                        for (int kk = in.point_res_begin[p]; kk < in.point_res_begin[p + 1]; kk++) {
-                            const int tg = in.res_target[kk], pos = res_pos_of[kk];
-                            if (first_pos[tg] < 0 || pos < first_pos[tg]) first_pos[tg] = pos;
-                            cnt[tg]++;
-                        }
-                    }
-                    for (int sl = 0; sl < N - 1; sl++) {
-                        const int tg = sl < f ? sl : sl + 1;
-                        top_items.push_back(make_int4(res_base + (cnt[tg] ? first_pos[tg] : 0), cnt[tg],
-                                                      pair_base + f + N * tg,
-                                                      D.top_item_base + pair_first[f + N * tg] + k));
-                    }
-                }
-                host_items.push_back(make_int2(first_sc, (int)sc_items.size() - first_sc));
-                frame_win.push_back(w);
-            }
-            D.n_top_items = (int)top_items.size() - D.top_item_base;
-            D.n_sc_items = (int)sc_items.size() - D.sc_item_base;
-        } else {
         // top items: chunks of `chunk` residuals of one bucket (one wave each)
         D.top_item_base = (int)top_items.size();
         const size_t pi0 = pair_items.size();
@@ -3308,7 +2614,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
             }
         }
         D.n_sc_items = (int)sc_items.size() - D.sc_item_base;
-        }
         D.sc_slab_base = sc_slab_total;
         sc_slab_total += (long long)D.n_sc_items * D.ntiles * 16;
         D.sys_base = sys_total;
@@ -3342,12 +2647,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     c->sc_smem_max = smem_max;
 
     int rc = 0;
-    // fused pass: ceil((N-1)/2) waves, one target per half-wave
-    c->fused_waves = c->fused_req ? c->max_frames / 2 : 0;
-    if (c->fused_waves) {
-        rc = allow_fused_lds(lin_lds_bytes(c->fused_waves));
-        if (rc) return rc;
-    }
 #define ALLOC(buf, n)                   \
     do {                                \
         rc = (buf).alloc(n);            \
@@ -3382,7 +2681,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_pt_rec, std::max<size_t>(1, (size_t)rec_base * 4));
     ALLOC(c->d_top_items, std::max<size_t>(1, top_items.size()));
     ALLOC(c->d_sc_items, std::max<size_t>(1, sc_items.size()));
-    ALLOC(c->d_pblocks, std::max<size_t>(1, pblocks.size()));
     ALLOC(c->d_pair_items, pair_items.size());
     ALLOC(c->d_host_items, host_items.size());
     ALLOC(c->d_top_slab, std::max<size_t>(1, top_items.size() * kTopVals));
@@ -3427,7 +2725,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     UP(c->d_rs_newenergy, rs_energy);
     UP(c->d_top_items, top_items);
     UP(c->d_sc_items, sc_items);
-    UP(c->d_pblocks, pblocks);
     UP(c->d_pair_items, pair_items);
     UP(c->d_host_items, host_items);
 #undef UP
@@ -3546,8 +2843,6 @@ int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
 
 int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
-    if (c->img_mode >= 2 && c->lin_variant != 3 && !c->marg)
-        return fail(-1, "quad / intensity-only image layouts need LIN_VARIANT 3");
     HIP_TRY(hipSetDevice(c->device));
     c->sys_host_valid = false;
     c->energy_valid = false;
@@ -3578,12 +2873,9 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     L.tiles_per_row = c->tiles_per_row;
     L.fix = fix;
     L.accumulate = accumulate;
-    L.pblocks = c->d_pblocks.p;
-    L.pt_nres = c->d_pt_nres.p;
-    L.pt_tgt = c->d_pt_tgt.p;
-    L.pt_out = c->d_pt_out.p;
-    L.sc_slab = c->d_sc_slab.p;
-    L.shift_prior = c->marg ? 0 : 1;
+    L.item_base = 0;
+    L.n_items = c->n_top_items;
+    L.n_blocks = (L.n_items + 3) / 4;
     PointParams Pp;
     Pp.items = c->d_sc_items.p;
     Pp.wins = c->d_wins.p;
@@ -3594,6 +2886,8 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.pt_out = c->d_pt_out.p;
     Pp.sc_slab = c->d_sc_slab.p;
     Pp.shift_prior = c->marg ? 0 : 1;
+    Pp.item_base = 0;
+    Pp.n_items = c->n_sc_items;
     StitchParams Sp;
     Sp.wins = c->d_wins.p;
     Sp.pair_win = c->d_pair_win.p;
@@ -3609,79 +2903,28 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.sys = c->d_sys.p;
     Sp.win_energy = c->d_win_energy.p;
     Sp.accumulate = accumulate;
+    Sp.pair_base = 0;
+    Sp.win_base = 0;
+    Sp.n_win = c->n_win;
     int kp_max = 0, n_max = 2;
     for (const WinDev &D : c->wd) {
         kp_max = std::max(kp_max, D.KP);
         n_max = std::max(n_max, D.N);
     }
     const size_t st_smem = stitch_smem_bytes(kp_max, n_max, &Sp.th_cap);
-
-    // Window groups pipelined over two streams: group g runs its three kernels in order on
-    // stream g % 2, and stream 1 starts after group 0's k_linearize, so one group's k_point_sc
-    // and k_stitch (latency-bound, few waves) overlap the next group's k_linearize (HBM-bound).
-    const int G = std::max(1, std::min(c->groups, c->n_win));
-    if (G > 1) {
-        HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-        HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-    }
-    for (int g = 0; g < G; g++) {
-        const int w0 = (int)((long long)c->n_win * g / G), w1 = (int)((long long)c->n_win * (g + 1) / G);
-        const WinDev &A = c->wd[w0], &B = c->wd[w1 - 1];
-        hipStream_t st = (g & 1) ? c->stream2 : c->stream;
-        const int ti0 = A.top_item_base, ti1 = B.top_item_base + B.n_top_items;
-        const int si0 = A.sc_item_base, si1 = B.sc_item_base + B.n_sc_items;
-        const int p0 = A.pair_base, p1 = B.pair_base + B.N * B.N;
-        const bool fused = c->fused_waves > 0;
-        if (fused ? si1 > si0 : ti1 > ti0) {
-            // fused: one workgroup per point block (= SC item); else 4 chunks per workgroup
-            L.item_base = fused ? si0 : ti0;
-            L.n_items = fused ? si1 - si0 : ti1 - ti0;
-            L.n_blocks = fused ? L.n_items : (L.n_items + 3) / 4;
-            rc = timed_launch(c, 0, st, [&] {
-                launch_linearize(c->lin_variant, c->img_mode, c->load3, c->xcd_remap, c->centre_first, L.n_blocks, st,
-                                 L, c->marg, c->fused_waves);
-            });
-            if (rc) return rc;
-        }
-        if (G > 1 && g == 0) {  // stream 1 starts once group 0 is past its gather
-            HIP_TRY(hipEventRecord(c->ev_lin0, c->stream));
-            HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_lin0, 0));
-        }
-        Sp.pair_base = p0;
-        Sp.win_base = w0;
-        Sp.n_win = w1 - w0;
-        Sp.part = 0;
-        // One group: k_stitch's Top half and setNewFrameEnergyTH need only k_linearize, so they run
-        // on stream 2 beside k_point_sc; the SC half follows k_point_sc on the context stream.
-        const bool split = G == 1 && accumulate && c->stitch_split;
-        if (split) {
-            HIP_TRY(hipEventRecord(c->ev_lin0, st));
-            HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_lin0, 0));
-            Sp.part = 1;
-            rc = timed_launch(c, 2, c->stream2,
-                              [&] { k_stitch<<<Sp.n_win + p1 - p0, kStThreads, st_smem, c->stream2>>>(Sp); });
-            if (rc) return rc;
-            Sp.part = 2;
-            Sp.n_win = 0;
-        }
-        if (accumulate && si1 > si0 && !fused) {
-            Pp.item_base = si0;
-            Pp.n_items = si1 - si0;
-            rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
-            if (rc) return rc;
-        }
-        rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + p1 - p0, kStThreads, st_smem, st>>>(Sp); });
+    hipStream_t st = c->stream;
+    if (L.n_items > 0) {
+        rc = timed_launch(c, 0, st, [&] {
+            if (c->marg) launch_linearize<true>(c->img_mode, L.n_blocks, st, L);
+            else launch_linearize<false>(c->img_mode, L.n_blocks, st, L);
+        });
         if (rc) return rc;
-        if (split) {  // join
-            HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
-            HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
-        }
     }
-    if (G > 1) {  // join: the context stream orders everything that follows
-        HIP_TRY(hipEventRecord(c->ev_join, c->stream2));
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    if (accumulate && Pp.n_items > 0) {
+        rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
+        if (rc) return rc;
     }
-    return 0;
+    return timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + c->n_pairs, kStThreads, st_smem, st>>>(Sp); });
 }
 
 int ldso_ba_activate_points(ldso_ba_ctx *c, int32_t win, int32_t n, const ldso_ct_immature *pts, int32_t min_obs,
@@ -4124,35 +3367,15 @@ int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *c, const float *dev_buf, int32
 
 int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
     if (!c) return fail(-1, "null ctx");
-    if (key == LDSO_BA_TUNE_LIN_VARIANT) {
-        if (value < 1 || value > 3) return fail(-1, "lin variant must be 1, 2 or 3");
-        c->lin_variant = value;
-        return 0;
-    }
     if (key == LDSO_BA_TUNE_TILED_IMAGES) {
         if (c->n_win) return fail(-1, "image layout must be chosen before ldso_ba_load");
-        if (value < 0 || value > 3) return fail(-1, "image layout must be 0, 1, 2 or 3");
+        if (value != 1 && value != 3) return fail(-1, "image layout must be 1 or 3");
         c->img_mode = value;
-        return 0;
-    }
-    if (key == LDSO_BA_TUNE_PIPELINE_GROUPS) {
-        if (value < 0 || value > 64) return fail(-1, "groups must be in [0, 64]");
-        c->groups_req = value;
-        c->groups = value ? value : 1;
         return 0;
     }
     if (key == LDSO_BA_TUNE_ITEM_ORDER) {
         if (c->n_win) return fail(-1, "item order must be chosen before ldso_ba_load");
         c->item_order = value != 0;
-        return 0;
-    }
-    if (key == LDSO_BA_TUNE_FUSED) {
-        if (c->n_win) return fail(-1, "fused pass must be chosen before ldso_ba_load");
-        c->fused_req = value != 0;
-        return 0;
-    }
-    if (key == LDSO_BA_TUNE_STITCH_SPLIT) {
-        c->stitch_split = value != 0;
         return 0;
     }
     if (key == LDSO_BA_TUNE_TIMING_MASK) {
@@ -4163,18 +3386,6 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
         if (value != 0 && value != 16 && value != 32 && value != 64) return fail(-1, "chunk must be 0, 16, 32 or 64");
         if (c->n_win) return fail(-1, "chunk size must be chosen before ldso_ba_load");
         c->top_chunk = value;
-        return 0;
-    }
-    if (key == LDSO_BA_TUNE_LOAD3) {
-        c->load3 = value != 0;
-        return 0;
-    }
-    if (key == LDSO_BA_TUNE_XCD_REMAP) {
-        c->xcd_remap = value != 0;
-        return 0;
-    }
-    if (key == LDSO_BA_TUNE_CENTRE_FIRST) {
-        c->centre_first = value != 0;
         return 0;
     }
     return fail(-1, "unknown tuning key");

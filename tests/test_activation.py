@@ -76,7 +76,7 @@ def test_oracle_activation_outliers_fail(built):
 # GPU: ldso_ba_activate_points against the oracle
 # ------------------------------------------------------------------------------------------
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,img_mode", [(dict(n_frames=7, n_points=2000, seed=1), m) for m in (3, 0, 1, 2)] +
+@pytest.mark.parametrize("cfg,img_mode", [(dict(n_frames=7, n_points=2000, seed=1), m) for m in (3, 1)] +
                          [(dict(n_frames=11, n_points=3000, seed=3), 3)])
 def test_gpu_activation_matches_oracle(built, cfg, img_mode):
     from ldso_amd import BAContext
