@@ -18,6 +18,8 @@ from ldso_amd import BAContext, synth
 B = WINDOWS
 ws = [synth.make_window(**synth.S7, seed=1000 + i) for i in range(B)]
 c = BAContext(0)
+if os.environ.get("LDSO_AB_TAPS"):
+    c.set_tuning(12, int(os.environ["LDSO_AB_TAPS"]))
 c.load(ws)
 for _ in range(3):
     c.linearize()
@@ -54,7 +56,10 @@ def main():
     res = {l: [] for l in a.libs}
     for _ in range(a.rounds):
         for l in a.libs:
-            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(l))
+            path, _, taps = l.partition(":")
+            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(path))
+            if taps:
+                env["LDSO_AB_TAPS"] = taps
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
             if p.returncode != 0 or not line:
@@ -67,7 +72,7 @@ def main():
             for mode, kt in r.items():
                 for k, v in kt.items():
                     best[(mode, k)] = min(best.get((mode, k), 1e9), v)
-        print(os.path.basename(l), " ".join(f"{m}:{k}={v:.1f}us" for (m, k), v in sorted(best.items())))
+        print(l, " ".join(f"{m}:{k}={v:.1f}us" for (m, k), v in sorted(best.items())))
 
 
 if __name__ == "__main__":
