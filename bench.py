@@ -6,12 +6,15 @@ seven kernels on the context's stream).  Each GPU holds `--windows` independent 
 (7 keyframes, 2000 active points, 640x480, distinct seeds), so per-GPU work is fixed as GPUs
 are added ("scaling": "weak"; no collective is needed between independent windows).
 
-value  = residuals processed by all ranks per step / max-over-ranks step time.
 roofline: dominant kernel k_linearize, algorithmic bytes per residual
           = 276 B (23 unique 12-B texels) + 8 B state + 88 B/(N-1) point data, times the
           residuals that do gather (not OOB before the pass), / its mean HIP-event duration.
-cpu_baseline: the oracle restatement (oracle/, 6-thread IndexThreadReduce like the reference,
-          NUM_THREADS = 6) on one S7 window for ~10 s, same pass.
+value  = residuals that gather in the pass (R_active: not OOB going in, OOB being sticky within
+          optimize()) of all ranks per step / max-over-ranks step time.
+cpu_baseline: the oracle restatement (oracle/cpu_baseline.py) compiled -O3 -march=native on the
+          box, on one S7 window, median pass over >= 10 s: (ii) one pinned worker per physical
+          core of socket 0 (the "single-socket" figure of SURVEY §8d) and (i) 6 threads as the
+          reference's IndexThreadReduce.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--windows B] [--mode replicas|shard]
 """
@@ -48,22 +51,18 @@ def load_pmc(workload):
     return None
 
 
-def cpu_baseline(seconds=10.0, threads=6):
-    import oracle
-    from ldso_amd import synth
+def cpu_baseline(seconds=10.0):
+    """oracle/cpu_baseline.py in a child process (it pins its own threads): the restatement built
+    -O3 -march=native on this host, (i) 6 threads as the reference's IndexThreadReduce, (ii) one
+    worker per physical core of socket 0 within the job's CPU share, pinned.  None on failure."""
+    import subprocess
 
-    w = synth.make_window(**synth.S7, seed=1)
-    ow = oracle.OracleWindow(w, threads=threads)
-    ow.time_iterations(1)  # warm-up (thread pool spin-up, page faults)
-    iters, el = 0, 0.0
-    while el < seconds:
-        n = max(1, iters or 4)
-        el += ow.time_iterations(n)
-        iters += n
-    R = w.n_residuals
-    return {"value": R * iters / el, "unit": "point-residuals/s", "cores": threads, "kind": "port",
-            "sample": f"1 S7 window (seed 1, R={R}), {iters} passes of linearizeAll+applyRes+"
-                      f"accumulate{{AF,LF,SCF}}+stitch in {el:.1f} s, {threads}-thread IndexThreadReduce"}
+    try:
+        p = subprocess.run([sys.executable, "-m", "oracle.cpu_baseline", "--seconds", str(seconds)], cwd=ROOT,
+                           capture_output=True, text=True, timeout=600)
+        return json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else None
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return None
 
 
 def secondary_s11(device, windows=8, steps=20):
@@ -387,17 +386,17 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        tot = torch.tensor([R_rank], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([R_rank, n_gather], dtype=torch.float64, device="cuda")
         dist.all_reduce(tot)
-        R_total = float(tot.item())
+        R_total, G_total = float(tot[0].item()), float(tot[1].item())
     else:
-        R_total = float(R_rank)
+        R_total, G_total = float(R_rank), float(n_gather)
     if args.mode == "shard":
         R_job = float(sum(w.n_residuals for w in windows))  # each residual counted once
     else:
         R_job = R_total
     ms_step = 1e3 * el / args.steps
-    value = R_job * args.steps / el
+    value = G_total * args.steps / el  # R_active: residuals that gather (OOB ones return at once)
 
     klin_ms, klin_n = ktimes["k_linearize"]
     klin_avg_s = klin_ms / max(1, klin_n) / 1e3
@@ -456,11 +455,11 @@ def main():
         tracker["trace_new_coarse"] = trace_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
         tracker["activate_points"] = activation_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
 
-    cpu = cpu16 = None
+    cpu = cpu6 = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.cpu_seconds)  # the reference's own IndexThreadReduce (NUM_THREADS = 6)
-        # every core this job may use on the GPU box's host (16 per GPU there)
-        cpu16 = cpu_baseline(args.cpu_seconds, threads=min(16, os.cpu_count() or 16))
+        cb = cpu_baseline(args.cpu_seconds)
+        if cb:
+            cpu, cpu6 = cb["socket_pinned"], cb["six_threads"]
 
     if rank == 0:
         out = {
@@ -482,6 +481,7 @@ def main():
                 "points_per_window": P,
                 "windows_per_gpu": B,
                 "residuals_per_step": int(R_job),
+                "residuals_active_per_step": int(G_total),
                 "image": "640x480",
                 "parallelism": f"{args.mode}{world}" if world > 1 else "single",
             },
@@ -503,12 +503,12 @@ def main():
             "s11": s11,
             "tracker": tracker,
             "cpu_baseline": cpu,
-            "cpu_baseline_all_job_cores": cpu16,
+            "cpu_baseline_six_threads": cpu6,
         }
         if cpu is not None:
             out["speedup_vs_cpu"] = value / cpu["value"]
-        if cpu16 is not None:
-            out["speedup_vs_cpu_all_job_cores"] = value / cpu16["value"]
+        if cpu6 is not None:
+            out["speedup_vs_cpu_six_threads"] = value / cpu6["value"]
         print(json.dumps(out))
     ctx.close()
     if dist is not None:

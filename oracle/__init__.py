@@ -316,3 +316,43 @@ def ip_trace(dI0, w, h, krki, kt, aff, pts):
                           _p(np.ascontiguousarray(aff, np.float32), f32p), int(pts.size), pts.ctypes.data,
                           _p(counts, i32p))
     return counts
+
+
+# ---- CPU baseline timing build (bench.py cpu_baseline leg only) -----------------------------
+NATIVE_FLAGS = ["-O3", "-march=native", "-std=c++17", "-fPIC", "-shared"]
+
+
+def build_timing_lib(out_path: str) -> str:
+    """The same restatement compiled for speed the way the reference is (CMakeLists.txt:55-56:
+    -O3 -march=native; FP contraction left at the compiler default, i.e. allowed).  Built on
+    the machine that runs it; used for timing only, never as the checker."""
+    src = [os.path.join(HERE, "ldso_oracle.cpp"), os.path.join(HERE, "ldso_oracle_tracker.cpp")]
+    subprocess.run(["g++"] + NATIVE_FLAGS + ["-o", out_path] + src + ["-lpthread"], check=True, timeout=300)
+    return out_path
+
+
+class TimingWindow:
+    """oracle_create / oracle_time_iterations through a separately loaded timing build."""
+
+    def __init__(self, window, threads: int, lib_path: str):
+        self._lib = C.CDLL(lib_path)
+        self._lib.oracle_set_threads.argtypes = [C.c_int]
+        self._lib.oracle_create.restype = C.c_void_p
+        self._lib.oracle_create.argtypes = [C.c_void_p]
+        self._lib.oracle_destroy.argtypes = [C.c_void_p]
+        self._lib.oracle_time_iterations.restype = C.c_double
+        self._lib.oracle_time_iterations.argtypes = [C.c_void_p, C.c_int]
+        self._lib.oracle_set_threads(int(threads))
+        s = window.c_struct()
+        self._h = self._lib.oracle_create(C.byref(s))
+        window._keep = []
+        if not self._h:
+            raise ValueError("oracle_create rejected the window")
+
+    def time_iterations(self, iters: int) -> float:
+        return float(self._lib.oracle_time_iterations(self._h, int(iters)))
+
+    def close(self):
+        if self._h:
+            self._lib.oracle_destroy(self._h)
+            self._h = None
