@@ -1,28 +1,44 @@
 /*
  * energy_functional.h -- C++ host face of the MI355X bundle-adjustment hot path.
  *
- * Mirrors the class surface LDSO's FullSystem drives once per Gauss-Newton iteration (names,
- * fields and call order of the reference; paths relative to n-lalanne/LDSO):
+ * The class surface LDSO's FullSystem drives (names, members, argument order and shared_ptr /
+ * weak_ptr ownership of the reference; paths relative to n-lalanne/LDSO):
  *
- *   FrameHessian         include/internal/FrameHessian.h      (state, state_zero, dI, frameEnergyTH)
- *   PointHessian         include/internal/PointHessian.h      (u, v, idepth, color, weights, residuals)
- *   PointFrameResidual   include/internal/Residuals.h:42-131   (state_*, centerProjectedTo, JpJdF)
- *   CalibHessian         include/internal/CalibHessian.h       (value_scaledf)
- *   EnergyFunctional     include/internal/OptimizationBackend/EnergyFunctional.h:55-149
- *                        insertFrame / insertPoint / insertResidual / dropResidual / removePoint /
- *                        makeIDX / solveSystemF / resubstituteF_MT / lastX
+ *   EnergyFunctional     include/internal/OptimizationBackend/EnergyFunctional.h:55-186
+ *                        insertResidual / insertFrame / dropResidual / marginalizeFrame /
+ *                        removePoint / marginalizePointsF / dropPointsF / solveSystemF /
+ *                        calcMEnergyF / calcLEnergyF_MT / makeIDX / setDeltaF / setAdjointsF /
+ *                        resubstituteF_MT; public frames, nPoints, nFrames, nResiduals, HM, bM,
+ *                        resInA/L/M, lastX, lastNullspaces_*, connectivityMap
+ *   PointFrameResidual   include/internal/Residuals.h:42-131 (linearize, resetOOB, applyRes,
+ *                        setState, isActive, fixLinearizationF, takeData's JpJdF, state_*)
+ *   FrameHessian         include/internal/FrameHessian.h (state, state_zero, step, prior, delta,
+ *                        delta_prior, idx, frameID, frameEnergyTH, flaggedForMarginalization, dI)
+ *   PointHessian         include/internal/PointHessian.h (u, v, idepth*, color, weights, priorF,
+ *                        deltaF, residuals, HdiF, bdSumF, idepth_hessian, step, setIdepth*)
+ *   CalibHessian         include/internal/CalibHessian.h (value_scaledf, value_minus_value_zero, step)
  *   + linearizeAll(fix)  FullSystem::linearizeAll (FullSystem.cc:1716-1769) with applyRes and
  *                        setNewFrameEnergyTH, and the accumulate{AF,LF,SCF} of the next solve
  *
- * Every call goes through the C ABI of include/ldso_ba.h into the HIP kernels; nothing here
- * computes on the CPU except packing.  Objects are owned by the caller (the reference holds
- * them in shared_ptr; here raw pointers that must outlive their EnergyFunctional membership).
- * Like the reference, nothing throws: failures leave ok() false and lastError() set.
+ * It lives in namespace ldso_amd, not ldso::internal: the reference's own FrameHessian /
+ * PointHessian carry the frontend's state (images, pyramids, features) and stay where they are;
+ * INTEGRATION.md §3 gives the literal forwarding bodies that make the reference's
+ * EnergyFunctional.cc / Residuals.cc methods call these.  Eigen's VecX / MatXX are mirrored by
+ * the small row-major VecX / MatXX below (this header needs no Eigen).
+ *
+ * Every number comes from the HIP path or from the library's host helpers through the C ABI of
+ * include/ldso_ba.h; nothing here computes except packing.  Like the reference, nothing throws:
+ * failures leave ok() false and lastError() set.
  */
 #ifndef LDSO_AMD_ENERGY_FUNCTIONAL_H_
 #define LDSO_AMD_ENERGY_FUNCTIONAL_H_
 
 #include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstddef>
+#include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -30,54 +46,156 @@
 
 namespace ldso_amd {
 
+using std::shared_ptr;
+using std::weak_ptr;
+
+constexpr int CPARS = 4;                  // NumTypes.h:25
+constexpr float SCALE_IDEPTH = 1.0f;      // Settings.h:28
 using Vec3 = std::array<double, 3>;
 
-enum ResState { IN = 0, OOB = 1, OUTLIER = 2 };  // Residuals.h:33
+// Eigen::VectorXd stand-in (the members the reference's callers use)
+struct VecX {
+    std::vector<double> v;
+    VecX() = default;
+    explicit VecX(int n, double x = 0.0) : v((size_t)n, x) {}
+    static VecX Zero(int n) { return VecX(n); }
+    static VecX Constant(int n, double x) { return VecX(n, x); }
+    int size() const { return (int)v.size(); }
+    double &operator[](int i) { return v[(size_t)i]; }
+    double operator[](int i) const { return v[(size_t)i]; }
+    double &operator()(int i) { return v[(size_t)i]; }
+    double operator()(int i) const { return v[(size_t)i]; }
+    double *data() { return v.data(); }
+    const double *data() const { return v.data(); }
+    double dot(const VecX &o) const {
+        double s = 0;
+        for (size_t i = 0; i < v.size(); i++) s += v[i] * o.v[i];
+        return s;
+    }
+    double norm() const { return std::sqrt(dot(*this)); }
+};
+
+// Eigen::MatrixXd stand-in, row-major
+struct MatXX {
+    int r = 0, c = 0;
+    std::vector<double> a;
+    MatXX() = default;
+    MatXX(int rows, int cols) : r(rows), c(cols), a((size_t)rows * cols, 0.0) {}
+    static MatXX Zero(int rows, int cols) { return MatXX(rows, cols); }
+    int rows() const { return r; }
+    int cols() const { return c; }
+    double &operator()(int i, int j) { return a[(size_t)i * c + j]; }
+    double operator()(int i, int j) const { return a[(size_t)i * c + j]; }
+    double *data() { return a.data(); }
+    const double *data() const { return a.data(); }
+};
+
+enum ResState { IN = 0, OOB, OUTLIER };  // Residuals.h:33
+// Point::PointStatus (include/Point.h): the states EnergyFunctional reads through frame->features
+// in makeIDX / marginalizePointsF / dropPointsF; here a field of the PointHessian itself
+enum class PointStatus { ACTIVE = 0, OUTLIER, OUT, MARGINALIZED };
 
 struct CalibHessian {
-    int wG0 = 0, hG0 = 0;                            // level-0 image size (GlobalCalib wG[0], hG[0])
-    float value_scaledf[4] = {0, 0, 0, 0};           // fxl, fyl, cxl, cyl
-    float value_minus_value_zero[4] = {0, 0, 0, 0};  // cDeltaF source (EnergyFunctional::setDeltaF)
+    int wG0 = 0, hG0 = 0;                             // level-0 image size (GlobalCalib wG[0], hG[0])
+    float value_scaledf[4] = {0, 0, 0, 0};            // fxl, fyl, cxl, cyl
+    double value_minus_value_zero[4] = {0, 0, 0, 0};  // cDeltaF source (setDeltaF)
+    double step[4] = {0, 0, 0, 0};                    // resubstituteF_MT: -x.head<CPARS>()
 };
 
 struct FrameHessian {
-    int idx = -1;                      // position in the window (EnergyFunctional::makeIDX)
+    int idx = 0;                       // position in the window (makeIDX)
+    int frameID = 0;                   // keyframe id: 0 carries getPrior()'s strong pose prior
+    bool flaggedForMarginalization = false;
     double worldToCam_evalPT[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};  // [R | t], row-major
     double state[10] = {0};            // FrameHessian::state (xi, a, b, ...)
     double state_zero[10] = {0};       // FrameHessian::state_zero
+    double step[10] = {0};             // resubstituteF_MT: -x.segment<8>(CPARS + 8 idx)
     double ab_exposure = 1;
-    bool isFirstFrame = false;         // frame->id == 0: the strong priors of getPrior()
     const float *dI = nullptr;         // level-0 [I, dx, dy] per pixel (FrameHessian::dI)
-    float frameEnergyTH = 8 * 8 * 8;   // FrameHessian::frameEnergyTH (written back for the newest frame)
+    float frameEnergyTH = 8 * 8 * 8;   // written back for the newest frame by linearizeAll
+    double prior[8] = {0}, delta[8] = {0}, delta_prior[8] = {0};  // takeData / setDeltaF
+    // FrameHessian::takeData (FrameHessian.cc:131-135): prior, delta, delta_prior
+    void takeData();
 };
 
+class EnergyFunctional;
 struct PointFrameResidual;
 
 struct PointHessian {
-    FrameHessian *host = nullptr;
+    weak_ptr<FrameHessian> host;
     float u = 0, v = 0;
-    float idepth_scaled = 0, idepth_zero_scaled = 0;
+    float idepth = 0, idepth_zero = 0, idepth_scaled = 0, idepth_zero_scaled = 0;
     float color[8] = {0}, weights[8] = {0};
     float priorF = 0, deltaF = 0;
-    std::vector<PointFrameResidual *> residuals;
+    std::vector<shared_ptr<PointFrameResidual>> residuals;
     // written back by linearizeAll / resubstituteF_MT
     float HdiF = 0, bdSumF = 0, idepth_hessian = 0, step = 0;
+    PointStatus status = PointStatus::ACTIVE;
+    bool alreadyRemoved = false;
     int idxInPoints = -1;
+    // PointHessian::setIdepth / setIdepthZero (PointHessian.h)
+    void setIdepth(float x) {
+        idepth = x;
+        idepth_scaled = SCALE_IDEPTH * x;
+    }
+    void setIdepthZero(float x) {
+        idepth_zero = x;
+        idepth_zero_scaled = SCALE_IDEPTH * x;
+    }
 };
 
 struct PointFrameResidual {
-    PointHessian *point = nullptr;
-    FrameHessian *host = nullptr, *target = nullptr;
-    ResState state_state = IN, state_NewState = OUTLIER;
-    float state_energy = 0, state_NewEnergy = 0, state_NewEnergyWithOutlier = 0;
+    PointFrameResidual() = default;
+    PointFrameResidual(shared_ptr<PointHessian> point_, shared_ptr<FrameHessian> host_,
+                       shared_ptr<FrameHessian> target_)
+        : point(point_), host(host_), target(target_) {
+        resetOOB();
+    }
+
+    // Residuals.cc:15-217.  The device linearises residuals a window at a time: this runs the
+    // linearizeAll pass of the EnergyFunctional the residual was inserted into (applyRes
+    // included, as every reference call site does next) and returns this residual's energy.
+    double linearize(shared_ptr<CalibHessian> &HCalib);
+    // Residuals.h:63-68
+    void resetOOB() {
+        state_NewEnergy = state_energy = 0;
+        state_NewState = OUTLIER;
+        setState(IN);
+    }
+    // Residuals.h:70-88 (the device pass has already taken the Jacobians: JpJdF below)
+    void applyRes(bool copyJacobians) {
+        if (copyJacobians) {
+            if (state_state == OOB) return;
+            isActiveAndIsGoodNEW = state_NewState == IN;
+        }
+        state_state = state_NewState;
+        state_energy = state_NewEnergy;
+    }
+    void setState(ResState s) { state_state = s; }
+    bool isActive() const { return isActiveAndIsGoodNEW; }
+    // Residuals.cc:219-245: marks the residual linearised; its res_toZeroF is formed on the
+    // device by marginalizePointsF (ldso_ba_marginalize_points), the only consumer.
+    void fixLinearizationF(shared_ptr<EnergyFunctional> ef);
+
+    ResState state_state = OUTLIER;
+    double state_energy = 0;
+    ResState state_NewState = OUTLIER;
+    double state_NewEnergy = 0;
+    double state_NewEnergyWithOutlier = 0;
+    weak_ptr<PointHessian> point;
+    weak_ptr<FrameHessian> host;
+    weak_ptr<FrameHessian> target;
+    bool isNew = true;
     float centerProjectedTo[3] = {0, 0, 0};
     float relBS = 0;                  // linearizeAll_Reductor's maxRelBaseline term (fix pass)
-    bool isNew = true;
-    bool isActiveAndIsGoodNEW = false;
+    int hostIDX = 0, targetIDX = 0;
     float JpJdF[8] = {0};
+    bool isLinearized = false;
+    bool isActiveAndIsGoodNEW = false;
+    weak_ptr<EnergyFunctional> ef;    // set by EnergyFunctional::insertResidual
 };
 
-class EnergyFunctional {
+class EnergyFunctional : public std::enable_shared_from_this<EnergyFunctional> {
 public:
     explicit EnergyFunctional(int device = 0);
     ~EnergyFunctional();
@@ -87,49 +205,82 @@ public:
     bool ok() const { return err_.empty(); }
     const std::string &lastError() const { return err_; }
 
-    // structure (EnergyFunctional.cc:45-108, 500-521); any change re-uploads the window
-    void insertFrame(FrameHessian *fh, const CalibHessian &Hcalib);
-    void insertPoint(PointHessian *ph);
-    void insertResidual(PointFrameResidual *r);
-    void dropResidual(PointFrameResidual *r);
-    void removePoint(PointHessian *p);
+    // ---- EnergyFunctional.h:55-186 -------------------------------------------------------
+    void insertResidual(shared_ptr<PointFrameResidual> r);
+    void insertFrame(shared_ptr<FrameHessian> fh, shared_ptr<CalibHessian> Hcalib);
+    void dropResidual(shared_ptr<PointFrameResidual> r);
+    void marginalizeFrame(shared_ptr<FrameHessian> fh);
+    void removePoint(shared_ptr<PointHessian> ph);
+    // every allPoints entry with status MARGINALIZED: FullSystem::flagPointsForRemoval's
+    // resetOOB / linearize / applyRes / fixLinearizationF of its residuals and the addPoint<2> +
+    // SC addPoint(p, false) + stitch of marginalizePointsF, in one device call; then
+    // HM += margWeightFac H, bM += margWeightFac b, removePoint, makeIDX
+    void marginalizePointsF();
+    void dropPointsF();  // removes the points with status OUTLIER or OUT
+    void solveSystemF(int iteration, double lambda, shared_ptr<CalibHessian> HCalib);
+    void solveSystemF(int iteration, double lambda, shared_ptr<CalibHessian> HCalib, std::nullptr_t /*HInertial*/) {
+        solveSystemF(iteration, lambda, HCalib);
+    }
+    double calcMEnergyF();
+    double calcLEnergyF_MT();
     void makeIDX();
-    void setCalib(const CalibHessian &Hcalib);
+    void setDeltaF(shared_ptr<CalibHessian> HCalib);
+    void setAdjointsF(shared_ptr<CalibHessian> Hcalib);
+    void resubstituteF_MT(const VecX &x, shared_ptr<CalibHessian> HCalib, bool MT = true);
 
-    // PointFrameResidual::resetOOB for every residual (FullSystem.cc:876-879)
+    // ---- FullSystem-side passes served by the device ---------------------------------------
+    // PointHessian activation (FullSystem::activatePointsMT adds it to its host's features,
+    // which makeIDX then collects)
+    void insertPoint(shared_ptr<PointHessian> ph);
+    // PointFrameResidual::resetOOB for every active residual (FullSystem.cc:866-869)
     void resetOOB();
     // FullSystem::linearizeAll(fix) + applyRes + setNewFrameEnergyTH; with fix = false also the
     // accumulation of the stitched system for the following solveSystemF.  Returns (E, 0, #IN).
     Vec3 linearizeAll(bool fixLinearization);
-    // EnergyFunctional::solveSystemF (non-VI, FIX_LAMBDA, ORTHOGONALIZE_X_LATER): fills lastX
-    void solveSystemF(int iteration, double lambda);
-    // EnergyFunctional::resubstituteF_MT: frame steps are -lastX, point steps go to p->step
-    void resubstituteF_MT(const std::vector<double> &x, double lambda);
 
-    int nFrames = 0, nPoints = 0, nResiduals = 0;
-    std::vector<FrameHessian *> frames;
-    std::vector<PointHessian *> allPoints;
-    std::vector<double> lastX;
-    // last stitched system (row-major (8N+4)^2 / (8N+4)), as accumulateAF/LF/SCF leave them
-    std::vector<double> HA_top, bA_top, HL_top, bL_top, H_sc, b_sc;
+    std::vector<shared_ptr<FrameHessian>> frames;
+    int nPoints = 0, nFrames = 0, nResiduals = 0;
+    MatXX HM = MatXX::Zero(CPARS, CPARS);  // marginalisation prior H
+    VecX bM = VecX::Zero(CPARS);           // marginalisation prior b
+    int resInA = 0, resInL = 0, resInM = 0;
+    VecX lastX;
+    std::vector<VecX> lastNullspaces_forLogging, lastNullspaces_pose, lastNullspaces_scale, lastNullspaces_affA,
+        lastNullspaces_affB;
+    // (host frameID << 32) + target frameID -> {active residuals, marginalised residuals}
+    std::map<uint64_t, std::array<int, 2>> connectivityMap;
+    std::vector<shared_ptr<PointHessian>> allPoints;
+    std::vector<shared_ptr<PointHessian>> allPointsToMarg;
+    // setDeltaF / setAdjointsF results (adHTdeltaF [N*N][8] float, index h + N t)
+    std::vector<float> adHTdeltaF;
+    float cDeltaF[4] = {0, 0, 0, 0};
+    std::vector<double> adHost, adTarget;  // [N*N][64]
+    double cPrior[4] = {0, 0, 0, 0};
+    // the stitched blocks of the last solveSystemF (row-major (8N+4)^2 / (8N+4))
+    MatXX HA_top, HL_top, H_sc;
+    VecX bA_top, bL_top, b_sc;
 
     ldso_ba_ctx *context() { return ctx_; }
 
 private:
     bool upload();
     void fail(const char *what);
+    void packFrames(std::vector<ldso_ba_frame_state> &fs) const;
     ldso_ba_ctx *ctx_ = nullptr;
+    ldso_ba_ctx *margCtx_ = nullptr;
+    int device_ = 0;
+    double currentLambda_ = 0;  // EnergyFunctional::currentLambda (set by solveSystemF)
     CalibHessian calib_;
     bool dirty_ = true;
     std::string err_;
-    // SoA mirror (ldso_ba_window)
+    // SoA mirror (ldso_ba_window) of the loaded window
     std::vector<ldso_ba_frame_state> fs_;
-    std::vector<float> dI_, frameTH_, precalc_, pointData_, resEnergy_, cDelta_;
+    std::vector<float> dI_, frameTH_, precalc_, pointData_, resEnergy_;
     std::vector<double> adH_, adT_, cPrior_, fPrior_, fDelta_, fDeltaPrior_;
     std::vector<int32_t> pointHost_, resBegin_, resTarget_;
     std::vector<int8_t> resState_;
     std::vector<uint8_t> resFlags_;
     std::vector<PointFrameResidual *> resPtr_;
+    std::vector<PointHessian *> ptPtr_;
     int width_ = 0, height_ = 0;
 };
 

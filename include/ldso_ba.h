@@ -155,6 +155,26 @@ int ldso_ba_marginalize_frame(int32_t n_frames, int32_t idx, const double *HM, c
                               const double *prior, const double *delta_prior, double *HM_out,
                               double *bM_out);
 
+/* EnergyFunctional::setDeltaF's adHTdeltaF (EnergyFunctional.cc:523-533): [N*N][8] float (index
+ * h + N t) = delta_h^T adHostF + delta_t^T adTargetF, from the frames' delta [N][8]
+ * (ldso_ba_frame_take_data) and the adjoints of ldso_ba_set_adjoints. */
+int ldso_ba_ad_ht_delta(int32_t n_frames, const double *delta, const double *ad_host, const double *ad_target,
+                        float *out);
+
+/* EnergyFunctional::calcMEnergyF (EnergyFunctional.cc:473-479): out = d^T (2 bM + HM d), d =
+ * [cDeltaF; delta of every frame] (getStitchedDeltaF), HM row-major (8N+4)^2. */
+int ldso_ba_calc_m_energy(int32_t n_frames, const double *HM, const double *bM, const float *c_delta,
+                          const double *delta, double *out);
+
+/* EnergyFunctional::calcLEnergyF_MT (EnergyFunctional.cc:481-498, calcLEnergyPt :751-806): frame
+ * priors (prior, delta_prior [N][8]), calibration prior (cPrior [4], cDeltaF [4]) and every
+ * point's deltaF^2 priorF (Accumulator11 over 50-point chunks).  The linearised-residual term is
+ * empty in this library (residuals are linearised only inside ldso_ba_marginalize_points, which
+ * consumes their points). */
+int ldso_ba_calc_l_energy(int32_t n_frames, const double *prior, const double *delta_prior, const double *c_prior,
+                          const float *c_delta, int32_t n_points, const float *deltaF, const float *priorF,
+                          double *out);
+
 /* ---- device context --------------------------------------------------------------- */
 
 /* Create a context on HIP device `device` with its own non-blocking stream. */

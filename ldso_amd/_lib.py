@@ -121,6 +121,9 @@ ABI = [
     ("ldso_ba_num_kernels", C.c_int32, []),
     ("ldso_ba_stats", C.c_int, [C.c_void_p, i64p, i64p, i64p]),
     ("ldso_ba_marginalize_frame", C.c_int, [C.c_int32, C.c_int32, f64p, f64p, f64p, f64p, f64p, f64p]),
+    ("ldso_ba_ad_ht_delta", C.c_int, [C.c_int32, f64p, f64p, f64p, f32p]),
+    ("ldso_ba_calc_m_energy", C.c_int, [C.c_int32, f64p, f64p, f32p, f64p, f64p]),
+    ("ldso_ba_calc_l_energy", C.c_int, [C.c_int32, f64p, f64p, f64p, f32p, C.c_int32, f32p, f32p, f64p]),
     ("ldso_ba_load_marginalization", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(LdsoBaWindow)]),
     ("ldso_ba_marginalize_points", C.c_int, [C.c_void_p, f32p, f64p, f64p]),
     ("ldso_ba_activate_points", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]),

@@ -1,6 +1,7 @@
-// energy_functional.cpp -- the C++ host face (include/ldso_amd/energy_functional.h) packed onto
-// the C ABI of include/ldso_ba.h.  Packing only: every number is computed by the HIP path or by
-// the library's host helpers (precalc, adjoints, priors, nullspaces, solve).
+// energy_functional.cpp -- the C++ host face (include/ldso_amd/energy_functional.h) on the C ABI
+// of include/ldso_ba.h.  Packing and bookkeeping only: every number is computed by the HIP path
+// or by the library's host helpers (precalc, adjoints, priors, deltas, energies, nullspaces,
+// solve, frame marginalisation).
 #include "../../include/ldso_amd/energy_functional.h"
 
 #include <algorithm>
@@ -8,7 +9,123 @@
 
 namespace ldso_amd {
 
-EnergyFunctional::EnergyFunctional(int device) {
+namespace {
+
+constexpr float kIdepthFixPriorMargFac = 600.0f * 600.0f;  // setting_idepthFixPriorMargFac (Setting.cc:17)
+constexpr double kMargWeightFac = 0.5 * 0.5;                // setting_margWeightFac (Setting.cc:45)
+
+uint64_t conn_key(const PointFrameResidual &r) {
+    return ((uint64_t)r.host.lock()->frameID << 32) + (uint64_t)r.target.lock()->frameID;
+}
+
+void frame_state(const FrameHessian &F, ldso_ba_frame_state &S) {
+    std::memset(&S, 0, sizeof(S));
+    std::memcpy(S.world_to_cam_evalpt, F.worldToCam_evalPT, sizeof(S.world_to_cam_evalpt));
+    std::memcpy(S.state, F.state, sizeof(S.state));
+    std::memcpy(S.state_zero, F.state_zero, sizeof(S.state_zero));
+    S.ab_exposure = F.ab_exposure;
+    S.is_first_frame = F.frameID == 0 ? 1 : 0;
+}
+
+// points + residuals of one ldso_ba_window (caller point order = the order given)
+struct PointPack {
+    std::vector<int32_t> host, begin, target;
+    std::vector<float> data, energy;
+    std::vector<int8_t> state;
+    std::vector<uint8_t> flags;
+    std::vector<PointFrameResidual *> res;
+    void build(const std::vector<PointHessian *> &pts) {
+        host.assign(pts.size(), 0);
+        data.assign(pts.size() * LDSO_BA_POINT_STRIDE, 0.f);
+        begin.assign(pts.size() + 1, 0);
+        target.clear();
+        energy.clear();
+        state.clear();
+        flags.clear();
+        res.clear();
+        for (size_t q = 0; q < pts.size(); q++) {
+            const PointHessian &p = *pts[q];
+            host[q] = p.host.lock()->idx;
+            float *d = &data[q * LDSO_BA_POINT_STRIDE];
+            d[0] = p.u;
+            d[1] = p.v;
+            d[2] = p.idepth_scaled;
+            d[3] = p.idepth_zero_scaled;
+            d[4] = p.priorF;
+            d[5] = p.deltaF;
+            std::memcpy(d + 8, p.color, sizeof(p.color));
+            std::memcpy(d + 16, p.weights, sizeof(p.weights));
+            for (const shared_ptr<PointFrameResidual> &r : p.residuals) {
+                target.push_back(r->target.lock()->idx);
+                state.push_back((int8_t)r->state_state);
+                energy.push_back((float)r->state_energy);
+                flags.push_back((uint8_t)((r->isActiveAndIsGoodNEW ? LDSO_BA_FLAG_ACTIVE : 0u) |
+                                          (r->isNew ? LDSO_BA_FLAG_NEW : 0u)));
+                res.push_back(r.get());
+            }
+            begin[q + 1] = (int32_t)target.size();
+        }
+    }
+    void into(ldso_ba_window &w) {
+        w.n_points = (int32_t)host.size();
+        w.n_residuals = (int32_t)target.size();
+        w.point_host = host.data();
+        w.point_data = data.data();
+        w.point_res_begin = begin.data();
+        w.res_target = target.data();
+        w.res_state = state.data();
+        w.res_energy = energy.data();
+        w.res_flags = flags.data();
+    }
+};
+
+// write a device pass's per-residual results back into the residual objects
+bool read_residuals(ldso_ba_ctx *ctx, const std::vector<PointFrameResidual *> &res) {
+    const size_t R = res.size();
+    if (!R) return true;
+    std::vector<int8_t> ns(R), st(R);
+    std::vector<float> se(R), ewo(R), ctr(3 * R), jp(8 * R), rb(R);
+    std::vector<uint8_t> fl(R);
+    if (ldso_ba_get_residuals(ctx, 0, ns.data(), st.data(), se.data(), ewo.data(), ctr.data(), fl.data(), jp.data(),
+                              rb.data()))
+        return false;
+    for (size_t k = 0; k < R; k++) {
+        PointFrameResidual &r = *res[k];
+        r.state_NewState = (ResState)ns[k];
+        r.state_state = (ResState)st[k];
+        r.state_energy = se[k];
+        r.state_NewEnergy = se[k];
+        r.state_NewEnergyWithOutlier = ewo[k];
+        std::memcpy(r.centerProjectedTo, &ctr[3 * k], 3 * sizeof(float));
+        r.isActiveAndIsGoodNEW = (fl[k] & LDSO_BA_FLAG_ACTIVE) != 0;
+        if (r.isActiveAndIsGoodNEW) std::memcpy(r.JpJdF, &jp[8 * k], 8 * sizeof(float));
+        r.relBS = rb[k];
+    }
+    return true;
+}
+
+}  // namespace
+
+void FrameHessian::takeData() {
+    ldso_ba_frame_state S;
+    frame_state(*this, S);
+    ldso_ba_frame_take_data(1, &S, prior, delta, delta_prior);
+}
+
+double PointFrameResidual::linearize(shared_ptr<CalibHessian> &HCalib) {
+    (void)HCalib;  // the window's calibration is its EnergyFunctional's (insertFrame / setAdjointsF)
+    shared_ptr<EnergyFunctional> e = ef.lock();
+    if (!e) return state_energy;
+    e->linearizeAll(false);
+    return state_NewEnergy;
+}
+
+void PointFrameResidual::fixLinearizationF(shared_ptr<EnergyFunctional> e) {
+    (void)e;
+    isLinearized = true;
+}
+
+EnergyFunctional::EnergyFunctional(int device) : device_(device) {
     if (ldso_ba_create(device, &ctx_) != 0) {
         ctx_ = nullptr;
         fail("ldso_ba_create");
@@ -16,66 +133,248 @@ EnergyFunctional::EnergyFunctional(int device) {
 }
 
 EnergyFunctional::~EnergyFunctional() {
+    if (margCtx_) ldso_ba_destroy(margCtx_);
     if (ctx_) ldso_ba_destroy(ctx_);
 }
 
-void EnergyFunctional::fail(const char *what) {
-    err_ = std::string(what) + ": " + ldso_ba_last_error();
+void EnergyFunctional::fail(const char *what) { err_ = std::string(what) + ": " + ldso_ba_last_error(); }
+
+void EnergyFunctional::packFrames(std::vector<ldso_ba_frame_state> &fs) const {
+    fs.resize(frames.size());
+    for (size_t f = 0; f < frames.size(); f++) frame_state(*frames[f], fs[f]);
 }
 
-void EnergyFunctional::setCalib(const CalibHessian &Hcalib) {
-    calib_ = Hcalib;
-    width_ = Hcalib.wG0;
-    height_ = Hcalib.hG0;
-}
-
-void EnergyFunctional::insertFrame(FrameHessian *fh, const CalibHessian &Hcalib) {
-    setCalib(Hcalib);
-    fh->idx = (int)frames.size();
-    frames.push_back(fh);
-    nFrames = (int)frames.size();
-    dirty_ = true;
-}
-
-void EnergyFunctional::insertPoint(PointHessian *ph) {
-    allPoints.push_back(ph);
-    nPoints = (int)allPoints.size();
-    dirty_ = true;
-}
-
-void EnergyFunctional::insertResidual(PointFrameResidual *r) {
-    r->point->residuals.push_back(r);
+// EnergyFunctional.cc:45-49 (the caller has pushed r into its point's residuals)
+void EnergyFunctional::insertResidual(shared_ptr<PointFrameResidual> r) {
+    r->ef = weak_from_this();
+    connectivityMap[conn_key(*r)][0]++;
     nResiduals++;
     dirty_ = true;
 }
 
-void EnergyFunctional::dropResidual(PointFrameResidual *r) {
-    auto &v = r->point->residuals;
-    auto it = std::find(v.begin(), v.end(), r);
-    if (it != v.end()) {
-        v.erase(it);
+// EnergyFunctional.cc:51-98 (the non-VI part): HM, bM grow by the frame's 8 zero rows/columns
+void EnergyFunctional::insertFrame(shared_ptr<FrameHessian> fh, shared_ptr<CalibHessian> Hcalib) {
+    fh->takeData();
+    frames.push_back(fh);
+    fh->idx = (int)frames.size();
+    nFrames++;
+    const int n = 8 * nFrames + CPARS;
+    MatXX H2(n, n);
+    VecX b2(n);
+    for (int i = 0; i < HM.rows(); i++) {
+        b2[i] = bM[i];
+        for (int j = 0; j < HM.cols(); j++) H2(i, j) = HM(i, j);
+    }
+    HM = H2;
+    bM = b2;
+    calib_ = *Hcalib;
+    width_ = Hcalib->wG0;
+    height_ = Hcalib->hG0;
+    setAdjointsF(Hcalib);
+    makeIDX();
+    for (const shared_ptr<FrameHessian> &fh2 : frames) {
+        connectivityMap[((uint64_t)fh->frameID << 32) + (uint64_t)fh2->frameID] = {0, 0};
+        if (fh2 != fh) connectivityMap[((uint64_t)fh2->frameID << 32) + (uint64_t)fh->frameID] = {0, 0};
+    }
+    dirty_ = true;
+}
+
+void EnergyFunctional::insertPoint(shared_ptr<PointHessian> ph) {
+    ph->status = PointStatus::ACTIVE;
+    ph->alreadyRemoved = false;
+    allPoints.push_back(ph);
+    nPoints++;
+    dirty_ = true;
+}
+
+// EnergyFunctional.cc:100-107
+void EnergyFunctional::dropResidual(shared_ptr<PointFrameResidual> r) {
+    shared_ptr<PointHessian> p = r->point.lock();
+    if (p) {
+        auto &v = p->residuals;
+        auto it = std::find(v.begin(), v.end(), r);
+        if (it != v.end()) v.erase(it);
+    }
+    connectivityMap[conn_key(*r)][0]--;
+    nResiduals--;
+    dirty_ = true;
+}
+
+// EnergyFunctional.cc:109-191: the dense reorder / prior / Schur step on the host
+// (ldso_ba_marginalize_frame), then the frame leaves the window
+void EnergyFunctional::marginalizeFrame(shared_ptr<FrameHessian> fh) {
+    const int no = 8 * nFrames + CPARS, nn = no - 8;
+    MatXX Ho(nn, nn);
+    VecX bo(nn);
+    if (ldso_ba_marginalize_frame(nFrames, fh->idx, HM.data(), bM.data(), fh->prior, fh->delta_prior, Ho.data(),
+                                  bo.data())) {
+        fail("ldso_ba_marginalize_frame");
+        return;
+    }
+    HM = Ho;
+    bM = bo;
+    for (size_t i = (size_t)fh->idx; i + 1 < frames.size(); i++) {
+        frames[i] = frames[i + 1];
+        frames[i]->idx = (int)i;
+    }
+    frames.pop_back();
+    nFrames--;
+    makeIDX();
+    dirty_ = true;
+}
+
+// EnergyFunctional.cc:193-203
+void EnergyFunctional::removePoint(shared_ptr<PointHessian> ph) {
+    for (const shared_ptr<PointFrameResidual> &r : ph->residuals) {
+        connectivityMap[conn_key(*r)][0]--;
         nResiduals--;
-        dirty_ = true;
     }
+    ph->residuals.clear();
+    if (!ph->alreadyRemoved) nPoints--;
+    ph->alreadyRemoved = true;
+    dirty_ = true;
 }
 
-void EnergyFunctional::removePoint(PointHessian *p) {
-    auto it = std::find(allPoints.begin(), allPoints.end(), p);
-    if (it != allPoints.end()) {
-        nResiduals -= (int)p->residuals.size();
-        allPoints.erase(it);
-        nPoints = (int)allPoints.size();
-        dirty_ = true;
+// EnergyFunctional.cc:205-262 with FullSystem.cc:1384-1404 (see the header)
+void EnergyFunctional::marginalizePointsF() {
+    allPointsToMarg.clear();
+    for (const shared_ptr<PointHessian> &p : allPoints)
+        if (p->status == PointStatus::MARGINALIZED && !p->alreadyRemoved) allPointsToMarg.push_back(p);
+    if (allPointsToMarg.empty()) return;
+    if (!upload()) return;  // current frame terms; the parent window lends its device images
+    if (!margCtx_ && ldso_ba_create(device_, &margCtx_)) {
+        margCtx_ = nullptr;
+        fail("ldso_ba_create (marginalisation)");
+        return;
     }
+    std::vector<PointHessian *> pts;
+    for (const shared_ptr<PointHessian> &p : allPointsToMarg) pts.push_back(p.get());
+    PointPack pk;
+    pk.build(pts);
+    ldso_ba_window w;
+    std::memset(&w, 0, sizeof(w));
+    w.n_frames = nFrames;
+    w.width = width_;
+    w.height = height_;
+    std::memcpy(w.calib, calib_.value_scaledf, sizeof(w.calib));
+    w.frame_energy_th = frameTH_.data();
+    w.precalc = precalc_.data();
+    w.ad_host = adH_.data();
+    w.ad_target = adT_.data();
+    w.c_prior = cPrior_.data();
+    w.c_delta = cDeltaF;
+    w.frame_prior = fPrior_.data();
+    w.frame_delta_prior = fDeltaPrior_.data();
+    pk.into(w);
+    const int n = 8 * nFrames + CPARS;
+    std::vector<double> H((size_t)n * n), b(n);
+    if (ldso_ba_load_marginalization(margCtx_, ctx_, 0, &w) ||
+        ldso_ba_marginalize_points(margCtx_, adHTdeltaF.data(), H.data(), b.data())) {
+        fail("ldso_ba_marginalize_points");
+        return;
+    }
+    if (!read_residuals(margCtx_, pk.res)) {
+        fail("ldso_ba_get_residuals (marginalisation)");
+        return;
+    }
+    int nres = 0;
+    for (PointFrameResidual *r : pk.res) {
+        if (r->isActive()) {
+            r->isLinearized = true;  // fixLinearizationF
+            connectivityMap[conn_key(*r)][1]++;
+            nres++;
+        }
+    }
+    for (const shared_ptr<PointHessian> &p : allPointsToMarg) p->priorF *= kIdepthFixPriorMargFac;
+    resInM += nres;
+    for (int i = 0; i < n; i++) {
+        bM[i] += kMargWeightFac * b[i];
+        for (int j = 0; j < n; j++) HM(i, j) += kMargWeightFac * H[(size_t)i * n + j];
+    }
+    for (const shared_ptr<PointHessian> &p : allPointsToMarg) removePoint(p);
+    makeIDX();
 }
 
-// EnergyFunctional::makeIDX (EnergyFunctional.cc:500-521): frame indices, points in host-frame order
+// EnergyFunctional.cc:264-278
+void EnergyFunctional::dropPointsF() {
+    for (const shared_ptr<PointHessian> &p : allPoints)
+        if ((p->status == PointStatus::OUTLIER || p->status == PointStatus::OUT) && !p->alreadyRemoved) removePoint(p);
+    makeIDX();
+}
+
+// EnergyFunctional.cc:500-521: frame indices; the active, not removed points in host-frame order
 void EnergyFunctional::makeIDX() {
     for (size_t i = 0; i < frames.size(); i++) frames[i]->idx = (int)i;
-    std::stable_sort(allPoints.begin(), allPoints.end(),
-                     [](const PointHessian *a, const PointHessian *b) { return a->host->idx < b->host->idx; });
-    for (size_t i = 0; i < allPoints.size(); i++) allPoints[i]->idxInPoints = (int)i;
+    std::vector<shared_ptr<PointHessian>> keep;
+    for (const shared_ptr<PointHessian> &p : allPoints)
+        if (!p->alreadyRemoved && p->status == PointStatus::ACTIVE) keep.push_back(p);
+    std::stable_sort(keep.begin(), keep.end(), [](const shared_ptr<PointHessian> &a, const shared_ptr<PointHessian> &b) {
+        return a->host.lock()->idx < b->host.lock()->idx;
+    });
+    allPoints.swap(keep);
+    for (size_t i = 0; i < allPoints.size(); i++) {
+        allPoints[i]->idxInPoints = (int)i;
+        for (const shared_ptr<PointFrameResidual> &r : allPoints[i]->residuals) {
+            r->hostIDX = r->host.lock()->idx;
+            r->targetIDX = r->target.lock()->idx;
+        }
+    }
+    nPoints = (int)allPoints.size();
     dirty_ = true;
+}
+
+// EnergyFunctional.cc:551-609 (ldso_ba_set_adjoints)
+void EnergyFunctional::setAdjointsF(shared_ptr<CalibHessian> Hcalib) {
+    (void)Hcalib;
+    std::vector<ldso_ba_frame_state> fs;
+    packFrames(fs);
+    adHost.assign((size_t)nFrames * nFrames * 64, 0.0);
+    adTarget.assign((size_t)nFrames * nFrames * 64, 0.0);
+    if (nFrames && ldso_ba_set_adjoints(nFrames, fs.data(), adHost.data(), adTarget.data(), cPrior))
+        fail("ldso_ba_set_adjoints");
+}
+
+// EnergyFunctional.cc:523-549: frames' delta / delta_prior, adHTdeltaF, cDeltaF, points' deltaF
+void EnergyFunctional::setDeltaF(shared_ptr<CalibHessian> HCalib) {
+    for (int k = 0; k < 4; k++) cDeltaF[k] = (float)HCalib->value_minus_value_zero[k];
+    std::vector<double> delta((size_t)8 * nFrames);
+    for (int f = 0; f < nFrames; f++) {
+        frames[f]->takeData();
+        std::memcpy(&delta[(size_t)8 * f], frames[f]->delta, 8 * sizeof(double));
+    }
+    adHTdeltaF.assign((size_t)nFrames * nFrames * 8, 0.f);
+    if (nFrames && ldso_ba_ad_ht_delta(nFrames, delta.data(), adHost.data(), adTarget.data(), adHTdeltaF.data()))
+        fail("ldso_ba_ad_ht_delta");
+    for (const shared_ptr<PointHessian> &p : allPoints) p->deltaF = p->idepth - p->idepth_zero;
+    calib_ = *HCalib;
+}
+
+// EnergyFunctional.cc:473-479
+double EnergyFunctional::calcMEnergyF() {
+    std::vector<double> delta((size_t)8 * nFrames);
+    for (int f = 0; f < nFrames; f++) std::memcpy(&delta[(size_t)8 * f], frames[f]->delta, 8 * sizeof(double));
+    double e = 0;
+    if (ldso_ba_calc_m_energy(nFrames, HM.data(), bM.data(), cDeltaF, delta.data(), &e)) fail("ldso_ba_calc_m_energy");
+    return e;
+}
+
+// EnergyFunctional.cc:481-498
+double EnergyFunctional::calcLEnergyF_MT() {
+    std::vector<double> prior((size_t)8 * nFrames), dprior((size_t)8 * nFrames);
+    for (int f = 0; f < nFrames; f++) {
+        std::memcpy(&prior[(size_t)8 * f], frames[f]->prior, 8 * sizeof(double));
+        std::memcpy(&dprior[(size_t)8 * f], frames[f]->delta_prior, 8 * sizeof(double));
+    }
+    std::vector<float> dd(allPoints.size()), pf(allPoints.size());
+    for (size_t q = 0; q < allPoints.size(); q++) {
+        dd[q] = allPoints[q]->deltaF;
+        pf[q] = allPoints[q]->priorF;
+    }
+    double e = 0;
+    if (ldso_ba_calc_l_energy(nFrames, prior.data(), dprior.data(), cPrior, cDeltaF, (int32_t)dd.size(), dd.data(),
+                              pf.data(), &e))
+        fail("ldso_ba_calc_l_energy");
+    return e;
 }
 
 bool EnergyFunctional::upload() {
@@ -86,17 +385,7 @@ bool EnergyFunctional::upload() {
         return false;
     }
     // frame-level terms from the current states (setPrecalcValues, setAdjointsF, takeData)
-    fs_.resize(N);
-    for (int f = 0; f < N; f++) {
-        const FrameHessian &F = *frames[f];
-        ldso_ba_frame_state &S = fs_[f];
-        std::memset(&S, 0, sizeof(S));
-        std::memcpy(S.world_to_cam_evalpt, F.worldToCam_evalPT, sizeof(S.world_to_cam_evalpt));
-        std::memcpy(S.state, F.state, sizeof(S.state));
-        std::memcpy(S.state_zero, F.state_zero, sizeof(S.state_zero));
-        S.ab_exposure = F.ab_exposure;
-        S.is_first_frame = F.isFirstFrame ? 1 : 0;
-    }
+    packFrames(fs_);
     precalc_.assign((size_t)N * N * LDSO_BA_PRECALC_STRIDE, 0.f);
     adH_.assign((size_t)N * N * 64, 0.0);
     adT_.assign((size_t)N * N * 64, 0.0);
@@ -104,7 +393,6 @@ bool EnergyFunctional::upload() {
     fPrior_.assign((size_t)N * 8, 0.0);
     fDelta_.assign((size_t)N * 8, 0.0);
     fDeltaPrior_.assign((size_t)N * 8, 0.0);
-    cDelta_.assign(calib_.value_minus_value_zero, calib_.value_minus_value_zero + 4);
     if (ldso_ba_frame_precalc(N, fs_.data(), calib_.value_scaledf, precalc_.data()) ||
         ldso_ba_set_adjoints(N, fs_.data(), adH_.data(), adT_.data(), cPrior_.data()) ||
         ldso_ba_frame_take_data(N, fs_.data(), fPrior_.data(), fDelta_.data(), fDeltaPrior_.data())) {
@@ -113,43 +401,23 @@ bool EnergyFunctional::upload() {
     }
     frameTH_.resize(N);
     for (int f = 0; f < N; f++) frameTH_[f] = frames[f]->frameEnergyTH;
-    // points and residuals in makeIDX order
-    const int P = nPoints;
-    pointHost_.resize(P);
-    pointData_.assign((size_t)P * LDSO_BA_POINT_STRIDE, 0.f);
-    resBegin_.assign(P + 1, 0);
-    resTarget_.clear();
-    resState_.clear();
-    resEnergy_.clear();
-    resFlags_.clear();
-    resPtr_.clear();
-    for (int q = 0; q < P; q++) {
-        const PointHessian &p = *allPoints[q];
-        pointHost_[q] = p.host->idx;
-        float *d = &pointData_[(size_t)q * LDSO_BA_POINT_STRIDE];
-        d[0] = p.u;
-        d[1] = p.v;
-        d[2] = p.idepth_scaled;
-        d[3] = p.idepth_zero_scaled;
-        d[4] = p.priorF;
-        d[5] = p.deltaF;
-        std::memcpy(d + 8, p.color, sizeof(p.color));
-        std::memcpy(d + 16, p.weights, sizeof(p.weights));
-        for (PointFrameResidual *r : p.residuals) {
-            resTarget_.push_back(r->target->idx);
-            resState_.push_back((int8_t)r->state_state);
-            resEnergy_.push_back(r->state_energy);
-            resFlags_.push_back((uint8_t)((r->isActiveAndIsGoodNEW ? LDSO_BA_FLAG_ACTIVE : 0u) |
-                                          (r->isNew ? LDSO_BA_FLAG_NEW : 0u)));
-            resPtr_.push_back(r);
-        }
-        resBegin_[q + 1] = (int32_t)resTarget_.size();
-    }
+    ptPtr_.clear();
+    for (const shared_ptr<PointHessian> &p : allPoints) ptPtr_.push_back(p.get());
+    PointPack pk;
+    pk.build(ptPtr_);
+    pointHost_ = pk.host;
+    pointData_ = pk.data;
+    resBegin_ = pk.begin;
+    resTarget_ = pk.target;
+    resState_ = pk.state;
+    resEnergy_ = pk.energy;
+    resFlags_ = pk.flags;
+    resPtr_ = pk.res;
     nResiduals = (int)resPtr_.size();
     ldso_ba_window w;
     std::memset(&w, 0, sizeof(w));
     w.n_frames = N;
-    w.n_points = P;
+    w.n_points = (int32_t)pointHost_.size();
     w.n_residuals = nResiduals;
     w.width = width_;
     w.height = height_;
@@ -166,7 +434,7 @@ bool EnergyFunctional::upload() {
     w.ad_host = adH_.data();
     w.ad_target = adT_.data();
     w.c_prior = cPrior_.data();
-    w.c_delta = cDelta_.data();
+    w.c_delta = cDeltaF;
     w.frame_prior = fPrior_.data();
     w.frame_delta_prior = fDeltaPrior_.data();
     w.point_host = pointHost_.data();
@@ -186,12 +454,9 @@ bool EnergyFunctional::upload() {
 }
 
 void EnergyFunctional::resetOOB() {
-    for (PointHessian *p : allPoints)
-        for (PointFrameResidual *r : p->residuals) {  // Residuals.h:63-68
-            r->state_NewEnergy = r->state_energy = 0;
-            r->state_NewState = OUTLIER;
-            r->state_state = IN;
-        }
+    for (const shared_ptr<PointHessian> &p : allPoints)
+        for (const shared_ptr<PointFrameResidual> &r : p->residuals)
+            if (!r->isLinearized) r->resetOOB();  // FullSystem.cc:866-869
     if (!dirty_ && ctx_ && ldso_ba_reset_oob(ctx_, 0)) fail("ldso_ba_reset_oob");
 }
 
@@ -207,72 +472,79 @@ Vec3 EnergyFunctional::linearizeAll(bool fixLinearization) {
         fail("ldso_ba_get_energy");
         return out;
     }
-    const int R = nResiduals, P = nPoints, N = nFrames;
-    std::vector<int8_t> ns(R), st(R);
-    std::vector<float> se(R), ewo(R), ctr((size_t)3 * R), jp((size_t)8 * R), rb(R);
-    std::vector<uint8_t> fl(R);
-    if (R && ldso_ba_get_residuals(ctx_, 0, ns.data(), st.data(), se.data(), ewo.data(), ctr.data(), fl.data(),
-                                   jp.data(), rb.data())) {
+    if (!read_residuals(ctx_, resPtr_)) {
         fail("ldso_ba_get_residuals");
         return out;
     }
-    for (int k = 0; k < R; k++) {
-        PointFrameResidual &r = *resPtr_[k];
-        r.state_NewState = (ResState)ns[k];
-        r.state_state = (ResState)st[k];
-        r.state_energy = se[k];
-        r.state_NewEnergy = se[k];
-        r.state_NewEnergyWithOutlier = ewo[k];
-        std::memcpy(r.centerProjectedTo, &ctr[(size_t)3 * k], 3 * sizeof(float));
-        r.isActiveAndIsGoodNEW = (fl[k] & LDSO_BA_FLAG_ACTIVE) != 0;
-        if (r.isActiveAndIsGoodNEW) std::memcpy(r.JpJdF, &jp[(size_t)8 * k], 8 * sizeof(float));
-        r.relBS = rb[k];
-    }
+    const int P = (int)ptPtr_.size(), N = nFrames;
     std::vector<float> hdi(P), bds(P), ih(P), th(N);
     if (P && ldso_ba_get_points(ctx_, 0, hdi.data(), bds.data(), ih.data(), nullptr, nullptr, nullptr)) {
         fail("ldso_ba_get_points");
         return out;
     }
     for (int q = 0; q < P; q++) {
-        allPoints[q]->HdiF = hdi[q];
-        allPoints[q]->bdSumF = bds[q];
-        allPoints[q]->idepth_hessian = ih[q];
+        ptPtr_[q]->HdiF = hdi[q];
+        ptPtr_[q]->bdSumF = bds[q];
+        ptPtr_[q]->idepth_hessian = ih[q];
     }
     if (ldso_ba_get_frame_energy_th(ctx_, 0, th.data()) == 0)
         for (int f = 0; f < N; f++) frames[f]->frameEnergyTH = th[f];
+    if (!fixLinearization) resInA = (int)e[2];
     out = {e[0], e[1], e[2]};
     return out;
 }
 
-void EnergyFunctional::solveSystemF(int iteration, double lambda) {
-    const int n = 8 * nFrames + 4;
-    HA_top.assign((size_t)n * n, 0.0);
-    bA_top.assign(n, 0.0);
-    HL_top.assign((size_t)n * n, 0.0);
-    bL_top.assign(n, 0.0);
-    H_sc.assign((size_t)n * n, 0.0);
-    b_sc.assign(n, 0.0);
+// EnergyFunctional.cc:280-471, non-VI branch: the stitched blocks of the last linearizeAll,
+// HM / bM, the pose and scale nullspaces (FullSystem::getNullspaces) and the host LDL^T
+void EnergyFunctional::solveSystemF(int iteration, double lambda, shared_ptr<CalibHessian> HCalib) {
+    (void)HCalib;
+    currentLambda_ = lambda;
+    const int n = 8 * nFrames + CPARS;
+    HA_top = MatXX(n, n);
+    HL_top = MatXX(n, n);
+    H_sc = MatXX(n, n);
+    bA_top = VecX(n);
+    bL_top = VecX(n);
+    b_sc = VecX(n);
     if (ldso_ba_get_system(ctx_, 0, HA_top.data(), bA_top.data(), HL_top.data(), bL_top.data(), H_sc.data(),
                            b_sc.data())) {
         fail("ldso_ba_get_system");
         return;
     }
+    std::vector<ldso_ba_frame_state> fs;
+    packFrames(fs);
     std::vector<double> ns((size_t)7 * n);
-    if (ldso_ba_nullspaces(nFrames, fs_.data(), ns.data())) {
+    if (ldso_ba_nullspaces(nFrames, fs.data(), ns.data())) {
         fail("ldso_ba_nullspaces");
         return;
     }
-    lastX.assign(n, 0.0);
-    if (ldso_ba_solve(ctx_, 0, iteration, lambda, ns.data(), 7, lastX.data())) fail("ldso_ba_solve");
+    lastNullspaces_pose.assign(6, VecX(n));
+    lastNullspaces_scale.assign(1, VecX(n));
+    for (int k = 0; k < 7; k++)
+        std::memcpy((k < 6 ? lastNullspaces_pose[k] : lastNullspaces_scale[0]).data(), &ns[(size_t)k * n],
+                    n * sizeof(double));
+    lastNullspaces_forLogging = lastNullspaces_pose;
+    lastNullspaces_forLogging.push_back(lastNullspaces_scale[0]);
+    lastX = VecX(n);
+    if (ldso_ba_solve_system(nFrames, iteration, lambda, HA_top.data(), bA_top.data(), HL_top.data(), bL_top.data(),
+                             HM.data(), bM.data(), H_sc.data(), b_sc.data(), ns.data(), 7, lastX.data()))
+        fail("ldso_ba_solve_system");
 }
 
-void EnergyFunctional::resubstituteF_MT(const std::vector<double> &x, double lambda) {
-    std::vector<float> step(nPoints);
-    if (ldso_ba_resubstitute(ctx_, 0, x.data(), lambda, step.data())) {
+// EnergyFunctional.cc:611-667: calibration and frame steps are -x, point steps from the device
+void EnergyFunctional::resubstituteF_MT(const VecX &x, shared_ptr<CalibHessian> HCalib, bool MT) {
+    (void)MT;
+    for (int k = 0; k < CPARS; k++) HCalib->step[k] = -x[k];
+    for (const shared_ptr<FrameHessian> &h : frames) {
+        for (int k = 0; k < 8; k++) h->step[k] = -x[CPARS + 8 * h->idx + k];
+        h->step[8] = h->step[9] = 0;
+    }
+    std::vector<float> step(ptPtr_.size());
+    if (ldso_ba_resubstitute(ctx_, 0, x.data(), currentLambda_, step.data())) {
         fail("ldso_ba_resubstitute");
         return;
     }
-    for (int q = 0; q < nPoints; q++) allPoints[q]->step = step[q];
+    for (size_t q = 0; q < ptPtr_.size(); q++) ptPtr_[q]->step = step[q];
 }
 
 }  // namespace ldso_amd

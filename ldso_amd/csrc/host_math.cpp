@@ -578,3 +578,77 @@ int marginalize_frame(int N, int idx, const double *HM, const double *bM, const 
 }
 
 }  // namespace ldso_ba
+
+namespace ldso_ba {
+
+// EnergyFunctional::setDeltaF's adHTdeltaF (EnergyFunctional.cc:523-533): for every (h, t),
+// delta_h^T adHostF + delta_t^T adTargetF in float (Mat18f = Vec8f^T * Mat88f), index h + N t.
+int ad_ht_delta(int N, const double *delta, const double *adH, const double *adT, float *out) {
+    for (int h = 0; h < N; h++)
+        for (int t = 0; t < N; t++) {
+            const int idx = h + t * N;
+            float dh[8], dt[8];
+            for (int k = 0; k < 8; k++) {
+                dh[k] = (float)delta[8 * h + k];
+                dt[k] = (float)delta[8 * t + k];
+            }
+            for (int j = 0; j < 8; j++) {
+                float a = 0.f, b = 0.f;
+                for (int k = 0; k < 8; k++) {
+                    a += dh[k] * (float)adH[(size_t)idx * 64 + k * 8 + j];
+                    b += dt[k] * (float)adT[(size_t)idx * 64 + k * 8 + j];
+                }
+                out[(size_t)idx * 8 + j] = a + b;
+            }
+        }
+    return 0;
+}
+
+// EnergyFunctional::calcMEnergyF (EnergyFunctional.cc:473-479): delta^T (2 bM + HM delta) with
+// delta = getStitchedDeltaF() = [cDeltaF; frames' delta] (EnergyFunctional.h:192-198).
+double calc_m_energy(int N, const double *HM, const double *bM, const float *c_delta, const double *frame_delta) {
+    const int n = 8 * N + 4;
+    std::vector<double> d(n);
+    for (int i = 0; i < 4; i++) d[i] = (double)c_delta[i];
+    for (int i = 0; i < 8 * N; i++) d[4 + i] = frame_delta[i];
+    double e = 0;
+    for (int r = 0; r < n; r++) {
+        double hd = 0;
+        for (int c = 0; c < n; c++) hd += HM[(size_t)r * n + c] * d[c];
+        e += d[r] * (2 * bM[r] + hd);
+    }
+    return e;
+}
+
+// EnergyFunctional::calcLEnergyF_MT (EnergyFunctional.cc:481-498) with calcLEnergyPt
+// (:751-806): the frame priors in double, the calibration prior in float, and per point the
+// Accumulator11 float sums (MatrixAccumulators.h:68-123) over IndexThreadReduce chunks of 50
+// points, each chunk's float total added to the double stats in chunk order.  The
+// linearised-residual term (2 res_toZeroF + J delta) J delta is empty: residuals are only ever
+// linearised inside marginalizePointsF, which removes their points in the same call
+// (ldso_ba_marginalize_points), exactly as FullSystem::flagPointsForRemoval + marginalizePointsF.
+double calc_l_energy(int N, const double *frame_prior, const double *frame_delta_prior, const double *c_prior,
+                     const float *c_delta, int n_points, const float *deltaF, const float *priorF) {
+    double E = 0;
+    for (int f = 0; f < N; f++) {
+        double s = 0;
+        for (int k = 0; k < 8; k++)
+            s += frame_delta_prior[8 * f + k] * frame_prior[8 * f + k] * frame_delta_prior[8 * f + k];
+        E += s;
+    }
+    float sc = 0.f;
+    for (int k = 0; k < 4; k++) sc += c_delta[k] * (float)c_prior[k] * c_delta[k];
+    E += sc;
+    double stats = 0;
+    for (int c0 = 0; c0 < n_points; c0 += 50) {
+        float acc = 0.f;  // Accumulator11::SSEData[0]; finish() moves it through the 1k / 1m stages
+        for (int q = c0; q < n_points && q < c0 + 50; q++) acc += deltaF[q] * deltaF[q] * priorF[q];
+        float a1k = 0.f, a1m = 0.f;
+        a1k += acc;
+        a1m += a1k;
+        stats += (double)(((a1m + 0.f) + 0.f) + 0.f);
+    }
+    return E + stats;
+}
+
+}  // namespace ldso_ba

@@ -1280,7 +1280,10 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 // the host's order, so x is bit-identical to ldso_ba_solve's.  H lives in LDS (n <= kSolveMaxDim).
 // ============================================================================================
 constexpr int kSolveMaxDim = 8 * 11 + 4;  // windows up to 11 keyframes (68 KB of LDS for H)
-constexpr int kSolveThreads = 256;        // 4 wavefronts share the assembly and the LDL^T updates
+#ifndef LDSO_SOLVE_THREADS
+#define LDSO_SOLVE_THREADS 256
+#endif
+constexpr int kSolveThreads = LDSO_SOLVE_THREADS;  // wavefronts share the assembly and the LDL^T updates
 // Round-robin (circle method) schedule of the 7 x 7 Jacobi sweep: 7 rounds of 3 disjoint pairs
 // (p < q); player r sits out round r.  Shared with host_math.cpp's project_out.
 __device__ constexpr int kJacobiRounds[7][3][2] = {
@@ -2339,6 +2342,26 @@ int ldso_ba_marginalize_frame(int32_t n, int32_t idx, const double *HM, const do
         !bM_out)
         return fail(-1, "bad arguments");
     return marginalize_frame(n, idx, HM, bM, prior, delta_prior, HM_out, bM_out);
+}
+
+int ldso_ba_ad_ht_delta(int32_t n, const double *delta, const double *adH, const double *adT, float *out) {
+    if (n < 1 || n > LDSO_BA_MAX_FRAMES || !delta || !adH || !adT || !out) return fail(-1, "bad arguments");
+    return ad_ht_delta(n, delta, adH, adT, out);
+}
+int ldso_ba_calc_m_energy(int32_t n, const double *HM, const double *bM, const float *c_delta, const double *delta,
+                          double *out) {
+    if (n < 1 || n > LDSO_BA_MAX_FRAMES || !HM || !bM || !c_delta || !delta || !out) return fail(-1, "bad arguments");
+    *out = calc_m_energy(n, HM, bM, c_delta, delta);
+    return 0;
+}
+int ldso_ba_calc_l_energy(int32_t n, const double *prior, const double *delta_prior, const double *c_prior,
+                          const float *c_delta, int32_t n_points, const float *deltaF, const float *priorF,
+                          double *out) {
+    if (n < 1 || n > LDSO_BA_MAX_FRAMES || !prior || !delta_prior || !c_prior || !c_delta || n_points < 0 ||
+        (n_points > 0 && (!deltaF || !priorF)) || !out)
+        return fail(-1, "bad arguments");
+    *out = calc_l_energy(n, prior, delta_prior, c_prior, c_delta, n_points, deltaF, priorF);
+    return 0;
 }
 
 int ldso_ba_validate_window(const ldso_ba_window *w) {

@@ -96,6 +96,10 @@ int nullspaces(int N, const ldso_ba_frame_state *fr, double *out);
 int solve_system(int N, int iteration, double lambda, const double *HA, const double *bA, const double *HL,
                  const double *bL, const double *HM, const double *bM, const double *Hsc, const double *bsc,
                  const double *ns, int n_null, double *x_out);
+int ad_ht_delta(int N, const double *delta, const double *adH, const double *adT, float *out);
+double calc_m_energy(int N, const double *HM, const double *bM, const float *c_delta, const double *frame_delta);
+double calc_l_energy(int N, const double *frame_prior, const double *frame_delta_prior, const double *c_prior,
+                     const float *c_delta, int n_points, const float *deltaF, const float *priorF);
 int marginalize_frame(int N, int idx, const double *HM, const double *bM, const double *prior,
                       const double *delta_prior, double *HM_out, double *bM_out);
 

@@ -60,6 +60,9 @@ def lib():
             "oracle_frame_take_data": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p]),
             "oracle_nullspaces": (C.c_int, [C.c_int, C.c_void_p, f64p]),
             "oracle_time_iterations": (C.c_double, [C.c_void_p, C.c_int]),
+            "oracle_ad_ht_delta": (C.c_int, [C.c_int, f64p, f64p, f64p, f32p]),
+            "oracle_calc_m_energy": (C.c_double, [C.c_int, f64p, f64p, f32p, f64p]),
+            "oracle_calc_l_energy": (C.c_double, [C.c_int, f64p, f64p, f64p, f32p, C.c_int, f32p, f32p]),
             "oracle_marginalize_points": (C.c_int, [C.c_void_p, C.c_int, i32p, f32p, f64p, f64p]),
             "oracle_ct_levels": (C.c_int, [C.c_int, C.c_int]),
             "oracle_ct_make_k": (None, [f32p, C.c_int, C.c_int, C.c_int, f32p]),

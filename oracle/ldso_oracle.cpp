@@ -2046,4 +2046,63 @@ int oracle_activate_points(oracle_window *ow, int n, const ldso_ct_immature *pts
     return 0;
 }
 
+// EnergyFunctional::setDeltaF (EnergyFunctional.cc:523-533): adHTdeltaF[h + t N] =
+// frames[h]->delta^T (float) * adHostF + frames[t]->delta^T * adTargetF, Mat18f row times Mat88f
+// (each output column a k-ascending float dot product).
+int oracle_ad_ht_delta(int N, const double *delta, const double *adH, const double *adT, float *out) {
+    for (int h = 0; h < N; h++)
+        for (int t = 0; t < N; t++) {
+            const int idx = h + t * N;
+            for (int j = 0; j < 8; j++) {
+                float lh = 0.f, lt = 0.f;
+                for (int k = 0; k < 8; k++) lh += (float)delta[8 * h + k] * (float)adH[(size_t)idx * 64 + k * 8 + j];
+                for (int k = 0; k < 8; k++) lt += (float)delta[8 * t + k] * (float)adT[(size_t)idx * 64 + k * 8 + j];
+                out[(size_t)idx * 8 + j] = lh + lt;
+            }
+        }
+    return 0;
+}
+
+// EnergyFunctional::calcMEnergyF (EnergyFunctional.cc:473-479): delta.dot(2 * bM + HM * delta),
+// delta = getStitchedDeltaF() (EnergyFunctional.h:192-198: cDeltaF then each frame's delta).
+double oracle_calc_m_energy(int N, const double *HM, const double *bM, const float *cDeltaF, const double *delta) {
+    const int n = 8 * N + 4;
+    std::vector<double> d(n), Hd(n, 0.0);
+    for (int i = 0; i < 4; i++) d[i] = (double)cDeltaF[i];
+    for (int f = 0; f < N; f++)
+        for (int k = 0; k < 8; k++) d[4 + 8 * f + k] = delta[8 * f + k];
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < n; c++) Hd[r] += HM[(size_t)r * n + c] * d[c];
+    double e = 0.0;
+    for (int r = 0; r < n; r++) e += d[r] * (2 * bM[r] + Hd[r]);
+    return e;
+}
+
+// EnergyFunctional::calcLEnergyF_MT (EnergyFunctional.cc:481-498) with calcLEnergyPt (:751-806)
+// over IndexThreadReduce chunks of 50 points (red->reduce(..., 50)), one Accumulator11
+// (MatrixAccumulators.h:68-123) per chunk, chunk totals summed into stats[0] in order.  Only the
+// per-point prior term: no residual of an optimised window is linearised (see ldso_ba.h).
+double oracle_calc_l_energy(int N, const double *prior, const double *delta_prior, const double *cPrior,
+                            const float *cDeltaF, int n_points, const float *deltaF, const float *priorF) {
+    double E = 0;
+    for (int f = 0; f < N; f++) {
+        double dot = 0;
+        for (int k = 0; k < 8; k++) dot += (delta_prior[8 * f + k] * prior[8 * f + k]) * delta_prior[8 * f + k];
+        E += dot;
+    }
+    float cdot = 0.f;
+    for (int k = 0; k < 4; k++) cdot += (cDeltaF[k] * (float)cPrior[k]) * cDeltaF[k];
+    E += cdot;
+    double stat0 = 0;
+    for (int lo = 0; lo < n_points; lo += 50) {
+        float sse[4] = {0, 0, 0, 0}, sse1k[4] = {0, 0, 0, 0}, sse1m[4] = {0, 0, 0, 0};
+        const int hi = std::min(n_points, lo + 50);
+        for (int q = lo; q < hi; q++) sse[0] += deltaF[q] * deltaF[q] * priorF[q];  // updateSingle
+        for (int k = 0; k < 4; k++) sse1k[k] += sse[k];                           // finish(): shiftUp(true)
+        for (int k = 0; k < 4; k++) sse1m[k] += sse1k[k];
+        stat0 += sse1m[0] + sse1m[1] + sse1m[2] + sse1m[3];
+    }
+    return E + stat0;
+}
+
 }  // extern "C"

@@ -82,6 +82,13 @@ int oracle_nullspaces(int n_frames, const ldso_ba_frame_state *frames, double *o
 int oracle_marginalize_points(oracle_window *ow, int n, const int *pts, const float *adHTdeltaF, double *H,
                               double *b);
 
+/* EnergyFunctional::setDeltaF's adHTdeltaF, calcMEnergyF and calcLEnergyF_MT (the prior terms). */
+int oracle_ad_ht_delta(int n_frames, const double *delta, const double *ad_host, const double *ad_target, float *out);
+double oracle_calc_m_energy(int n_frames, const double *HM, const double *bM, const float *c_delta,
+                            const double *delta);
+double oracle_calc_l_energy(int n_frames, const double *prior, const double *delta_prior, const double *c_prior,
+                            const float *c_delta, int n_points, const float *deltaF, const float *priorF);
+
 /* ---- coarse tracker (ldso_oracle_tracker.cpp; the checker of include/ldso_ct.h) ---------- */
 int oracle_ct_levels(int w, int h);
 /* per level 13 floats {fx, fy, cx, cy, Ki[9]} */

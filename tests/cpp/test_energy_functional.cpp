@@ -1,9 +1,18 @@
 // test_energy_functional.cpp -- the C++ host face (include/ldso_amd/energy_functional.h) driven
-// the way FullSystem::optimize drives LDSO's EnergyFunctional, checked against the CPU oracle
-// (oracle/, test infrastructure) on the same seeded synthetic window.
+// through a whole keyframe cycle the way FullSystem drives LDSO's EnergyFunctional, each device
+// result checked against the CPU oracle (oracle/, test infrastructure) on the same inputs:
 //
-//   test_energy_functional --cpu   structure bookkeeping and the no-device error path
-//   test_energy_functional         GPU parity over two GN iterations (load, then update path)
+//   insertFrame / insertPoint / insertResidual / makeIDX / setAdjointsF / setDeltaF
+//   optimize x3: resetOOB, linearizeAll (+applyRes, accumulate), solveSystemF, resubstituteF_MT,
+//                the step (test harness: additive frame states, point setIdepth/setIdepthZero),
+//                setDeltaF, calcLEnergyF_MT / calcMEnergyF
+//   flagPointsForRemoval (frame 0's points + every 7th point MARGINALIZED, some OUT),
+//   marginalizePointsF, dropPointsF, marginalizeFrame(frame 0) + dropResidual of its
+//   observations, setAdjointsF / setDeltaF
+//   optimize x2 with the marginalisation prior HM / bM in the solve
+//
+//   test_energy_functional --cpu   bookkeeping and the no-device error path
+//   test_energy_functional         the GPU cycle
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -17,14 +26,14 @@
 using namespace ldso_amd;
 
 static int g_fail = 0;
-#define CHECK(cond, ...)                                  \
-    do {                                                  \
-        if (!(cond)) {                                    \
+#define CHECK(cond, ...)                                     \
+    do {                                                     \
+        if (!(cond)) {                                       \
             std::printf("FAIL %s:%d: ", __FILE__, __LINE__); \
-            std::printf(__VA_ARGS__);                     \
-            std::printf("\n");                            \
-            g_fail++;                                     \
-        }                                                 \
+            std::printf(__VA_ARGS__);                        \
+            std::printf("\n");                               \
+            g_fail++;                                        \
+        }                                                    \
     } while (0)
 
 struct Synth {
@@ -52,76 +61,75 @@ struct Synth {
     }
 };
 
-// the LDSO object graph of a synthetic window
+// the LDSO object graph of a synthetic window (shared_ptr ownership, as the reference)
 struct Graph {
-    CalibHessian calib;
-    std::vector<std::unique_ptr<FrameHessian>> frames;
-    std::vector<std::unique_ptr<PointHessian>> points;
-    std::vector<std::unique_ptr<PointFrameResidual>> res;
+    shared_ptr<CalibHessian> calib = std::make_shared<CalibHessian>();
+    std::vector<shared_ptr<FrameHessian>> frames;
+    std::vector<shared_ptr<PointHessian>> points;
     explicit Graph(const Synth &S) {
-        calib.wG0 = S.w;
-        calib.hG0 = S.h;
-        std::memcpy(calib.value_scaledf, S.calib, sizeof(S.calib));
+        calib->wG0 = S.w;
+        calib->hG0 = S.h;
+        std::memcpy(calib->value_scaledf, S.calib, sizeof(S.calib));
         for (int f = 0; f < S.N; f++) {
-            auto F = std::make_unique<FrameHessian>();
+            auto F = std::make_shared<FrameHessian>();
+            F->frameID = f;
             std::memcpy(F->worldToCam_evalPT, S.fs[f].world_to_cam_evalpt, sizeof(F->worldToCam_evalPT));
             std::memcpy(F->state, S.fs[f].state, sizeof(F->state));
             std::memcpy(F->state_zero, S.fs[f].state_zero, sizeof(F->state_zero));
             F->ab_exposure = S.fs[f].ab_exposure;
-            F->isFirstFrame = S.fs[f].is_first_frame != 0;
             F->dI = &S.dI[(size_t)f * S.w * S.h * 3];
             F->frameEnergyTH = S.th[f];
-            frames.push_back(std::move(F));
+            frames.push_back(F);
         }
         for (int p = 0; p < S.P; p++) {
-            auto Pt = std::make_unique<PointHessian>();
+            auto Pt = std::make_shared<PointHessian>();
             const float *d = &S.pd[(size_t)p * LDSO_BA_POINT_STRIDE];
-            Pt->host = frames[S.ph[p]].get();
+            Pt->host = frames[S.ph[p]];
             Pt->u = d[0];
             Pt->v = d[1];
-            Pt->idepth_scaled = d[2];
-            Pt->idepth_zero_scaled = d[3];
+            Pt->setIdepth(d[2]);
+            Pt->setIdepthZero(d[3]);
             Pt->priorF = d[4];
             Pt->deltaF = d[5];
             std::memcpy(Pt->color, d + 8, sizeof(Pt->color));
             std::memcpy(Pt->weights, d + 16, sizeof(Pt->weights));
-            points.push_back(std::move(Pt));
-        }
-        for (int p = 0; p < S.P; p++)
             for (int k = S.rb[p]; k < S.rb[p + 1]; k++) {
-                auto r = std::make_unique<PointFrameResidual>();
-                r->point = points[p].get();
-                r->host = points[p]->host;
-                r->target = frames[S.rt[k]].get();
+                auto r = std::make_shared<PointFrameResidual>(Pt, frames[S.ph[p]], frames[S.rt[k]]);
                 r->state_state = (ResState)S.rs[k];
                 r->state_energy = S.re[k];
                 r->isNew = (S.rf[k] & LDSO_BA_FLAG_NEW) != 0;
                 r->isActiveAndIsGoodNEW = (S.rf[k] & LDSO_BA_FLAG_ACTIVE) != 0;
-                res.push_back(std::move(r));
+                Pt->residuals.push_back(r);
             }
+            points.push_back(Pt);
+        }
     }
     void insertInto(EnergyFunctional &ef) {
-        for (auto &F : frames) ef.insertFrame(F.get(), calib);
-        for (auto &P : points) ef.insertPoint(P.get());
-        for (auto &r : res) ef.insertResidual(r.get());
+        for (auto &F : frames) ef.insertFrame(F, calib);
+        for (auto &P : points) {
+            ef.insertPoint(P);
+            for (auto &r : P->residuals) ef.insertResidual(r);
+        }
         ef.makeIDX();
+        ef.setAdjointsF(calib);
+        ef.setDeltaF(calib);
     }
 };
 
-// The oracle's window in the EnergyFunctional's (makeIDX) point order.
+// The oracle's window built from the EnergyFunctional's current objects (makeIDX order)
 struct OracleWin {
     std::vector<int32_t> ph, rb, rt;
-    std::vector<float> pd, re, precalc, th;
+    std::vector<float> pd, re, precalc, th, dI, cdelta;
     std::vector<int8_t> rs;
     std::vector<uint8_t> rf;
     std::vector<double> adH, adT, cp, fp, fd, fdp;
-    std::vector<float> cdelta;
     std::vector<ldso_ba_frame_state> fs;
     std::vector<PointFrameResidual *> order;
     ldso_ba_window w;
     OracleWin(const Synth &S, EnergyFunctional &ef) {
-        const int N = S.N;
+        const int N = ef.nFrames;
         fs.resize(N);
+        dI.resize((size_t)N * S.w * S.h * 3);
         for (int f = 0; f < N; f++) {
             const FrameHessian &F = *ef.frames[f];
             std::memset(&fs[f], 0, sizeof(fs[f]));
@@ -129,7 +137,9 @@ struct OracleWin {
             std::memcpy(fs[f].state, F.state, sizeof(F.state));
             std::memcpy(fs[f].state_zero, F.state_zero, sizeof(F.state_zero));
             fs[f].ab_exposure = F.ab_exposure;
-            fs[f].is_first_frame = F.isFirstFrame;
+            fs[f].is_first_frame = F.frameID == 0;
+            std::memcpy(&dI[(size_t)f * S.w * S.h * 3], F.dI, (size_t)S.w * S.h * 3 * sizeof(float));
+            th.push_back(F.frameEnergyTH);
         }
         precalc.resize((size_t)N * N * LDSO_BA_PRECALC_STRIDE);
         adH.resize((size_t)N * N * 64);
@@ -138,24 +148,23 @@ struct OracleWin {
         fp.resize(8 * N);
         fd.resize(8 * N);
         fdp.resize(8 * N);
-        cdelta.assign(4, 0.f);
+        cdelta.assign(ef.cDeltaF, ef.cDeltaF + 4);
         oracle_frame_precalc(N, fs.data(), S.calib, precalc.data());
         oracle_set_adjoints(N, fs.data(), adH.data(), adT.data(), cp.data());
         oracle_frame_take_data(N, fs.data(), fp.data(), fd.data(), fdp.data());
-        th = S.th;
         rb.push_back(0);
-        for (PointHessian *p : ef.allPoints) {
-            ph.push_back(p->host->idx);
+        for (auto &p : ef.allPoints) {
+            ph.push_back(p->host.lock()->idx);
             float d[LDSO_BA_POINT_STRIDE] = {p->u, p->v, p->idepth_scaled, p->idepth_zero_scaled, p->priorF, p->deltaF};
             std::memcpy(d + 8, p->color, sizeof(p->color));
             std::memcpy(d + 16, p->weights, sizeof(p->weights));
             pd.insert(pd.end(), d, d + LDSO_BA_POINT_STRIDE);
-            for (PointFrameResidual *r : p->residuals) {
-                rt.push_back(r->target->idx);
+            for (auto &r : p->residuals) {
+                rt.push_back(r->target.lock()->idx);
                 rs.push_back((int8_t)r->state_state);
-                re.push_back(r->state_energy);
+                re.push_back((float)r->state_energy);
                 rf.push_back((r->isActiveAndIsGoodNEW ? 1 : 0) | (r->isNew ? 2 : 0));
-                order.push_back(r);
+                order.push_back(r.get());
             }
             rb.push_back((int32_t)rt.size());
         }
@@ -166,7 +175,7 @@ struct OracleWin {
         w.width = S.w;
         w.height = S.h;
         std::memcpy(w.calib, S.calib, sizeof(w.calib));
-        w.dI = S.dI.data();
+        w.dI = dI.data();
         w.frame_energy_th = th.data();
         w.precalc = precalc.data();
         w.ad_host = adH.data();
@@ -185,110 +194,262 @@ struct OracleWin {
     }
 };
 
-static int cpu_tests() {
-    Synth S(4, 60, 160, 120, 3);
-    Graph G(S);
-    EnergyFunctional ef(1 << 20);  // no such device: reported, never thrown
-    CHECK(!ef.ok(), "creating a context on a missing device must fail");
-    CHECK(!ef.lastError().empty(), "error message expected");
-    G.insertInto(ef);
-    CHECK(ef.nFrames == 4 && ef.nPoints == 60 && ef.nResiduals == 180, "counts %d %d %d", ef.nFrames, ef.nPoints,
-          ef.nResiduals);
-    for (size_t i = 1; i < ef.allPoints.size(); i++)
-        CHECK(ef.allPoints[i - 1]->host->idx <= ef.allPoints[i]->host->idx, "makeIDX host order");
-    ef.dropResidual(G.res[0].get());
-    CHECK(ef.nResiduals == 179 && G.points[0]->residuals.size() == 2, "dropResidual");
-    ef.removePoint(G.points[1].get());
-    CHECK(ef.nPoints == 59 && ef.nResiduals == 176, "removePoint");
-    const Vec3 e = ef.linearizeAll(false);
-    CHECK(e[0] == 0 && !ef.ok(), "linearize without a device reports an error");
-    return 0;
-}
-
-static double rel(const std::vector<double> &a, const std::vector<double> &b) {
+static double rel(const double *a, const double *b, size_t n) {
     double num = 0, den = 0;
-    for (size_t i = 0; i < a.size(); i++) {
+    for (size_t i = 0; i < n; i++) {
         num += (a[i] - b[i]) * (a[i] - b[i]);
         den += b[i] * b[i];
     }
     return std::sqrt(num / (den > 0 ? den : 1));
 }
 
-static void compare_iteration(const Synth &S, EnergyFunctional &ef, oracle_window *ow, OracleWin &O, const Vec3 &e,
-                              int it) {
-    double eo[3];
-    const int R = ef.nResiduals, N = ef.nFrames, n = 8 * N + 4;
-    std::vector<double> HA(n * n), bA(n), HL(n * n), bL(n), Hsc(n * n), bsc(n);
-    oracle_linearize_all(ow, 0, eo);  // the pass ldso_ba_linearize(0, 1) runs
-    oracle_apply_res(ow);
-    oracle_accumulate(ow, HA.data(), bA.data(), HL.data(), bL.data(), Hsc.data(), bsc.data());
-    CHECK(e[2] == eo[2], "it %d: #IN %g vs %g", it, e[2], eo[2]);
-    CHECK(std::fabs(e[0] - eo[0]) <= 1e-9 * std::fabs(eo[0]), "it %d: energy %.17g vs %.17g", it, e[0], eo[0]);
-    std::vector<int8_t> ns(R), st(R);
-    std::vector<float> se(R), ewo(R), ctr(3 * R), jp(8 * R), rb(R);
-    std::vector<uint8_t> fl(R);
-    oracle_get_residuals(ow, ns.data(), st.data(), se.data(), ewo.data(), ctr.data(), fl.data(), jp.data(), rb.data());
-    int bad = 0;
-    for (int k = 0; k < R; k++) {
-        const PointFrameResidual &r = *O.order[k];
-        bad += r.state_NewState != ns[k] || r.state_state != st[k] || r.state_energy != se[k] ||
-               r.state_NewEnergyWithOutlier != ewo[k] || r.isActiveAndIsGoodNEW != ((fl[k] & 1) != 0) ||
-               std::memcmp(r.centerProjectedTo, &ctr[3 * k], 12) != 0 ||
-               (r.isActiveAndIsGoodNEW && std::memcmp(r.JpJdF, &jp[8 * k], 32) != 0);
-    }
-    CHECK(bad == 0, "it %d: %d residuals differ from the oracle", it, bad);
-    std::vector<float> th(N);
-    oracle_get_frame_energy_th(ow, th.data());
-    for (int f = 0; f < N; f++) CHECK(ef.frames[f]->frameEnergyTH == th[f], "it %d: frameEnergyTH[%d]", it, f);
-    // system (tolerance: reassociated float partial sums), solve on the same system, resubstitute
-    ef.solveSystemF(it, 1e-5);
-    CHECK(ef.ok(), "solveSystemF: %s", ef.lastError().c_str());
-    CHECK(rel(ef.HA_top, HA) < 1e-5 && rel(ef.H_sc, Hsc) < 1e-5 && rel(ef.bA_top, bA) < 1e-5 &&
-              rel(ef.b_sc, bsc) < 1e-5,
-          "it %d: stitched system %.2e %.2e", it, rel(ef.HA_top, HA), rel(ef.H_sc, Hsc));
-    std::vector<double> ns7((size_t)7 * n), xo(n);
-    oracle_nullspaces(N, O.fs.data(), ns7.data());
-    oracle_solve_system(N, it, 1e-5, ef.HA_top.data(), ef.bA_top.data(), ef.HL_top.data(), ef.bL_top.data(), nullptr,
-                        nullptr, ef.H_sc.data(), ef.b_sc.data(), ns7.data(), 7, xo.data());
-    CHECK(rel(ef.lastX, xo) < 1e-9, "it %d: solve %.2e", it, rel(ef.lastX, xo));
-    ef.resubstituteF_MT(ef.lastX, 1e-5);
-    std::vector<float> so(ef.nPoints);
-    oracle_resubstitute(ow, ef.lastX.data(), 1e-5, so.data());
-    double num = 0, den = 0;
-    for (int q = 0; q < ef.nPoints; q++) {
-        num += (ef.allPoints[q]->step - so[q]) * (double)(ef.allPoints[q]->step - so[q]);
-        den += (double)so[q] * so[q];
-    }
-    CHECK(std::sqrt(num) <= 1e-3 * std::sqrt(den) + 1e-12, "it %d: resubstitute", it);
-    (void)S;
+// worst per 8x8-block relative Frobenius error (blocks: calibration, then frames)
+static double block_err(const MatXX &G, const MatXX &O) {
+    const int n = O.rows(), nb = (n - 4) / 8 + 1;
+    auto lo = [](int k) { return k == 0 ? 0 : 4 + 8 * (k - 1); };
+    auto hi = [](int k) { return k == 0 ? 4 : 4 + 8 * k; };
+    double scale = 0;
+    for (double v : O.a) scale += v * v;
+    scale = std::sqrt(scale);
+    double worst = 0;
+    for (int a = 0; a < nb; a++)
+        for (int b = 0; b < nb; b++) {
+            double num = 0, den = 0;
+            for (int i = lo(a); i < hi(a); i++)
+                for (int j = lo(b); j < hi(b); j++) {
+                    num += (G(i, j) - O(i, j)) * (G(i, j) - O(i, j));
+                    den += O(i, j) * O(i, j);
+                }
+            worst = std::fmax(worst, std::sqrt(num) / std::fmax(std::sqrt(den), 1e-9 * scale + 1e-300));
+        }
+    return worst;
 }
+
+static int cpu_tests() {
+    Synth S(4, 60, 160, 120, 3);
+    Graph G(S);
+    auto ef = std::make_shared<EnergyFunctional>(1 << 20);  // no such device: reported, never thrown
+    CHECK(!ef->ok(), "creating a context on a missing device must fail");
+    CHECK(!ef->lastError().empty(), "error message expected");
+    G.insertInto(*ef);
+    CHECK(ef->nFrames == 4 && ef->nPoints == 60 && ef->nResiduals == 180, "counts %d %d %d", ef->nFrames,
+          ef->nPoints, ef->nResiduals);
+    CHECK(ef->HM.rows() == 8 * 4 + CPARS && ef->bM.size() == 8 * 4 + CPARS, "HM / bM grow with insertFrame");
+    for (size_t i = 1; i < ef->allPoints.size(); i++)
+        CHECK(ef->allPoints[i - 1]->host.lock()->idx <= ef->allPoints[i]->host.lock()->idx, "makeIDX host order");
+    int conn = 0;
+    for (auto &kv : ef->connectivityMap) conn += kv.second[0];
+    CHECK(conn == 180, "connectivity map counts %d", conn);
+    auto r0 = G.points[0]->residuals[0];
+    ef->dropResidual(r0);
+    CHECK(ef->nResiduals == 179 && G.points[0]->residuals.size() == 2, "dropResidual");
+    ef->removePoint(G.points[1]);
+    CHECK(ef->nPoints == 59 && ef->nResiduals == 176, "removePoint");
+    G.points[2]->status = PointStatus::OUT;
+    ef->dropPointsF();
+    CHECK(ef->nPoints == 58 && (int)ef->allPoints.size() == 58, "dropPointsF");
+    const double eL = ef->calcLEnergyF_MT(), eM = ef->calcMEnergyF();
+    CHECK(std::isfinite(eL) && eM == 0.0, "host energies without a device: %g %g", eL, eM);
+    const Vec3 e = ef->linearizeAll(false);
+    CHECK(e[0] == 0 && !ef->ok(), "linearize without a device reports an error");
+    return 0;
+}
+
+struct Cycle {
+    const Synth &S;
+    EnergyFunctional &ef;
+    MatXX HMo;
+    VecX bMo;
+    Cycle(const Synth &S_, EnergyFunctional &ef_) : S(S_), ef(ef_), HMo(ef_.HM), bMo(ef_.bM) {}
+
+    void iteration(int it, const shared_ptr<CalibHessian> &calib) {
+        const int N = ef.nFrames, n = 8 * N + 4;
+        OracleWin O(S, ef);  // the inputs this pass sees
+        oracle_set_threads(0);
+        oracle_window *ow = oracle_create(&O.w);
+        CHECK(ow != nullptr, "oracle window");
+        if (!ow) return;
+        const Vec3 e = ef.linearizeAll(false);
+        CHECK(ef.ok(), "it %d linearizeAll: %s", it, ef.lastError().c_str());
+        double eo[3];
+        oracle_linearize_all(ow, 0, eo);
+        oracle_apply_res(ow);
+        std::vector<double> HA(n * n), bA(n), HL(n * n), bL(n), Hsc(n * n), bsc(n);
+        oracle_accumulate(ow, HA.data(), bA.data(), HL.data(), bL.data(), Hsc.data(), bsc.data());
+        CHECK(e[2] == eo[2], "it %d: #IN %g vs %g", it, e[2], eo[2]);
+        CHECK(std::fabs(e[0] - eo[0]) <= 1e-9 * std::fabs(eo[0]), "it %d: energy %.17g vs %.17g", it, e[0], eo[0]);
+        CHECK(ef.resInA == (int)eo[2], "it %d: resInA", it);
+        const int R = (int)O.order.size();
+        std::vector<int8_t> ns(R), st(R);
+        std::vector<float> se(R), ewo(R), ctr(3 * R), jp(8 * R), rbs(R);
+        std::vector<uint8_t> fl(R);
+        oracle_get_residuals(ow, ns.data(), st.data(), se.data(), ewo.data(), ctr.data(), fl.data(), jp.data(),
+                             rbs.data());
+        int bad = 0;
+        for (int k = 0; k < R; k++) {
+            const PointFrameResidual &r = *O.order[k];
+            bad += r.state_NewState != ns[k] || r.state_state != st[k] || (float)r.state_energy != se[k] ||
+                   (float)r.state_NewEnergyWithOutlier != ewo[k] || r.isActiveAndIsGoodNEW != ((fl[k] & 1) != 0) ||
+                   std::memcmp(r.centerProjectedTo, &ctr[3 * k], 12) != 0 ||
+                   (r.isActiveAndIsGoodNEW && std::memcmp(r.JpJdF, &jp[8 * k], 32) != 0);
+        }
+        CHECK(bad == 0, "it %d: %d of %d residuals differ from the oracle", it, bad, R);
+        std::vector<float> th(N);
+        oracle_get_frame_energy_th(ow, th.data());
+        for (int f = 0; f < N; f++) CHECK(ef.frames[f]->frameEnergyTH == th[f], "it %d: frameEnergyTH[%d]", it, f);
+
+        ef.solveSystemF(it, 1e-5, calib);
+        CHECK(ef.ok(), "it %d solveSystemF: %s", it, ef.lastError().c_str());
+        CHECK(rel(ef.HA_top.data(), HA.data(), n * n) < 1e-5 && rel(ef.H_sc.data(), Hsc.data(), n * n) < 1e-5 &&
+                  rel(ef.bA_top.data(), bA.data(), n) < 1e-5 && rel(ef.b_sc.data(), bsc.data(), n) < 1e-5,
+              "it %d: stitched system %.2e %.2e", it, rel(ef.HA_top.data(), HA.data(), n * n),
+              rel(ef.H_sc.data(), Hsc.data(), n * n));
+        // the solver on the same system and marginalisation prior as the oracle's
+        std::vector<double> ns7((size_t)7 * n), xo(n);
+        oracle_nullspaces(N, O.fs.data(), ns7.data());
+        oracle_solve_system(N, it, 1e-5, ef.HA_top.data(), ef.bA_top.data(), ef.HL_top.data(), ef.bL_top.data(),
+                            ef.HM.data(), ef.bM.data(), ef.H_sc.data(), ef.b_sc.data(), ns7.data(), 7, xo.data());
+        CHECK(rel(ef.lastX.data(), xo.data(), n) < 1e-9, "it %d: solve %.2e", it, rel(ef.lastX.data(), xo.data(), n));
+        CHECK((int)ef.lastNullspaces_pose.size() == 6 && (int)ef.lastNullspaces_scale.size() == 1 &&
+                  rel(ef.lastNullspaces_pose[0].data(), ns7.data(), n) == 0.0,
+              "it %d: lastNullspaces", it);
+
+        ef.resubstituteF_MT(ef.lastX, calib);
+        CHECK(ef.ok(), "it %d resubstituteF_MT: %s", it, ef.lastError().c_str());
+        std::vector<float> so(ef.allPoints.size());
+        oracle_resubstitute(ow, ef.lastX.data(), 1e-5, so.data());
+        double num = 0, den = 0;
+        for (size_t q = 0; q < so.size(); q++) {
+            num += (ef.allPoints[q]->step - so[q]) * (double)(ef.allPoints[q]->step - so[q]);
+            den += (double)so[q] * so[q];
+        }
+        CHECK(std::sqrt(num) <= 1e-3 * std::sqrt(den) + 1e-12, "it %d: resubstitute", it);
+        CHECK(calib->step[0] == -ef.lastX[0] && ef.frames[N - 1]->step[0] == -ef.lastX[4 + 8 * (N - 1)],
+              "it %d: calibration / frame steps", it);
+        oracle_destroy(ow);
+
+        // doStepFromBackup (test harness) + setPrecalcValues' setDeltaF
+        for (auto &F : ef.frames)
+            for (int k = 0; k < 8; k++) F->state[k] += F->step[k];
+        for (auto &p : ef.allPoints) {
+            p->setIdepth(p->idepth + p->step);
+            p->setIdepthZero(p->idepth);
+        }
+        ef.setDeltaF(calib);
+        energies(it);
+    }
+
+    void energies(int it) {
+        const int N = ef.nFrames;
+        std::vector<double> prior(8 * N), dprior(8 * N), delta(8 * N);
+        for (int f = 0; f < N; f++) {
+            std::memcpy(&prior[8 * f], ef.frames[f]->prior, 64);
+            std::memcpy(&dprior[8 * f], ef.frames[f]->delta_prior, 64);
+            std::memcpy(&delta[8 * f], ef.frames[f]->delta, 64);
+        }
+        std::vector<float> dd, pf;
+        for (auto &p : ef.allPoints) {
+            dd.push_back(p->deltaF);
+            pf.push_back(p->priorF);
+        }
+        const double eL = ef.calcLEnergyF_MT();
+        const double eLo = oracle_calc_l_energy(N, prior.data(), dprior.data(), ef.cPrior, ef.cDeltaF, (int)dd.size(),
+                                                dd.data(), pf.data());
+        CHECK(eL == eLo, "it %d: calcLEnergyF_MT %.17g vs %.17g", it, eL, eLo);
+        const double eM = ef.calcMEnergyF();
+        const double eMo = oracle_calc_m_energy(N, HMo.data(), bMo.data(), ef.cDeltaF, delta.data());
+        CHECK(std::fabs(eM - eMo) <= 1e-4 * std::fabs(eMo) + 1e-12, "it %d: calcMEnergyF %.17g vs %.17g", it, eM, eMo);
+    }
+};
 
 static int gpu_tests() {
     Synth S(6, 800, 320, 240, 21);
     Graph G(S);
-    EnergyFunctional ef(0);
-    CHECK(ef.ok(), "context: %s", ef.lastError().c_str());
-    if (!ef.ok()) return 1;
-    G.insertInto(ef);
-    OracleWin O(S, ef);
-    oracle_set_threads(0);
-    oracle_window *ow = oracle_create(&O.w);
-    // iteration 0: FullSystem::optimize's resetOOB + linearizeAll(false) + solve + resubstitute
-    ef.resetOOB();
-    oracle_reset_oob(ow);
-    Vec3 e = ef.linearizeAll(false);
-    CHECK(ef.ok(), "linearizeAll: %s", ef.lastError().c_str());
-    compare_iteration(S, ef, ow, O, e, 0);
-    // iteration 1: a step on the newest frame (the update path, no structural change)
-    FrameHessian *nf = ef.frames.back();
-    nf->state[0] += 1e-4;
-    nf->state[4] -= 2e-4;
-    OracleWin O2(S, ef);
-    oracle_update(ow, &O2.w);
-    e = ef.linearizeAll(false);
-    CHECK(ef.ok(), "linearizeAll (update): %s", ef.lastError().c_str());
-    compare_iteration(S, ef, ow, O2, e, 2);
-    oracle_destroy(ow);
+    auto ef = std::make_shared<EnergyFunctional>(0);
+    CHECK(ef->ok(), "context: %s", ef->lastError().c_str());
+    if (!ef->ok()) return 1;
+    G.insertInto(*ef);
+    Cycle C(S, *ef);
+    // FullSystem::optimize: resetOOB of every active residual, then GN iterations
+    ef->resetOOB();
+    for (int it = 0; it < 3; it++) C.iteration(it, G.calib);
+
+    // flagPointsForRemoval: frame 0 leaves; its points and every 7th point are marginalised, a few
+    // points are dropped (OUT)
+    auto f0 = ef->frames[0];
+    f0->flaggedForMarginalization = true;
+    int k = 0, nmarg = 0, nout = 0;
+    for (auto &p : ef->allPoints) {
+        if (p->host.lock() == f0 || k % 7 == 0) {
+            p->status = PointStatus::MARGINALIZED;
+            nmarg++;
+        } else if (k % 29 == 3) {
+            p->status = PointStatus::OUT;
+            nout++;
+        }
+        k++;
+    }
+    {
+        OracleWin O(S, *ef);
+        oracle_window *ow = oracle_create(&O.w);
+        std::vector<int> pts;
+        for (size_t q = 0; q < ef->allPoints.size(); q++)
+            if (ef->allPoints[q]->status == PointStatus::MARGINALIZED) pts.push_back((int)q);
+        const int n = 8 * ef->nFrames + 4;
+        std::vector<double> H((size_t)n * n), b(n);
+        oracle_marginalize_points(ow, (int)pts.size(), pts.data(), ef->adHTdeltaF.data(), H.data(), b.data());
+        for (int i = 0; i < n; i++) {
+            C.bMo[i] += 0.25 * b[i];
+            for (int j = 0; j < n; j++) C.HMo(i, j) += 0.25 * H[(size_t)i * n + j];
+        }
+        oracle_destroy(ow);
+    }
+    const int pts_before = ef->nPoints;
+    ef->marginalizePointsF();
+    CHECK(ef->ok(), "marginalizePointsF: %s", ef->lastError().c_str());
+    CHECK(ef->nPoints == pts_before - nmarg && ef->resInM > 0, "marginalizePointsF removed %d of %d points",
+          pts_before - ef->nPoints, nmarg);
+    CHECK(block_err(ef->HM, C.HMo) < 1e-4, "HM after marginalizePointsF: %.2e", block_err(ef->HM, C.HMo));
+    CHECK(rel(ef->bM.data(), C.bMo.data(), ef->bM.size()) < 1e-4, "bM after marginalizePointsF");
+    ef->dropPointsF();
+    CHECK(ef->nPoints == pts_before - nmarg - nout, "dropPointsF");
+
+    // FullSystem::marginalizeFrame: the Schur step, then every observation of frame 0 dropped
+    {
+        const int N = ef->nFrames, n = 8 * N + 4;
+        ldso_ba_frame_state s0;
+        std::memset(&s0, 0, sizeof(s0));
+        std::memcpy(s0.world_to_cam_evalpt, f0->worldToCam_evalPT, sizeof(f0->worldToCam_evalPT));
+        std::memcpy(s0.state, f0->state, sizeof(f0->state));
+        std::memcpy(s0.state_zero, f0->state_zero, sizeof(f0->state_zero));
+        s0.ab_exposure = f0->ab_exposure;
+        s0.is_first_frame = 1;
+        double pr[8], dl[8], dp[8];
+        oracle_frame_take_data(1, &s0, pr, dl, dp);
+        MatXX Ho(n - 8, n - 8);
+        VecX bo(n - 8);
+        ldso_ba_marginalize_frame(N, f0->idx, C.HMo.data(), C.bMo.data(), pr, dp, Ho.data(), bo.data());
+        C.HMo = Ho;
+        C.bMo = bo;
+    }
+    ef->marginalizeFrame(f0);
+    CHECK(ef->ok() && ef->nFrames == S.N - 1 && ef->HM.rows() == 8 * (S.N - 1) + 4, "marginalizeFrame: %s",
+          ef->lastError().c_str());
+    CHECK(block_err(ef->HM, C.HMo) < 1e-4, "HM after marginalizeFrame: %.2e", block_err(ef->HM, C.HMo));
+    for (auto &p : std::vector<shared_ptr<PointHessian>>(ef->allPoints)) {
+        const auto rs = p->residuals;
+        for (auto &r : rs)
+            if (r->target.lock() == f0) ef->dropResidual(r);
+    }
+    ef->makeIDX();
+    ef->setAdjointsF(G.calib);
+    ef->setDeltaF(G.calib);
+    for (auto &p : ef->allPoints)
+        for (auto &r : p->residuals) CHECK(r->target.lock() != f0 && r->host.lock() != f0, "stale observation");
+
+    // optimize again on the 5-frame window, HM / bM in the solve
+    ef->resetOOB();
+    for (int it = 0; it < 2; it++) C.iteration(3 + it, G.calib);
     return 0;
 }
 

@@ -1,7 +1,8 @@
-"""The C++ host face (include/ldso_amd/energy_functional.h: FrameHessian, PointHessian,
-PointFrameResidual, EnergyFunctional with insert*/makeIDX/linearizeAll/solveSystemF/
-resubstituteF_MT) exercised by its own C++ test program, tests/cpp/test_energy_functional.cpp,
-against the oracle on the same synthetic window."""
+"""The C++ host face (include/ldso_amd/energy_functional.h: the EnergyFunctional.h:55-186 surface
+with shared_ptr ownership, PointFrameResidual / FrameHessian / PointHessian / CalibHessian)
+exercised by its own C++ test program, tests/cpp/test_energy_functional.cpp: a whole keyframe
+cycle (insert, optimize x3, flag + marginalizePointsF, dropPointsF, marginalizeFrame, optimize x2
+with HM / bM) against the oracle on the same inputs."""
 import os
 import subprocess
 
@@ -23,6 +24,6 @@ def test_cpp_host_structure_and_errors(built):
 
 
 @pytest.mark.gpu
-def test_cpp_host_gn_iterations_match_oracle(built):
+def test_cpp_host_keyframe_cycle_matches_oracle(built):
     p = run()
     assert p.returncode == 0 and "0 failure(s)" in p.stdout
