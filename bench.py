@@ -320,21 +320,17 @@ def main():
         shard = (rank, world)
     windows = [synth.make_window(n_frames=N, n_points=P, seed=s) for s in seeds]
     ctx = BAContext(local_rank)
+    if args.mode == "shard" and dist is not None:
+        from ldso_amd import dist as ldist
+
+        ldist.attach_rccl(ctx, dist)  # the library's own RCCL exchange ends every pass
     ctx.load(windows, shard_rank=shard[0], shard_count=shard[1])
     for w in windows:
         w.dI = None  # images now live in HBM only
     R_rank = ctx.stats()["residuals"]
 
-    packed = None
-    if args.mode == "shard" and dist is not None:
-        from ldso_amd import dist as ldist
-
-        packed = ldist.ShardExchange(ctx, dist)
-
     def step():
         ctx.linearize(fix=False, accumulate=True)
-        if packed is not None:
-            packed()
 
     for _ in range(args.warmup):
         step()

@@ -267,6 +267,7 @@ private:
     void packFrames(std::vector<ldso_ba_frame_state> &fs) const;
     ldso_ba_ctx *ctx_ = nullptr;
     ldso_ba_ctx *margCtx_ = nullptr;
+    std::vector<shared_ptr<PointHessian>> registry_;  // every inserted point not yet removed
     int device_ = 0;
     double currentLambda_ = 0;  // EnergyFunctional::currentLambda (set by solveSystemF)
     CalibHessian calib_;

@@ -175,6 +175,21 @@ int ldso_ba_calc_l_energy(int32_t n_frames, const double *prior, const double *d
                           const float *c_delta, int32_t n_points, const float *deltaF, const float *priorF,
                           double *out);
 
+/* ---- multi-GPU -------------------------------------------------------
+ * Points are sharded by host frame: in host-frame order the window's points are cut into
+ * `count` contiguous runs of equal residual counts (ldso_ba_load keeps run `rank`); a host is
+ * split only where a cut falls inside it.  points_out (may be NULL) receives the caller indices
+ * of run `rank`, *n_out their number. */
+int ldso_ba_shard_points(const ldso_ba_window *w, int32_t rank, int32_t count, int32_t *points_out,
+                         int32_t *n_out);
+/* The packed layout the ranks reduce (ldso_ba_packed_system): upper triangles, row-major,
+ * [HA (dim(dim+1)/2), bA (dim), Hsc (dim(dim+1)/2), bsc (dim)]; unpack_upper mirrors to full. */
+int ldso_ba_pack_upper(int32_t dim, const double *HA, const double *bA, const double *Hsc, const double *bsc,
+                        double *packed);
+int ldso_ba_unpack_upper(int32_t dim, const double *packed, double *HA, double *bA, double *Hsc, double *bsc);
+/* setNewFrameEnergyTH over gathered newest-frame NewEnergyWithOutlier values (< 0 = padding). */
+int ldso_ba_frame_threshold(const float *values, int64_t n, float *th_out);
+
 /* ---- device context --------------------------------------------------------------- */
 
 /* Create a context on HIP device `device` with its own non-blocking stream. */
@@ -183,6 +198,16 @@ void ldso_ba_destroy(ldso_ba_ctx *ctx);
 
 /* The HIP stream (hipStream_t) every kernel of this context is launched on. */
 void *ldso_ba_stream(ldso_ba_ctx *ctx);
+
+/* In-library exchange over RCCL (xGMI): rank 0 makes the id, the caller hands it to every rank
+ * (any channel), each rank attaches its context.  From then on every ldso_ba_linearize ends,
+ * stream-ordered and without a host synchronisation, with the exchange of SURVEY §8e: a sum
+ * all-reduce (fp64) of the packed systems (with accumulate), of the energy / #IN pairs, and an
+ * all-gather of the newest-frame energies followed by the exact threshold re-selection.  Load
+ * each rank with ldso_ba_load(ctx, n, windows, rank, world). */
+#define LDSO_BA_COMM_ID_BYTES 128
+int ldso_ba_comm_unique_id(uint8_t *id_out);
+int ldso_ba_comm_init(ldso_ba_ctx *ctx, const uint8_t *id, int32_t rank, int32_t world);
 
 /* (Re)build the device mirror of n_windows windows (EnergyFunctional::insertFrame /
  * insertResidual / dropResidual / makeIDX all end here).  shard_count > 1 keeps only the

@@ -114,6 +114,12 @@ ABI = [
     ("ldso_ba_newest_stride", C.c_int, [C.c_void_p, i64p]),
     ("ldso_ba_export_newest", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
     ("ldso_ba_frame_threshold_gathered", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64]),
+    ("ldso_ba_shard_points", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, i32p, i32p]),
+    ("ldso_ba_pack_upper", C.c_int, [C.c_int32, f64p, f64p, f64p, f64p, f64p]),
+    ("ldso_ba_unpack_upper", C.c_int, [C.c_int32, f64p, f64p, f64p, f64p, f64p]),
+    ("ldso_ba_frame_threshold", C.c_int, [f32p, C.c_int64, f32p]),
+    ("ldso_ba_comm_unique_id", C.c_int, [C.c_void_p]),
+    ("ldso_ba_comm_init", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("ldso_ba_set_tuning", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),

@@ -49,6 +49,13 @@ class BAContext:
             w._keep = []  # host copies are no longer referenced by the device
         return self
 
+    def comm_init(self, unique_id, rank: int, world: int):
+        """Attach to an RCCL communicator (ldso_ba_comm_init); unique_id: 128 bytes from
+        ldso_ba_comm_unique_id on rank 0.  See ldso_amd.dist.attach_rccl."""
+        uid = np.frombuffer(bytes(unique_id), np.uint8).copy()
+        L.check(self._lib.ldso_ba_comm_init(self._h, uid.ctypes.data, int(rank), int(world)))
+        return self
+
     def load_marginalization(self, parent: "BAContext", parent_win: int, window: Window):
         """Make this context the marginalisation context of `parent`'s window `parent_win` for the
         points (and residuals) of `window` (ldso_ba_load_marginalization: images are borrowed)."""

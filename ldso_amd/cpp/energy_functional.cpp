@@ -182,6 +182,7 @@ void EnergyFunctional::insertFrame(shared_ptr<FrameHessian> fh, shared_ptr<Calib
 void EnergyFunctional::insertPoint(shared_ptr<PointHessian> ph) {
     ph->status = PointStatus::ACTIVE;
     ph->alreadyRemoved = false;
+    registry_.push_back(ph);
     allPoints.push_back(ph);
     nPoints++;
     dirty_ = true;
@@ -238,7 +239,7 @@ void EnergyFunctional::removePoint(shared_ptr<PointHessian> ph) {
 // EnergyFunctional.cc:205-262 with FullSystem.cc:1384-1404 (see the header)
 void EnergyFunctional::marginalizePointsF() {
     allPointsToMarg.clear();
-    for (const shared_ptr<PointHessian> &p : allPoints)
+    for (const shared_ptr<PointHessian> &p : registry_)
         if (p->status == PointStatus::MARGINALIZED && !p->alreadyRemoved) allPointsToMarg.push_back(p);
     if (allPointsToMarg.empty()) return;
     if (!upload()) return;  // current frame terms; the parent window lends its device images
@@ -247,6 +248,7 @@ void EnergyFunctional::marginalizePointsF() {
         fail("ldso_ba_create (marginalisation)");
         return;
     }
+    // the parent window as loaded holds every point still flagged ACTIVE before this call
     std::vector<PointHessian *> pts;
     for (const shared_ptr<PointHessian> &p : allPointsToMarg) pts.push_back(p.get());
     PointPack pk;
@@ -297,17 +299,22 @@ void EnergyFunctional::marginalizePointsF() {
 
 // EnergyFunctional.cc:264-278
 void EnergyFunctional::dropPointsF() {
-    for (const shared_ptr<PointHessian> &p : allPoints)
+    for (const shared_ptr<PointHessian> &p : registry_)
         if ((p->status == PointStatus::OUTLIER || p->status == PointStatus::OUT) && !p->alreadyRemoved) removePoint(p);
     makeIDX();
 }
 
 // EnergyFunctional.cc:500-521: frame indices; the active, not removed points in host-frame order
+// (the reference walks its frames' features; registry_ is that list)
 void EnergyFunctional::makeIDX() {
     for (size_t i = 0; i < frames.size(); i++) frames[i]->idx = (int)i;
-    std::vector<shared_ptr<PointHessian>> keep;
-    for (const shared_ptr<PointHessian> &p : allPoints)
-        if (!p->alreadyRemoved && p->status == PointStatus::ACTIVE) keep.push_back(p);
+    std::vector<shared_ptr<PointHessian>> keep, live;
+    for (const shared_ptr<PointHessian> &p : registry_) {
+        if (p->alreadyRemoved) continue;
+        live.push_back(p);
+        if (p->status == PointStatus::ACTIVE) keep.push_back(p);
+    }
+    registry_.swap(live);
     std::stable_sort(keep.begin(), keep.end(), [](const shared_ptr<PointHessian> &a, const shared_ptr<PointHessian> &b) {
         return a->host.lock()->idx < b->host.lock()->idx;
     });
@@ -319,7 +326,6 @@ void EnergyFunctional::makeIDX() {
             r->targetIDX = r->target.lock()->idx;
         }
     }
-    nPoints = (int)allPoints.size();
     dirty_ = true;
 }
 

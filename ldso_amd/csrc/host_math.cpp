@@ -90,20 +90,47 @@ struct Pose {  // rigid transform x -> R x + t (Sophus SE3 convention)
         for (int i = 0; i < 3; i++) p.t[i] = V(i, 0) * xi[0] + V(i, 1) * xi[1] + V(i, 2) * xi[2];
         return p;
     }
+    // Sophus SE3::log (se3.hpp:220-253) on the rotation matrix: Eigen's matrix -> quaternion
+    // (Quaternion.h, quaternionbase_assign_impl), SO3::logAndTheta's atan form (so3.hpp:239-283),
+    // and V^-1 with the half-angle factor; epsilon 1e-10 (common.hpp:144).  Stable for every
+    // angle (no 1 - cos(theta) cancellation).
     void log(double xi[6]) const {
-        double cs = std::max(-1.0, std::min(1.0, 0.5 * (R(0, 0) + R(1, 1) + R(2, 2) - 1)));
-        double th = std::acos(cs);
-        double f = th < 1e-10 ? 0.5 + th * th / 12 : th / (2 * std::sin(th));
-        double w[3] = {f * (R(2, 1) - R(1, 2)), f * (R(0, 2) - R(2, 0)), f * (R(1, 0) - R(0, 1))};
-        double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-        th = std::sqrt(th2);
-        double d = th < 1e-10 ? 1.0 / 12 + th2 / 720 : (1 - th * std::sin(th) / (2 * (1 - std::cos(th)))) / th2;
-        Mat3 W = skew(w), W2 = W * W;
+        double q[4];  // x, y, z, w
+        double tr = R(0, 0) + R(1, 1) + R(2, 2);
+        if (tr > 0) {
+            double t = std::sqrt(tr + 1.0);
+            q[3] = 0.5 * t;
+            t = 0.5 / t;
+            q[0] = (R(2, 1) - R(1, 2)) * t;
+            q[1] = (R(0, 2) - R(2, 0)) * t;
+            q[2] = (R(1, 0) - R(0, 1)) * t;
+        } else {
+            int i = 0;
+            if (R(1, 1) > R(0, 0)) i = 1;
+            if (R(2, 2) > R(i, i)) i = 2;
+            const int j = (i + 1) % 3, k = (j + 1) % 3;
+            double t = std::sqrt(R(i, i) - R(j, j) - R(k, k) + 1.0);
+            q[i] = 0.5 * t;
+            t = 0.5 / t;
+            q[3] = (R(k, j) - R(j, k)) * t;
+            q[j] = (R(j, i) + R(i, j)) * t;
+            q[k] = (R(k, i) + R(i, k)) * t;
+        }
+        const double n2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2], n = std::sqrt(n2), w = q[3];
+        double f;
+        if (n < 1e-10) f = 2.0 / w - 2.0 * n2 / (w * (w * w));
+        else if (std::fabs(w) < 1e-10) f = (w > 0 ? M_PI : -M_PI) / n;
+        else f = 2.0 * std::atan(n / w) / n;
+        const double th = f * n;
+        const double om[3] = {f * q[0], f * q[1], f * q[2]};
+        Mat3 W = skew(om), W2 = W * W;
+        const double d = std::fabs(th) < 1e-10 ? 1.0 / 12.0
+                                               : (1.0 - th * std::cos(0.5 * th) / (2.0 * std::sin(0.5 * th))) / (th * th);
         for (int i = 0; i < 3; i++) {
             double s = 0;
             for (int k = 0; k < 3; k++) s += ((i == k ? 1.0 : 0.0) - 0.5 * W(i, k) + d * W2(i, k)) * t[k];
             xi[i] = s;
-            xi[3 + i] = w[i];
+            xi[3 + i] = om[i];
         }
     }
     // Adj = [R, [t]x R; 0, R]

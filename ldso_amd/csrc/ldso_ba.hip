@@ -28,6 +28,7 @@
 // reference's statement order, so states, energies, JpJdF and the per-point sums are
 // bit-identical to the CPU restatement; the H/b sums are reassociated (tolerance-checked).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -2097,6 +2098,13 @@ struct ldso_ba_ctx {
     DevBuf<int2> d_pair_items, d_host_items;
     DevBuf<float> d_top_slab, d_sc_slab;
     DevBuf<double> d_item_energy, d_sys, d_win_energy;
+    // in-library multi-GPU exchange (ldso_ba_comm_init): RCCL communicator over this context's
+    // device, the newest-frame energy slot stride (max over ranks, set at the first exchange
+    // after a load) and its staging buffers
+    ncclComm_t comm = nullptr;
+    int comm_rank = 0, comm_world = 1;
+    int64_t x_stride = 0;
+    DevBuf<float> d_x_local, d_x_gathered;
     DevBuf<float> d_xad;            // [win][kXadStride]
     DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
     DevBuf<int> d_pt_win;
@@ -2304,6 +2312,10 @@ size_t stitch_smem_bytes(int KP, int N, int *th_cap) {
 
 }  // namespace
 
+namespace {
+void shard_points(const ldso_ba_window &in, int rank, int count, std::vector<int> &out);
+}  // namespace
+
 // =========================================================================================
 // C ABI
 // =========================================================================================
@@ -2361,6 +2373,73 @@ int ldso_ba_calc_l_energy(int32_t n, const double *prior, const double *delta_pr
         (n_points > 0 && (!deltaF || !priorF)) || !out)
         return fail(-1, "bad arguments");
     *out = calc_l_energy(n, prior, delta_prior, c_prior, c_delta, n_points, deltaF, priorF);
+    return 0;
+}
+
+int ldso_ba_shard_points(const ldso_ba_window *w, int32_t rank, int32_t count, int32_t *points_out,
+                         int32_t *n_out) {
+    if (!w || !n_out || count < 1 || rank < 0 || rank >= count) return fail(-1, "bad arguments");
+    if (int rc = check_window(*w, false)) return rc;
+    std::vector<int> pts;
+    shard_points(*w, rank, count, pts);
+    if (points_out) std::memcpy(points_out, pts.data(), pts.size() * sizeof(int32_t));
+    *n_out = (int32_t)pts.size();
+    return 0;
+}
+
+int ldso_ba_pack_upper(int32_t dim, const double *HA, const double *bA, const double *Hsc, const double *bsc,
+                        double *packed) {
+    if (dim < 1 || !HA || !bA || !Hsc || !bsc || !packed) return fail(-1, "bad arguments");
+    const long long pl = packed_len(dim);
+    long long q = 0;
+    for (int r = 0; r < dim; r++)
+        for (int c = r; c < dim; c++, q++) {
+            packed[q] = HA[(size_t)r * dim + c];
+            packed[pl + dim + q] = Hsc[(size_t)r * dim + c];
+        }
+    for (int r = 0; r < dim; r++) {
+        packed[pl + r] = bA[r];
+        packed[2 * pl + dim + r] = bsc[r];
+    }
+    return 0;
+}
+
+int ldso_ba_unpack_upper(int32_t dim, const double *packed, double *HA, double *bA, double *Hsc, double *bsc) {
+    if (dim < 1 || !packed) return fail(-1, "bad arguments");
+    const long long pl = packed_len(dim);
+    long long q = 0;
+    for (int r = 0; r < dim; r++)
+        for (int c = r; c < dim; c++, q++) {
+            if (HA) HA[(size_t)r * dim + c] = HA[(size_t)c * dim + r] = packed[q];
+            if (Hsc) Hsc[(size_t)r * dim + c] = Hsc[(size_t)c * dim + r] = packed[pl + dim + q];
+        }
+    for (int r = 0; r < dim; r++) {
+        if (bA) bA[r] = packed[pl + r];
+        if (bsc) bsc[r] = packed[2 * pl + dim + r];
+    }
+    return 0;
+}
+
+// setNewFrameEnergyTH (FullSystem.cc:2078-2109) over gathered NewEnergyWithOutlier values (< 0:
+// padding, skipped): the host form of k_frame_th, for callers that gather the slots themselves
+int ldso_ba_frame_threshold(const float *values, int64_t n, float *th_out) {
+    if (!th_out || n < 0 || (n > 0 && !values)) return fail(-1, "bad arguments");
+    std::vector<float> v;
+    v.reserve((size_t)n);
+    for (int64_t i = 0; i < n; i++)
+        if (values[i] >= 0) v.push_back(values[i]);
+    if (v.empty()) {
+        *th_out = 12 * 12 * LDSO_BA_PATTERN_NUM;
+        return 0;
+    }
+    const int nth = (int)(kFrameEnergyTHN * (float)v.size());
+    std::nth_element(v.begin(), v.begin() + nth, v.end());
+    const float x = sqrtf(v[nth]);
+    float th = x * kFrameEnergyTHFacMedian;
+    th = 26.0f * kFrameEnergyTHConstWeight + th * (1 - kFrameEnergyTHConstWeight);
+    th = th * th;
+    th *= kOverallEnergyTHWeight * kOverallEnergyTHWeight;
+    *th_out = th;
     return 0;
 }
 
@@ -2433,6 +2512,9 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_item_energy.release();
     c->d_sys.release();
     c->d_win_energy.release();
+    c->d_x_local.release();
+    c->d_x_gathered.release();
+    if (c->comm) (void)ncclCommDestroy(c->comm);
     c->d_xad.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -2443,6 +2525,23 @@ void *ldso_ba_stream(ldso_ba_ctx *c) { return c ? (void *)c->stream : nullptr; }
 }  // extern "C"
 
 namespace {
+// SURVEY.md §8e's partition: points in host-frame order, cut into shard_count contiguous runs of
+// (as nearly as possible) equal residual counts, so a shard holds whole host frames except at
+// its two ends (a host is split only where a cut falls inside it, e.g. when shards outnumber
+// hosts).  Rank r owns the points whose first residual lies in [r T / G, (r + 1) T / G).
+void shard_points(const ldso_ba_window &in, int rank, int count, std::vector<int> &out) {
+    out.clear();
+    const long long T = in.n_residuals;
+    long long acc = 0;
+    for (int f = 0; f < in.n_frames; f++)
+        for (int p = 0; p < in.n_points; p++) {
+            if (in.point_host[p] != f) continue;
+            const long long owner = T > 0 ? std::min<long long>(count - 1, acc * count / T) : p % count;
+            if (owner == rank) out.push_back(p);
+            acc += in.point_res_begin[p + 1] - in.point_res_begin[p];
+        }
+}
+
 // parent != nullptr: a marginalisation context over `ws[0]` whose frames are the parent's window
 // parent_win (images borrowed, not uploaded; priorF scaled by setting_idepthFixPriorMargFac)
 int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32_t shard_rank, int32_t shard_count,
@@ -2458,6 +2557,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_win = n_windows;
+    c->x_stride = 0;  // the exchange re-agrees on the newest-frame slot stride
     c->width = ws[0].width;
     c->height = ws[0].height;
     c->npix = c->width * c->height;
@@ -2518,14 +2618,8 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
             H.adHF[k] = (float)in.ad_host[k];
             H.adTF[k] = (float)in.ad_target[k];
         }
-        // points: stable order by host frame, then round-robin shard
-        std::vector<int> order;
-        order.reserve(in.n_points);
-        for (int f = 0; f < N; f++)
-            for (int p = 0; p < in.n_points; p++)
-                if (in.point_host[p] == f) order.push_back(p);
-        for (size_t q = 0; q < order.size(); q++)
-            if ((int)(q % shard_count) == shard_rank) H.pt_orig.push_back(order[q]);
+        // points of this shard (host-frame partition, shard_points)
+        shard_points(in, shard_rank, shard_count, H.pt_orig);
         const int P = (int)H.pt_orig.size();
         H.P = P;
         // residual bucket sort by pair index h + N t (stable in point order)
@@ -2864,6 +2958,75 @@ int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+#define NCCL_TRY(expr)                                                                            \
+    do {                                                                                          \
+        ncclResult_t r_ = (expr);                                                                 \
+        if (r_ != ncclSuccess) return fail(-2, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// SURVEY.md §8e's exchange, stream-ordered after k_stitch on the context stream (no host
+// synchronisation): one fp64 sum all-reduce of every window's packed {HA, bA, Hsc, bsc} (priors
+// are in rank 0's share only), one of the linearizeAll energy / #IN pairs, and an all-gather of
+// the newest-frame NewEnergyWithOutlier slots after which k_frame_th re-selects the exact
+// setNewFrameEnergyTH threshold on every rank.
+int comm_exchange(ldso_ba_ctx *c, bool accumulate) {
+    hipStream_t st = c->stream;
+    if (c->x_stride == 0) {  // first exchange since the load: agree on the slot stride
+        int64_t m = 1;
+        for (const WinDev &D : c->wd) m = std::max<int64_t>(m, D.newest_end - D.newest_begin);
+        DevBuf<int64_t> t;
+        if (int rc = t.alloc(1)) return rc;
+        HIP_TRY(hipMemcpyAsync(t.p, &m, sizeof(m), hipMemcpyHostToDevice, st));
+        NCCL_TRY(ncclAllReduce(t.p, t.p, 1, ncclInt64, ncclMax, c->comm, st));
+        HIP_TRY(hipMemcpyAsync(&m, t.p, sizeof(m), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        t.release();
+        c->x_stride = m;
+        if (int rc = c->d_x_local.alloc((size_t)c->n_win * m)) return rc;
+        if (int rc = c->d_x_gathered.alloc((size_t)c->comm_world * c->n_win * m)) return rc;
+    }
+    if (accumulate) NCCL_TRY(ncclAllReduce(c->d_sys.p, c->d_sys.p, c->d_sys.n, ncclFloat64, ncclSum, c->comm, st));
+    NCCL_TRY(ncclAllReduce(c->d_win_energy.p, c->d_win_energy.p, (size_t)2 * c->n_win, ncclFloat64, ncclSum, c->comm,
+                           st));
+    const long long stride = c->x_stride;
+    const dim3 grid((unsigned)std::min<long long>((stride + 255) / 256, 64), (unsigned)c->n_win);
+    k_export_newest<<<grid, 256, 0, st>>>(c->d_wins.p, c->d_rs_energy_wo.p, c->d_x_local.p, stride);
+    HIP_TRY(hipGetLastError());
+    NCCL_TRY(ncclAllGather(c->d_x_local.p, c->d_x_gathered.p, (size_t)c->n_win * stride, ncclFloat32, c->comm, st));
+    return timed_launch(c, 4, st, [&] {
+        k_frame_th<<<c->n_win, kStThreads, 0, st>>>(c->d_wins.p, c->d_x_gathered.p, c->comm_world, c->n_win, stride,
+                                                    c->d_frame_th.p);
+    });
+}
+}  // namespace
+
+extern "C" {
+
+int ldso_ba_comm_unique_id(uint8_t *id_out) {
+    if (!id_out) return fail(-1, "null id");
+    static_assert(sizeof(ncclUniqueId) == LDSO_BA_COMM_ID_BYTES, "RCCL unique id size");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return 0;
+}
+
+int ldso_ba_comm_init(ldso_ba_ctx *c, const uint8_t *id_in, int32_t rank, int32_t world) {
+    if (!c || !id_in || world < 1 || rank < 0 || rank >= world) return fail(-1, "bad arguments");
+    if (c->comm) return fail(-1, "communicator already initialised");
+    HIP_TRY(hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id_in, sizeof(id));
+    NCCL_TRY(ncclCommInitRank(&c->comm, world, id, rank));
+    c->comm_rank = rank;
+    c->comm_world = world;
+    c->x_stride = 0;
+    return 0;
+}
+
 int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
     HIP_TRY(hipSetDevice(c->device));
@@ -2947,7 +3110,9 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
         if (rc) return rc;
     }
-    return timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + c->n_pairs, kStThreads, st_smem, st>>>(Sp); });
+    rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + c->n_pairs, kStThreads, st_smem, st>>>(Sp); });
+    if (rc || !c->comm) return rc;
+    return comm_exchange(c, accumulate != 0);
 }
 
 int ldso_ba_activate_points(ldso_ba_ctx *c, int32_t win, int32_t n, const ldso_ct_immature *pts, int32_t min_obs,

@@ -1,28 +1,79 @@
 """Multi-GPU sharding of one window's points.
 
-Points are ordered by host frame and dealt round-robin to ranks (ldso_ba_load with
-shard_rank / shard_count), so every rank sees every host frame and any number of ranks stays
-balanced (including more ranks than keyframes).  Images and frame-pair tables are replicated.
-Every H/b term is a sum over points, so the only exchange per GN iteration is ONE all-reduce
-(sum, fp64) of the packed upper triangles {HA, bA, Hsc, bsc} of every window
-(2 * ((8N+4)(8N+5)/2 + 8N+4) doubles: 30 KB at N=7, 70 KB at N=11).  Priors (HL, bL) are added
-once, by rank 0 (the host builds them from the window's priors).  Each rank then solves the
-small system redundantly; resubstitution is shard-local.
+Points are sharded by host frame (ldso_ba_load(rank, world) / ldso_ba_shard_points): in
+host-frame order the points are cut into `world` contiguous runs of equal residual counts, so a
+rank holds whole host frames except where a cut falls inside one.  Images and frame-pair tables
+are replicated.  Every H/b term is a sum over points, so the exchange per GN iteration is ONE
+fp64 sum all-reduce of the packed upper triangles {HA, bA, Hsc, bsc} of every window
+(2 * ((8N+4)(8N+5)/2 + 8N+4) doubles: 30 KB at N=7, 70 KB at N=11), one of the energy / #IN
+pairs, and one all-gather of the newest frame's NewEnergyWithOutlier slots after which every
+rank re-selects the exact setNewFrameEnergyTH threshold (nth_element is not additive).  Priors
+(HL, bL) are in rank 0's share only.  Each rank then solves the small system redundantly;
+resubstitution is shard-local.
 
-The newest frame's energy threshold (setNewFrameEnergyTH, an nth_element over all residuals
-into the newest frame) is the one non-additive quantity: each rank exports its newest-frame
-NewEnergyWithOutlier segment, one all-gather (fixed slot size, set at load) brings every
-rank's values everywhere, and every rank re-selects the same exact threshold on the device.
+The product runs this exchange itself over RCCL, stream-ordered inside ldso_ba_linearize, once
+the context is attached to a communicator (attach_rccl: ldso_ba_comm_unique_id on rank 0, the
+id handed to the other ranks, ldso_ba_comm_init).  torch.distributed only carries the 128-byte
+id.  The gloo test (tests/test_multigpu_gloo.py) rehearses the same contract on CPU through the
+library's host entry points (shard_points, pack_upper / unpack_upper, frame_threshold).
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
+from . import _lib as L
 
-def shard_points(point_host, n_frames, rank, world):
-    """Caller point indices owned by `rank` (mirror of ldso_ba_load's rule)."""
-    order = [p for f in range(n_frames) for p in np.flatnonzero(np.asarray(point_host) == f)]
-    return np.array([p for q, p in enumerate(order) if q % world == rank], dtype=np.int64)
+
+def shard_points(window, rank, world):
+    """Caller point indices ldso_ba_load keeps on `rank` (the library's own partition)."""
+    s = window.c_struct(with_images=False)
+    out = np.zeros(window.n_points, np.int32)
+    n = C.c_int32()
+    L.check(L.lib().ldso_ba_shard_points(C.byref(s), int(rank), int(world), L.ptr(out, L.i32p), C.byref(n)))
+    window._keep = []
+    return out[: n.value].astype(np.int64)
+
+
+def pack_upper(sysm):
+    """{HA, bA, Hsc, bsc} of one window in the packed layout the ranks reduce (ldso_ba_pack_upper)."""
+    d = sysm["HA"].shape[0]
+    out = np.zeros(d * (d + 1) + 2 * d, np.float64)
+    a = {k: np.ascontiguousarray(sysm[k], np.float64) for k in ("HA", "bA", "Hsc", "bsc")}
+    L.check(L.lib().ldso_ba_pack_upper(d, L.ptr(a["HA"], L.f64p), L.ptr(a["bA"], L.f64p), L.ptr(a["Hsc"], L.f64p),
+                                       L.ptr(a["bsc"], L.f64p), L.ptr(out, L.f64p)))
+    return out
+
+
+def unpack_upper(packed, dim):
+    o = {"HA": np.zeros((dim, dim)), "bA": np.zeros(dim), "Hsc": np.zeros((dim, dim)), "bsc": np.zeros(dim)}
+    p = np.ascontiguousarray(packed, np.float64)
+    L.check(L.lib().ldso_ba_unpack_upper(dim, L.ptr(p, L.f64p), L.ptr(o["HA"], L.f64p), L.ptr(o["bA"], L.f64p),
+                                         L.ptr(o["Hsc"], L.f64p), L.ptr(o["bsc"], L.f64p)))
+    return o
+
+
+def frame_threshold(values):
+    """setNewFrameEnergyTH over gathered NewEnergyWithOutlier values (ldso_ba_frame_threshold)."""
+    v = np.ascontiguousarray(values, np.float32)
+    out = np.zeros(1, np.float32)
+    L.check(L.lib().ldso_ba_frame_threshold(L.ptr(v, L.f32p), v.size, L.ptr(out, L.f32p)))
+    return out[0]
+
+
+def attach_rccl(ctx, dist):
+    """Attach `ctx` to an RCCL communicator over the torch.distributed group's ranks (which only
+    carry the 128-byte id); from then on ldso_ba_linearize ends with the in-library exchange."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    uid = np.zeros(128, np.uint8)
+    if rank == 0:
+        L.check(L.lib().ldso_ba_comm_unique_id(uid.ctypes.data))
+    box = [bytes(uid)]
+    dist.broadcast_object_list(box, src=0)
+    uid = np.frombuffer(box[0], np.uint8).copy()
+    L.check(L.lib().ldso_ba_comm_init(ctx._h, uid.ctypes.data, rank, world))
+    return ctx
 
 
 def allreduce_packed(tensor, dist):
@@ -47,92 +98,3 @@ def subset_window(window, points):
         setattr(w, k, getattr(window, k)[res].copy())
     w._keep = []
     return w
-
-
-def packed_upper(sysm):
-    """{HA, bA, Hsc, bsc} of one window as ldso_ba's packed layout (upper triangles, row-major)."""
-    iu = np.triu_indices(sysm["HA"].shape[0])
-    return np.concatenate([sysm["HA"][iu], sysm["bA"], sysm["Hsc"][iu], sysm["bsc"]])
-
-
-def frame_threshold(values):
-    """setNewFrameEnergyTH (FullSystem.cc:2078-2109) over NewEnergyWithOutlier values (host
-    restatement for tests; the product selects on the device, ldso_ba_frame_threshold_gathered)."""
-    v = np.asarray(values, np.float32)
-    v = v[v >= 0]
-    if v.size == 0:
-        return np.float32(12 * 12 * 8)
-    nth = int(np.float32(0.7) * np.float32(v.size))
-    x = np.float32(np.sqrt(np.partition(v, nth)[nth]))
-    th = np.float32(26.0 * 0.5) + (x * np.float32(1.5)) * np.float32(0.5)
-    return np.float32(th * th)
-
-
-class PackedSystem:
-    """Device-side exchange buffer for a BAContext: copy out, all-reduce, copy back."""
-
-    def __init__(self, ctx):
-        import torch
-
-        self.ctx = ctx
-        _, n, _ = ctx.packed_system()
-        self.n = n
-        self.buf = torch.empty(n, dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
-
-    def allreduce(self, dist):
-        import torch
-
-        from . import _lib as L
-
-        L.check(self.ctx._lib.ldso_ba_copy_packed(self.ctx._h, self.buf.data_ptr(), self.n, 0))
-        allreduce_packed(self.buf, dist)
-        torch.cuda.current_stream().synchronize()
-        L.check(self.ctx._lib.ldso_ba_copy_packed(self.ctx._h, self.buf.data_ptr(), self.n, 1))
-
-
-class NewestThreshold:
-    """All-gather of the newest-frame energies + device re-selection of the frame threshold."""
-
-    def __init__(self, ctx, dist):
-        import ctypes as C
-
-        import torch
-
-        from . import _lib as L
-
-        self.ctx, self.dist = ctx, dist
-        s = C.c_int64()
-        L.check(ctx._lib.ldso_ba_newest_stride(ctx._h, C.byref(s)))
-        dev = torch.device("cuda", torch.cuda.current_device())
-        t = torch.tensor([max(1, s.value)], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        self.stride = int(t.item())
-        self.world = dist.get_world_size()
-        nw = len(ctx.windows)
-        self.local = torch.empty(nw * self.stride, dtype=torch.float32, device=dev)
-        self.gathered = torch.empty(self.world * nw * self.stride, dtype=torch.float32, device=dev)
-
-    def exchange(self):
-        import torch
-
-        from . import _lib as L
-
-        L.check(self.ctx._lib.ldso_ba_export_newest(self.ctx._h, self.local.data_ptr(), self.stride))
-        self.dist.all_gather_into_tensor(self.gathered, self.local)
-        torch.cuda.current_stream().synchronize()
-        L.check(self.ctx._lib.ldso_ba_frame_threshold_gathered(self.ctx._h, self.gathered.data_ptr(), self.world,
-                                                               self.stride))
-
-
-class ShardExchange:
-    """Per-GN-iteration exchange of a point-sharded context: one fp64 all-reduce of the
-    packed systems and one all-gather of the newest-frame energies."""
-
-    def __init__(self, ctx, dist):
-        self.packed = PackedSystem(ctx)
-        self.th = NewestThreshold(ctx, dist)
-        self.dist = dist
-
-    def __call__(self):
-        self.packed.allreduce(self.dist)
-        self.th.exchange()

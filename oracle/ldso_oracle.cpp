@@ -1274,29 +1274,50 @@ SE3d se3_exp(const double a[6]) {
     for (int i = 0; i < 3; i++) T.t[i] = V[i * 3] * up[0] + V[i * 3 + 1] * up[1] + V[i * 3 + 2] * up[2];
     return T;
 }
+// Sophus::SE3::log (thirdparty/Sophus/sophus/se3.hpp:220-253): the rotation as a unit quaternion
+// (Eigen Quaternion(Matrix3), Quaternion.h quaternionbase_assign_impl), SO3::logAndTheta
+// (so3.hpp:239-283, atan form), V^-1 with theta cos(theta/2) / (2 sin(theta/2)); epsilon 1e-10
 void se3_log(const SE3d &T, double out[6]) {
     const double *R = T.R;
-    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
-    c = std::max(-1.0, std::min(1.0, c));
-    double th = std::acos(c);
-    double w[3];
-    double v[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
-    double f;
-    if (th < 1e-10) f = 0.5 + th * th / 12.0;
-    else f = th / (2 * std::sin(th));
-    for (int i = 0; i < 3; i++) w[i] = f * v[i];
-    double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    th = std::sqrt(th2);
+    double q[4];  // x, y, z, w
+    const double tr = R[0] + R[4] + R[8];
+    if (tr > 0) {
+        double t = std::sqrt(tr + 1.0);
+        q[3] = 0.5 * t;
+        t = 0.5 / t;
+        q[0] = (R[7] - R[5]) * t;
+        q[1] = (R[2] - R[6]) * t;
+        q[2] = (R[3] - R[1]) * t;
+    } else {
+        int i = 0;
+        if (R[4] > R[0]) i = 1;
+        if (R[8] > R[i * 4]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        double t = std::sqrt(R[i * 4] - R[j * 4] - R[k * 4] + 1.0);
+        q[i] = 0.5 * t;
+        t = 0.5 / t;
+        q[3] = (R[k * 3 + j] - R[j * 3 + k]) * t;
+        q[j] = (R[j * 3 + i] + R[i * 3 + j]) * t;
+        q[k] = (R[k * 3 + i] + R[i * 3 + k]) * t;
+    }
+    const double squared_n = q[0] * q[0] + q[1] * q[1] + q[2] * q[2];
+    const double n = std::sqrt(squared_n), w = q[3];
+    double two_atan_nbyw_by_n;
+    if (n < 1e-10) two_atan_nbyw_by_n = 2.0 / w - 2.0 * squared_n / (w * (w * w));
+    else if (std::fabs(w) < 1e-10) two_atan_nbyw_by_n = (w > 0 ? M_PI : -M_PI) / n;
+    else two_atan_nbyw_by_n = 2.0 * std::atan(n / w) / n;
+    const double theta = two_atan_nbyw_by_n * n;
+    double w3[3] = {two_atan_nbyw_by_n * q[0], two_atan_nbyw_by_n * q[1], two_atan_nbyw_by_n * q[2]};
     double W[9], W2[9];
-    hat(w, W);
+    hat(w3, W);
     mm3(W, W, W2);
     double D;
-    if (th < 1e-10) D = 1.0 / 12.0 + th2 / 720.0;
-    else D = (1.0 - (th * std::sin(th)) / (2 * (1 - std::cos(th)))) / th2;
+    if (std::fabs(theta) < 1e-10) D = 1.0 / 12.0;
+    else D = (1.0 - theta * std::cos(0.5 * theta) / (2.0 * std::sin(0.5 * theta))) / (theta * theta);
     double Vi[9];
     for (int i = 0; i < 9; i++) Vi[i] = ((i % 4 == 0) ? 1.0 : 0.0) - 0.5 * W[i] + D * W2[i];
     for (int i = 0; i < 3; i++) out[i] = Vi[i * 3] * T.t[0] + Vi[i * 3 + 1] * T.t[1] + Vi[i * 3 + 2] * T.t[2];
-    for (int i = 0; i < 3; i++) out[3 + i] = w[i];
+    for (int i = 0; i < 3; i++) out[3 + i] = w3[i];
 }
 SE3d se3_mul(const SE3d &A, const SE3d &B) {
     SE3d C;

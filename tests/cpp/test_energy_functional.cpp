@@ -260,13 +260,26 @@ struct Cycle {
     EnergyFunctional &ef;
     MatXX HMo;
     VecX bMo;
+    std::unique_ptr<OracleWin> Op;
+    oracle_window *ow = nullptr;
     Cycle(const Synth &S_, EnergyFunctional &ef_) : S(S_), ef(ef_), HMo(ef_.HM), bMo(ef_.bM) {}
+    ~Cycle() {
+        if (ow) oracle_destroy(ow);
+    }
 
-    void iteration(int it, const shared_ptr<CalibHessian> &calib) {
+    // reload: the face re-uploads the window (structure changed) and the oracle is created anew;
+    // otherwise both keep their residual states and take the new frame / point values
+    void iteration(int it, const shared_ptr<CalibHessian> &calib, bool reload) {
         const int N = ef.nFrames, n = 8 * N + 4;
-        OracleWin O(S, ef);  // the inputs this pass sees
+        Op.reset(new OracleWin(S, ef));  // the inputs this pass sees
+        OracleWin &O = *Op;
         oracle_set_threads(0);
-        oracle_window *ow = oracle_create(&O.w);
+        if (reload || !ow) {
+            if (ow) oracle_destroy(ow);
+            ow = oracle_create(&O.w);
+        } else {
+            CHECK(oracle_update(ow, &O.w) == 0, "oracle_update");
+        }
         CHECK(ow != nullptr, "oracle window");
         if (!ow) return;
         const Vec3 e = ef.linearizeAll(false);
@@ -285,15 +298,23 @@ struct Cycle {
         std::vector<uint8_t> fl(R);
         oracle_get_residuals(ow, ns.data(), st.data(), se.data(), ewo.data(), ctr.data(), fl.data(), jp.data(),
                              rbs.data());
-        int bad = 0;
+        int bad = 0, why[7] = {0, 0, 0, 0, 0, 0, 0};
         for (int k = 0; k < R; k++) {
             const PointFrameResidual &r = *O.order[k];
-            bad += r.state_NewState != ns[k] || r.state_state != st[k] || (float)r.state_energy != se[k] ||
-                   (float)r.state_NewEnergyWithOutlier != ewo[k] || r.isActiveAndIsGoodNEW != ((fl[k] & 1) != 0) ||
-                   std::memcmp(r.centerProjectedTo, &ctr[3 * k], 12) != 0 ||
-                   (r.isActiveAndIsGoodNEW && std::memcmp(r.JpJdF, &jp[8 * k], 32) != 0);
+            const bool d[7] = {r.state_NewState != ns[k], r.state_state != st[k], (float)r.state_energy != se[k],
+                               (float)r.state_NewEnergyWithOutlier != ewo[k],
+                               r.isActiveAndIsGoodNEW != ((fl[k] & 1) != 0),
+                               std::memcmp(r.centerProjectedTo, &ctr[3 * k], 12) != 0,
+                               r.isActiveAndIsGoodNEW && std::memcmp(r.JpJdF, &jp[8 * k], 32) != 0};
+            bool any = false;
+            for (int q = 0; q < 7; q++) {
+                why[q] += d[q];
+                any = any || d[q];
+            }
+            bad += any;
         }
-        CHECK(bad == 0, "it %d: %d of %d residuals differ from the oracle", it, bad, R);
+        CHECK(bad == 0, "it %d: %d of %d residuals differ from the oracle (new_state %d state %d energy %d e_wo %d "
+              "active %d centre %d JpJdF %d)", it, bad, R, why[0], why[1], why[2], why[3], why[4], why[5], why[6]);
         std::vector<float> th(N);
         oracle_get_frame_energy_th(ow, th.data());
         for (int f = 0; f < N; f++) CHECK(ef.frames[f]->frameEnergyTH == th[f], "it %d: frameEnergyTH[%d]", it, f);
@@ -326,7 +347,6 @@ struct Cycle {
         CHECK(std::sqrt(num) <= 1e-3 * std::sqrt(den) + 1e-12, "it %d: resubstitute", it);
         CHECK(calib->step[0] == -ef.lastX[0] && ef.frames[N - 1]->step[0] == -ef.lastX[4 + 8 * (N - 1)],
               "it %d: calibration / frame steps", it);
-        oracle_destroy(ow);
 
         // doStepFromBackup (test harness) + setPrecalcValues' setDeltaF
         for (auto &F : ef.frames)
@@ -372,7 +392,7 @@ static int gpu_tests() {
     Cycle C(S, *ef);
     // FullSystem::optimize: resetOOB of every active residual, then GN iterations
     ef->resetOOB();
-    for (int it = 0; it < 3; it++) C.iteration(it, G.calib);
+    for (int it = 0; it < 3; it++) C.iteration(it, G.calib, it == 0);
 
     // flagPointsForRemoval: frame 0 leaves; its points and every 7th point are marginalised, a few
     // points are dropped (OUT)
@@ -391,7 +411,7 @@ static int gpu_tests() {
     }
     {
         OracleWin O(S, *ef);
-        oracle_window *ow = oracle_create(&O.w);
+        oracle_window *ow = oracle_create(&O.w);  // marginalisation relinearises from resetOOB
         std::vector<int> pts;
         for (size_t q = 0; q < ef->allPoints.size(); q++)
             if (ef->allPoints[q]->status == PointStatus::MARGINALIZED) pts.push_back((int)q);
@@ -449,7 +469,7 @@ static int gpu_tests() {
 
     // optimize again on the 5-frame window, HM / bM in the solve
     ef->resetOOB();
-    for (int it = 0; it < 2; it++) C.iteration(3 + it, G.calib);
+    for (int it = 0; it < 2; it++) C.iteration(3 + it, G.calib, it == 0);
     return 0;
 }
 

@@ -82,3 +82,23 @@ def test_calc_l_energy(built):
     kat = (dprior * prior * dprior).sum() + float((cd.astype(np.float64) ** 2 * cp).sum()) + \
         float((deltaF.astype(np.float64) ** 2 * priorF).sum())
     assert abs(e[0] - kat) <= 1e-5 * abs(kat)
+
+
+def test_frame_delta_is_stable_for_small_rotations(built):
+    """get_state_minus_stateZero (FrameHessian.h:59-64) through Sophus' atan-form SE3::log: finite
+    and first-order exact for rotation increments down to 1e-12 (the 1 - cos form cancels to 0/0)."""
+    w = synth.make_window(n_frames=3, n_points=10, width=160, height=120, seed=7)
+    fr = np.ascontiguousarray(w.frames).copy()
+    for mag in (1e-12, 1e-9, 1e-8, 1e-6, 1e-3):
+        fr["state"][:] = fr["state_zero"]
+        fr["state"][1, 3:6] += mag * np.array([1.0, -2.0, 0.5])
+        fr["state"][1, 0:3] += mag * np.array([0.3, 0.1, -0.2])
+        delta, pr, dp = np.zeros((3, 8)), np.zeros((3, 8)), np.zeros((3, 8))
+        L.check(L.lib().ldso_ba_frame_take_data(3, fr.ctypes.data, L.ptr(pr, L.f64p), L.ptr(delta, L.f64p),
+                                                L.ptr(dp, L.f64p)))
+        od = np.zeros((3, 8))
+        oracle.lib().oracle_frame_take_data(3, fr.ctypes.data, oracle._p(pr, oracle.f64p), oracle._p(od, oracle.f64p),
+                                            oracle._p(dp, oracle.f64p))
+        np.testing.assert_array_equal(delta, od)
+        assert np.all(np.isfinite(delta))
+        np.testing.assert_allclose(delta[1, 3:6], mag * np.array([1.0, -2.0, 0.5]), rtol=1e-3 if mag > 1e-10 else 0.2)

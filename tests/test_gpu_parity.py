@@ -387,3 +387,32 @@ def test_device_solve_rejects_windows_above_eleven_keyframes(built):
     with pytest.raises(RuntimeError, match="11 keyframes"):
         c.solve_device(0)
     c.close()
+
+
+def test_rccl_world1_exchange_keeps_results(built):
+    """ldso_ba_comm_init with one rank: every pass ends with the in-library RCCL exchange
+    (all-reduce of the packed systems and energies, all-gather of the newest-frame energies and
+    k_frame_th's re-selection) on the context stream; a single rank's results must equal those
+    of a context without a communicator (the H blocks up to the f64-atomic order of k_stitch)."""
+    from ldso_amd import _lib as L
+
+    cfg = dict(n_frames=6, n_points=700, seed=51)
+    a = BAContext(0).load([synth.make_window(**cfg)])
+    uid = np.zeros(128, np.uint8)
+    L.check(L.lib().ldso_ba_comm_unique_id(uid.ctypes.data))
+    b = BAContext(0).comm_init(uid.tobytes(), 0, 1).load([synth.make_window(**cfg)], shard_rank=0, shard_count=1)
+    for _ in range(3):
+        a.linearize(fix=False, accumulate=True)
+        b.linearize(fix=False, accumulate=True)
+    ra, rb = a.residuals(0), b.residuals(0)
+    for k in ("new_state", "state", "state_energy", "new_energy_wo", "jpjdf"):
+        np.testing.assert_array_equal(ra[k], rb[k], err_msg=k)
+    np.testing.assert_array_equal(a.frame_energy_th(0), b.frame_energy_th(0))
+    np.testing.assert_array_equal(a.energy(0), b.energy(0))
+    sa, sb = a.system(0), b.system(0)
+    for k in ("HA", "Hsc", "bA", "bsc"):
+        assert np.abs(sa[k] - sb[k]).max() <= 1e-12 * np.abs(sa[k]).max(), k
+    with pytest.raises(RuntimeError, match="already"):
+        b.comm_init(uid.tobytes(), 0, 1)
+    a.close()
+    b.close()
