@@ -339,6 +339,32 @@ int ldso_ba_resubstitute_device(ldso_ba_ctx *ctx, double lambda, float *point_st
 int ldso_ba_iterate(ldso_ba_ctx *ctx, int32_t iteration, double lambda, const double *ns, int32_t n_null,
                     double *x_out, float *point_step_out, double *energy_out);
 
+/* FullSystem::optimize (FullSystem.cc:844-976) on the device for every loaded window, with
+ * setting_forceAceptStep (the default) and the non-momentum doStepFromBackup: resetOOB, one
+ * linearizeAll + applyRes, then n_its times {solveSystemF (k_solve; orthogonalize with ns from
+ * iteration 2), resubstituteF_MT, doStepFromBackup (FullSystem.cc:1843-1922: frame states by
+ * log(exp(step) exp(state)), CalibHessian::setValue, point setIdepth / setIdepthZero) +
+ * setPrecalcValues (FrameFramePrecalc::Set for every pair, the prior vector), linearizeAll +
+ * applyRes}, all on the context stream with no host round trip; one synchronisation at the end.
+ *   frames [sum N]: the windows' frame states back to back; calib_value / calib_value_zero
+ *   [n_windows][4]: CalibHessian::value / value_zero (unscaled: value_scaled = 50 value);
+ *   ns: [7][sum (8N+4)] nullspaces (ldso_ba_nullspaces per window, back to back) or NULL.
+ * Outputs (any may be NULL): energy_out [n_its + 1][n_windows][3] = (E, 0, #IN) of the initial
+ * and every iteration's linearizeAll; frames_out / calib_out the stepped states; idepth_out
+ * [sum P] the points' idepth, caller order.  The reference's early exit (canbreak) is the
+ * caller's: it runs exactly n_its iterations.  Afterwards the context's precalc, calibration,
+ * priors and point data are the stepped ones (ldso_ba_update overrides them as before). */
+int ldso_ba_optimize(ldso_ba_ctx *ctx, int32_t n_its, const ldso_ba_frame_state *frames, const double *calib_value,
+                     const double *calib_value_zero, const double *ns, double *energy_out,
+                     ldso_ba_frame_state *frames_out, double *calib_out, float *idepth_out);
+
+/* doStepFromBackup's frame and calibration step on the host (the same se3.h statements as the
+ * device loop): out[f] = in[f] stepped by -x[4 + 8f ..]; calib_value (if not NULL) += -x[0..3],
+ * with value_scaledf and cDeltaF = value - value_zero returned if the pointers are not NULL. */
+int ldso_ba_frame_step(int32_t n_frames, const ldso_ba_frame_state *in, const double *x, ldso_ba_frame_state *out,
+                       double *calib_value, const double *calib_value_zero, float *calib_scaled_out,
+                       float *c_delta_out);
+
 /* Per-kernel HIP-event timing (bench/profiling).  When enabled every kernel launch of
  * ldso_ba_linearize is bracketed by events; get returns summed ms and launch counts for
  * n_kernels <= 16 slots in the order of ldso_ba_kernel_name(i). */

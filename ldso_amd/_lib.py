@@ -120,6 +120,9 @@ ABI = [
     ("ldso_ba_frame_threshold", C.c_int, [f32p, C.c_int64, f32p]),
     ("ldso_ba_comm_unique_id", C.c_int, [C.c_void_p]),
     ("ldso_ba_comm_init", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
+    ("ldso_ba_optimize", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, f64p, f64p, f64p, f64p, C.c_void_p, f64p,
+                                   f32p]),
+    ("ldso_ba_frame_step", C.c_int, [C.c_int32, C.c_void_p, f64p, C.c_void_p, f64p, f64p, f32p, f32p]),
     ("ldso_ba_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("ldso_ba_set_tuning", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),

@@ -49,6 +49,27 @@ class BAContext:
             w._keep = []  # host copies are no longer referenced by the device
         return self
 
+    def optimize(self, n_its: int, calib_value=None, calib_value_zero=None, nullspaces=None):
+        """FullSystem::optimize on the device (ldso_ba_optimize): n_its GN iterations of every
+        loaded window with no host round trip.  calib_value / calib_value_zero: [n_windows][4]
+        CalibHessian::value / value_zero (default: each window's calib / 50, i.e. no calibration
+        delta).  Returns (energies [n_its + 1][n_windows][3], frames, calib_value, idepths)."""
+        nw = len(self.windows)
+        frames = np.ascontiguousarray(np.concatenate([np.ascontiguousarray(w.frames) for w in self.windows]))
+        if calib_value is None:
+            calib_value = np.stack([w.calib.astype(np.float64) * (1.0 / 50.0) for w in self.windows])
+        calib_value = np.ascontiguousarray(calib_value, np.float64).reshape(nw, 4)
+        cz = calib_value.copy() if calib_value_zero is None else np.ascontiguousarray(calib_value_zero, np.float64)
+        ns = self._ns_all(nullspaces)
+        e = np.zeros((n_its + 1, nw, 3), np.float64)
+        fo = np.zeros_like(frames)
+        co = np.zeros((nw, 4), np.float64)
+        idep = np.zeros(sum(w.n_points for w in self.windows), np.float32)
+        L.check(self._lib.ldso_ba_optimize(self._h, int(n_its), frames.ctypes.data, L.ptr(calib_value, L.f64p),
+                                           L.ptr(cz, L.f64p), L.ptr(ns, L.f64p), L.ptr(e, L.f64p), fo.ctypes.data,
+                                           L.ptr(co, L.f64p), L.ptr(idep, L.f32p)))
+        return e, fo, co, self._split(idep, [w.n_points for w in self.windows])
+
     def comm_init(self, unique_id, rank: int, world: int):
         """Attach to an RCCL communicator (ldso_ba_comm_init); unique_id: 128 bytes from
         ldso_ba_comm_unique_id on rank 0.  See ldso_amd.dist.attach_rccl."""

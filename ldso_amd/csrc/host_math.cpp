@@ -9,173 +9,12 @@
 
 #include "../../include/ldso_ba.h"
 #include "ldso_ba_internal.h"
+#include "se3.h"
 
 namespace ldso_ba {
 
-namespace {
-
-constexpr double kScaleXiTrans = 0.5, kScaleXiRot = 1.0, kScaleA = 10.0, kScaleB = 1000.0;
-
-struct Mat3 {
-    double m[9];
-    double &operator()(int r, int c) { return m[r * 3 + c]; }
-    double operator()(int r, int c) const { return m[r * 3 + c]; }
-    static Mat3 eye() {
-        Mat3 a{};
-        a(0, 0) = a(1, 1) = a(2, 2) = 1;
-        return a;
-    }
-};
-Mat3 operator*(const Mat3 &a, const Mat3 &b) {
-    Mat3 c{};
-    for (int r = 0; r < 3; r++)
-        for (int k = 0; k < 3; k++)
-            for (int q = 0; q < 3; q++) c(r, q) += a(r, k) * b(k, q);
-    return c;
-}
-Mat3 skew(const double v[3]) {
-    Mat3 s{};
-    s(0, 1) = -v[2];
-    s(0, 2) = v[1];
-    s(1, 0) = v[2];
-    s(1, 2) = -v[0];
-    s(2, 0) = -v[1];
-    s(2, 1) = v[0];
-    return s;
-}
-
-struct Pose {  // rigid transform x -> R x + t (Sophus SE3 convention)
-    Mat3 R;
-    double t[3];
-    static Pose identity() {
-        Pose p;
-        p.R = Mat3::eye();
-        p.t[0] = p.t[1] = p.t[2] = 0;
-        return p;
-    }
-    Pose operator*(const Pose &b) const {
-        Pose c;
-        c.R = R * b.R;
-        for (int i = 0; i < 3; i++) c.t[i] = R(i, 0) * b.t[0] + R(i, 1) * b.t[1] + R(i, 2) * b.t[2] + t[i];
-        return c;
-    }
-    Pose inverse() const {
-        Pose c;
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) c.R(i, j) = R(j, i);
-        for (int i = 0; i < 3; i++) c.t[i] = -(c.R(i, 0) * t[0] + c.R(i, 1) * t[1] + c.R(i, 2) * t[2]);
-        return c;
-    }
-    // exp of the tangent [upsilon(3), omega(3)] (thirdparty/Sophus/sophus/se3.hpp)
-    static Pose exp(const double xi[6]) {
-        const double *w = xi + 3;
-        double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2], th = std::sqrt(th2);
-        double a, b, c;
-        if (th < 1e-10) {
-            a = 1 - th2 / 6;
-            b = 0.5 - th2 / 24;
-            c = 1.0 / 6 - th2 / 120;
-        } else {
-            a = std::sin(th) / th;
-            b = (1 - std::cos(th)) / th2;
-            c = (th - std::sin(th)) / (th2 * th);
-        }
-        Mat3 W = skew(w), W2 = W * W, I = Mat3::eye();
-        Pose p;
-        Mat3 V;
-        for (int k = 0; k < 9; k++) {
-            p.R.m[k] = I.m[k] + a * W.m[k] + b * W2.m[k];
-            V.m[k] = I.m[k] + b * W.m[k] + c * W2.m[k];
-        }
-        for (int i = 0; i < 3; i++) p.t[i] = V(i, 0) * xi[0] + V(i, 1) * xi[1] + V(i, 2) * xi[2];
-        return p;
-    }
-    // Sophus SE3::log (se3.hpp:220-253) on the rotation matrix: Eigen's matrix -> quaternion
-    // (Quaternion.h, quaternionbase_assign_impl), SO3::logAndTheta's atan form (so3.hpp:239-283),
-    // and V^-1 with the half-angle factor; epsilon 1e-10 (common.hpp:144).  Stable for every
-    // angle (no 1 - cos(theta) cancellation).
-    void log(double xi[6]) const {
-        double q[4];  // x, y, z, w
-        double tr = R(0, 0) + R(1, 1) + R(2, 2);
-        if (tr > 0) {
-            double t = std::sqrt(tr + 1.0);
-            q[3] = 0.5 * t;
-            t = 0.5 / t;
-            q[0] = (R(2, 1) - R(1, 2)) * t;
-            q[1] = (R(0, 2) - R(2, 0)) * t;
-            q[2] = (R(1, 0) - R(0, 1)) * t;
-        } else {
-            int i = 0;
-            if (R(1, 1) > R(0, 0)) i = 1;
-            if (R(2, 2) > R(i, i)) i = 2;
-            const int j = (i + 1) % 3, k = (j + 1) % 3;
-            double t = std::sqrt(R(i, i) - R(j, j) - R(k, k) + 1.0);
-            q[i] = 0.5 * t;
-            t = 0.5 / t;
-            q[3] = (R(k, j) - R(j, k)) * t;
-            q[j] = (R(j, i) + R(i, j)) * t;
-            q[k] = (R(k, i) + R(i, k)) * t;
-        }
-        const double n2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2], n = std::sqrt(n2), w = q[3];
-        double f;
-        if (n < 1e-10) f = 2.0 / w - 2.0 * n2 / (w * (w * w));
-        else if (std::fabs(w) < 1e-10) f = (w > 0 ? M_PI : -M_PI) / n;
-        else f = 2.0 * std::atan(n / w) / n;
-        const double th = f * n;
-        const double om[3] = {f * q[0], f * q[1], f * q[2]};
-        Mat3 W = skew(om), W2 = W * W;
-        const double d = std::fabs(th) < 1e-10 ? 1.0 / 12.0
-                                               : (1.0 - th * std::cos(0.5 * th) / (2.0 * std::sin(0.5 * th))) / (th * th);
-        for (int i = 0; i < 3; i++) {
-            double s = 0;
-            for (int k = 0; k < 3; k++) s += ((i == k ? 1.0 : 0.0) - 0.5 * W(i, k) + d * W2(i, k)) * t[k];
-            xi[i] = s;
-            xi[3 + i] = om[i];
-        }
-    }
-    // Adj = [R, [t]x R; 0, R]
-    void adjoint(double A[36]) const {
-        std::memset(A, 0, 36 * sizeof(double));
-        Mat3 tR = skew(t) * R;
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) {
-                A[i * 6 + j] = R(i, j);
-                A[i * 6 + 3 + j] = tR(i, j);
-                A[(i + 3) * 6 + 3 + j] = R(i, j);
-            }
-    }
-};
-
-Pose eval_pose(const ldso_ba_frame_state &f) {
-    Pose p;
-    std::memcpy(p.R.m, f.world_to_cam_evalpt, 9 * sizeof(double));
-    std::memcpy(p.t, f.world_to_cam_evalpt + 9, 3 * sizeof(double));
-    return p;
-}
-// FrameHessian::setState (FrameHessian.h:95-114): PRE_worldToCam = exp(state_scaled[0:6]) * evalPT
-Pose current_pose(const ldso_ba_frame_state &f) {
-    double eps[6];
-    for (int i = 0; i < 6; i++) eps[i] = (i < 3 ? kScaleXiTrans : kScaleXiRot) * f.state[i];
-    return Pose::exp(eps) * eval_pose(f);
-}
-// AffLight::fromToVecExposure (include/AffLight.h:27-35), float arithmetic as in the reference
-void affine_from_to(float expF, float expT, float aF, float bF, float aT, float bT, float &a, float &b) {
-    if (expF == 0 || expT == 0) expF = expT = 1;
-    a = std::exp(aT - aF) * expT / expF;
-    b = bT - a * bF;
-}
-
-}  // namespace
-
 // FrameFramePrecalc::Set (src/internal/FrameFramePrecalc.cc:6-35) for all (h,t)
 int frame_precalc(int N, const ldso_ba_frame_state *fr, const float calib[4], float *out) {
-    const float fx = calib[0], fy = calib[1], cx = calib[2], cy = calib[3];
-    // K and Eigen's cofactor K.inverse() (InverseImpl.h, compute_inverse<.,.,3>)
-    const float K[9] = {fx, 0, cx, 0, fy, cy, 0, 0, 1};
-    const float invdet = 1.0f / (fy * fx);
-    const float Ki[9] = {fy * invdet, 0 * invdet, (0 * cy - cx * fy) * invdet,
-                         0 * invdet,  fx * invdet, (cx * 0 - fx * cy) * invdet,
-                         0 * invdet,  0 * invdet, (fx * fy - 0 * 0) * invdet};
     std::vector<Pose> ev(N), cur(N);
     for (int f = 0; f < N; f++) {
         ev[f] = eval_pose(fr[f]);
@@ -183,34 +22,9 @@ int frame_precalc(int N, const ldso_ba_frame_state *fr, const float calib[4], fl
     }
     for (int h = 0; h < N; h++) {
         const Pose evInvH = ev[h].inverse(), curInvH = cur[h].inverse();
-        for (int t = 0; t < N; t++) {
-            float *o = out + (size_t)(h + N * t) * LDSO_BA_PRECALC_STRIDE;
-            std::memset(o, 0, LDSO_BA_PRECALC_STRIDE * sizeof(float));
-            const Pose l0 = ev[t] * evInvH;   // leftToLeft_0
-            const Pose l = cur[t] * curInvH;  // leftToLeft
-            float R[9], tt[3];
-            for (int k = 0; k < 9; k++) {
-                o[12 + k] = (float)l0.R.m[k];  // PRE_RTll_0
-                o[27 + k] = R[k] = (float)l.R.m[k];  // PRE_RTll
-            }
-            for (int k = 0; k < 3; k++) {
-                o[21 + k] = (float)l0.t[k];  // PRE_tTll_0
-                o[36 + k] = tt[k] = (float)l.t[k];  // PRE_tTll
-            }
-            float KR[9];
-            for (int r = 0; r < 3; r++)
-                for (int c = 0; c < 3; c++) KR[r * 3 + c] = K[r * 3] * R[c] + K[r * 3 + 1] * R[3 + c] + K[r * 3 + 2] * R[6 + c];
-            for (int r = 0; r < 3; r++)
-                for (int c = 0; c < 3; c++) o[r * 3 + c] = KR[r * 3] * Ki[c] + KR[r * 3 + 1] * Ki[3 + c] + KR[r * 3 + 2] * Ki[6 + c];
-            for (int r = 0; r < 3; r++) o[9 + r] = K[r * 3] * tt[0] + K[r * 3 + 1] * tt[1] + K[r * 3 + 2] * tt[2];
-            float a, b;
-            affine_from_to((float)fr[h].ab_exposure, (float)fr[t].ab_exposure, (float)(kScaleA * fr[h].state[6]),
-                           (float)(kScaleB * fr[h].state[7]), (float)(kScaleA * fr[t].state[6]),
-                           (float)(kScaleB * fr[t].state[7]), a, b);
-            o[24] = (float)(double)a;
-            o[25] = (float)(double)b;
-            o[26] = (float)(fr[h].state_zero[7] * kScaleB);  // PRE_b0_mode = aff_g2l_0().b
-        }
+        for (int t = 0; t < N; t++)
+            pair_precalc(ev[t], evInvH, cur[t], curInvH, calib, fr[h], fr[t],
+                         out + (size_t)(h + N * t) * LDSO_BA_PRECALC_STRIDE);
     }
     return 0;
 }
@@ -252,33 +66,9 @@ int set_adjoints(int N, const ldso_ba_frame_state *fr, double *adH, double *adT,
 
 // FrameHessian::takeData / getPrior / get_state_minus_stateZero (FrameHessian.h:59-70,142-174)
 int frame_take_data(int N, const ldso_ba_frame_state *fr, double *prior, double *delta, double *delta_prior) {
-    for (int f = 0; f < N; f++) {
-        const ldso_ba_frame_state &F = fr[f];
-        double p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (F.is_first_frame) {
-            p[0] = p[1] = p[2] = kInitialTransPrior;
-            p[3] = p[4] = p[5] = kInitialRotPrior;
-            p[6] = kInitialAffAPrior;
-            p[7] = kInitialAffBPrior;
-        } else {
-            p[6] = kAffineOptModeA < 0 ? kInitialAffAPrior : kAffineOptModeA;
-            p[7] = kAffineOptModeB < 0 ? kInitialAffBPrior : kAffineOptModeB;
-        }
-        double mz[6], z[6], lg[6];
-        for (int i = 0; i < 6; i++) {
-            mz[i] = -F.state_zero[i];
-            z[i] = F.state[i];
-        }
-        if (prior) std::memcpy(prior + 8 * f, p, sizeof(p));
-        if (delta) {
-            (Pose::exp(mz) * Pose::exp(z)).log(lg);
-            for (int i = 0; i < 8; i++) delta[8 * f + i] = i < 6 ? lg[i] : F.state[i] - F.state_zero[i];
-        }
-        if (delta_prior) {
-            Pose::exp(z).log(lg);
-            for (int i = 0; i < 8; i++) delta_prior[8 * f + i] = i < 6 ? lg[i] : F.state[i];
-        }
-    }
+    for (int f = 0; f < N; f++)
+        frame_take_data_one(fr[f], prior ? prior + 8 * f : nullptr, delta ? delta + 8 * f : nullptr,
+                            delta_prior ? delta_prior + 8 * f : nullptr);
     return 0;
 }
 

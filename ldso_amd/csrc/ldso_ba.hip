@@ -42,6 +42,7 @@
 #include "../../include/ldso_ba.h"
 #include "../../include/ldso_ct.h"
 #include "ldso_ba_internal.h"
+#include "se3.h"
 
 using namespace ldso_ba;
 
@@ -1985,6 +1986,90 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
 // gradients with makeImages' rule.  That is exact only if the caller's gradients ARE makeImages'
 // (FrameHessian.cc:96-101): every pixel the taps can reach (x in [1, w-2], y in [1, h-2]) is
 // checked and *mismatch is set if not (the context then falls back to layout 1).
+// ============================================================================================
+// Device GN loop (ldso_ba_optimize): FullSystem::doStepFromBackup +
+// setPrecalcValues without a host round trip.  k_frame_step: one block per window, se3.h's
+// statements (the host helpers' own code): calibration and frame steps from x, then
+// FrameFramePrecalc::Set for every pair and the solver's prior vector (takeData's prior /
+// delta_prior, cPrior * cDeltaF).  k_point_step: setIdepth / setIdepthZero(idepth_backup + step),
+// deltaF = 0 (setDeltaF).
+// ============================================================================================
+struct FrameStepParams {
+    WinDev *wins;
+    ldso_ba_frame_state *fstate;  // [frames]
+    double *calib_val;            // [win][4] CalibHessian::value
+    const double *calib_zero;     // [win][4] value_zero
+    const double *cprior;         // [win][4] cPrior
+    const int *add_priors;        // [win]
+    const double *x;              // [vec]
+    float *precalc;               // [pairs][LDSO_BA_PRECALC_STRIDE]
+    double *prior;                // [vec][2]: HL diagonal, bL
+};
+__global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
+    __shared__ double poses[LDSO_BA_MAX_FRAMES][4][12];  // ev, ev^-1, cur, cur^-1: R (9), t (3)
+    __shared__ float calib[4];
+    WinDev &W = P.wins[blockIdx.x];
+    const int N = W.N, tid = threadIdx.x;
+    const double *xw = P.x + W.vec_base;
+    ldso_ba_frame_state *fs = P.fstate + W.frame_base;
+    if (tid < N) {
+        ldso_ba_frame_state o;
+        frame_step_one(fs[tid], xw + 4 + 8 * tid, o);
+        fs[tid] = o;
+        const Pose e = eval_pose(o), c = current_pose(o);
+        const Pose ps[4] = {e, e.inverse(), c, c.inverse()};
+        for (int q = 0; q < 4; q++) {
+            for (int k = 0; k < 9; k++) poses[tid][q][k] = ps[q].R.m[k];
+            for (int k = 0; k < 3; k++) poses[tid][q][9 + k] = ps[q].t[k];
+        }
+    } else if (tid == 64) {
+        double *v = P.calib_val + 4 * blockIdx.x;
+        float cd[4];
+        calib_step(v, xw, P.calib_zero + 4 * blockIdx.x, calib, cd);
+        for (int k = 0; k < 4; k++) {
+            W.calib[k] = calib[k];
+            W.cdelta[k] = cd[k];
+        }
+        const bool add = P.add_priors[blockIdx.x] != 0;
+        for (int k = 0; k < 4; k++) {  // calibration prior: cPrior, cPrior * cDeltaF (upload_priors)
+            P.prior[2 * (W.vec_base + k)] = add ? P.cprior[4 * blockIdx.x + k] : 0.0;
+            P.prior[2 * (W.vec_base + k) + 1] = add ? P.cprior[4 * blockIdx.x + k] * (double)cd[k] : 0.0;
+        }
+    }
+    __syncthreads();
+    auto pose = [&](int f, int q) {
+        Pose p;
+        for (int k = 0; k < 9; k++) p.R.m[k] = poses[f][q][k];
+        for (int k = 0; k < 3; k++) p.t[k] = poses[f][q][9 + k];
+        return p;
+    };
+    for (int e = tid; e < N * N; e += blockDim.x) {
+        const int h = e % N, t = e / N;
+        pair_precalc(pose(t, 0), pose(h, 1), pose(t, 2), pose(h, 3), calib, fs[h], fs[t],
+                     P.precalc + (size_t)(W.pair_base + e) * LDSO_BA_PRECALC_STRIDE);
+    }
+    if (tid < N) {
+        double pr[8], dp[8];
+        frame_take_data_one(fs[tid], pr, nullptr, dp);
+        const bool add = P.add_priors[blockIdx.x] != 0;
+        for (int i = 0; i < 8; i++) {
+            const int q = W.vec_base + 4 + 8 * tid + i;
+            P.prior[2 * q] = add ? pr[i] : 0.0;
+            P.prior[2 * q + 1] = add ? pr[i] * dp[i] : 0.0;
+        }
+    }
+}
+__global__ __launch_bounds__(256) void k_point_step(float *pt_data, const float *pt_step, int n) {
+#pragma clang fp contract(off)
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    float *d = pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+    const float idepth = d[2] + 1.0f * pt_step[p];
+    d[2] = kScaleIdepth * idepth;  // setIdepth
+    d[3] = kScaleIdepth * idepth;  // setIdepthZero (LDSO's doStepFromBackup)
+    d[5] = idepth - idepth;        // setDeltaF: idepth - idepth_zero
+}
+
 __global__ void k_intensity_image(const float *__restrict__ src, float *dst, int w, int h, int tpr8, int hp,
                                   int *mismatch) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2105,6 +2190,12 @@ struct ldso_ba_ctx {
     int comm_rank = 0, comm_world = 1;
     int64_t x_stride = 0;
     DevBuf<float> d_x_local, d_x_gathered;
+    bool ns_resident = false;  // d_ns holds the nullspaces of the loaded windows (ldso_ba_optimize)
+    // device GN loop (ldso_ba_optimize): frame states, CalibHessian::value / value_zero and the
+    // prior switches per window, the energy history
+    DevBuf<ldso_ba_frame_state> d_fstate;
+    DevBuf<double> d_calib_val, d_calib_zero, d_cprior, d_ehist;
+    DevBuf<int> d_add_priors;
     DevBuf<float> d_xad;            // [win][kXadStride]
     DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
     DevBuf<int> d_pt_win;
@@ -2514,6 +2605,12 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_win_energy.release();
     c->d_x_local.release();
     c->d_x_gathered.release();
+    c->d_fstate.release();
+    c->d_calib_val.release();
+    c->d_calib_zero.release();
+    c->d_cprior.release();
+    c->d_ehist.release();
+    c->d_add_priors.release();
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->d_xad.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2557,7 +2654,8 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_win = n_windows;
-    c->x_stride = 0;  // the exchange re-agrees on the newest-frame slot stride
+    c->x_stride = 0;
+    c->ns_resident = false;  // the exchange re-agrees on the newest-frame slot stride
     c->width = ws[0].width;
     c->height = ws[0].height;
     c->npix = c->width * c->height;
@@ -3419,7 +3517,7 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
     S.ns = c->d_ns.p;
     S.x = c->d_x.p;
     S.iteration = iteration;
-    S.n_null = (iteration >= 2 && ns) ? n_null : 0;
+    S.n_null = (iteration >= 2 && (ns || c->ns_resident)) ? n_null : 0;
     const size_t smem = solve_smem_bytes(dmax);
     static std::once_flag once;
     std::call_once(once, [] {
@@ -3492,6 +3590,128 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
         }
     }
     return ldso_ba_sync(c);
+}
+
+int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *frames, const double *calib_value,
+                     const double *calib_value_zero, const double *ns, double *energy_out,
+                     ldso_ba_frame_state *frames_out, double *calib_out, float *idepth_out) {
+    if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
+    if (n_its < 0 || !frames || !calib_value || !calib_value_zero) return fail(-1, "bad arguments");
+    if (c->marg) return fail(-1, "not on a marginalisation context");
+    HIP_TRY(hipSetDevice(c->device));
+    const int nw = c->n_win;
+    int rc;
+    if ((rc = c->d_fstate.alloc(c->n_frames)) || (rc = c->d_calib_val.alloc((size_t)4 * nw)) ||
+        (rc = c->d_calib_zero.alloc((size_t)4 * nw)) || (rc = c->d_cprior.alloc((size_t)4 * nw)) ||
+        (rc = c->d_add_priors.alloc(nw)) || (rc = c->d_ehist.alloc((size_t)2 * nw * (n_its + 1))))
+        return rc;
+    std::vector<double> cp((size_t)4 * nw);
+    std::vector<int> ap(nw);
+    for (int w = 0; w < nw; w++) {
+        for (int k = 0; k < 4; k++) cp[4 * w + k] = c->wh[w].c_prior[k];
+        ap[w] = c->wh[w].add_priors ? 1 : 0;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_fstate.p, frames, (size_t)c->n_frames * sizeof(ldso_ba_frame_state),
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_calib_val.p, calib_value, (size_t)4 * nw * sizeof(double), hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_calib_zero.p, calib_value_zero, (size_t)4 * nw * sizeof(double),
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_cprior.p, cp.data(), cp.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_add_priors.p, ap.data(), ap.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    c->ns_resident = false;
+    if (ns) {
+        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
+                               c->stream));
+        c->ns_resident = true;  // evalPT is fixed during optimize(): getNullspaces stays valid
+    }
+    FrameStepParams F;
+    F.wins = c->d_wins.p;
+    F.fstate = c->d_fstate.p;
+    F.calib_val = c->d_calib_val.p;
+    F.calib_zero = c->d_calib_zero.p;
+    F.cprior = c->d_cprior.p;
+    F.add_priors = c->d_add_priors.p;
+    F.x = c->d_x.p;
+    F.precalc = c->d_precalc.p;
+    F.prior = c->d_prior.p;
+    auto keep_energy = [&](int slot) -> int {
+        HIP_TRY(hipMemcpyAsync(c->d_ehist.p + (size_t)2 * nw * slot, c->d_win_energy.p, (size_t)2 * nw * sizeof(double),
+                               hipMemcpyDeviceToDevice, c->stream));
+        return 0;
+    };
+    // FullSystem::optimize (FullSystem.cc:853-976) with setting_forceAceptStep: resetOOB, then
+    // linearizeAll + applyRes (+ the accumulation solveSystemF uses), and per iteration
+    // solveSystemF, resubstituteF_MT, doStepFromBackup + setPrecalcValues, linearizeAll + applyRes
+    if ((rc = ldso_ba_reset_oob(c, -1)) || (rc = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0)) || (rc = keep_energy(0)))
+        return rc;
+    for (int it = 0; it < n_its; it++) {
+        if ((rc = ldso_ba_solve_device(c, it, 1e-5, nullptr, ns ? 7 : 0, nullptr))) return rc;
+        if ((rc = ldso_ba_resubstitute_device(c, 1e-5, nullptr))) return rc;
+        k_frame_step<<<nw, 256, 0, c->stream>>>(F);
+        HIP_TRY(hipGetLastError());
+        if (c->P_tot) {
+            k_point_step<<<(c->P_tot + 255) / 256, 256, 0, c->stream>>>(c->d_pt_data.p, c->d_pt_step.p, c->P_tot);
+            HIP_TRY(hipGetLastError());
+        }
+        if ((rc = ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0)) || (rc = keep_energy(it + 1))) return rc;
+    }
+    if (energy_out) {
+        std::vector<double> e((size_t)2 * nw * (n_its + 1));
+        HIP_TRY(hipMemcpyAsync(e.data(), c->d_ehist.p, e.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        if ((rc = ldso_ba_sync(c))) return rc;
+        for (int s = 0; s <= n_its; s++)
+            for (int w = 0; w < nw; w++) {
+                double *o = energy_out + ((size_t)s * nw + w) * 3;
+                o[0] = e[(size_t)2 * (s * nw + w)];
+                o[1] = 0;
+                o[2] = e[(size_t)2 * (s * nw + w) + 1];
+            }
+    }
+    if (frames_out)
+        HIP_TRY(hipMemcpyAsync(frames_out, c->d_fstate.p, (size_t)c->n_frames * sizeof(ldso_ba_frame_state),
+                               hipMemcpyDeviceToHost, c->stream));
+    if (calib_out)
+        HIP_TRY(hipMemcpyAsync(calib_out, c->d_calib_val.p, (size_t)4 * nw * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream));
+    std::vector<float> pd;
+    if (idepth_out && c->P_tot) {
+        pd.resize((size_t)c->P_tot * LDSO_BA_POINT_STRIDE);
+        HIP_TRY(hipMemcpyAsync(pd.data(), c->d_pt_data.p, pd.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    }
+    if ((rc = ldso_ba_sync(c))) return rc;
+    if (idepth_out) {
+        long long out_base = 0;  // windows back to back, each in its caller point order
+        for (int w = 0; w < nw; w++) {
+            const WinDev &D = c->wd[w];
+            const WinHost &H = c->wh[w];
+            for (int q = 0; q < D.P; q++)
+                idepth_out[out_base + H.pt_orig[q]] = pd[(size_t)(D.point_base + q) * LDSO_BA_POINT_STRIDE + 2];
+            out_base += H.P_all;
+        }
+    }
+    // the host mirror of WinDev (calibration, cDeltaF) follows the device
+    HIP_TRY(hipMemcpy(c->wd.data(), c->d_wins.p, (size_t)nw * sizeof(WinDev), hipMemcpyDeviceToHost));
+    c->sys_host_valid = false;
+    c->energy_valid = false;
+    return 0;
+}
+
+int ldso_ba_frame_step(int32_t n, const ldso_ba_frame_state *in, const double *x, ldso_ba_frame_state *out,
+                       double *calib_value, const double *calib_value_zero, float *calib_scaled_out,
+                       float *c_delta_out) {
+    if (n < 1 || n > LDSO_BA_MAX_FRAMES || !in || !x || !out) return fail(-1, "bad arguments");
+    for (int f = 0; f < n; f++) frame_step_one(in[f], x + 4 + 8 * f, out[f]);
+    if (calib_value) {
+        float sf[4], cd[4];
+        const double zero[4] = {0, 0, 0, 0};
+        calib_step(calib_value, x, calib_value_zero ? calib_value_zero : zero, sf, cd);
+        for (int k = 0; k < 4; k++) {
+            if (calib_scaled_out) calib_scaled_out[k] = sf[k];
+            if (c_delta_out) c_delta_out[k] = cd[k];
+        }
+    }
+    return 0;
 }
 
 int ldso_ba_packed_system(ldso_ba_ctx *c, void **dev_ptr, int64_t *n_doubles, int64_t *stride) {

@@ -1,0 +1,131 @@
+"""FullSystem::optimize on the device (FullSystem.cc:844-976, 1843-1922):
+ldso_ba_optimize runs resetOOB + linearizeAll and n GN iterations (solveSystemF, resubstituteF_MT,
+doStepFromBackup + setPrecalcValues, linearizeAll) with no host round trip.
+
+The check is the same loop driven from the host: the oracle's linearize / accumulate / solve /
+resubstitute, the step with the library's host doStepFromBackup (ldso_ba_frame_step, the se3.h
+statements the device runs), the window's frame terms refreshed on the host
+(Window.refresh_frame_terms) and the points' idepth updated as setIdepth / setIdepthZero.  Host
+and device share every statement; only libm's sin / cos / atan / exp may differ in the last
+ulp between glibc and the device library, so: energies 1e-6 relative, #IN within 0.2 %, frame
+states 1e-9, point idepths 1e-5 relative (float steps through a reassociated H).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from ldso_amd import _lib as L
+from ldso_amd import synth
+
+
+def frame_step(frames, x, cval, czero):
+    out = np.zeros_like(frames)
+    sf = np.zeros(4, np.float32)
+    cd = np.zeros(4, np.float32)
+    L.check(L.lib().ldso_ba_frame_step(len(frames), np.ascontiguousarray(frames).ctypes.data,
+                                       L.ptr(np.ascontiguousarray(x, np.float64), L.f64p), out.ctypes.data,
+                                       L.ptr(cval, L.f64p), L.ptr(czero, L.f64p), L.ptr(sf, L.f32p),
+                                       L.ptr(cd, L.f32p)))
+    return out, sf, cd
+
+
+def test_frame_step_known_answers(built):
+    """log(exp(step) exp(state)): a pure-rotation step about the state's own axis adds angles; a
+    pure-translation step leaves the rotation; the calibration step is value - x[0:4]."""
+    w = synth.make_window(n_frames=3, n_points=10, width=160, height=120, seed=3)
+    fr = np.ascontiguousarray(w.frames).copy()
+    fr["state"][:] = 0
+    fr["state"][1, 3:6] = [0.01, -0.02, 0.03]
+    n = 8 * 3 + 4
+    x = np.zeros(n)
+    x[4 + 8 + 3:4 + 8 + 6] = -0.5 * np.array([0.01, -0.02, 0.03])  # step = -x: half the angle again
+    x[4 + 16 + 0:4 + 16 + 3] = [-1e-3, 2e-3, 0]                    # frame 2: translation only
+    x[4 + 16 + 6:4 + 16 + 8] = [-0.1, 0.2]                         # affine a, b add
+    x[0:4] = [0.5, -0.25, 1.0, 0.0]
+    cval = np.array([7.68, 8.64, 6.39, 4.79])
+    cz = cval.copy()
+    out, sf, cd = frame_step(fr, x, cval, cz)
+    np.testing.assert_allclose(out["state"][1, 3:6], 1.5 * np.array([0.01, -0.02, 0.03]), rtol=1e-12)
+    np.testing.assert_allclose(out["state"][1, 0:3], 0, atol=1e-15)
+    np.testing.assert_allclose(out["state"][2, 0:3], [1e-3, -2e-3, 0], rtol=1e-12, atol=1e-18)
+    np.testing.assert_array_equal(out["state"][2, 3:6], 0)
+    np.testing.assert_array_equal(out["state"][2, 6:8], [0.1, -0.2])
+    np.testing.assert_array_equal(out["state"][0], 0)
+    np.testing.assert_array_equal(cval, np.array([7.68, 8.64, 6.39, 4.79]) - x[0:4])
+    np.testing.assert_array_equal(sf, (np.array([50.0, 50.0, 50.0, 50.0]) * cval).astype(np.float32))
+    np.testing.assert_array_equal(cd, (cval - cz).astype(np.float32))
+
+
+def host_optimize(w, n_its, ns):
+    """The same loop from the host: oracle pass/solve/resubstitute + host doStepFromBackup."""
+    ow = oracle.OracleWindow(w, threads=0)
+    ow.reset_oob()
+    e, sysm = ow.iteration()
+    energies = [e]
+    cval = w.calib.astype(np.float64) * (1.0 / 50.0)
+    czero = cval.copy()
+    frames = np.ascontiguousarray(w.frames).copy()
+    for it in range(n_its):
+        x = oracle.solve_system(w.n_frames, it, 1e-5, sysm, nullspaces=ns)
+        step = ow.resubstitute(x, 1e-5)
+        frames, sf, cd = frame_step(frames, x, cval, czero)
+        w.frames = frames
+        w.calib = sf.copy()
+        w.c_delta = cd.copy()
+        w.point_data = w.point_data.copy()
+        idepth = (w.point_data[:, 2] + np.float32(1.0) * step).astype(np.float32)
+        w.point_data[:, 2] = idepth
+        w.point_data[:, 3] = idepth
+        w.point_data[:, 5] = idepth - idepth
+        w.refresh_frame_terms()
+        ow.update(w)
+        e, sysm = ow.iteration()
+        energies.append(e)
+    return np.array(energies), frames, cval, w.point_data[:, 2].copy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [dict(n_frames=5, n_points=500, seed=61), dict(synth.S7, seed=62)], ids=["N5", "S7"])
+def test_device_optimize_matches_host_loop(built, cfg):
+    from ldso_amd import BAContext
+
+    n_its = 3
+    w = synth.make_window(**cfg)
+    ns = w.nullspaces()
+    ctx = BAContext(0).load([w])
+    e_dev, fr_dev, c_dev, idep_dev = ctx.optimize(n_its, nullspaces=[ns])
+    e_host, fr_host, c_host, idep_host = host_optimize(synth.make_window(**cfg), n_its, ns)
+    for s in range(n_its + 1):
+        assert abs(e_dev[s, 0, 0] - e_host[s][0]) <= 1e-6 * abs(e_host[s][0]), (s, e_dev[s, 0], e_host[s])
+        assert abs(e_dev[s, 0, 2] - e_host[s][2]) <= 2e-3 * e_host[s][2], (s, e_dev[s, 0], e_host[s])
+    np.testing.assert_allclose(fr_dev["state"], fr_host["state"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(c_dev[0], c_host, rtol=1e-9)
+    np.testing.assert_allclose(idep_dev[0], idep_host, rtol=1e-5, atol=1e-7)
+    assert e_dev[-1, 0, 0] < e_dev[0, 0, 0]  # the GN iterations reduce the energy
+    # the context keeps the stepped state: a further pass starts from it
+    ctx.linearize()
+    assert abs(ctx.energy(0)[0] - e_dev[-1, 0, 0]) <= 1e-9 * abs(e_dev[-1, 0, 0])
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_device_optimize_batched_windows(built):
+    """Every resident window runs its own loop; each equals the same window optimised alone."""
+    from ldso_amd import BAContext
+
+    cfgs = [dict(n_frames=4, n_points=300, seed=71), dict(n_frames=6, n_points=400, seed=72)]
+    ws = [synth.make_window(**c) for c in cfgs]
+    both = BAContext(0).load(ws)
+    e2, fr2, _, id2 = both.optimize(2, nullspaces=[w.nullspaces() for w in ws])
+    off = 0
+    for i, c in enumerate(cfgs):
+        w = synth.make_window(**c)
+        one = BAContext(0).load([w])
+        e1, fr1, _, id1 = one.optimize(2, nullspaces=[w.nullspaces()])
+        np.testing.assert_allclose(e2[:, i, 0], e1[:, 0, 0], rtol=1e-9)
+        np.testing.assert_array_equal(e2[:, i, 2], e1[:, 0, 2])
+        np.testing.assert_allclose(fr2["state"][off:off + w.n_frames], fr1["state"], rtol=1e-9, atol=1e-15)
+        np.testing.assert_allclose(id2[i], id1[0], rtol=1e-6)
+        off += w.n_frames
+        one.close()
+    both.close()
