@@ -65,6 +65,17 @@ def cpu_baseline(seconds=10.0):
         return None
 
 
+def time_optimize(ctx, nss, n_its=6, reps=10):
+    """ms per ldso_ba_optimize(n_its) call (host clock) and per GN iteration of it."""
+    for _ in range(2):
+        ctx.optimize(n_its, nullspaces=nss)
+    t = time.perf_counter()
+    for _ in range(reps):
+        ctx.optimize(n_its, nullspaces=nss)
+    ms = 1e3 * (time.perf_counter() - t) / reps
+    return {"n_its": n_its, "ms_per_optimize": ms, "ms_per_iteration": ms / n_its, "windows": len(nss)}
+
+
 def secondary_s11(device, windows=8, steps=20):
     """BASELINE config[3]'s window shape (11 keyframes, 8000 points, 640x480) on ONE GPU, batched
     like the headline (a parity/scaling case in BASELINE.json, reported beside the headline, not
@@ -377,6 +388,7 @@ def main():
             ctx.iterate(2, 1e-5, nss, fetch_steps=False)
         gn_ms = 1e3 * (time.perf_counter() - t1) / it_reps
         gn = {"ms_per_iteration": gn_ms, "windows": B, "windows_per_s": B / (gn_ms / 1e3)}
+        gn["optimize"] = time_optimize(ctx, nss, n_its=6, reps=3)
 
     if dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
@@ -439,6 +451,10 @@ def main():
         # GN iteration = pass + solve + resubstitute with x and the point steps on the host
         single = {"ms_per_pass": sw_ms, "point_residuals_per_s": sw.n_residuals / (sw_ms / 1e3),
                   "ms_per_gn_iteration_host_solve": ms_solve, "ms_per_gn_iteration_device_solve": ms_solve_dev}
+        # FullSystem::optimize(setting_maxOptIterations = 6) entirely on the device (ldso_ba_optimize:
+        # resetOOB + linearizeAll, then 6 x {solve, resubstitute, doStepFromBackup + setPrecalcValues,
+        # linearizeAll}; one synchronisation), host clock around the call
+        single["optimize"] = time_optimize(c1, [ns], n_its=6)
         c1.close()
 
     s11 = None
