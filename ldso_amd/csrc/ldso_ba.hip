@@ -83,6 +83,7 @@ struct WinDev {
     int K, KP, ntiles, pad0;
     long long sc_slab_base;  // floats
     long long sys_base;      // doubles: packed system
+    long long stage_base;    // doubles: k_stitch contribution records, N^2 pairs x stage_rec(N)
     int newest_begin, newest_end;
     int rec_base;            // record slots: rec_base + s * P + q (s = target slot of host's point q)
     int vec_base;            // per-window (8N+4)-vectors (priors, x): vec_base + i
@@ -94,6 +95,20 @@ struct WinDev {
 
 __host__ __device__ inline long long packed_len(int D) { return (long long)D * (D + 1) / 2; }
 __host__ __device__ inline long long sys_len(int D) { return 2 * (packed_len(D) + D); }
+
+// k_stitch's contribution record of one (h, t) pair (doubles): every term the reference's
+// stitchDouble adds for this pair, stored instead of accumulated, so that k_stitch_sum can add
+// each output element's terms in one fixed order (bitwise repeatable, no atomics).
+//   Top  (AccumulatedTopHessian.cc:213-239): T1 (h,h) 8x8, T2 (t,t) 8x8, T3 AH A AT^T 8x8,
+//        T4a/T4b the (calib, h) / (calib, t) 8x4 column blocks [rr * 4 + cc], T5 the 4x4
+//        calibration block, T6a/T6b b(h) / b(t), T7 b(calib)
+//   SC   (AccumulatedSCHessian.cc:80-114, i = h, j = t): S1 the (j, k) blocks for the N-1 k != i,
+//        S2 H(j, i), S3 H(i, i), S4a/S4b (calib, i) / (calib, j) [rr * 4 + cc], S5a/S5b b(i) / b(j),
+//        S6 accHcc / accbc [r * 5 + c] (only in the record of host i's first target)
+enum : int { kT1 = 0, kT2 = 64, kT3 = 128, kT4a = 192, kT4b = 224, kT5 = 256, kT6a = 272, kT6b = 280, kT7 = 288,
+             kS1 = 292 };
+__host__ __device__ inline int stage_rec(int N) { return 520 + 64 * (N - 1); }
+__host__ __device__ inline int st_S2(int N) { return kS1 + 64 * (N - 1); }
 
 // ============================================================================================
 // k_linearize
@@ -925,6 +940,7 @@ struct StitchParams {
     const double *__restrict__ adH;
     const double *__restrict__ adT;
     double *sys;
+    double *stage;  // k_stitch -> k_stitch_sum contribution records (WinDev::stage_base)
     double *win_energy;
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
@@ -1114,10 +1130,8 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     const int tid = threadIdx.x;
     if (h == t) return;
     if (!P.accumulate) return;
-    double *sys = P.sys + W.sys_base;
-    const long long pl = packed_len(D);
-    double *HA = sys, *bA = sys + pl, *Hs = sys + pl + D, *bs = sys + 2 * pl + D;
-    const int hI = 4 + 8 * h, tI = 4 + 8 * t;
+    (void)D;
+    double *rec = P.stage + W.stage_base + (size_t)aidx * stage_rec(N);
 
     // All global loads of both halves are issued first (one round trip for the block): the
     // Top bucket partial sums and pair adjoints, and the SC rows of G_i with the host's adjoints.
@@ -1172,106 +1186,186 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     __syncthreads();
 
     // ---------------- Top: bucket (h, t) ------------------------------------------------
-    if (do_top) {
-        if (tid < 169) A[tid] = acc[top_slot(tid / 13, tid % 13)];
-        __syncthreads();
-        if (tid < 128) {
-            const int l = tid & 63, r = l >> 3, c = l & 7;
-            const double *Ad = tid < 64 ? AH : AT;
-            double sacc = 0;
-            for (int k = 0; k < 8; k++) sacc += Ad[r * 8 + k] * A[(4 + k) * 13 + 4 + c];
-            (tid < 64 ? TH : TT)[l] = sacc;
+    if (tid < 169) A[tid] = acc[top_slot(tid / 13, tid % 13)];
+    __syncthreads();
+    if (tid < 128) {
+        const int l = tid & 63, r = l >> 3, c = l & 7;
+        const double *Ad = tid < 64 ? AH : AT;
+        double sacc = 0;
+        for (int k = 0; k < 8; k++) sacc += Ad[r * 8 + k] * A[(4 + k) * 13 + 4 + c];
+        (tid < 64 ? TH : TT)[l] = sacc;
+    }
+    __syncthreads();
+    if (tid < 192) {
+        const int which = tid >> 6, l = tid & 63, r = l >> 3, c = l & 7;
+        double v = 0;
+        if (which == 0) {  // H(h,h) += AH A AH^T
+            for (int k = 0; k < 8; k++) v += TH[r * 8 + k] * AH[c * 8 + k];
+            rec[kT1 + l] = v;
+        } else if (which == 1) {  // H(t,t) += AT A AT^T
+            for (int k = 0; k < 8; k++) v += TT[r * 8 + k] * AT[c * 8 + k];
+            rec[kT2 + l] = v;
+        } else {  // H(h,t) += AH A AT^T; the (t,h) term is its transpose (symmetrisation)
+            for (int k = 0; k < 8; k++) v += TH[r * 8 + k] * AT[c * 8 + k];
+            rec[kT3 + l] = v;
         }
-        __syncthreads();
-        if (tid < 192) {
-            const int which = tid >> 6, l = tid & 63, r = l >> 3, c = l & 7;
-            double v = 0;
-            if (which == 0) {  // H(h,h) += AH A AH^T (upper half of the diagonal block)
-                for (int k = 0; k < 8; k++) v += TH[r * 8 + k] * AH[c * 8 + k];
-                if (c >= r) atomicAdd(&HA[pk_index(hI + r, hI + c, D)], v);
-            } else if (which == 1) {  // H(t,t) += AT A AT^T
-                for (int k = 0; k < 8; k++) v += TT[r * 8 + k] * AT[c * 8 + k];
-                if (c >= r) atomicAdd(&HA[pk_index(tI + r, tI + c, D)], v);
-            } else {  // H(h,t) += AH A AT^T; the (t,h) term folds in transposed (symmetrisation)
-                for (int k = 0; k < 8; k++) v += TH[r * 8 + k] * AT[c * 8 + k];
-                if (h < t) atomicAdd(&HA[pk_index(hI + r, tI + c, D)], v);
-                else atomicAdd(&HA[pk_index(tI + c, hI + r, D)], v);
-            }
-        } else {  // 64 threads: H(h,c) = AH A_8C and H(t,c) = AT A_8C, stored as H(c, frame)
-            const int l = tid - 192, which = l >> 5, rr = (l & 31) >> 2, cc = l & 3;
-            const double *Ad = which == 0 ? AH : AT;
-            double v = 0;
-            for (int k = 0; k < 8; k++) v += Ad[rr * 8 + k] * A[(4 + k) * 13 + cc];
-            atomicAdd(&HA[pk_index(cc, (which == 0 ? hI : tI) + rr, D)], v);
-        }
-        if (tid < 16) {
-            const int r = tid >> 2, c = tid & 3;
-            if (c >= r) atomicAdd(&HA[pk_index(r, c, D)], A[r * 13 + c]);
-        } else if (tid < 32) {
-            const int l = tid - 16, which = l >> 3, r = l & 7;
-            const double *Ad = which == 0 ? AH : AT;
-            double v = 0;
-            for (int k = 0; k < 8; k++) v += Ad[r * 8 + k] * A[(4 + k) * 13 + 12];
-            atomicAdd(&bA[(which == 0 ? hI : tI) + r], v);
-        } else if (tid < 36) {
-            atomicAdd(&bA[tid - 32], A[(tid - 32) * 13 + 12]);
-        }
+    } else {  // 64 threads: H(h,c) = AH A_8C and H(t,c) = AT A_8C
+        const int l = tid - 192, which = l >> 5, rr = (l & 31) >> 2, cc = l & 3;
+        const double *Ad = which == 0 ? AH : AT;
+        double v = 0;
+        for (int k = 0; k < 8; k++) v += Ad[rr * 8 + k] * A[(4 + k) * 13 + cc];
+        rec[(which == 0 ? kT4a : kT4b) + rr * 4 + cc] = v;
+    }
+    if (tid < 16) {
+        rec[kT5 + tid] = A[(tid >> 2) * 13 + (tid & 3)];
+    } else if (tid < 32) {
+        const int l = tid - 16, which = l >> 3, r = l & 7;
+        const double *Ad = which == 0 ? AH : AT;
+        double v = 0;
+        for (int k = 0; k < 8; k++) v += Ad[r * 8 + k] * A[(4 + k) * 13 + 12];
+        rec[(which == 0 ? kT6a : kT6b) + r] = v;
+    } else if (tid < 36) {
+        rec[kT7 + tid - 32] = A[(tid - 32) * 13 + 12];
     }
 
     // ---------------- SC: host i = h, target j = t ---------------------------------------
-    if (do_sc) {
-        // per k != i: X_k = AT_ij D_jk, S_k = D_jk AH_ik^T
-        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
-            const int s = e >> 6, r = (e >> 3) & 7, c = e & 7;
-            const double *Dm = Gj + 8 * s;  // D_jk[r][c] = Gj[r * KP + 8 s + c]
-            double x = 0, sv = 0;
-            for (int q = 0; q < 8; q++) {
-                x += At[r * 8 + q] * Dm[q * KP + c];
-                sv += Dm[r * KP + q] * AHk[s * 64 + c * 8 + q];
-            }
-            X[e] = x;
-            Sk[e] = sv;
+    // per k != i: X_k = AT_ij D_jk, S_k = D_jk AH_ik^T
+    for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
+        const int s = e >> 6, r = (e >> 3) & 7, c = e & 7;
+        const double *Dm = Gj + 8 * s;  // D_jk[r][c] = Gj[r * KP + 8 s + c]
+        double x = 0, sv = 0;
+        for (int q = 0; q < 8; q++) {
+            x += At[r * 8 + q] * Dm[q * KP + c];
+            sv += Dm[r * KP + q] * AHk[s * 64 + c * 8 + q];
         }
-        __syncthreads();
-        // H(j,k) += AT_ij D_jk AT_ik^T, upper triangle only (j < k, or the upper half at j == k)
-        for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
-            const int s = e >> 6, k = s + (s >= i), r = (e >> 3) & 7, c = e & 7;
-            if (j > k || (j == k && c < r)) continue;
-            double v = 0;
-            for (int q = 0; q < 8; q++) v += X[s * 64 + r * 8 + q] * ATk[s * 64 + c * 8 + q];
-            atomicAdd(&Hs[pk_index(4 + 8 * j + r, 4 + 8 * k + c, D)], v);
+        X[e] = x;
+        Sk[e] = sv;
+    }
+    __syncthreads();
+    // H(j,k) += AT_ij D_jk AT_ik^T (k_stitch_sum keeps the upper-triangle ones)
+    for (int e = tid; e < (N - 1) * 64; e += kStThreads) {
+        const int s = e >> 6, r = (e >> 3) & 7, c = e & 7;
+        double v = 0;
+        for (int q = 0; q < 8; q++) v += X[s * 64 + r * 8 + q] * ATk[s * 64 + c * 8 + q];
+        rec[kS1 + e] = v;
+    }
+    const int s2 = st_S2(N);
+    if (tid < 64) {
+        const int r = tid >> 3, c = tid & 7;
+        double hji = 0, hii = 0;
+        for (int q = 0; q < 8; q++) {
+            double sq = 0;  // S = sum_k S_k, fixed order
+            for (int s = 0; s < N - 1; s++) sq += Sk[s * 64 + q * 8 + c];
+            hji += At[r * 8 + q] * sq;
+            hii += Ah[r * 8 + q] * sq;
         }
-        if (tid < 64) {
-            const int r = tid >> 3, c = tid & 7;
-            double hji = 0, hii = 0;
-            for (int q = 0; q < 8; q++) {
-                double sq = 0;  // S = sum_k S_k, fixed order
-                for (int s = 0; s < N - 1; s++) sq += Sk[s * 64 + q * 8 + c];
-                hji += At[r * 8 + q] * sq;
-                hii += Ah[r * 8 + q] * sq;
-            }
-            // H(j,i) += sum_k AT_ij D AH_ik^T; its upper position is (j,i) or (i,j)^T
-            if (j < i) atomicAdd(&Hs[pk_index(4 + 8 * j + r, 4 + 8 * i + c, D)], hji);
-            else atomicAdd(&Hs[pk_index(4 + 8 * i + c, 4 + 8 * j + r, D)], hji);
-            if (c >= r) atomicAdd(&Hs[pk_index(4 + 8 * i + r, 4 + 8 * i + c, D)], hii);  // H(i,i)
-        } else if (tid < 128) {  // H(i,c) += AH_ij E, H(j,c) += AT_ij E (stored as H(c, frame))
-            const int l = tid - 64, which = l >> 5, rr = (l & 31) >> 2, cc = l & 3;
-            const double *Ad = which == 0 ? Ah : At;
-            double v = 0;
-            for (int q = 0; q < 8; q++) v += Ad[rr * 8 + q] * Gj[q * KP + Kc + cc];
-            atomicAdd(&Hs[pk_index(cc, 4 + 8 * (which == 0 ? i : j) + rr, D)], v);
-        } else if (tid < 144) {  // b(i) += AH_ij EB, b(j) += AT_ij EB
-            const int l = tid - 128, which = l >> 3, rr = l & 7;
-            const double *Ad = which == 0 ? Ah : At;
-            double v = 0;
-            for (int q = 0; q < 8; q++) v += Ad[rr * 8 + q] * Gj[q * KP + Kc + 4];
-            atomicAdd(&bs[4 + 8 * (which == 0 ? i : j) + rr], v);
-        } else if (sj == 0 && tid < 164) {  // H_cc += accHcc, b_c += accbc
-            const int l = tid - 144, r = l / 5, c = l % 5;
-            if (c == 4) atomicAdd(&bs[r], Cc[l]);
-            else if (c >= r) atomicAdd(&Hs[pk_index(r, c, D)], Cc[l]);
+        rec[s2 + tid] = hji;       // H(j,i) += sum_k AT_ij D AH_ik^T
+        rec[s2 + 64 + tid] = hii;  // H(i,i)
+    } else if (tid < 128) {  // H(i,c) += AH_ij E, H(j,c) += AT_ij E
+        const int l = tid - 64, which = l >> 5, rr = (l & 31) >> 2, cc = l & 3;
+        const double *Ad = which == 0 ? Ah : At;
+        double v = 0;
+        for (int q = 0; q < 8; q++) v += Ad[rr * 8 + q] * Gj[q * KP + Kc + cc];
+        rec[s2 + 128 + which * 32 + rr * 4 + cc] = v;
+    } else if (tid < 144) {  // b(i) += AH_ij EB, b(j) += AT_ij EB
+        const int l = tid - 128, which = l >> 3, rr = l & 7;
+        const double *Ad = which == 0 ? Ah : At;
+        double v = 0;
+        for (int q = 0; q < 8; q++) v += Ad[rr * 8 + q] * Gj[q * KP + Kc + 4];
+        rec[s2 + 192 + which * 8 + rr] = v;
+    } else if (sj == 0 && tid < 164) {  // H_cc += accHcc, b_c += accbc (once per host)
+        rec[s2 + 208 + tid - 144] = Cc[tid - 144];
+    }
+}
+
+// Sum of every stitch term of one packed output element, in one fixed order over the window's
+// pairs (t major, h minor): HA / bA from the Top records, Hsc / bsc from the SC records.  One
+// thread per element of {HA upper, bA, Hsc upper, bsc} of every window; writes every element
+// (no memset, no atomics: the stitched system is bitwise repeatable).
+__global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ wins, const int2 *__restrict__ blocks,
+                                                     const double *__restrict__ stage, double *sys) {
+    const int2 bw = blocks[blockIdx.x];  // {window, first element of this block}
+    const WinDev &W = wins[bw.x];
+    const int N = W.N, D = W.D;
+    const long long pl = packed_len(D), n_el = 2 * (pl + D);
+    const long long e = (long long)bw.y + threadIdx.x;
+    if (e >= n_el) return;
+    const int R = stage_rec(N), s2 = st_S2(N);
+    const double *st = stage + W.stage_base;
+    auto recp = [&](int h, int t) { return st + (size_t)(h + N * t) * R; };
+    const bool sc = e >= pl + D;
+    long long q = sc ? e - (pl + D) : e;
+    double v = 0;
+    if (q >= pl) {  // b element
+        const int r = (int)(q - pl);
+        if (r < 4) {
+            for (int t = 0; t < N; t++)
+                for (int h = 0; h < N; h++) {
+                    if (h == t) continue;
+                    if (!sc) v += recp(h, t)[kT7 + r];
+                    else if ((h == 0 ? 1 : 0) == t) v += recp(h, t)[s2 + 208 + r * 5 + 4];
+                }
+        } else {
+            const int f = (r - 4) >> 3, rr = (r - 4) & 7;
+            for (int t = 0; t < N; t++)
+                for (int h = 0; h < N; h++) {
+                    if (h == t) continue;
+                    const double *p = recp(h, t);
+                    if (h == f) v += p[(sc ? s2 + 192 : kT6a) + rr];
+                    if (t == f) v += p[(sc ? s2 + 200 : kT6b) + rr];
+                }
+        }
+    } else {  // upper element (row, col) of the packed triangle
+        int row = (int)((2 * D + 1 - sqrt((double)(2 * D + 1) * (2 * D + 1) - 8.0 * (double)q)) * 0.5);
+        row = row < 0 ? 0 : (row > D - 1 ? D - 1 : row);
+        while (row < D - 1 && pk_index(row + 1, row + 1, D) <= q) row++;
+        while (row > 0 && pk_index(row, row, D) > q) row--;
+        const int col = row + (int)(q - pk_index(row, row, D));
+        if (col < 4) {  // calibration block (row <= col < 4)
+            for (int t = 0; t < N; t++)
+                for (int h = 0; h < N; h++) {
+                    if (h == t) continue;
+                    if (!sc) v += recp(h, t)[kT5 + row * 4 + col];
+                    else if ((h == 0 ? 1 : 0) == t) v += recp(h, t)[s2 + 208 + row * 5 + col];
+                }
+        } else if (row < 4) {  // (calib cc = row, frame f, rr)
+            const int f = (col - 4) >> 3, rr = (col - 4) & 7, cc = row;
+            for (int t = 0; t < N; t++)
+                for (int h = 0; h < N; h++) {
+                    if (h == t) continue;
+                    const double *p = recp(h, t);
+                    if (h == f) v += p[(sc ? s2 + 128 : kT4a) + rr * 4 + cc];
+                    if (t == f) v += p[(sc ? s2 + 160 : kT4b) + rr * 4 + cc];
+                }
+        } else {
+            const int f1 = (row - 4) >> 3, r = (row - 4) & 7, f2 = (col - 4) >> 3, c = (col - 4) & 7;
+            for (int t = 0; t < N; t++)
+                for (int h = 0; h < N; h++) {
+                    if (h == t) continue;
+                    const double *p = recp(h, t);
+                    if (!sc) {
+                        if (f1 == f2) {
+                            if (h == f1) v += p[kT1 + r * 8 + c];
+                            if (t == f1) v += p[kT2 + r * 8 + c];
+                        } else {
+                            if (h == f1 && t == f2) v += p[kT3 + r * 8 + c];  // H(h,t), h < t
+                            if (h == f2 && t == f1) v += p[kT3 + c * 8 + r];  // H(h,t)^T, h > t
+                        }
+                    } else {
+                        const int i = h, j = t;
+                        if (f1 == f2) {
+                            if (j == f1) v += p[kS1 + (f1 - (f1 > i ? 1 : 0)) * 64 + r * 8 + c];  // H(j,j) from S1
+                            if (i == f1) v += p[s2 + 64 + r * 8 + c];                          // H(i,i)
+                        } else {
+                            if (j == f1 && i != f2) v += p[kS1 + (f2 - (f2 > i ? 1 : 0)) * 64 + r * 8 + c];
+                            if (i == f2 && j == f1) v += p[s2 + r * 8 + c];  // H(j,i), j < i
+                            if (i == f1 && j == f2) v += p[s2 + c * 8 + r];  // H(j,i)^T, j > i
+                        }
+                    }
+                }
         }
     }
+    sys[W.sys_base + e] = v;
 }
 
 // ============================================================================================
@@ -2182,7 +2276,9 @@ struct ldso_ba_ctx {
     DevBuf<int4> d_top_items, d_sc_items;
     DevBuf<int2> d_pair_items, d_host_items;
     DevBuf<float> d_top_slab, d_sc_slab;
-    DevBuf<double> d_item_energy, d_sys, d_win_energy;
+    DevBuf<double> d_item_energy, d_sys, d_win_energy, d_stage;
+    DevBuf<int2> d_sum_blocks;  // k_stitch_sum: {window, first packed element} per 256-thread block
+    int n_sum_blocks = 0;
     // in-library multi-GPU exchange (ldso_ba_comm_init): RCCL communicator over this context's
     // device, the newest-frame energy slot stride (max over ranks, set at the first exchange
     // after a load) and its staging buffers
@@ -2603,6 +2699,8 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_item_energy.release();
     c->d_sys.release();
     c->d_win_energy.release();
+    c->d_stage.release();
+    c->d_sum_blocks.release();
     c->d_x_local.release();
     c->d_x_gathered.release();
     c->d_fstate.release();
@@ -2685,7 +2783,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     std::vector<int8_t> rs_state;
     std::vector<float> rs_energy, pt_data, precalc, frame_th;
     std::vector<double> adH, adT;
-    long long sc_slab_total = 0, sys_total = 0;
+    long long sc_slab_total = 0, sys_total = 0, stage_total = 0;
     int vec_total = 0;
     std::vector<int> pt_win;
     // residuals per k_linearize wave: 64 when the grid is large anyway; small workloads (one
@@ -2833,6 +2931,8 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         sc_slab_total += (long long)D.n_sc_items * D.ntiles * 16;
         D.sys_base = sys_total;
         sys_total += sys_len(D.D);
+        D.stage_base = stage_total;
+        stage_total += (long long)N * N * stage_rec(N);
         D.newest_begin = res_base + bucket_start[N * (N - 1)];
         D.newest_end = res_base + bucket_start[N * N];
         D.rec_base = rec_base;
@@ -2902,6 +3002,17 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_sc_slab, std::max<size_t>(1, (size_t)sc_slab_total));
     ALLOC(c->d_item_energy, std::max<size_t>(1, top_items.size() * 2));
     ALLOC(c->d_sys, (size_t)sys_total);
+    ALLOC(c->d_stage, (size_t)std::max<long long>(1, stage_total));
+    {
+        std::vector<int2> sb;
+        for (int w = 0; w < n_windows; w++) {
+            const long long n_el = sys_len(c->wd[w].D);
+            for (long long e0 = 0; e0 < n_el; e0 += 256) sb.push_back(make_int2(w, (int)e0));
+        }
+        c->n_sum_blocks = (int)sb.size();
+        ALLOC(c->d_sum_blocks, sb.size());
+        HIP_TRY(hipMemcpyAsync(c->d_sum_blocks.p, sb.data(), sb.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+    }
     ALLOC(c->d_win_energy, (size_t)n_windows * 2);
     ALLOC(c->d_xad, (size_t)n_windows * kXadStride);
     ALLOC(c->d_prior, (size_t)2 * vec_total);
@@ -3131,8 +3242,6 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     c->sys_host_valid = false;
     c->energy_valid = false;
     int rc;
-    if (accumulate) HIP_TRY(hipMemsetAsync(c->d_sys.p, 0, c->d_sys.bytes(), c->stream));
-
     LinParams L;
     L.items = c->d_top_items.p;
     L.wins = c->d_wins.p;
@@ -3185,6 +3294,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.adH = c->d_adH.p;
     Sp.adT = c->d_adT.p;
     Sp.sys = c->d_sys.p;
+    Sp.stage = c->d_stage.p;
     Sp.win_energy = c->d_win_energy.p;
     Sp.accumulate = accumulate;
     Sp.pair_base = 0;
@@ -3209,6 +3319,10 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         if (rc) return rc;
     }
     rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + c->n_pairs, kStThreads, st_smem, st>>>(Sp); });
+    if (!rc && accumulate)
+        rc = timed_launch(c, 2, st, [&] {
+            k_stitch_sum<<<c->n_sum_blocks, 256, 0, st>>>(c->d_wins.p, c->d_sum_blocks.p, c->d_stage.p, c->d_sys.p);
+        });
     if (rc || !c->comm) return rc;
     return comm_exchange(c, accumulate != 0);
 }
