@@ -124,23 +124,26 @@ void ldlt_solve(int n, std::vector<double> &A, std::vector<double> &b) {
             std::swap(at(k, k), at(piv, piv));
         }
         const double d = at(k, k);
-        // trailing update with the unscaled column k: A(i,j) -= (A(i,k) / d) A(j,k), then L(i,k)
+        // trailing update with the unscaled column c = A(., k): A(i,j) = fma(-(c_i c_j), 1/d,
+        // A(i,j)) -- symmetric in i and j, so the device kernels may update either triangle --
+        // then L(i,k) = c_i / d
+        const double rd = d != 0 ? 1.0 / d : 0.0;
         for (int i = k + 1; i < n; i++) col[i] = at(i, k);
         for (int i = k + 1; i < n; i++) {
-            const double l = d != 0 ? col[i] / d : 0.0;
+            const double ci = col[i];
             double *row = &at(i, 0);
-            for (int j = k + 1; j <= i; j++) row[j] -= l * col[j];
-            row[k] = l;
+            for (int j = k + 1; j <= i; j++) row[j] = std::fma(-(ci * col[j]), rd, row[j]);
+            row[k] = d != 0 ? ci / d : 0.0;
         }
     }
     std::vector<double> y(n);
     for (int i = 0; i < n; i++) y[i] = b[perm[i]];
     for (int i = 0; i < n; i++)
-        for (int j = 0; j < i; j++) y[i] -= at(i, j) * y[j];
+        for (int j = 0; j < i; j++) y[i] = std::fma(-at(i, j), y[j], y[i]);
     for (int i = 0; i < n; i++) y[i] = at(i, i) != 0 ? y[i] / at(i, i) : 0.0;
     // back substitution column by column (j descending), the order k_solve uses on the GPU
     for (int j = n - 1; j >= 0; j--)
-        for (int i = 0; i < j; i++) y[i] -= at(j, i) * y[j];
+        for (int i = 0; i < j; i++) y[i] = std::fma(-at(j, i), y[j], y[i]);
     for (int i = 0; i < n; i++) b[perm[i]] = y[i];
 }
 

@@ -93,6 +93,33 @@ struct WinDev {
     float cdelta[4];         // EnergyFunctional::cDeltaF (marginalisation pass only)
 };
 
+#ifdef LDSO_EXP_STAMPS  // diagnostic builds only: s_memtime stamps of block 0 into LDS (a global
+// store would hold up the next fence), copied out at the end of the kernel
+__device__ unsigned long long g_stamps[64];
+__shared__ unsigned long long g_lds_stamps[64];
+#define LDSO_STAMP(i)                                                                              \
+    do {                                                                                           \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_lds_stamps[i] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define LDSO_STAMPW(k, i)                                                                          \
+    do {                                                                                           \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && k == 10)                                 \
+            g_lds_stamps[16 + (threadIdx.x >> 6) * 8 + (i)] = __builtin_amdgcn_s_memtime();        \
+    } while (0)
+#define LDSO_STAMP_FLUSH()                                                                         \
+    do {                                                                                           \
+        if (blockIdx.x == 0) g_stamps[threadIdx.x & 63] = g_lds_stamps[threadIdx.x & 63];          \
+    } while (0)
+#else
+#define LDSO_STAMP(i) ((void)0)
+#define LDSO_STAMPW(k, i) ((void)0)
+#define LDSO_STAMP_FLUSH() ((void)0)
+#endif
+// a debugging / A-B switch from the environment: set and not "0"
+inline bool getenv_flag(const char *name) {
+    const char *v = std::getenv(name);
+    return v && *v && !(v[0] == '0' && v[1] == 0);
+}
 __host__ __device__ inline long long packed_len(int D) { return (long long)D * (D + 1) / 2; }
 __host__ __device__ inline long long sys_len(int D) { return 2 * (packed_len(D) + D); }
 
@@ -1395,7 +1422,7 @@ struct SolveParams {
 };
 // H's row stride in LDS: odd (in doubles), so a column walk touches 32 distinct bank pairs
 __host__ __device__ inline int solve_ld(int n) { return n | 1; }
-size_t solve_smem_bytes(int n) {
+__host__ __device__ inline size_t solve_smem_bytes(int n) {
     return ((size_t)n * solve_ld(n) + 7 * (size_t)n + 9 * (size_t)n + 7 * 7 * 3 + 64) * sizeof(double) +
            ((size_t)n + 1) * sizeof(int) + kSolveThreads * sizeof(double);
 }
@@ -1434,249 +1461,203 @@ __device__ __forceinline__ unsigned long long abs_key(double v) {
     return a == a ? (unsigned long long)__double_as_longlong(a) : 0ull;
 }
 
-__global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
+// LDS layout shared by both solve kernels (doubles unless noted)
+struct SolveLds {
+    double *H, *b, *sc, *y, *col, *Nm, *lr, *G, *V, *Gi, *misc;
+    int *perm;
+    __device__ SolveLds(double *lds, int n) {
+        H = lds;                  // [n][ld] row-major (the host's [n][n]); lower triangle used
+        b = H + (size_t)n * solve_ld(n);
+        sc = b + n;
+        y = sc + n;
+        col = y + n;
+        Nm = col + n;             // [n][7]
+        lr = Nm + 7 * (size_t)n;  // [n]
+        G = lr + n;
+        V = G + 49;
+        Gi = V + 49;              // (N^T N)^-1 of the fast projection path
+        misc = Gi + 49;           // ntx[7], fast flag, coef[7], rd
+        perm = reinterpret_cast<int *>(misc + 16);
+    }
+};
+
+// ---- assembly (EnergyFunctional.cc:342-378), every thread of the block, each element in the
+// host's order of operations: H = (HL + 0) + HA, diagonal *= (1 + lambda), H -= Hsc * scl,
+// mirror, H(i,j) *= s_i s_j.  Every global load is issued up front (one memory round trip):
+// the packed upper elements f = tid + kThreads u, and for row tid < n its diagonal, prior and
+// b terms; the Jacobi scale of row tid from its diagonal, a barrier, then every element
+// straight into its scaled lower position (c, r) (products of two scales commute exactly).
+// Ends with a block barrier.
+template <int kThreads>
+__device__ __forceinline__ void solve_assemble(const SolveParams &P, const WinDev &W, const SolveLds &S, int tid) {
 #pragma clang fp contract(off)
-    extern __shared__ double lds[];
-    const WinDev &W = P.wins[blockIdx.x];
-    const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = W.D, ld = solve_ld(n);
     const long long pl = packed_len(n);
     const double *HA = P.sys + W.sys_base, *bA = HA + pl, *Hs = HA + pl + n, *bs = HA + 2 * pl + n;
-    const int ld = solve_ld(n);
-    double *H = lds;                  // [n][ld] row-major (the host's [n][n]); lower triangle used
-    double *b = H + (size_t)n * ld;   // [n]
-    double *sc = b + n, *y = sc + n, *col = y + n;
-    double *Nm = col + n;             // [n][7]
-    double *lr = Nm + 7 * (size_t)n;  // [n]: L(i,k) of the current step
-    double *G = lr + n, *V = G + 49, *misc = V + 49;  // misc: ntx[7], coef[7]
-    int *perm = reinterpret_cast<int *>(misc + 16);
-    // one private dummy slot per thread: masked-off update elements land there (no branches)
-    double *dummy = reinterpret_cast<double *>(perm + (n + 1) / 2 * 2) + tid;
-    // Strictly-lower elements (i, j), j < i, ordered by column j descending: the elements LDL^T
-    // step k updates (k < j < i) are exactly a prefix, so every step is element-parallel.  Wave w
-    // lane l always owns the elements e = l + 64 (w + 4 t).  Column n-2-mm holds mm+1 elements
-    // and starts at e = mm (mm + 1) / 2.  Entry: offset of (i, j) in H (16 bits) | i << 16 | j << 23.
-    constexpr int kWaves = kSolveThreads / 64;
-    constexpr int kOffRegs = ((kSolveMaxDim - 1) * kSolveMaxDim / 2 + 64 * kWaves - 1) / (64 * kWaves);
-    int tri[kOffRegs];
-    const int noff = n * (n - 1) / 2;
-#pragma unroll
-    for (int t = 0; t < kOffRegs; t++) {
-        const int e = lane + 64 * (wave + kWaves * t);
-        int mm = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
-        if (mm * (mm + 1) / 2 > e) mm--;
-        if ((mm + 1) * (mm + 2) / 2 <= e) mm++;
-        const int j = n - 2 - mm, i = j + 1 + (e - mm * (mm + 1) / 2);
-        tri[t] = e < noff ? ((i * ld + j) | (i << 16) | (j << 23)) : 0;  // padding: (0, 0), never stored
-    }
     const double lambda = 1e-5;  // SOLVER_FIX_LAMBDA
     const double scl = 1.0f / (1 + lambda);
-    auto at = [&](int r, int c) -> double & { return H[r * ld + c]; };
-    // ---- assembly (EnergyFunctional.cc:342-378), each element in the host's order of operations:
-    // H = (HL + 0) + HA, diagonal *= (1 + lambda), H -= Hsc * scl, mirror, H(i,j) *= s_i s_j.
-    // The diagonal first (the Jacobi scale needs it), then every packed upper element (r, c)
-    // straight into its scaled lower position (c, r); products of two scales commute exactly.
-    auto element = [&](int r, int c, double ha, double hs) {
-        double h = ((r == c ? P.prior[2 * (W.vec_base + r)] : 0.0) + 0.0) + ha;
-        if (r == c) h *= (1 + lambda);
+    auto element = [&](bool diag, double prior, double ha, double hs) {
+        double h = ((diag ? prior : 0.0) + 0.0) + ha;
+        if (diag) h *= (1 + lambda);
         return h - hs * scl;
     };
-    for (int i = tid; i < n; i += kSolveThreads) {
-        const long long q = pk_index(i, i, n);
-        sc[i] = 1.0 / sqrt(element(i, i, HA[q], Hs[q]) + 10);
-        perm[i] = i;
+    constexpr int kPer = (int)((kSolveMaxDim * (kSolveMaxDim + 1) / 2 + kThreads - 1) / kThreads);
+    static_assert(kSolveMaxDim <= kThreads, "one row per thread for the diagonal terms");
+    double ha[kPer], hs[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int f = tid + kThreads * u;
+        ha[u] = f < pl ? HA[f] : 0.0;
+        hs[u] = f < pl ? Hs[f] : 0.0;
     }
-    __syncthreads();
-    for (int i = tid; i < n; i += kSolveThreads) {
-        const double bl = P.prior[2 * (W.vec_base + i) + 1];
-        b[i] = (((bl + 0.0) + bA[i]) - bs[i] / (1 + lambda)) * sc[i];
+    LDSO_STAMP(9);
+    double dha = 0, dhs = 0, dpr = 0, bpr = 0, ba = 0, bsv = 0;
+    if (tid < n) {
+        const long long q = pk_index(tid, tid, n);
+        dha = HA[q];
+        dhs = Hs[q];
+        dpr = P.prior[2 * (W.vec_base + tid)];
+        bpr = P.prior[2 * (W.vec_base + tid) + 1];
+        ba = bA[tid];
+        bsv = bs[tid];
     }
-    constexpr int kAsmBatch = 4;
+    // the packed position of each element (index math only, overlapping the loads)
     const int n2 = 2 * n + 1;
-    for (int f0 = tid; f0 < pl; f0 += kSolveThreads * kAsmBatch) {
-        double ha[kAsmBatch], hs[kAsmBatch];
+    int rr[kPer], cc[kPer];
 #pragma unroll
-        for (int u = 0; u < kAsmBatch; u++) {
-            const int f = f0 + kSolveThreads * u;
-            ha[u] = f < pl ? HA[f] : 0.0;
-            hs[u] = f < pl ? Hs[f] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kAsmBatch; u++) {
-            const int f = f0 + kSolveThreads * u;
-            if (f >= pl) break;
-            // row r of the row-major packed upper triangle: r (2n - r + 1) / 2 <= f
-            int r = (int)((n2 - sqrtf(fmaxf(0.0f, (float)(n2 * n2) - 8.0f * f))) * 0.5f);
-            r = r < 0 ? 0 : (r > n - 1 ? n - 1 : r);
-            while (r < n - 1 && pk_index(r + 1, r + 1, n) <= f) r++;
-            while (r > 0 && pk_index(r, r, n) > f) r--;
-            const int c = r + (int)(f - pk_index(r, r, n));
-            at(c, r) = element(r, c, ha[u], hs[u]) * (sc[c] * sc[r]);
-        }
+    for (int u = 0; u < kPer; u++) {
+        const int f = tid + kThreads * u;
+        // row r of the row-major packed upper triangle: r (2n - r + 1) / 2 <= f
+        int r = (int)((n2 - sqrtf(fmaxf(0.0f, (float)(n2 * n2) - 8.0f * f))) * 0.5f);
+        r = r < 0 ? 0 : (r > n - 1 ? n - 1 : r);
+        while (r < n - 1 && pk_index(r + 1, r + 1, n) <= f) r++;
+        while (r > 0 && pk_index(r, r, n) > f) r--;
+        rr[u] = r;
+        cc[u] = r + (int)(f - pk_index(r, r, n));
+    }
+    LDSO_STAMP(10);
+    double sci = 0, hdiag = 0;
+    if (tid < n) {
+        hdiag = element(true, dpr, dha, dhs);
+        sci = 1.0 / sqrt(hdiag + 10);
+        S.sc[tid] = sci;
+        S.perm[tid] = tid;
     }
     __syncthreads();
-    // ---- LDL^T with symmetric diagonal pivoting (lower triangle).  Wave 0 runs the serial part
-    // of each step (pivot, swap, column k) with the diagonal in its registers (lane i mod 64); all
-    // waves then share the trailing update.
-    double dg0 = lane < n ? at(lane, lane) : 0.0, dg1 = lane + 64 < n ? at(lane + 64, lane + 64) : 0.0;
-    for (int k = 0; k < n; k++) {
-        if (wave == 0) {
-            // pivot = first index of the largest |diag| (the host's strict '>' scan from k: a NaN
-            // never wins, except that a NaN at k itself keeps k)
-            int piv;
-            {
-                const int i0 = lane, i1 = lane + 64;
-                const bool c0 = i0 >= k && i0 < n, c1 = i1 >= k && i1 < n;
-                const unsigned long long k0 = !c0 ? 0ull : (dg0 != dg0 && i0 == k) ? ~0ull : abs_key(dg0);
-                const unsigned long long k1 = !c1 ? 0ull : (dg1 != dg1 && i1 == k) ? ~0ull : abs_key(dg1);
-                const unsigned long long mx = wave_max_u64(k0 > k1 ? k0 : k1);
-                const unsigned long long b0 = __ballot(c0 && k0 == mx);
-                piv = b0 ? __builtin_ctzll(b0) : 64 + __builtin_ctzll(__ballot(c1 && k1 == mx));
-            }
-            // symmetric swap k <-> piv (lower triangle: (k,j)<->(piv,j) for j < k, (i,k)<->(piv,i)
-            // for k < i < piv, (i,k)<->(i,piv) for i > piv, the two diagonals), fused with taking
-            // column k: col = the new A(i,k), lr = L(i,k) = col / d, written back as L; the
-            // diagonal's share of the trailing update (A(i,i) -= L(i,k) col_i) happens here
-            const double dk = readlane_f64(k < 64 ? dg0 : dg1, k & 63);
-            const double d = readlane_f64(piv < 64 ? dg0 : dg1, piv & 63);
-            if (piv != k) {
-                if (lane == (k & 63)) (k < 64 ? dg0 : dg1) = d;
-                if (lane == (piv & 63)) (piv < 64 ? dg0 : dg1) = dk;
-                for (int j = lane; j < k; j += 64) {
-                    const double t = at(k, j), u = at(piv, j);
-                    at(k, j) = u;
-                    at(piv, j) = t;
-                }
-            }
-#pragma unroll
-            for (int sgm = 0; sgm < 2; sgm++) {
-                const int i = lane + 64 * sgm;
-                if (i <= k || i >= n) continue;
-                double *own = &at(i, k);
-                double *src = piv == k || i == piv ? own : (i < piv ? &at(piv, i) : &at(i, piv));
-                const double old = *own, v = *src;
-                *(src != own ? src : dummy) = old;
-                const double l = d != 0 ? v / d : 0.0;
-                col[i] = v;
-                lr[i] = l;
-                *own = l;
-                (sgm == 0 ? dg0 : dg1) -= l * v;
-            }
-            if (lane == 0 && piv != k) {
-                const int pt = perm[k];
-                perm[k] = perm[piv];
-                perm[piv] = pt;
-            }
-        }
-        __syncthreads();
-        const int m = (n - k - 2) * (n - k - 1) / 2;  // off-diagonal elements with k < j < i
-        constexpr int kUpdBatch = 6;
-#pragma unroll
-        for (int t0 = 0; t0 < kOffRegs; t0 += kUpdBatch) {
-            if (64 * (wave + kWaves * t0) >= m) continue;  // uniform per wave: chunks past the prefix
-            double a[kUpdBatch], l[kUpdBatch], cj[kUpdBatch], *dst[kUpdBatch];
-#pragma unroll
-            for (int u = 0; u < kUpdBatch; u++) {
-                if (t0 + u >= kOffRegs) continue;
-                const int x = tri[t0 + u], off = x & 0xFFFF, i = (x >> 16) & 0x7F, j = x >> 23;
-                l[u] = lr[i];
-                cj[u] = col[j];
-                a[u] = H[off];
-                dst[u] = lane + 64 * (wave + kWaves * (t0 + u)) < m ? H + off : dummy;
-            }
-#pragma unroll
-            for (int u = 0; u < kUpdBatch; u++) {
-                if (t0 + u >= kOffRegs) continue;
-                *dst[u] = a[u] - l[u] * cj[u];
-            }
-        }
-        __syncthreads();
+    if (tid < n) {
+        S.b[tid] = (((bpr + 0.0) + ba) - bsv / (1 + lambda)) * sci;
+        S.H[tid * ld + tid] = hdiag * (sci * sci);
     }
-    if (wave != 0) return;  // the rest is one wavefront's work (wave-level synchronisation only)
-    if (lane < n) at(lane, lane) = dg0;
-    if (lane + 64 < n) at(lane + 64, lane + 64) = dg1;
-    wave_lds_sync();
-    // ---- substitutions (column by column, as the host); y[i] lives in lane i (mod 64); the
-    // matrix entries of the next 4 columns are loaded ahead of the dependent chain
-    const int ia = lane, ib = lane + 64, ra = min(ia, n - 1), rb = min(ib, n - 1);
-    double ya = ia < n ? b[perm[ia]] : 0.0, yb = ib < n ? b[perm[ib]] : 0.0;
-    constexpr int kSubAhead = 4;
-    for (int j0 = 0; j0 < n; j0 += kSubAhead) {
-        double fa[kSubAhead], fb[kSubAhead];
+    LDSO_STAMP(11);
 #pragma unroll
-        for (int u = 0; u < kSubAhead; u++) {
-            const int j = min(j0 + u, n - 1);
-            fa[u] = at(ra, j);
-            fb[u] = at(rb, j);
-        }
-#pragma unroll
-        for (int u = 0; u < kSubAhead; u++) {
-            const int j = j0 + u;
-            if (j >= n) break;
-            const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
-            if (ia > j && ia < n) ya -= fa[u] * yj;
-            if (ib > j && ib < n) yb -= fb[u] * yj;
-        }
+    for (int u = 0; u < kPer; u++) {
+        const int f = tid + kThreads * u, r = rr[u], c = cc[u];
+        if (f >= pl) break;
+        if (r != c) S.H[c * ld + r] = element(false, 0.0, ha[u], hs[u]) * (S.sc[c] * S.sc[r]);
     }
-    if (ia < n) ya = at(ia, ia) != 0 ? ya / at(ia, ia) : 0.0;
-    if (ib < n) yb = at(ib, ib) != 0 ? yb / at(ib, ib) : 0.0;
-    for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
-        double fa[kSubAhead], fb[kSubAhead];
+    __syncthreads();
+}
+
+// ---- orthogonalize (EnergyFunctional.cc:809-841), iteration >= 2: x -= N (N^T N)^+ N^T x.
+// solve_ortho_prepare (one wavefront) does the x-independent half -- normalised nullspaces Nm,
+// G = Nm^T Nm and, for 7 nullspaces, the fast path's G^-1 (gram_pinv7; misc[7] = 1 when it
+// applies) -- so it can run beside the factorisation; raw: >= 7 n doubles of free LDS.
+__device__ __forceinline__ void solve_ortho_prepare(const SolveParams &P, const WinDev &W, const SolveLds &S,
+                                                    double *raw, int lane) {
+#pragma clang fp contract(off)
+    const int n = W.D, kk = P.n_null;
+    double *Nm = S.Nm, *lr = S.lr, *G = S.G, *V = S.V;
+    const double *ns = P.ns + (size_t)7 * W.vec_base;
+    for (int e = lane; e < kk * n; e += 64) raw[e] = ns[e];  // raw nullspaces [kk][n], coalesced
+    wave_lds_sync();
+    if (lane < kk) {
+        double s2 = 0;
+#pragma unroll 1
+        for (int i0 = 0; i0 < n; i0 += 4) {
+            double p[4];
 #pragma unroll
-        for (int u = 0; u < kSubAhead; u++) {
-            const int j = max(j0 - u, 0);
-            fa[u] = at(j, ra);
-            fb[u] = at(j, rb);
-        }
+            for (int u = 0; u < 4; u++) {
+                const double v = raw[lane * n + min(i0 + u, n - 1)];
+                p[u] = v * v;
+            }
 #pragma unroll
-        for (int u = 0; u < kSubAhead; u++) {
-            const int j = j0 - u;
-            if (j < 0) break;
-            const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
-            if (ia < j) ya -= fa[u] * yj;
-            if (ib < j) yb -= fb[u] * yj;
+            for (int u = 0; u < 4; u++) s2 = i0 + u < n ? s2 + p[u] : s2;
         }
+        lr[lane] = sqrt(s2);
     }
-    if (ia < n) b[perm[ia]] = ya;
-    if (ib < n) b[perm[ib]] = yb;
     wave_lds_sync();
-    for (int i = lane; i < n; i += 64) y[i] = sc[i] * b[i];  // x
+    for (int e = lane; e < kk * n; e += 64) {
+        const int i = e / kk, a = e - i * kk;
+        Nm[e] = raw[a * n + i] / lr[a];
+    }
     wave_lds_sync();
-    // ---- orthogonalize (EnergyFunctional.cc:809-841), iteration >= 2
+    if (lane < kk * kk) {
+        const int a = lane / kk, c = lane % kk;
+        double g = 0.0;
+#pragma unroll 1
+        for (int i0 = 0; i0 < n; i0 += 4) {
+            double p[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int ic = min(i0 + u, n - 1);
+                p[u] = Nm[(size_t)ic * kk + a] * Nm[(size_t)ic * kk + c];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) g = i0 + u < n ? g + p[u] : g;
+        }
+        G[lane] = g;
+        V[lane] = a == c ? 1.0 : 0.0;
+    }
+    wave_lds_sync();
+    bool fast = false;
+    if (kk == 7) {  // every lane redundantly; lane 0 stores
+        double g[7][7], gi[7][7];
+#pragma unroll
+        for (int r = 0; r < 7; r++)
+#pragma unroll
+            for (int q = 0; q < 7; q++) g[r][q] = G[r * 7 + q];
+        fast = gram_pinv7(g, gi);
+        if (lane == 0 && fast)
+#pragma unroll
+            for (int r = 0; r < 7; r++)
+#pragma unroll
+                for (int q = 0; q < 7; q++) S.Gi[r * 7 + q] = gi[r][q];
+    }
+    if (lane == 0) S.misc[7] = fast ? 1.0 : 0.0;
+    wave_lds_sync();
+}
+
+// the x-dependent half (one wavefront, after solve_ortho_prepare's results are visible): N^T y,
+// coef = G^-1 N^T y (fast path) or the round-robin Jacobi pseudo-inverse of host_math.cpp
+// project_out, y -= Nm coef; then x (= y) to global memory.
+__device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, const WinDev &W, const SolveLds &S,
+                                                        int lane) {
+#pragma clang fp contract(off)
+    const int n = W.D;
+    double *y = S.y, *Nm = S.Nm, *G = S.G;
     const int kk = P.n_null;
     if (P.iteration >= 2 && kk > 0) {
-        const double *ns = P.ns + (size_t)7 * W.vec_base;
-        double *raw = H;  // H is free after the substitutions: raw nullspaces [kk][n], coalesced
-        for (int e = lane; e < kk * n; e += 64) raw[e] = ns[e];
-        wave_lds_sync();
-        if (lane < kk) {
-            double s2 = 0;
-            for (int i = 0; i < n; i++) s2 += raw[lane * n + i] * raw[lane * n + i];
-            lr[lane] = sqrt(s2);
-        }
-        wave_lds_sync();
-        for (int e = lane; e < kk * n; e += 64) {
-            const int i = e / kk, a = e - i * kk;
-            Nm[e] = raw[a * n + i] / lr[a];
-        }
-        wave_lds_sync();
-        if (lane < kk * kk) {
-            const int a = lane / kk, c = lane % kk;
-            double g = 0.0;
-            for (int i = 0; i < n; i++) g += Nm[(size_t)i * kk + a] * Nm[(size_t)i * kk + c];
-            G[lane] = g;
-            V[lane] = a == c ? 1.0 : 0.0;
-        }
-        double *ntx = misc, *coef = misc + 8;
-        if (lane < kk) {
+        double *ntx = S.misc, *coef = S.misc + 8;
+        if (lane < kk) {  // a static trip count and unconditional (clamped) loads: only the adds chain
             double t = 0.0;
-            for (int i = 0; i < n; i++) t += Nm[(size_t)i * kk + lane] * y[i];
+            const int a = lane;
+#pragma unroll 1
+            for (int i0 = 0; i0 < n; i0 += 4) {
+                double p[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int ic = min(i0 + u, n - 1);
+                    p[u] = Nm[(size_t)ic * kk + a] * y[ic];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) t = i0 + u < n ? t + p[u] : t;
+            }
             ntx[lane] = t;
             coef[lane] = 0.0;
         }
         wave_lds_sync();
-        {  // (NtN)^+ NtX in registers, every lane redundantly (no LDS traffic, no synchronisation):
-            // the Cholesky fast path when G is well conditioned, else the round-robin Jacobi of
-            // host_math.cpp project_out
+        LDSO_STAMP(12);
+        {  // (NtN)^+ NtX in registers, every lane redundantly (no LDS traffic, no synchronisation)
             double g[7][7], v[7][7], nt[7], cf[7] = {0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
             for (int r = 0; r < 7; r++)
@@ -1687,8 +1668,15 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
                 }
 #pragma unroll
             for (int a = 0; a < 7; a++) nt[a] = a < kk ? ntx[a] : 0.0;
-            const bool fast = kk == 7 && gram_inverse_coef7(g, nt, cf);
-            for (int sweep = 0; sweep < 64 && !fast; sweep++) {
+            const bool fast = kk == 7 && S.misc[7] != 0.0;
+            if (fast) {  // coef = G^-1 N^T y, one row per lane
+                double gr[7];
+#pragma unroll
+                for (int b = 0; b < 7; b++) gr[b] = S.Gi[7 * min(lane, 6) + b];
+                if (lane < 7) coef[lane] = gram_apply7_row(gr, nt);
+                goto projected;
+            }
+            for (int sweep = 0; sweep < 64; sweep++) {
                 double off = 0;
 #pragma unroll
                 for (int p = 0; p < 7; p++)
@@ -1743,7 +1731,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
                 if (e < kk) smax = fmax(smax, sqrt(fmax(0.0, g[e][e])));
 #pragma unroll
             for (int e = 0; e < 7; e++) {
-                if (fast || e >= kk) continue;
+                if (e >= kk) continue;
                 const double ev = g[e][e];
                 if (!(sqrt(fmax(0.0, ev)) > kSolverModeDelta * smax)) continue;
                 double proj = 0;
@@ -1761,15 +1749,449 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
                 coef[lane] = mine;
             }
         }
+    projected:
         wave_lds_sync();
+        LDSO_STAMP(13);
         for (int i = lane; i < n; i += 64) {
             double t = 0;
-            for (int a = 0; a < kk; a++) t += Nm[(size_t)i * kk + a] * coef[a];
+#pragma unroll
+            for (int a = 0; a < 7; a++) {
+                const int ac = min(a, kk - 1);
+                const double p = Nm[(size_t)i * kk + ac] * coef[ac];
+                t = a < kk ? t + p : t;
+            }
             y[i] -= t;
         }
         wave_lds_sync();
     }
     for (int i = lane; i < n; i += 64) P.x[W.vec_base + i] = y[i];
+}
+
+// The trailing update of step k is A(i,j) = fma(-(c_i c_j), 1/d, A(i,j)) with c = column k and
+// d the pivot (host_math.cpp ldlt_solve states the same): symmetric in i and j, so a kernel may
+// hold both triangles and update either copy; L(i,k) = c_i / d is the exact quotient.
+__global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
+#pragma clang fp contract(off)
+    extern __shared__ double lds[];
+    const WinDev W = P.wins[blockIdx.x];  // a register copy: the helpers would re-read global memory after every LDS store
+    const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ld = solve_ld(n);
+    const SolveLds S(lds, n);
+    double *H = S.H, *b = S.b, *sc = S.sc, *y = S.y, *col = S.col, *misc = S.misc;
+    int *perm = S.perm;
+    // one private dummy slot per thread: masked-off update elements land there (no branches)
+    double *dummy = reinterpret_cast<double *>(perm + (n + 1) / 2 * 2) + tid;
+    // Strictly-lower elements (i, j), j < i, ordered by column j descending: the elements LDL^T
+    // step k updates (k < j < i) are exactly a prefix, so every step is element-parallel.  Wave w
+    // lane l always owns the elements e = l + 64 (w + 4 t).  Column n-2-mm holds mm+1 elements
+    // and starts at e = mm (mm + 1) / 2.  Entry: offset of (i, j) in H (16 bits) | i << 16 | j << 23.
+    constexpr int kWaves = kSolveThreads / 64;
+    constexpr int kOffRegs = ((kSolveMaxDim - 1) * kSolveMaxDim / 2 + 64 * kWaves - 1) / (64 * kWaves);
+    int tri[kOffRegs];
+    const int noff = n * (n - 1) / 2;
+#pragma unroll
+    for (int t = 0; t < kOffRegs; t++) {
+        const int e = lane + 64 * (wave + kWaves * t);
+        int mm = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
+        if (mm * (mm + 1) / 2 > e) mm--;
+        if ((mm + 1) * (mm + 2) / 2 <= e) mm++;
+        const int j = n - 2 - mm, i = j + 1 + (e - mm * (mm + 1) / 2);
+        tri[t] = e < noff ? ((i * ld + j) | (i << 16) | (j << 23)) : 0;  // padding: (0, 0), never stored
+    }
+    auto at = [&](int r, int c) -> double & { return H[r * ld + c]; };
+    solve_assemble<kSolveThreads>(P, W, S, tid);
+    // ---- LDL^T with symmetric diagonal pivoting (lower triangle).  Wave 0 runs the serial part
+    // of each step (pivot, swap, column k) with the diagonal in its registers (lane i mod 64); all
+    // waves then share the trailing update.
+    double dg0 = lane < n ? at(lane, lane) : 0.0, dg1 = lane + 64 < n ? at(lane + 64, lane + 64) : 0.0;
+    for (int k = 0; k < n; k++) {
+        if (wave == 0) {
+            // pivot = first index of the largest |diag| (the host's strict '>' scan from k: a NaN
+            // never wins, except that a NaN at k itself keeps k)
+            int piv;
+            {
+                const int i0 = lane, i1 = lane + 64;
+                const bool c0 = i0 >= k && i0 < n, c1 = i1 >= k && i1 < n;
+                const unsigned long long k0 = !c0 ? 0ull : (dg0 != dg0 && i0 == k) ? ~0ull : abs_key(dg0);
+                const unsigned long long k1 = !c1 ? 0ull : (dg1 != dg1 && i1 == k) ? ~0ull : abs_key(dg1);
+                const unsigned long long mx = wave_max_u64(k0 > k1 ? k0 : k1);
+                const unsigned long long b0 = __ballot(c0 && k0 == mx);
+                piv = b0 ? __builtin_ctzll(b0) : 64 + __builtin_ctzll(__ballot(c1 && k1 == mx));
+            }
+            // symmetric swap k <-> piv (lower triangle: (k,j)<->(piv,j) for j < k, (i,k)<->(piv,i)
+            // for k < i < piv, (i,k)<->(i,piv) for i > piv, the two diagonals), fused with taking
+            // column k: col = the new A(i,k), L(i,k) = col / d written back; the diagonal's share
+            // of the trailing update happens here
+            const double dk = readlane_f64(k < 64 ? dg0 : dg1, k & 63);
+            const double d = readlane_f64(piv < 64 ? dg0 : dg1, piv & 63);
+            const double rd = d != 0 ? 1.0 / d : 0.0;
+            if (piv != k) {
+                if (lane == (k & 63)) (k < 64 ? dg0 : dg1) = d;
+                if (lane == (piv & 63)) (piv < 64 ? dg0 : dg1) = dk;
+                for (int j = lane; j < k; j += 64) {
+                    const double t = at(k, j), u = at(piv, j);
+                    at(k, j) = u;
+                    at(piv, j) = t;
+                }
+            }
+#pragma unroll
+            for (int sgm = 0; sgm < 2; sgm++) {
+                const int i = lane + 64 * sgm;
+                if (i <= k || i >= n) continue;
+                double *own = &at(i, k);
+                double *src = piv == k || i == piv ? own : (i < piv ? &at(piv, i) : &at(i, piv));
+                const double old = *own, v = *src;
+                *(src != own ? src : dummy) = old;
+                col[i] = v;
+                *own = d != 0 ? v / d : 0.0;
+                double &dgi = sgm == 0 ? dg0 : dg1;
+                dgi = fma(-(v * v), rd, dgi);
+            }
+            if (lane == 0) {
+                misc[15] = rd;
+                if (piv != k) {
+                    const int pt = perm[k];
+                    perm[k] = perm[piv];
+                    perm[piv] = pt;
+                }
+            }
+        }
+        __syncthreads();
+        const int m = (n - k - 2) * (n - k - 1) / 2;  // off-diagonal elements with k < j < i
+        const double rd = misc[15];
+        constexpr int kUpdBatch = 6;
+#pragma unroll
+        for (int t0 = 0; t0 < kOffRegs; t0 += kUpdBatch) {
+            if (64 * (wave + kWaves * t0) >= m) continue;  // uniform per wave: chunks past the prefix
+            double a[kUpdBatch], ci[kUpdBatch], cj[kUpdBatch], *dst[kUpdBatch];
+#pragma unroll
+            for (int u = 0; u < kUpdBatch; u++) {
+                if (t0 + u >= kOffRegs) continue;
+                const int x = tri[t0 + u], off = x & 0xFFFF, i = (x >> 16) & 0x7F, j = x >> 23;
+                ci[u] = col[i];
+                cj[u] = col[j];
+                a[u] = H[off];
+                dst[u] = lane + 64 * (wave + kWaves * (t0 + u)) < m ? H + off : dummy;
+            }
+#pragma unroll
+            for (int u = 0; u < kUpdBatch; u++) {
+                if (t0 + u >= kOffRegs) continue;
+                *dst[u] = fma(-(ci[u] * cj[u]), rd, a[u]);
+            }
+        }
+        __syncthreads();
+    }
+    if (wave != 0) return;  // the rest is one wavefront's work (wave-level synchronisation only)
+    if (lane < n) at(lane, lane) = dg0;
+    if (lane + 64 < n) at(lane + 64, lane + 64) = dg1;
+    wave_lds_sync();
+    // ---- substitutions (column by column, as the host); y[i] lives in lane i (mod 64); the
+    // matrix entries of the next 4 columns are loaded ahead of the dependent chain
+    const int ia = lane, ib = lane + 64, ra = min(ia, n - 1), rb = min(ib, n - 1);
+    double ya = ia < n ? b[perm[ia]] : 0.0, yb = ib < n ? b[perm[ib]] : 0.0;
+    constexpr int kSubAhead = 4;
+    for (int j0 = 0; j0 < n; j0 += kSubAhead) {
+        double fa[kSubAhead], fb[kSubAhead];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = min(j0 + u, n - 1);
+            fa[u] = at(ra, j);
+            fb[u] = at(rb, j);
+        }
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = j0 + u;
+            if (j >= n) break;
+            const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+            if (ia > j && ia < n) ya = fma(-fa[u], yj, ya);
+            if (ib > j && ib < n) yb = fma(-fb[u], yj, yb);
+        }
+    }
+    if (ia < n) ya = at(ia, ia) != 0 ? ya / at(ia, ia) : 0.0;
+    if (ib < n) yb = at(ib, ib) != 0 ? yb / at(ib, ib) : 0.0;
+    for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
+        double fa[kSubAhead], fb[kSubAhead];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = max(j0 - u, 0);
+            fa[u] = at(j, ra);
+            fb[u] = at(j, rb);
+        }
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = j0 - u;
+            if (j < 0) break;
+            const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+            if (ia < j) ya = fma(-fa[u], yj, ya);
+            if (ib < j) yb = fma(-fb[u], yj, yb);
+        }
+    }
+    if (ia < n) b[perm[ia]] = ya;
+    if (ib < n) b[perm[ib]] = yb;
+    wave_lds_sync();
+    for (int i = lane; i < n; i += 64) y[i] = sc[i] * b[i];  // x
+    wave_lds_sync();
+    if (P.iteration >= 2 && P.n_null > 0) solve_ortho_prepare(P, W, S, H, lane);  // H is free now
+    solve_ortho_apply_store(P, W, S, lane);
+}
+
+// ============================================================================================
+// k_solve_reg: the same solve for windows of up to 7 keyframes (n <= 64), factorised out of
+// registers by four wavefronts without block barriers.  Lane p of wave w holds H(p, q) for the
+// 16 columns q = 16w .. 16w+15 of the scaled symmetric H (both triangles) and, in every wave,
+// the diagonal of row p.  Pivoting is logical: rows never move, pos tracks the host's index of
+// each physical row (the swap k <-> piv is bookkeeping), and every wave selects the pivot
+// itself from its copy of the diagonal (the copies are bitwise equal).  The wave owning the
+// pivot's column publishes it in LDS (one slot per step, then a ready flag; LDS requests of a
+// wave are served in order, so a flag seen set means the column is there).  Look-ahead: right
+// after a step's column arrives each wave updates the diagonal and picks the next pivot, and
+// its owner updates and publishes that one column before its own trailing update, so the
+// serial chain per step is read column -> diagonal -> pivot -> one fma -> publish; 1/d is
+// computed off that chain.  Every element sees the host's operations in the host's order (the
+// update is symmetric in i, j), so x stays bit-identical to ldso_ba_solve.
+// A fifth wave prepares the nullspace projection, then follows the published columns: L(i,k)
+// = c_i / d into Ls and the forward substitution step by step (the host's per-element order),
+// then the diagonal, the backward substitution and the projection -- all in physical row order
+// (b[perm[i]] = y_i makes the host's permutation disappear).
+// ============================================================================================
+constexpr int kSolveRegDim = 64;
+constexpr int kSolveLsLd = 65;            // odd: a column walk of Ls is bank-conflict free
+constexpr int kSolveRegThreads = 5 * 64;  // 4 factorisation waves + the substitution wave
+__host__ __device__ inline size_t solve_reg_base(int n) { return (solve_smem_bytes(n) + 15) / 16 * 2; }  // doubles
+__host__ __device__ inline size_t solve_reg_smem_bytes(int n) {
+    return solve_reg_base(n) * sizeof(double) +
+           ((size_t)kSolveRegDim * kSolveLsLd + kSolveRegDim * kSolveRegDim + kSolveRegDim + 7 * kSolveRegDim + 1) *
+               sizeof(double) +
+           2 * kSolveRegDim * sizeof(int) + 4 * kSolveRegDim * sizeof(unsigned long long);
+}
+struct RegLds {
+    double *cb, *Ls, *Dv, *raw;  // cb: [step][64] published columns (16-byte aligned); Dv: d of step
+    unsigned long long *pmax;    // [step][wave] pivot-key maxima, zeroed
+    int *pv, *flag;              // pivot row and ready flag of each step
+    __device__ RegLds(double *lds, int n) {
+        cb = lds + solve_reg_base(n);
+        Ls = cb + kSolveRegDim * kSolveRegDim;
+        Dv = Ls + kSolveRegDim * kSolveLsLd;
+        raw = Dv + kSolveRegDim;
+        pmax = reinterpret_cast<unsigned long long *>(raw + 7 * kSolveRegDim + 1);
+        pv = reinterpret_cast<int *>(pmax + 4 * kSolveRegDim);
+        flag = pv + kSolveRegDim;
+    }
+};
+#define LDSO_COMPILER_FENCE() asm volatile("" ::: "memory")
+// wave-wide maximum of a 32-bit key (0 = identity), broadcast: row_shr 1/2/4/8 within each row
+// of 16, then row_bcast15 / row_bcast31 carry rows 0-2 into lane 63
+__device__ __forceinline__ unsigned wave_max_u32(unsigned x) {
+#define LDSO_DPP_MAX32(CTRL, ROWS)                                                                          \
+    {                                                                                                       \
+        const unsigned o = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);         \
+        x = o > x ? o : x;                                                                                  \
+    }
+    LDSO_DPP_MAX32(0x111, 0xF)
+    LDSO_DPP_MAX32(0x112, 0xF)
+    LDSO_DPP_MAX32(0x114, 0xF)
+    LDSO_DPP_MAX32(0x118, 0xF)
+    LDSO_DPP_MAX32(0x142, 0xA)
+    LDSO_DPP_MAX32(0x143, 0xC)
+#undef LDSO_DPP_MAX32
+    return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+}
+// pivot of step k: the largest |diag| among the live rows, ties to the smallest host index; a
+// NaN never wins, except at the host's row k itself, which then keeps k (the host's strict '>'
+// scan from k).  The maximum of the order-preserving 64-bit keys: the high words by DPP first,
+// the low words among high-word ties.  (The LDSO_EXP_PIVOT_ATOMIC variant, an LDS atomic max
+// into this wave's zeroed slot of the step, measured slower: 650 vs 520 cycles per pivot.)
+__device__ __forceinline__ int reg_pivot(double dg, unsigned long long act, int pos, int k, int lane,
+                                         unsigned long long *slot) {
+    const bool live = (act >> lane) & 1;
+    const unsigned long long nank = __ballot(live && dg != dg && pos == k);
+    if (nank) return __builtin_amdgcn_readfirstlane(__builtin_ctzll(nank));
+    const unsigned long long key = live ? abs_key(dg) : 0ull;
+    unsigned long long cand;
+#ifndef LDSO_EXP_PIVOT_ATOMIC
+    (void)slot;
+    const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
+    const unsigned mh = wave_max_u32(hi);
+    cand = __ballot(live && hi == mh);
+    if (cand & (cand - 1)) {
+        const bool c = (cand >> lane) & 1;
+        const unsigned ml = wave_max_u32(c ? lo : 0u);
+        cand = __ballot(c && lo == ml);
+    }
+#else
+    __hip_atomic_fetch_max(slot, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    LDSO_COMPILER_FENCE();
+    const unsigned long long mx = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    cand = __ballot(live && key == mx);
+#endif
+    int piv = __builtin_ctzll(cand);
+    if (cand & (cand - 1)) {  // exact tie: the smallest host index
+        int best = __builtin_amdgcn_readlane(pos, piv);
+        for (unsigned long long m = cand & (cand - 1); m; m &= m - 1) {
+            const int l = __builtin_ctzll(m), pl = __builtin_amdgcn_readlane(pos, l);
+            if (pl < best) {
+                best = pl;
+                piv = l;
+            }
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(piv);
+}
+// column of step k, then its ready flag = pivot row + 1 (no wait: the LDS serves a wave's
+// requests in order).  The pivot row's own entry of the column is d.
+__device__ __forceinline__ void reg_publish(const RegLds &R, int k, int lane, double c, int piv) {
+    R.cb[k * kSolveRegDim + lane] = c;
+    LDSO_COMPILER_FENCE();
+    if (lane == 0) __hip_atomic_store(R.flag + k, piv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    LDSO_COMPILER_FENCE();
+}
+// poll the flag and the column together: a set flag read before the column read means the
+// column read returns the published value; returns the pivot row
+__device__ __forceinline__ int reg_wait(const RegLds &R, int k, int lane, double &v) {
+    int f;
+    do {
+        f = __hip_atomic_load(R.flag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        LDSO_COMPILER_FENCE();
+        v = R.cb[k * kSolveRegDim + lane];
+        LDSO_COMPILER_FENCE();
+        f = __builtin_amdgcn_readfirstlane(f);
+    } while (f == 0);
+    return f - 1;
+}
+__global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
+#pragma clang fp contract(off)
+    extern __shared__ double lds[];
+    const WinDev W = P.wins[blockIdx.x];  // a register copy (see k_solve)
+    const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ld = solve_ld(n);
+    const SolveLds S(lds, n);
+    const RegLds R(lds, n);
+    LDSO_STAMP(0);
+    for (int i = tid; i < kSolveRegDim; i += kSolveRegThreads) R.flag[i] = 0;
+    for (int i = tid; i < 4 * kSolveRegDim; i += kSolveRegThreads) R.pmax[i] = 0;
+    solve_assemble<kSolveRegThreads>(P, W, S, tid);  // its barriers also publish the flags
+    LDSO_STAMP(1);
+    if (wave == 4) {
+        // ---- the projection's x-independent half, then the substitutions (physical rows)
+        if (P.iteration >= 2 && P.n_null > 0) solve_ortho_prepare(P, W, S, R.raw, lane);
+        double y = lane < n ? S.b[lane] : 0.0;
+        unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);
+        for (int k = 0; k < n; k++) {  // forward: y_i = fma(-L(i,k), y_k, y_i), k ascending
+            double cl;
+            const int piv = reg_wait(R, k, lane, cl);
+            const double d = readlane_f64(cl, piv);
+            if (lane == 0) {
+                R.Dv[k] = d;
+                R.pv[k] = piv;
+            }
+            act &= ~(1ull << piv);
+            const double yk = readlane_f64(y, piv);
+            if ((act >> lane) & 1) {
+                const double l = d != 0 ? cl / d : 0.0;
+                R.Ls[k * kSolveLsLd + lane] = l;
+                y = fma(-l, yk, y);
+            }
+        }
+        LDSO_STAMP(5);
+        // to the host's order: lane i takes y_i = y of physical row pv[i]; then the diagonal
+        if (lane < n) S.col[lane] = y;
+        wave_lds_sync();
+        const int pvl = lane < n ? R.pv[lane] : 0;
+        double yl = lane < n ? S.col[pvl] : 0.0;
+        if (lane < n) {
+            const double dd = R.Dv[lane];
+            yl = dd != 0 ? yl / dd : 0.0;
+        }
+        // backward: y_i = fma(-L(j,i), y_j, y_i) for j descending, L(j,i) = Ls[i][pv[j]] (a
+        // rolled loop: this code runs once, so its size is instruction fetches)
+        const int me = min(lane, n - 1);
+        constexpr int kSubAhead = 4;
+#pragma unroll 1
+        for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
+            double fa[kSubAhead];
+#pragma unroll
+            for (int u = 0; u < kSubAhead; u++)
+                fa[u] = R.Ls[me * kSolveLsLd + __builtin_amdgcn_readlane(pvl, max(j0 - u, 0))];
+#pragma unroll
+            for (int u = 0; u < kSubAhead; u++) {
+                const int j = j0 - u;
+                if (j < 0) break;
+                const double t = fma(-fa[u], readlane_f64(yl, j), yl);
+                yl = lane < j ? t : yl;
+            }
+        }
+        if (lane < n) S.b[pvl] = yl;  // b[perm[i]] = y_i
+        wave_lds_sync();
+        y = lane < n ? S.b[lane] : 0.0;
+        if (lane < n) S.y[lane] = S.sc[lane] * y;  // x = s b, b[perm[i]] = y_i
+        wave_lds_sync();
+        LDSO_STAMP(7);
+        solve_ortho_apply_store(P, W, S, lane);
+        LDSO_STAMP(8);
+        LDSO_STAMP_FLUSH();
+        return;
+    }
+    typedef double d16 __attribute__((ext_vector_type(16)));
+    d16 rv;
+    const int q0 = 16 * wave;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int q = q0 + j, r = lane > q ? lane : q, c = lane > q ? q : lane;
+        rv[j] = q < n && lane < n ? S.H[r * ld + c] : 0.0;
+    }
+    double dg = lane < n ? S.H[lane * ld + lane] : 0.0;
+    int pos = lane;
+    unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);  // rows not yet pivoted
+    LDSO_STAMP(2);
+    int piv = reg_pivot(dg, act, pos, 0, lane, R.pmax + wave);
+    double d = readlane_f64(dg, piv);
+    double cl = 0.0;
+    if ((piv >> 4) == wave) {
+        cl = rv[piv & 15];
+        reg_publish(R, 0, lane, cl, piv);
+    }
+    double rd = d != 0 ? 1.0 / d : 0.0;
+    for (int k = 0; k < n; k++) {
+        LDSO_STAMPW(k, 0);
+        if ((piv >> 4) != wave) (void)reg_wait(R, k, lane, cl);  // column k of the host: A(i, k) after the swap
+        LDSO_STAMPW(k, 1);
+        const int kphys = __builtin_ctzll(__ballot(((act >> lane) & 1) && pos == k));
+        const int ppos = __builtin_amdgcn_readlane(pos, piv);
+        pos = lane == piv ? k : (lane == kphys ? ppos : pos);
+        act &= ~(1ull << piv);
+        dg = fma(-(cl * cl), rd, dg);
+        LDSO_STAMPW(k, 2);
+        int nxt = 0;
+        double cn = 0.0, rdn = 0.0;
+        if (k + 1 < n) {
+            nxt = reg_pivot(dg, act, pos, k + 1, lane, R.pmax + 4 * (k + 1) + wave);
+            LDSO_STAMPW(k, 3);
+            const double dn = readlane_f64(dg, nxt);
+            if ((nxt >> 4) == wave) {  // look-ahead: the next pivot's column first
+                cn = fma(-(cl * readlane_f64(cl, nxt)), rd, rv[nxt & 15]);
+                reg_publish(R, k + 1, lane, cn, nxt);
+                LDSO_STAMPW(k, 7);
+            }
+            LDSO_STAMPW(k, 4);
+            rdn = dn != 0 ? 1.0 / dn : 0.0;
+        }
+        LDSO_STAMPW(k, 5);
+        // trailing update of this wave's 16 columns, c_q broadcast from the published column
+        // (dead columns too: never read again; the look-ahead column gets the same bits again)
+        const double2 *cq2 = reinterpret_cast<const double2 *>(R.cb + k * kSolveRegDim + q0);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const double2 cq = cq2[u];
+            rv[2 * u] = fma(-(cl * cq.x), rd, rv[2 * u]);
+            rv[2 * u + 1] = fma(-(cl * cq.y), rd, rv[2 * u + 1]);
+        }
+        LDSO_STAMPW(k, 6);
+        piv = nxt;
+        cl = cn;
+        rd = rdn;
+        if (k == 0) LDSO_STAMP(3);
+        if (k == n / 2) LDSO_STAMP(4);
+    }
 }
 
 // ============================================================================================
@@ -3609,6 +4031,12 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
     return 0;
 }
 
+#ifdef LDSO_EXP_STAMPS
+extern "C" int ldso_ba_debug_stamps(unsigned long long *out) {
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)));
+    return 0;
+}
+#endif
 // ---- device-side solve / resubstitute ----------------------------------
 int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const double *ns, int32_t n_null,
                          double *x_out) {
@@ -3632,13 +4060,22 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
     S.x = c->d_x.p;
     S.iteration = iteration;
     S.n_null = (iteration >= 2 && (ns || c->ns_resident)) ? n_null : 0;
-    const size_t smem = solve_smem_bytes(dmax);
     static std::once_flag once;
     std::call_once(once, [] {
         (void)hipFuncSetAttribute((const void *)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)solve_smem_bytes(kSolveMaxDim));
+        (void)hipFuncSetAttribute((const void *)k_solve_reg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)solve_reg_smem_bytes(kSolveRegDim));
     });
-    int rc = timed_launch(c, 5, c->stream, [&] { k_solve<<<c->n_win, kSolveThreads, smem, c->stream>>>(S); });
+    // windows of up to 7 keyframes (n <= 64): the register factorisation; larger: the LDS one
+    const bool reg = dmax <= kSolveRegDim && !getenv_flag("LDSO_BA_SOLVE_LDS");
+    const size_t smem = reg ? solve_reg_smem_bytes(dmax) : solve_smem_bytes(dmax);
+    int rc = timed_launch(c, 5, c->stream, [&] {
+        if (reg)
+            k_solve_reg<<<c->n_win, kSolveRegThreads, smem, c->stream>>>(S);
+        else
+            k_solve<<<c->n_win, kSolveThreads, smem, c->stream>>>(S);
+    });
     if (rc) return rc;
     if (x_out) {
         HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,

@@ -42,7 +42,7 @@ constexpr float kMargWeightFac = 0.5f * 0.5f;               // :45
 // pseudo-inverse is the inverse: coef = G^-1 N^T x via Cholesky.  Returns false (coef untouched)
 // otherwise, and the caller runs the Jacobi eigen-decomposition.  One definition for the host
 // solver and k_solve, so both produce the same bits.
-LDSO_HD inline bool gram_inverse_coef7(const double (&G)[7][7], const double (&ntx)[7], double (&coef)[7]) {
+LDSO_HD inline bool gram_pinv7(const double (&G)[7][7], double (&Gi)[7][7]) {
 #pragma clang fp contract(off)
     double L[7][7], Li[7][7];
     for (int j = 0; j < 7; j++) {
@@ -67,7 +67,7 @@ LDSO_HD inline bool gram_inverse_coef7(const double (&G)[7][7], const double (&n
             for (int p = c; p < i; p++) t -= L[i][p] * Li[p][c];
             Li[i][c] = t / L[i][i];
         }
-    double Gi[7][7], f2 = 0, tr = 0;
+    double f2 = 0, tr = 0;
     for (int a = 0; a < 7; a++) {
         tr += G[a][a];
         for (int b = 0; b < 7; b++) {
@@ -77,12 +77,19 @@ LDSO_HD inline bool gram_inverse_coef7(const double (&G)[7][7], const double (&n
             f2 += t * t;
         }
     }
-    if (!(kSolverModeDelta * kSolverModeDelta * tr * sqrt(f2) < 0.5)) return false;
-    for (int a = 0; a < 7; a++) {
-        double t = 0;
-        for (int b = 0; b < 7; b++) t += Gi[a][b] * ntx[b];
-        coef[a] = t;
-    }
+    return kSolverModeDelta * kSolverModeDelta * tr * sqrt(f2) < 0.5;
+}
+// coef = G^-1 ntx, row by row (the second half of the fast path)
+LDSO_HD inline double gram_apply7_row(const double *Gi_row, const double *ntx) {
+#pragma clang fp contract(off)
+    double t = 0;
+    for (int b = 0; b < 7; b++) t += Gi_row[b] * ntx[b];
+    return t;
+}
+LDSO_HD inline bool gram_inverse_coef7(const double (&G)[7][7], const double (&ntx)[7], double (&coef)[7]) {
+    double Gi[7][7];
+    if (!gram_pinv7(G, Gi)) return false;
+    for (int a = 0; a < 7; a++) coef[a] = gram_apply7_row(Gi[a], ntx);
     return true;
 }
 

@@ -363,13 +363,19 @@ def test_windows_of_different_sizes_in_one_context(built):
     c.close()
 
 
-def test_device_solve_and_resubstitute_match_host_path(built):
-    """ldso_ba_solve_device / resubstitute_device (one wavefront per window) reproduce the host
-    solver and the host-staged resubstitution bit for bit, for a batch of windows of different
-    sizes, at iteration 0 (no orthogonalisation) and 2 (nullspace projection: the Cholesky path,
-    and the Jacobi path for a rank-deficient nullspace set)."""
+@pytest.mark.parametrize("kernel", ["reg", "lds", "lds_forced"])
+def test_device_solve_and_resubstitute_match_host_path(built, kernel, monkeypatch):
+    """ldso_ba_solve_device / resubstitute_device reproduce the host solver and the host-staged
+    resubstitution bit for bit, for a batch of windows of different sizes, at iteration 0 (no
+    orthogonalisation) and 2 (nullspace projection: the Cholesky path, and the Jacobi path for a
+    rank-deficient nullspace set).  Both factorisations: k_solve_reg (every window <= 7
+    keyframes) and k_solve (a window of 11 keyframes in the batch, or LDSO_BA_SOLVE_LDS=1)."""
     cfgs = [dict(n_frames=3, n_points=120, seed=70), dict(n_frames=7, n_points=900, seed=71),
             dict(n_frames=11, n_points=1200, seed=72), dict(n_frames=5, n_points=400, seed=73)]
+    if kernel != "lds":
+        cfgs = [cf for cf in cfgs if cf["n_frames"] <= 7] + [dict(n_frames=7, n_points=300, seed=75, baseline=0.2)]
+    if kernel == "lds_forced":
+        monkeypatch.setenv("LDSO_BA_SOLVE_LDS", "1")
     ws = [synth.make_window(**cf) for cf in cfgs]
     ns = [w.nullspaces() for w in ws]
     c = BAContext(0).load(ws)

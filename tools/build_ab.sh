@@ -8,6 +8,6 @@ while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   out=../../abl/$name; mkdir -p $out
   ( /opt/rocm/bin/hipcc $HIPFLAGS $flags -c -o $out/ldso_ba.o ldso_ba.hip &&
-    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libldso_ba.so $out/ldso_ba.o ../lib/ldso_ct.o ../lib/host_math.o ) &
+    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libldso_ba.so $out/ldso_ba.o ../lib/ldso_ct.o ../lib/host_math.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib ) &
 done
 wait

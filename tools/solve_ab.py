@@ -1,5 +1,6 @@
 """k_solve / GN-iteration timing of whole library builds (HIP events + host clock):
-  python tools/solve_ab.py lib1.so lib2.so ...   (each in its own process, LDSO_BA_LIB)"""
+  python tools/solve_ab.py lib1.so lib2.so@LDSO_BA_SOLVE_LDS=1 ...   (each in its own process,
+  LDSO_BA_LIB; '@NAME=VALUE' adds an environment variable to that process)"""
 import json
 import os
 import subprocess
@@ -41,12 +42,14 @@ for B in (1, 64):
     c.close()
 print("RESULT " + json.dumps(out))
 '''
-for lib in sys.argv[1:]:
+for arg in sys.argv[1:]:
+    lib, *extra = arg.split("@")
     env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(lib))
+    env.update(kv.split("=", 1) for kv in extra)
     p = subprocess.run([sys.executable, "-c", CHILD.replace("ROOT", repr(ROOT))], env=env, capture_output=True,
                        text=True, timeout=300)
     line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
     if p.returncode != 0 or not line:
-        print(lib, "FAILED", p.stderr[-2000:])
+        print(arg, "FAILED", p.stderr[-2000:])
         sys.exit(1)
-    print(lib, {k: round(v, 4) for k, v in json.loads(line[0][7:]).items()})
+    print(arg, {k: round(v, 4) for k, v in json.loads(line[0][7:]).items()})
