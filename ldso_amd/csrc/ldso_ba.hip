@@ -1308,7 +1308,79 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
 // Sum of every stitch term of one packed output element, in one fixed order over the window's
 // pairs (t major, h minor): HA / bA from the Top records, Hsc / bsc from the SC records.  One
 // thread per element of {HA upper, bA, Hsc upper, bsc} of every window; writes every element
-// (no memset, no atomics: the stitched system is bitwise repeatable).
+// (no memset, no atomics: the stitched system is bitwise repeatable).  Each element's terms
+// form one of five closed-form sequences (below), so the k-th term's record offset is a formula
+// and the loads go out eight at a time instead of one per visited pair.
+enum StitchSeq : int {
+    kSeqAll = 0,    // every pair (h, t), h != t, one record index
+    kSeqScCal = 1,  // the pairs (h, first target of h): (1..N-1, 0), then (0, 1)
+    kSeqAB = 2,     // (f, t) for t < f [A], (h, f) for h != f [B], (f, t) for t > f [A]
+    kSeqHaOff = 3,  // (f2, f1) then (f1, f2): H(h,t) of the two orientations
+    kSeqScOff = 4   // (h, f1) for h != f1 (S2 term at h = f2, S1 otherwise), then (f1, f2)
+};
+struct StitchTerms {
+    int seq, N, f, f2, idxA, idxB, s1rc, s2;  // s1rc >= 0: B index = kS1 + (F - (F > h)) * 64 + s1rc
+    int r, c;
+    __device__ int count() const {
+        switch (seq) {
+        case kSeqAll: return N * (N - 1);
+        case kSeqScCal: return N;
+        case kSeqAB: return 2 * (N - 1);
+        case kSeqHaOff: return 2;
+        default: return N;
+        }
+    }
+    __device__ long long offset(int k, int R) const {
+        int h, t, idx;
+        switch (seq) {
+        case kSeqAll: {
+            t = k / (N - 1);
+            const int hh = k - t * (N - 1);
+            h = hh < t ? hh : hh + 1;
+            idx = idxA;
+            break;
+        }
+        case kSeqScCal:
+            h = k < N - 1 ? k + 1 : 0;
+            t = k < N - 1 ? 0 : 1;
+            idx = idxA;
+            break;
+        case kSeqAB:
+            if (k < f) {
+                h = f;
+                t = k;
+                idx = idxA;
+            } else if (k - f < N - 1) {
+                const int kk = k - f;
+                h = kk < f ? kk : kk + 1;
+                t = f;
+                idx = s1rc >= 0 ? kS1 + (f - (f > h ? 1 : 0)) * 64 + s1rc : idxB;
+            } else {
+                h = f;
+                t = f + 1 + (k - f - (N - 1));
+                idx = idxA;
+            }
+            break;
+        case kSeqHaOff:
+            h = k == 0 ? f2 : f;
+            t = k == 0 ? f : f2;
+            idx = k == 0 ? kT3 + c * 8 + r : kT3 + r * 8 + c;
+            break;
+        default:  // kSeqScOff, f = f1
+            if (k < N - 1) {
+                h = k < f ? k : k + 1;
+                t = f;
+                idx = h == f2 ? s2 + r * 8 + c : kS1 + (f2 - (f2 > h ? 1 : 0)) * 64 + r * 8 + c;
+            } else {
+                h = f;
+                t = f2;
+                idx = s2 + c * 8 + r;
+            }
+            break;
+        }
+        return (long long)(h + N * t) * R + idx;
+    }
+};
 __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ wins, const int2 *__restrict__ blocks,
                                                      const double *__restrict__ stage, double *sys) {
     const int2 bw = blocks[blockIdx.x];  // {window, first element of this block}
@@ -1319,28 +1391,25 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
     if (e >= n_el) return;
     const int R = stage_rec(N), s2 = st_S2(N);
     const double *st = stage + W.stage_base;
-    auto recp = [&](int h, int t) { return st + (size_t)(h + N * t) * R; };
     const bool sc = e >= pl + D;
-    long long q = sc ? e - (pl + D) : e;
-    double v = 0;
+    const long long q = sc ? e - (pl + D) : e;
+    StitchTerms T;
+    T.N = N;
+    T.s2 = s2;
+    T.s1rc = -1;
+    T.f = T.f2 = T.r = T.c = 0;
+    T.idxA = T.idxB = 0;
     if (q >= pl) {  // b element
         const int r = (int)(q - pl);
         if (r < 4) {
-            for (int t = 0; t < N; t++)
-                for (int h = 0; h < N; h++) {
-                    if (h == t) continue;
-                    if (!sc) v += recp(h, t)[kT7 + r];
-                    else if ((h == 0 ? 1 : 0) == t) v += recp(h, t)[s2 + 208 + r * 5 + 4];
-                }
+            T.seq = sc ? kSeqScCal : kSeqAll;
+            T.idxA = sc ? s2 + 208 + r * 5 + 4 : kT7 + r;
         } else {
-            const int f = (r - 4) >> 3, rr = (r - 4) & 7;
-            for (int t = 0; t < N; t++)
-                for (int h = 0; h < N; h++) {
-                    if (h == t) continue;
-                    const double *p = recp(h, t);
-                    if (h == f) v += p[(sc ? s2 + 192 : kT6a) + rr];
-                    if (t == f) v += p[(sc ? s2 + 200 : kT6b) + rr];
-                }
+            const int rr = (r - 4) & 7;
+            T.seq = kSeqAB;
+            T.f = (r - 4) >> 3;
+            T.idxA = (sc ? s2 + 192 : kT6a) + rr;
+            T.idxB = (sc ? s2 + 200 : kT6b) + rr;
         }
     } else {  // upper element (row, col) of the packed triangle
         int row = (int)((2 * D + 1 - sqrt((double)(2 * D + 1) * (2 * D + 1) - 8.0 * (double)q)) * 0.5);
@@ -1349,48 +1418,45 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
         while (row > 0 && pk_index(row, row, D) > q) row--;
         const int col = row + (int)(q - pk_index(row, row, D));
         if (col < 4) {  // calibration block (row <= col < 4)
-            for (int t = 0; t < N; t++)
-                for (int h = 0; h < N; h++) {
-                    if (h == t) continue;
-                    if (!sc) v += recp(h, t)[kT5 + row * 4 + col];
-                    else if ((h == 0 ? 1 : 0) == t) v += recp(h, t)[s2 + 208 + row * 5 + col];
-                }
+            T.seq = sc ? kSeqScCal : kSeqAll;
+            T.idxA = sc ? s2 + 208 + row * 5 + col : kT5 + row * 4 + col;
         } else if (row < 4) {  // (calib cc = row, frame f, rr)
-            const int f = (col - 4) >> 3, rr = (col - 4) & 7, cc = row;
-            for (int t = 0; t < N; t++)
-                for (int h = 0; h < N; h++) {
-                    if (h == t) continue;
-                    const double *p = recp(h, t);
-                    if (h == f) v += p[(sc ? s2 + 128 : kT4a) + rr * 4 + cc];
-                    if (t == f) v += p[(sc ? s2 + 160 : kT4b) + rr * 4 + cc];
-                }
+            const int rr = (col - 4) & 7, cc = row;
+            T.seq = kSeqAB;
+            T.f = (col - 4) >> 3;
+            T.idxA = (sc ? s2 + 128 : kT4a) + rr * 4 + cc;
+            T.idxB = (sc ? s2 + 160 : kT4b) + rr * 4 + cc;
         } else {
             const int f1 = (row - 4) >> 3, r = (row - 4) & 7, f2 = (col - 4) >> 3, c = (col - 4) & 7;
-            for (int t = 0; t < N; t++)
-                for (int h = 0; h < N; h++) {
-                    if (h == t) continue;
-                    const double *p = recp(h, t);
-                    if (!sc) {
-                        if (f1 == f2) {
-                            if (h == f1) v += p[kT1 + r * 8 + c];
-                            if (t == f1) v += p[kT2 + r * 8 + c];
-                        } else {
-                            if (h == f1 && t == f2) v += p[kT3 + r * 8 + c];  // H(h,t), h < t
-                            if (h == f2 && t == f1) v += p[kT3 + c * 8 + r];  // H(h,t)^T, h > t
-                        }
-                    } else {
-                        const int i = h, j = t;
-                        if (f1 == f2) {
-                            if (j == f1) v += p[kS1 + (f1 - (f1 > i ? 1 : 0)) * 64 + r * 8 + c];  // H(j,j) from S1
-                            if (i == f1) v += p[s2 + 64 + r * 8 + c];                          // H(i,i)
-                        } else {
-                            if (j == f1 && i != f2) v += p[kS1 + (f2 - (f2 > i ? 1 : 0)) * 64 + r * 8 + c];
-                            if (i == f2 && j == f1) v += p[s2 + r * 8 + c];  // H(j,i), j < i
-                            if (i == f1 && j == f2) v += p[s2 + c * 8 + r];  // H(j,i)^T, j > i
-                        }
-                    }
+            T.r = r;
+            T.c = c;
+            if (f1 == f2) {
+                T.seq = kSeqAB;
+                T.f = f1;
+                if (!sc) {
+                    T.idxA = kT1 + r * 8 + c;  // h == f1
+                    T.idxB = kT2 + r * 8 + c;  // t == f1
+                } else {
+                    T.idxA = s2 + 64 + r * 8 + c;  // i == f1: H(i,i)
+                    T.s1rc = r * 8 + c;             // j == f1: H(j,j) from S1
                 }
+            } else {
+                T.seq = sc ? kSeqScOff : kSeqHaOff;
+                T.f = f1;
+                T.f2 = f2;
+            }
         }
+    }
+    const int cnt = T.count();
+    double v = 0;
+    constexpr int kBatch = 8;
+    for (int k0 = 0; k0 < cnt; k0 += kBatch) {
+        double x[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; u++) x[u] = st[k0 + u < cnt ? T.offset(k0 + u, R) : 0];
+#pragma unroll
+        for (int u = 0; u < kBatch; u++)
+            if (k0 + u < cnt) v += x[u];
     }
     sys[W.sys_base + e] = v;
 }
@@ -2575,6 +2641,14 @@ __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
         }
     }
 }
+// the energy history of ldso_ba_optimize: slot *slot <- the pass's energies, then *slot + 1
+// (a device-side counter, so one captured GN iteration replays unchanged)
+__global__ __launch_bounds__(256) void k_keep_energy(const double *src, double *hist, int *slot, int n2) {
+    const int s = *slot;
+    for (int i = threadIdx.x; i < n2; i += 256) hist[(size_t)s * n2 + i] = src[i];
+    __syncthreads();
+    if (threadIdx.x == 0) *slot = s + 1;
+}
 __global__ __launch_bounds__(256) void k_point_step(float *pt_data, const float *pt_step, int n) {
 #pragma clang fp contract(off)
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2713,6 +2787,7 @@ struct ldso_ba_ctx {
     // prior switches per window, the energy history
     DevBuf<ldso_ba_frame_state> d_fstate;
     DevBuf<double> d_calib_val, d_calib_zero, d_cprior, d_ehist;
+    DevBuf<int> d_eslot;
     DevBuf<int> d_add_priors;
     DevBuf<float> d_xad;            // [win][kXadStride]
     DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
@@ -3130,6 +3205,7 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_calib_zero.release();
     c->d_cprior.release();
     c->d_ehist.release();
+    c->d_eslot.release();
     c->d_add_priors.release();
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->d_xad.release();
@@ -4154,7 +4230,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     int rc;
     if ((rc = c->d_fstate.alloc(c->n_frames)) || (rc = c->d_calib_val.alloc((size_t)4 * nw)) ||
         (rc = c->d_calib_zero.alloc((size_t)4 * nw)) || (rc = c->d_cprior.alloc((size_t)4 * nw)) ||
-        (rc = c->d_add_priors.alloc(nw)) || (rc = c->d_ehist.alloc((size_t)2 * nw * (n_its + 1))))
+        (rc = c->d_add_priors.alloc(nw)) || (rc = c->d_ehist.alloc((size_t)2 * nw * (n_its + 1))) ||
+        (rc = c->d_eslot.alloc(1)))
         return rc;
     std::vector<double> cp((size_t)4 * nw);
     std::vector<int> ap(nw);
@@ -4186,27 +4263,66 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     F.x = c->d_x.p;
     F.precalc = c->d_precalc.p;
     F.prior = c->d_prior.p;
-    auto keep_energy = [&](int slot) -> int {
-        HIP_TRY(hipMemcpyAsync(c->d_ehist.p + (size_t)2 * nw * slot, c->d_win_energy.p, (size_t)2 * nw * sizeof(double),
-                               hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_eslot.p, 0, sizeof(int), c->stream));
+    auto keep_energy = [&]() -> int {
+        k_keep_energy<<<1, 256, 0, c->stream>>>(c->d_win_energy.p, c->d_ehist.p, c->d_eslot.p, 2 * nw);
+        HIP_TRY(hipGetLastError());
         return 0;
     };
-    // FullSystem::optimize (FullSystem.cc:853-976) with setting_forceAceptStep: resetOOB, then
-    // linearizeAll + applyRes (+ the accumulation solveSystemF uses), and per iteration
-    // solveSystemF, resubstituteF_MT, doStepFromBackup + setPrecalcValues, linearizeAll + applyRes
-    if ((rc = ldso_ba_reset_oob(c, -1)) || (rc = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0)) || (rc = keep_energy(0)))
-        return rc;
-    for (int it = 0; it < n_its; it++) {
-        if ((rc = ldso_ba_solve_device(c, it, 1e-5, nullptr, ns ? 7 : 0, nullptr))) return rc;
-        if ((rc = ldso_ba_resubstitute_device(c, 1e-5, nullptr))) return rc;
+    // one GN iteration: solveSystemF, resubstituteF_MT, doStepFromBackup + setPrecalcValues,
+    // linearizeAll + applyRes (+ the accumulation the next solve uses)
+    auto gn_iteration = [&](int it) -> int {
+        int r;
+        if ((r = ldso_ba_solve_device(c, it, 1e-5, nullptr, ns ? 7 : 0, nullptr))) return r;
+        if ((r = ldso_ba_resubstitute_device(c, 1e-5, nullptr))) return r;
         k_frame_step<<<nw, 256, 0, c->stream>>>(F);
         HIP_TRY(hipGetLastError());
         if (c->P_tot) {
             k_point_step<<<(c->P_tot + 255) / 256, 256, 0, c->stream>>>(c->d_pt_data.p, c->d_pt_step.p, c->P_tot);
             HIP_TRY(hipGetLastError());
         }
-        if ((rc = ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0)) || (rc = keep_energy(it + 1))) return rc;
+        if ((r = ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0)) || (r = keep_energy())) return r;
+        return 0;
+    };
+    // FullSystem::optimize (FullSystem.cc:853-976) with setting_forceAceptStep: resetOOB, then
+    // linearizeAll + applyRes, then the GN iterations.  Without a communicator or kernel timing,
+    // iterations after the first replay a captured HIP graph of one iteration: every launch
+    // argument of an iteration is the same except the solve's projection (iteration >= 2) and the
+    // last pass's accumulate flag, so at most three graphs, each captured once per call.
+    if ((rc = ldso_ba_reset_oob(c, -1)) || (rc = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0)) || (rc = keep_energy()))
+        return rc;
+    const bool use_graph = !c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH");
+    hipGraphExec_t gx[4] = {nullptr, nullptr, nullptr, nullptr};
+    auto variant = [&](int it) { return (it >= 2 ? 1 : 0) + (it + 1 < n_its ? 0 : 2); };
+    for (int it = 0; it < n_its && !rc; it++) {
+        const int v = variant(it);
+        if (!use_graph || it == 0) {
+            rc = gn_iteration(it);
+            continue;
+        }
+        if (!gx[v]) {
+            hipGraph_t g = nullptr;
+            HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            const int rcap = gn_iteration(it);
+            const hipError_t ecap = hipStreamEndCapture(c->stream, &g);
+            if (rcap || ecap != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                rc = rcap ? rcap : fail(-2, std::string("graph capture: ") + hipGetErrorString(ecap));
+                break;
+            }
+            const hipError_t ei = hipGraphInstantiate(&gx[v], g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (ei != hipSuccess) {
+                rc = fail(-2, std::string("graph instantiate: ") + hipGetErrorString(ei));
+                break;
+            }
+        }
+        const hipError_t el = hipGraphLaunch(gx[v], c->stream);
+        if (el != hipSuccess) rc = fail(-2, std::string("graph launch: ") + hipGetErrorString(el));
     }
+    for (hipGraphExec_t g : gx)
+        if (g) (void)hipGraphExecDestroy(g);
+    if (rc) return rc;
     if (energy_out) {
         std::vector<double> e((size_t)2 * nw * (n_its + 1));
         HIP_TRY(hipMemcpyAsync(e.data(), c->d_ehist.p, e.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
