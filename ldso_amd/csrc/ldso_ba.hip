@@ -1569,38 +1569,36 @@ __device__ __forceinline__ void solve_assemble(const SolveParams &P, const WinDe
     };
     constexpr int kPer = (int)((kSolveMaxDim * (kSolveMaxDim + 1) / 2 + kThreads - 1) / kThreads);
     static_assert(kSolveMaxDim <= kThreads, "one row per thread for the diagonal terms");
+#ifdef LDSO_EXP_STAMPS
+    if (__builtin_amdgcn_readfirstlane(n) > 0) LDSO_STAMP(14);  // the window descriptor has arrived
+#endif
+    // element u of this thread: f = tid + kThreads u in the "folded" order of the packed upper
+    // triangle (row p paired with row n-1-p: n/2 rows of n+1 elements, n = 8N+4 is even), decoded
+    // without loops; then unconditional loads at clamped positions (a guarded load becomes a
+    // branch with its own wait)
+    const int np1 = n + 1;
+    const float inv = 1.0f / (float)np1;
+    int rr[kPer], cc[kPer];
     double ha[kPer], hs[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; u++) {
-        const int f = tid + kThreads * u;
-        ha[u] = f < pl ? HA[f] : 0.0;
-        hs[u] = f < pl ? Hs[f] : 0.0;
+        const int f = min(tid + kThreads * u, (int)pl - 1);
+        int p = (int)((float)f * inv);
+        p = p * np1 > f ? p - 1 : ((p + 1) * np1 <= f ? p + 1 : p);
+        const int o = f - p * np1;
+        const bool first = o < n - p;
+        const int r = first ? p : n - 1 - p;
+        rr[u] = r;
+        cc[u] = first ? p + o : r + (o - (n - p));
+        const int q = r * (2 * n - r + 1) / 2 + (cc[u] - r);  // pk_index(r, c, n)
+        ha[u] = HA[q];
+        hs[u] = Hs[q];
     }
     LDSO_STAMP(9);
-    double dha = 0, dhs = 0, dpr = 0, bpr = 0, ba = 0, bsv = 0;
-    if (tid < n) {
-        const long long q = pk_index(tid, tid, n);
-        dha = HA[q];
-        dhs = Hs[q];
-        dpr = P.prior[2 * (W.vec_base + tid)];
-        bpr = P.prior[2 * (W.vec_base + tid) + 1];
-        ba = bA[tid];
-        bsv = bs[tid];
-    }
-    // the packed position of each element (index math only, overlapping the loads)
-    const int n2 = 2 * n + 1;
-    int rr[kPer], cc[kPer];
-#pragma unroll
-    for (int u = 0; u < kPer; u++) {
-        const int f = tid + kThreads * u;
-        // row r of the row-major packed upper triangle: r (2n - r + 1) / 2 <= f
-        int r = (int)((n2 - sqrtf(fmaxf(0.0f, (float)(n2 * n2) - 8.0f * f))) * 0.5f);
-        r = r < 0 ? 0 : (r > n - 1 ? n - 1 : r);
-        while (r < n - 1 && pk_index(r + 1, r + 1, n) <= f) r++;
-        while (r > 0 && pk_index(r, r, n) > f) r--;
-        rr[u] = r;
-        cc[u] = r + (int)(f - pk_index(r, r, n));
-    }
+    const int tr = min(tid, n - 1);
+    const long long qd = pk_index(tr, tr, n);
+    const double dha = HA[qd], dhs = Hs[qd], dpr = P.prior[2 * (W.vec_base + tr)],
+                 bpr = P.prior[2 * (W.vec_base + tr) + 1], ba = bA[tr], bsv = bs[tr];
     LDSO_STAMP(10);
     double sci = 0, hdiag = 0;
     if (tid < n) {
@@ -1618,8 +1616,7 @@ __device__ __forceinline__ void solve_assemble(const SolveParams &P, const WinDe
 #pragma unroll
     for (int u = 0; u < kPer; u++) {
         const int f = tid + kThreads * u, r = rr[u], c = cc[u];
-        if (f >= pl) break;
-        if (r != c) S.H[c * ld + r] = element(false, 0.0, ha[u], hs[u]) * (S.sc[c] * S.sc[r]);
+        if (f < pl && r != c) S.H[c * ld + r] = element(false, 0.0, ha[u], hs[u]) * (S.sc[c] * S.sc[r]);
     }
     __syncthreads();
 }
@@ -1723,7 +1720,17 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
         }
         wave_lds_sync();
         LDSO_STAMP(12);
-        {  // (NtN)^+ NtX in registers, every lane redundantly (no LDS traffic, no synchronisation)
+        if (kk == 7 && S.misc[7] != 0.0) {  // fast path: coef = G^-1 N^T y, one row per lane
+            if (lane < 7) {
+                double gr[7], nt[7];
+#pragma unroll
+                for (int b = 0; b < 7; b++) {
+                    gr[b] = S.Gi[7 * lane + b];
+                    nt[b] = ntx[b];
+                }
+                coef[lane] = gram_apply7_row(gr, nt);
+            }
+        } else {  // (NtN)^+ NtX in registers, every lane redundantly (no LDS traffic, no synchronisation)
             double g[7][7], v[7][7], nt[7], cf[7] = {0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
             for (int r = 0; r < 7; r++)
@@ -1734,14 +1741,6 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
                 }
 #pragma unroll
             for (int a = 0; a < 7; a++) nt[a] = a < kk ? ntx[a] : 0.0;
-            const bool fast = kk == 7 && S.misc[7] != 0.0;
-            if (fast) {  // coef = G^-1 N^T y, one row per lane
-                double gr[7];
-#pragma unroll
-                for (int b = 0; b < 7; b++) gr[b] = S.Gi[7 * min(lane, 6) + b];
-                if (lane < 7) coef[lane] = gram_apply7_row(gr, nt);
-                goto projected;
-            }
             for (int sweep = 0; sweep < 64; sweep++) {
                 double off = 0;
 #pragma unroll
@@ -1815,7 +1814,6 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
                 coef[lane] = mine;
             }
         }
-    projected:
         wave_lds_sync();
         LDSO_STAMP(13);
         for (int i = lane; i < n; i += 64) {
@@ -2070,9 +2068,7 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned x) {
 __device__ __forceinline__ int reg_pivot(double dg, unsigned long long act, int pos, int k, int lane,
                                          unsigned long long *slot) {
     const bool live = (act >> lane) & 1;
-    const unsigned long long nank = __ballot(live && dg != dg && pos == k);
-    if (nank) return __builtin_amdgcn_readfirstlane(__builtin_ctzll(nank));
-    const unsigned long long key = live ? abs_key(dg) : 0ull;
+    const unsigned long long key = !live ? 0ull : (dg != dg && pos == k) ? ~0ull : abs_key(dg);
     unsigned long long cand;
 #ifndef LDSO_EXP_PIVOT_ATOMIC
     (void)slot;
@@ -2113,6 +2109,7 @@ __device__ __forceinline__ void reg_publish(const RegLds &R, int k, int lane, do
 }
 // poll the flag and the column together: a set flag read before the column read means the
 // column read returns the published value; returns the pivot row
+template <bool kSleep = false>
 __device__ __forceinline__ int reg_wait(const RegLds &R, int k, int lane, double &v) {
     int f;
     do {
@@ -2121,6 +2118,7 @@ __device__ __forceinline__ int reg_wait(const RegLds &R, int k, int lane, double
         v = R.cb[k * kSolveRegDim + lane];
         LDSO_COMPILER_FENCE();
         f = __builtin_amdgcn_readfirstlane(f);
+        if (kSleep && f == 0) __builtin_amdgcn_s_sleep(2);
     } while (f == 0);
     return f - 1;
 }
@@ -2137,6 +2135,8 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
     for (int i = tid; i < 4 * kSolveRegDim; i += kSolveRegThreads) R.pmax[i] = 0;
     solve_assemble<kSolveRegThreads>(P, W, S, tid);  // its barriers also publish the flags
     LDSO_STAMP(1);
+    if (wave == 4) __builtin_amdgcn_s_setprio(0);  // the factorisation's chain first
+    else __builtin_amdgcn_s_setprio(2);
     if (wave == 4) {
         // ---- the projection's x-independent half, then the substitutions (physical rows)
         if (P.iteration >= 2 && P.n_null > 0) solve_ortho_prepare(P, W, S, R.raw, lane);
@@ -2144,7 +2144,7 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
         unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);
         for (int k = 0; k < n; k++) {  // forward: y_i = fma(-L(i,k), y_k, y_i), k ascending
             double cl;
-            const int piv = reg_wait(R, k, lane, cl);
+            const int piv = reg_wait<true>(R, k, lane, cl);  // off the critical chain: poll gently
             const double d = readlane_f64(cl, piv);
             if (lane == 0) {
                 R.Dv[k] = d;

@@ -96,6 +96,28 @@ __global__ void probe(double *out, unsigned long long *cyc, double a, double b, 
     out[lane] = x + u;
     if (lane == 0) cyc[sel] = t1 - t0;
 }
+// one block gathers 2 x 1830 doubles (the solve's assembly pattern) from a buffer another
+// kernel wrote: cycles from the first load to the last value in registers
+__global__ void writer(double *buf, int n) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) buf[i] = i * 1e-3;
+}
+__global__ void __launch_bounds__(320) gather(const double *buf, double *out, unsigned long long *cyc, int pl) {
+    const int tid = threadIdx.x;
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    double a[6], b[6];
+#pragma unroll
+    for (int u = 0; u < 6; u++) {
+        const int f = min(tid + 320 * u, pl - 1);
+        a[u] = buf[f];
+        b[u] = buf[pl + f];
+    }
+    double s = 0;
+#pragma unroll
+    for (int u = 0; u < 6; u++) s += a[u] * b[u];
+    unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[tid] = s;
+    if (tid == 0) cyc[11] = t1 - t0;
+}
 int main() {
     double *out;
     unsigned long long *cyc, h[16];
@@ -107,6 +129,24 @@ int main() {
     for (int rep = 0; rep < 3; rep++)
         for (int s = 0; s < 9; s++) probe<<<1, 64>>>(out, cyc, 1.0000001, 0.9999999, s);
     probe_ifetch<<<1, 64>>>((float *)out, cyc, 1.0f);
+    double *big, *o2;
+    hipMalloc(&big, 64 << 20);
+    hipMalloc(&o2, 4096);
+    for (int r = 0; r < 5; r++) {
+        writer<<<64, 256>>>(big, 4096);
+        gather<<<1, 320>>>(big, o2, cyc, 1830);
+        hipDeviceSynchronize();
+        unsigned long long c;
+        hipMemcpy(&c, cyc + 11, 8, hipMemcpyDeviceToHost);
+        printf("gather 2x1830 doubles after a writer kernel: %llu cycles\n", c);
+    }
+    for (int r = 0; r < 3; r++) {
+        gather<<<1, 320>>>(big, o2, cyc, 1830);
+        hipDeviceSynchronize();
+        unsigned long long c;
+        hipMemcpy(&c, cyc + 11, 8, hipMemcpyDeviceToHost);
+        printf("gather again (no writer): %llu cycles\n", c);
+    }
     hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
     printf("2048 dependent-ish fma_f32 straight line: first pass %llu cycles, second pass %llu\n", h[9], h[10]);
     for (int s = 0; s < 9; s++) printf("%-30s %.1f cycles/rep\n", names[s], (double)h[s] / R);

@@ -30,7 +30,8 @@ for it in (0, 2):
         acc.append(st.astype(np.int64) - int(st[0]))
     med = np.median(np.array(acc[5:]), axis=0)
     print(f"iteration {it}: " + ", ".join(f"{nm} {v:.0f}" for nm, v in zip(names, med[:9])))
-    print("  assembly: loads issued %.0f, index math %.0f, diag+barrier %.0f" % tuple(med[9:12]))
+    print("  assembly: window descriptor at %.0f, loads issued %.0f, index math %.0f, diag+barrier %.0f"
+          % (med[14], med[9], med[10], med[11]))
     print("  projection: ntx at %.0f, coef at %.0f" % tuple(med[12:14]))
     for w in range(4):
         ph = med[16 + 8 * w:16 + 8 * w + 8]
