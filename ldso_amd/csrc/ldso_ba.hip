@@ -31,6 +31,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2302,6 +2303,7 @@ struct ResubParams {
     const float *__restrict__ pt_out;
     const int *__restrict__ pt_host;
     float *pt_step;
+    float *pt_data;  // non-null: apply doStepFromBackup's point step in place (ldso_ba_optimize)
     int begin, count;
     float lambda;
 };
@@ -2535,8 +2537,18 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
     if (k >= P.count) return;
     const int p = P.begin + k;
     const float *po = P.pt_out + (size_t)p * 12;
+    // doStepFromBackup's point step (setIdepth / setIdepthZero / setDeltaF)
+    auto apply = [&](float step) {
+        if (!P.pt_data) return;
+        float *d = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+        const float idepth = d[2] + 1.0f * step;
+        d[2] = kScaleIdepth * idepth;  // setIdepth
+        d[3] = kScaleIdepth * idepth;  // setIdepthZero (LDSO's doStepFromBackup)
+        d[5] = idepth - idepth;        // setDeltaF: idepth - idepth_zero
+    };
     if (po[9] == 0) {
         P.pt_step[p] = 0;
+        apply(0.0f);
         return;
     }
     const int w = P.pt_win[p];
@@ -2559,8 +2571,13 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
                          xa[6] * j1.z + xa[7] * j1.w;
         b -= dd;
     }
-    if (!isfinite(b)) return;  // reference returns from the chunk; the step is left unchanged
-    P.pt_step[p] = -b * po[0] / (1 + P.lambda);
+    if (!isfinite(b)) {  // reference returns from the chunk; the step is left unchanged
+        apply(P.pt_step[p]);
+        return;
+    }
+    const float step = -b * po[0] / (1 + P.lambda);
+    P.pt_step[p] = step;
+    apply(step);
 }
 
 // image layout 3 (default): the intensity channel only, band-interleaved (band_offset: an 8x4
@@ -2573,8 +2590,9 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
 // setPrecalcValues without a host round trip.  k_frame_step: one block per window, se3.h's
 // statements (the host helpers' own code): calibration and frame steps from x, then
 // FrameFramePrecalc::Set for every pair and the solver's prior vector (takeData's prior /
-// delta_prior, cPrior * cDeltaF).  k_point_step: setIdepth / setIdepthZero(idepth_backup + step),
-// deltaF = 0 (setDeltaF).
+// delta_prior, cPrior * cDeltaF), with k_xad's xAd for the resubstitution computed in the same
+// launch.  The point step -- setIdepth / setIdepthZero(idepth_backup + step), deltaF = 0
+// (setDeltaF) -- is applied by k_resubstitute as it computes the step.
 // ============================================================================================
 struct FrameStepParams {
     WinDev *wins;
@@ -2586,6 +2604,8 @@ struct FrameStepParams {
     const double *x;              // [vec]
     float *precalc;               // [pairs][LDSO_BA_PRECALC_STRIDE]
     double *prior;                // [vec][2]: HL diagonal, bL
+    const double *adH, *adT;      // non-null: also k_xad's xAd for the resubstitution (fused)
+    float *xad;
 };
 __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
     __shared__ double poses[LDSO_BA_MAX_FRAMES][4][12];  // ev, ev^-1, cur, cur^-1: R (9), t (3)
@@ -2593,6 +2613,20 @@ __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
     WinDev &W = P.wins[blockIdx.x];
     const int N = W.N, tid = threadIdx.x;
     const double *xw = P.x + W.vec_base;
+    if (P.xad) {  // k_xad's statements: x is the step's input, so the order does not matter
+#pragma clang fp contract(off)
+        float *o = P.xad + (size_t)blockIdx.x * kXadStride;
+        for (int e = tid; e < N * N * 8; e += blockDim.x) {
+            const int cc = e & 7, ht = e >> 3, h = ht / N, t = ht % N;
+            const double *AH = P.adH + (size_t)(W.pair_base + h + N * t) * 64,
+                         *AT = P.adT + (size_t)(W.pair_base + h + N * t) * 64;
+            float s1 = 0, s2 = 0;
+            for (int k = 0; k < 8; k++) s1 += (float)xw[4 + 8 * h + k] * (float)AH[k * 8 + cc];
+            for (int k = 0; k < 8; k++) s2 += (float)xw[4 + 8 * t + k] * (float)AT[k * 8 + cc];
+            o[(size_t)(N * h + t) * 8 + cc] = s1 + s2;
+        }
+        if (tid < 4) o[(size_t)N * N * 8 + tid] = (float)xw[tid];
+    }
     ldso_ba_frame_state *fs = P.fstate + W.frame_base;
     if (tid < N) {
         ldso_ba_frame_state o;
@@ -2641,6 +2675,11 @@ __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
         }
     }
 }
+// idepth of every resident point (point-data column 2), compacted for one small download
+__global__ __launch_bounds__(256) void k_gather_idepth(const float *__restrict__ pt_data, float *out, int n) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q < n) out[q] = pt_data[(size_t)q * LDSO_BA_POINT_STRIDE + 2];
+}
 // the energy history of ldso_ba_optimize: slot *slot <- the pass's energies, then *slot + 1
 // (a device-side counter, so one captured GN iteration replays unchanged)
 __global__ __launch_bounds__(256) void k_keep_energy(const double *src, double *hist, int *slot, int n2) {
@@ -2648,16 +2687,6 @@ __global__ __launch_bounds__(256) void k_keep_energy(const double *src, double *
     for (int i = threadIdx.x; i < n2; i += 256) hist[(size_t)s * n2 + i] = src[i];
     __syncthreads();
     if (threadIdx.x == 0) *slot = s + 1;
-}
-__global__ __launch_bounds__(256) void k_point_step(float *pt_data, const float *pt_step, int n) {
-#pragma clang fp contract(off)
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    float *d = pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-    const float idepth = d[2] + 1.0f * pt_step[p];
-    d[2] = kScaleIdepth * idepth;  // setIdepth
-    d[3] = kScaleIdepth * idepth;  // setIdepthZero (LDSO's doStepFromBackup)
-    d[5] = idepth - idepth;        // setDeltaF: idepth - idepth_zero
 }
 
 __global__ void k_intensity_image(const float *__restrict__ src, float *dst, int w, int h, int tpr8, int hp,
@@ -2702,11 +2731,14 @@ void launch_linearize(int img_mode, int nb, hipStream_t st, const LinParams &L) 
 // ============================================================================================
 // host side
 // ============================================================================================
+// bumped by every device (re)allocation: a captured graph is valid while it is unchanged
+std::atomic<unsigned long long> g_alloc_gen{1};
 template <typename T>
 struct DevBuf {
     T *p = nullptr;
     size_t n = 0;
     int alloc(size_t count) {
+        g_alloc_gen.fetch_add(1);
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -2719,7 +2751,9 @@ struct DevBuf {
         n = count;  // only a successful allocation counts as capacity
         return 0;
     }
+    int ensure(size_t count) { return n >= count && p ? 0 : alloc(count); }  // keeps the pointer if it fits
     void release() {
+        g_alloc_gen.fetch_add(1);
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -2750,6 +2784,9 @@ struct PendingEv {
 struct ldso_ba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // ldso_ba_optimize's captured GN iterations: [projection][last pass][nullspaces given]
+    hipGraphExec_t opt_graph[8] = {};
+    unsigned long long opt_graph_gen[8] = {};
     int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
@@ -2965,8 +3002,9 @@ int upload_priors(ldso_ba_ctx *c, int win) {
     return 0;
 }
 
-int launch_resubstitute(ldso_ba_ctx *c, int begin, int count, double lambda) {
+int launch_resubstitute(ldso_ba_ctx *c, int begin, int count, double lambda, bool apply_step = false) {
     ResubParams R;
+    R.pt_data = apply_step ? c->d_pt_data.p : nullptr;
     R.xad = c->d_xad.p;
     R.wins = c->d_wins.p;
     R.pt_win = c->d_pt_win.p;
@@ -3154,6 +3192,8 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (hipGraphExec_t &g : c->opt_graph)
+        if (g) (void)hipGraphExecDestroy(g);
     drain_events(c);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->pin_sys) (void)hipHostFree(c->pin_sys);
@@ -4228,10 +4268,11 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     HIP_TRY(hipSetDevice(c->device));
     const int nw = c->n_win;
     int rc;
-    if ((rc = c->d_fstate.alloc(c->n_frames)) || (rc = c->d_calib_val.alloc((size_t)4 * nw)) ||
-        (rc = c->d_calib_zero.alloc((size_t)4 * nw)) || (rc = c->d_cprior.alloc((size_t)4 * nw)) ||
-        (rc = c->d_add_priors.alloc(nw)) || (rc = c->d_ehist.alloc((size_t)2 * nw * (n_its + 1))) ||
-        (rc = c->d_eslot.alloc(1)))
+    // ensure(): the buffers keep their addresses across calls, so cached graphs stay valid
+    if ((rc = c->d_fstate.ensure(c->n_frames)) || (rc = c->d_calib_val.ensure((size_t)4 * nw)) ||
+        (rc = c->d_calib_zero.ensure((size_t)4 * nw)) || (rc = c->d_cprior.ensure((size_t)4 * nw)) ||
+        (rc = c->d_add_priors.ensure(nw)) || (rc = c->d_ehist.ensure((size_t)2 * nw * (n_its + 1))) ||
+        (rc = c->d_eslot.ensure(1)))
         return rc;
     std::vector<double> cp((size_t)4 * nw);
     std::vector<int> ap(nw);
@@ -4263,6 +4304,9 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     F.x = c->d_x.p;
     F.precalc = c->d_precalc.p;
     F.prior = c->d_prior.p;
+    F.adH = c->d_adH.p;
+    F.adT = c->d_adT.p;
+    F.xad = c->d_xad.p;
     HIP_TRY(hipMemsetAsync(c->d_eslot.p, 0, sizeof(int), c->stream));
     auto keep_energy = [&]() -> int {
         k_keep_energy<<<1, 256, 0, c->stream>>>(c->d_win_energy.p, c->d_ehist.p, c->d_eslot.p, 2 * nw);
@@ -4274,13 +4318,11 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     auto gn_iteration = [&](int it) -> int {
         int r;
         if ((r = ldso_ba_solve_device(c, it, 1e-5, nullptr, ns ? 7 : 0, nullptr))) return r;
-        if ((r = ldso_ba_resubstitute_device(c, 1e-5, nullptr))) return r;
+        // k_xad + the frame / calibration step + FrameFramePrecalc in one launch, then the
+        // resubstitution with the point step applied in place
         k_frame_step<<<nw, 256, 0, c->stream>>>(F);
         HIP_TRY(hipGetLastError());
-        if (c->P_tot) {
-            k_point_step<<<(c->P_tot + 255) / 256, 256, 0, c->stream>>>(c->d_pt_data.p, c->d_pt_step.p, c->P_tot);
-            HIP_TRY(hipGetLastError());
-        }
+        if (c->P_tot && (r = launch_resubstitute(c, 0, c->P_tot, 1e-5, true))) return r;
         if ((r = ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0)) || (r = keep_energy())) return r;
         return 0;
     };
@@ -4288,19 +4330,25 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     // linearizeAll + applyRes, then the GN iterations.  Without a communicator or kernel timing,
     // iterations after the first replay a captured HIP graph of one iteration: every launch
     // argument of an iteration is the same except the solve's projection (iteration >= 2) and the
-    // last pass's accumulate flag, so at most three graphs, each captured once per call.
+    // last pass's accumulate flag, so at most three graphs; they are cached in the context and
+    // re-captured only after a device (re)allocation.
     if ((rc = ldso_ba_reset_oob(c, -1)) || (rc = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0)) || (rc = keep_energy()))
         return rc;
     const bool use_graph = !c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH");
-    hipGraphExec_t gx[4] = {nullptr, nullptr, nullptr, nullptr};
-    auto variant = [&](int it) { return (it >= 2 ? 1 : 0) + (it + 1 < n_its ? 0 : 2); };
+    auto variant = [&](int it) { return (it >= 2 ? 1 : 0) + (it + 1 < n_its ? 0 : 2) + (ns ? 4 : 0); };
     for (int it = 0; it < n_its && !rc; it++) {
         const int v = variant(it);
         if (!use_graph || it == 0) {
             rc = gn_iteration(it);
             continue;
         }
-        if (!gx[v]) {
+        hipGraphExec_t &gx = c->opt_graph[v];
+        const unsigned long long gen = g_alloc_gen.load();
+        if (gx && c->opt_graph_gen[v] != gen) {
+            (void)hipGraphExecDestroy(gx);
+            gx = nullptr;
+        }
+        if (!gx) {
             hipGraph_t g = nullptr;
             HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
             const int rcap = gn_iteration(it);
@@ -4310,18 +4358,18 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
                 rc = rcap ? rcap : fail(-2, std::string("graph capture: ") + hipGetErrorString(ecap));
                 break;
             }
-            const hipError_t ei = hipGraphInstantiate(&gx[v], g, nullptr, nullptr, 0);
+            const hipError_t ei = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
             (void)hipGraphDestroy(g);
             if (ei != hipSuccess) {
+                gx = nullptr;
                 rc = fail(-2, std::string("graph instantiate: ") + hipGetErrorString(ei));
                 break;
             }
+            c->opt_graph_gen[v] = gen;
         }
-        const hipError_t el = hipGraphLaunch(gx[v], c->stream);
+        const hipError_t el = hipGraphLaunch(gx, c->stream);
         if (el != hipSuccess) rc = fail(-2, std::string("graph launch: ") + hipGetErrorString(el));
     }
-    for (hipGraphExec_t g : gx)
-        if (g) (void)hipGraphExecDestroy(g);
     if (rc) return rc;
     if (energy_out) {
         std::vector<double> e((size_t)2 * nw * (n_its + 1));
@@ -4341,10 +4389,18 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     if (calib_out)
         HIP_TRY(hipMemcpyAsync(calib_out, c->d_calib_val.p, (size_t)4 * nw * sizeof(double), hipMemcpyDeviceToHost,
                                c->stream));
-    std::vector<float> pd;
-    if (idepth_out && c->P_tot) {
-        pd.resize((size_t)c->P_tot * LDSO_BA_POINT_STRIDE);
-        HIP_TRY(hipMemcpyAsync(pd.data(), c->d_pt_data.p, pd.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    if (idepth_out && c->P_tot) {  // the idepth column only, into the pinned step buffer
+        if (c->pin_step_n < (size_t)c->P_tot) {
+            if (c->pin_step) (void)hipHostFree(c->pin_step);
+            c->pin_step = nullptr;
+            c->pin_step_n = 0;
+            HIP_TRY(hipHostMalloc(&c->pin_step, (size_t)c->P_tot * sizeof(float), hipHostMallocDefault));
+            c->pin_step_n = c->P_tot;
+        }
+        k_gather_idepth<<<(c->P_tot + 255) / 256, 256, 0, c->stream>>>(c->d_pt_data.p, c->d_pt_step.p, c->P_tot);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->pin_step, c->d_pt_step.p, (size_t)c->P_tot * sizeof(float), hipMemcpyDeviceToHost,
+                               c->stream));
     }
     if ((rc = ldso_ba_sync(c))) return rc;
     if (idepth_out) {
@@ -4352,8 +4408,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         for (int w = 0; w < nw; w++) {
             const WinDev &D = c->wd[w];
             const WinHost &H = c->wh[w];
-            for (int q = 0; q < D.P; q++)
-                idepth_out[out_base + H.pt_orig[q]] = pd[(size_t)(D.point_base + q) * LDSO_BA_POINT_STRIDE + 2];
+            for (int q = 0; q < D.P; q++) idepth_out[out_base + H.pt_orig[q]] = c->pin_step[D.point_base + q];
             out_base += H.P_all;
         }
     }

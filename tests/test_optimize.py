@@ -142,9 +142,10 @@ def test_device_optimize_batched_windows(built):
 
 @pytest.mark.gpu
 def test_graph_replay_equals_direct_launches(built, monkeypatch):
-    """ldso_ba_optimize replays captured HIP graphs of one GN iteration after the first; the
-    result must equal direct launches bit for bit (LDSO_BA_NO_GRAPH=1), over enough iterations
-    to use every graph variant (before / after the projection starts, the last pass)."""
+    """ldso_ba_optimize replays captured HIP graphs of one GN iteration after the first (cached in
+    the context across calls); the result must equal direct launches bit for bit
+    (LDSO_BA_NO_GRAPH=1), over enough iterations to use every graph variant (before / after the
+    projection starts, the last pass) and over a second call that reuses them."""
     from ldso_amd import BAContext
 
     cfg = dict(synth.S7, seed=63)
@@ -153,7 +154,8 @@ def test_graph_replay_equals_direct_launches(built, monkeypatch):
         monkeypatch.setenv("LDSO_BA_NO_GRAPH", env)
         w = synth.make_window(**cfg)
         ctx = BAContext(0).load([w])
-        outs.append(ctx.optimize(6, nullspaces=[w.nullspaces()]))
+        # twice on one context: the second call replays the graphs cached by the first
+        outs.append(ctx.optimize(6, nullspaces=[w.nullspaces()]) + ctx.optimize(4, nullspaces=[w.nullspaces()]))
         ctx.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
