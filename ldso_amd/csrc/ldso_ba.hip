@@ -1450,7 +1450,7 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
     }
     const int cnt = T.count();
     double v = 0;
-    constexpr int kBatch = 8;
+    constexpr int kBatch = 24;  // the 42-term calibration sums in two round trips
     for (int k0 = 0; k0 < cnt; k0 += kBatch) {
         double x[kBatch];
 #pragma unroll
