@@ -118,6 +118,18 @@ __global__ void __launch_bounds__(320) gather(const double *buf, double *out, un
     out[tid] = s;
     if (tid == 0) cyc[11] = t1 - t0;
 }
+// the shader clock while one wave spins: s_memtime ticks per s_memrealtime tick (100 MHz)
+__global__ void clock_probe(unsigned long long *cyc, int iters) {
+    const unsigned long long m0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    float x = threadIdx.x;
+    for (int i = 0; i < iters; i++) x = x * 1.0000001f + 1e-7f;
+    const unsigned long long m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        cyc[12] = m1 - m0;
+        cyc[13] = r1 - r0;
+        cyc[14] = (unsigned long long)x;
+    }
+}
 int main() {
     double *out;
     unsigned long long *cyc, h[16];
@@ -139,6 +151,14 @@ int main() {
         unsigned long long c;
         hipMemcpy(&c, cyc + 11, 8, hipMemcpyDeviceToHost);
         printf("gather 2x1830 doubles after a writer kernel: %llu cycles\n", c);
+    }
+    for (int iters : {1000, 100000, 1000000}) {
+        clock_probe<<<1, 64>>>(cyc, iters);
+        hipDeviceSynchronize();
+        unsigned long long c[2];
+        hipMemcpy(c, cyc + 12, 16, hipMemcpyDeviceToHost);
+        printf("clock probe %d iters: %llu memtime ticks over %llu realtime ticks = %.3f GHz\n", iters, c[0], c[1],
+               c[1] ? (double)c[0] / c[1] * 0.1 : 0.0);
     }
     for (int r = 0; r < 3; r++) {
         gather<<<1, 320>>>(big, o2, cyc, 1830);
