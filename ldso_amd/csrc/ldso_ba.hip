@@ -2027,19 +2027,17 @@ __host__ __device__ inline size_t solve_reg_smem_bytes(int n) {
     return solve_reg_base(n) * sizeof(double) +
            ((size_t)kSolveRegDim * kSolveLsLd + kSolveRegDim * kSolveRegDim + kSolveRegDim + 7 * kSolveRegDim + 1) *
                sizeof(double) +
-           2 * kSolveRegDim * sizeof(int) + 4 * kSolveRegDim * sizeof(unsigned long long);
+           2 * kSolveRegDim * sizeof(int);
 }
 struct RegLds {
     double *cb, *Ls, *Dv, *raw;  // cb: [step][64] published columns (16-byte aligned); Dv: d of step
-    unsigned long long *pmax;    // [step][wave] pivot-key maxima, zeroed
     int *pv, *flag;              // pivot row and ready flag of each step
     __device__ RegLds(double *lds, int n) {
         cb = lds + solve_reg_base(n);
         Ls = cb + kSolveRegDim * kSolveRegDim;
         Dv = Ls + kSolveRegDim * kSolveLsLd;
         raw = Dv + kSolveRegDim;
-        pmax = reinterpret_cast<unsigned long long *>(raw + 7 * kSolveRegDim + 1);
-        pv = reinterpret_cast<int *>(pmax + 4 * kSolveRegDim);
+        pv = reinterpret_cast<int *>(raw + 7 * kSolveRegDim + 1);
         flag = pv + kSolveRegDim;
     }
 };
@@ -2064,29 +2062,18 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned x) {
 // pivot of step k: the largest |diag| among the live rows, ties to the smallest host index; a
 // NaN never wins, except at the host's row k itself, which then keeps k (the host's strict '>'
 // scan from k).  The maximum of the order-preserving 64-bit keys: the high words by DPP first,
-// the low words among high-word ties.  (The LDSO_EXP_PIVOT_ATOMIC variant, an LDS atomic max
-// into this wave's zeroed slot of the step, measured slower: 650 vs 520 cycles per pivot.)
-__device__ __forceinline__ int reg_pivot(double dg, unsigned long long act, int pos, int k, int lane,
-                                         unsigned long long *slot) {
+// the low words among high-word ties (an LDS atomic-max variant measured slower).
+__device__ __forceinline__ int reg_pivot(double dg, unsigned long long act, int pos, int k, int lane) {
     const bool live = (act >> lane) & 1;
     const unsigned long long key = !live ? 0ull : (dg != dg && pos == k) ? ~0ull : abs_key(dg);
-    unsigned long long cand;
-#ifndef LDSO_EXP_PIVOT_ATOMIC
-    (void)slot;
     const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
     const unsigned mh = wave_max_u32(hi);
-    cand = __ballot(live && hi == mh);
+    unsigned long long cand = __ballot(live && hi == mh);
     if (cand & (cand - 1)) {
         const bool c = (cand >> lane) & 1;
         const unsigned ml = wave_max_u32(c ? lo : 0u);
         cand = __ballot(c && lo == ml);
     }
-#else
-    __hip_atomic_fetch_max(slot, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    LDSO_COMPILER_FENCE();
-    const unsigned long long mx = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    cand = __ballot(live && key == mx);
-#endif
     int piv = __builtin_ctzll(cand);
     if (cand & (cand - 1)) {  // exact tie: the smallest host index
         int best = __builtin_amdgcn_readlane(pos, piv);
@@ -2133,7 +2120,6 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
     const RegLds R(lds, n);
     LDSO_STAMP(0);
     for (int i = tid; i < kSolveRegDim; i += kSolveRegThreads) R.flag[i] = 0;
-    for (int i = tid; i < 4 * kSolveRegDim; i += kSolveRegThreads) R.pmax[i] = 0;
     solve_assemble<kSolveRegThreads>(P, W, S, tid);  // its barriers also publish the flags
     LDSO_STAMP(1);
     if (wave == 4) __builtin_amdgcn_s_setprio(0);  // the factorisation's chain first
@@ -2210,7 +2196,7 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
     int pos = lane;
     unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);  // rows not yet pivoted
     LDSO_STAMP(2);
-    int piv = reg_pivot(dg, act, pos, 0, lane, R.pmax + wave);
+    int piv = reg_pivot(dg, act, pos, 0, lane);
     double d = readlane_f64(dg, piv);
     double cl = 0.0;
     if ((piv >> 4) == wave) {
@@ -2231,7 +2217,7 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
         int nxt = 0;
         double cn = 0.0, rdn = 0.0;
         if (k + 1 < n) {
-            nxt = reg_pivot(dg, act, pos, k + 1, lane, R.pmax + 4 * (k + 1) + wave);
+            nxt = reg_pivot(dg, act, pos, k + 1, lane);
             LDSO_STAMPW(k, 3);
             const double dn = readlane_f64(dg, nxt);
             if ((nxt >> 4) == wave) {  // look-ahead: the next pivot's column first
