@@ -970,6 +970,8 @@ struct StitchParams {
     double *sys;
     double *stage;  // k_stitch -> k_stitch_sum contribution records (WinDev::stage_base)
     double *win_energy;
+    double *ehist;         // non-null (ldso_ba_optimize): also win_energy into slot *eslot of the history
+    const int *eslot;      // (k_frame_step advances it once per GN iteration)
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
     int pair_base;  // first global pair of this launch
@@ -1103,8 +1105,14 @@ __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &
     }
     __syncthreads();
     if (tid == 0) {
-        P.win_energy[2 * w] = (red[0] + red[2]) + (red[4] + red[6]);
-        P.win_energy[2 * w + 1] = (red[1] + red[3]) + (red[5] + red[7]);
+        const double e = (red[0] + red[2]) + (red[4] + red[6]), nin = (red[1] + red[3]) + (red[5] + red[7]);
+        P.win_energy[2 * w] = e;
+        P.win_energy[2 * w + 1] = nin;
+        if (P.ehist) {  // the optimize() energy history, without a launch of its own
+            double *hs = P.ehist + (size_t)(*P.eslot) * 2 * P.n_win;
+            hs[2 * w] = e;
+            hs[2 * w + 1] = nin;
+        }
     }
 }
 
@@ -2592,6 +2600,7 @@ struct FrameStepParams {
     double *prior;                // [vec][2]: HL diagonal, bL
     const double *adH, *adT;      // non-null: also k_xad's xAd for the resubstitution (fused)
     float *xad;
+    int *eslot;                   // non-null: the energy-history slot the next pass writes, advanced here
 };
 __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
     __shared__ double poses[LDSO_BA_MAX_FRAMES][4][12];  // ev, ev^-1, cur, cur^-1: R (9), t (3)
@@ -2599,6 +2608,7 @@ __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
     WinDev &W = P.wins[blockIdx.x];
     const int N = W.N, tid = threadIdx.x;
     const double *xw = P.x + W.vec_base;
+    if (P.eslot && blockIdx.x == 0 && tid == 0) *P.eslot += 1;
     if (P.xad) {  // k_xad's statements: x is the step's input, so the order does not matter
 #pragma clang fp contract(off)
         float *o = P.xad + (size_t)blockIdx.x * kXadStride;
@@ -2661,18 +2671,16 @@ __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
         }
     }
 }
+// ldso_ba_optimize's energy history with a communicator (the window blocks of k_stitch write it
+// otherwise): slot *slot <- the all-reduced energies
+__global__ __launch_bounds__(256) void k_energy_to_history(const double *src, double *hist, const int *slot, int n2) {
+    const int s = *slot;
+    for (int i = threadIdx.x; i < n2; i += 256) hist[(size_t)s * n2 + i] = src[i];
+}
 // idepth of every resident point (point-data column 2), compacted for one small download
 __global__ __launch_bounds__(256) void k_gather_idepth(const float *__restrict__ pt_data, float *out, int n) {
     const int q = blockIdx.x * 256 + threadIdx.x;
     if (q < n) out[q] = pt_data[(size_t)q * LDSO_BA_POINT_STRIDE + 2];
-}
-// the energy history of ldso_ba_optimize: slot *slot <- the pass's energies, then *slot + 1
-// (a device-side counter, so one captured GN iteration replays unchanged)
-__global__ __launch_bounds__(256) void k_keep_energy(const double *src, double *hist, int *slot, int n2) {
-    const int s = *slot;
-    for (int i = threadIdx.x; i < n2; i += 256) hist[(size_t)s * n2 + i] = src[i];
-    __syncthreads();
-    if (threadIdx.x == 0) *slot = s + 1;
 }
 
 __global__ void k_intensity_image(const float *__restrict__ src, float *dst, int w, int h, int tpr8, int hp,
@@ -2771,6 +2779,7 @@ struct ldso_ba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     // ldso_ba_optimize's captured GN iterations: [projection][last pass][nullspaces given]
+    bool opt_hist = false;  // inside ldso_ba_optimize: passes also write the energy history
     hipGraphExec_t opt_graph[8] = {};
     unsigned long long opt_graph_gen[8] = {};
     int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major
@@ -3820,6 +3829,8 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.sys = c->d_sys.p;
     Sp.stage = c->d_stage.p;
     Sp.win_energy = c->d_win_energy.p;
+    Sp.ehist = c->opt_hist && !c->comm ? c->d_ehist.p : nullptr;  // with RCCL: after the exchange
+    Sp.eslot = c->d_eslot.p;
     Sp.accumulate = accumulate;
     Sp.pair_base = 0;
     Sp.win_base = 0;
@@ -3848,7 +3859,12 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
             k_stitch_sum<<<c->n_sum_blocks, 256, 0, st>>>(c->d_wins.p, c->d_sum_blocks.p, c->d_stage.p, c->d_sys.p);
         });
     if (rc || !c->comm) return rc;
-    return comm_exchange(c, accumulate != 0);
+    rc = comm_exchange(c, accumulate != 0);
+    if (!rc && c->opt_hist) {  // the reduced energies into the optimize() history
+        k_energy_to_history<<<1, 256, 0, st>>>(c->d_win_energy.p, c->d_ehist.p, c->d_eslot.p, 2 * c->n_win);
+        HIP_TRY(hipGetLastError());
+    }
+    return rc;
 }
 
 int ldso_ba_activate_points(ldso_ba_ctx *c, int32_t win, int32_t n, const ldso_ct_immature *pts, int32_t min_obs,
@@ -4293,12 +4309,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     F.adH = c->d_adH.p;
     F.adT = c->d_adT.p;
     F.xad = c->d_xad.p;
+    F.eslot = c->d_eslot.p;
     HIP_TRY(hipMemsetAsync(c->d_eslot.p, 0, sizeof(int), c->stream));
-    auto keep_energy = [&]() -> int {
-        k_keep_energy<<<1, 256, 0, c->stream>>>(c->d_win_energy.p, c->d_ehist.p, c->d_eslot.p, 2 * nw);
-        HIP_TRY(hipGetLastError());
-        return 0;
-    };
     // one GN iteration: solveSystemF, resubstituteF_MT, doStepFromBackup + setPrecalcValues,
     // linearizeAll + applyRes (+ the accumulation the next solve uses)
     auto gn_iteration = [&](int it) -> int {
@@ -4309,8 +4321,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         k_frame_step<<<nw, 256, 0, c->stream>>>(F);
         HIP_TRY(hipGetLastError());
         if (c->P_tot && (r = launch_resubstitute(c, 0, c->P_tot, 1e-5, true))) return r;
-        if ((r = ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0)) || (r = keep_energy())) return r;
-        return 0;
+        return ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0);
     };
     // FullSystem::optimize (FullSystem.cc:853-976) with setting_forceAceptStep: resetOOB, then
     // linearizeAll + applyRes, then the GN iterations.  Without a communicator or kernel timing,
@@ -4318,8 +4329,11 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     // argument of an iteration is the same except the solve's projection (iteration >= 2) and the
     // last pass's accumulate flag, so at most three graphs; they are cached in the context and
     // re-captured only after a device (re)allocation.
-    if ((rc = ldso_ba_reset_oob(c, -1)) || (rc = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0)) || (rc = keep_energy()))
+    c->opt_hist = true;  // every pass of this call writes its energies into the history too
+    if ((rc = ldso_ba_reset_oob(c, -1)) || (rc = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0))) {
+        c->opt_hist = false;
         return rc;
+    }
     const bool use_graph = !c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH");
     auto variant = [&](int it) { return (it >= 2 ? 1 : 0) + (it + 1 < n_its ? 0 : 2) + (ns ? 4 : 0); };
     for (int it = 0; it < n_its && !rc; it++) {
@@ -4356,6 +4370,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         const hipError_t el = hipGraphLaunch(gx, c->stream);
         if (el != hipSuccess) rc = fail(-2, std::string("graph launch: ") + hipGetErrorString(el));
     }
+    c->opt_hist = false;
     if (rc) return rc;
     if (energy_out) {
         std::vector<double> e((size_t)2 * nw * (n_its + 1));

@@ -446,3 +446,24 @@ def test_rccl_world1_exchange_keeps_results(built):
         b.comm_init(uid.tobytes(), 0, 1)
     a.close()
     b.close()
+
+
+def test_rccl_world1_optimize_keeps_results(built):
+    """ldso_ba_optimize on a context with a (world-1) communicator -- direct launches, the
+    exchange after every pass, the energy history written after it -- equals the same call on a
+    context without one (graph replay), bit for bit."""
+    from ldso_amd import _lib as L
+
+    cfg = dict(n_frames=6, n_points=700, seed=52)
+    w = synth.make_window(**cfg)
+    ns = [w.nullspaces()]
+    a = BAContext(0).load([synth.make_window(**cfg)])
+    uid = np.zeros(128, np.uint8)
+    L.check(L.lib().ldso_ba_comm_unique_id(uid.ctypes.data))
+    b = BAContext(0).comm_init(uid.tobytes(), 0, 1).load([synth.make_window(**cfg)], shard_rank=0, shard_count=1)
+    ra = a.optimize(4, nullspaces=ns)
+    rb = b.optimize(4, nullspaces=ns)
+    for x, y in zip(ra, rb):
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+    a.close()
+    b.close()
