@@ -2780,8 +2780,13 @@ struct ldso_ba_ctx {
     hipStream_t stream = nullptr;
     // ldso_ba_optimize's captured GN iterations: [projection][last pass][nullspaces given]
     bool opt_hist = false;  // inside ldso_ba_optimize: passes also write the energy history
-    hipGraphExec_t opt_graph[8] = {};
-    unsigned long long opt_graph_gen[8] = {};
+    // captured launch sequences: ldso_ba_optimize's GN iterations [projection][last pass][ns given]
+    // and ldso_ba_iterate's pass + solve + resubstitution [projection]
+    struct Graph {
+        hipGraphExec_t exec = nullptr;
+        unsigned long long gen = 0, key = 0;
+    };
+    Graph opt_graph[8], it_graph[2];
     int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
@@ -3187,8 +3192,10 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (hipGraphExec_t &g : c->opt_graph)
-        if (g) (void)hipGraphExecDestroy(g);
+    for (auto &g : c->opt_graph)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    for (auto &g : c->it_graph)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
     drain_events(c);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->pin_sys) (void)hipHostFree(c->pin_sys);
@@ -4236,17 +4243,95 @@ int ldso_ba_resubstitute_device(ldso_ba_ctx *c, double lambda, float *point_step
     return 0;
 }
 
+}  // extern "C"
+namespace {
+// Launch a captured sequence: replay g if it was captured under the current allocation
+// generation and key, else capture `body`'s launches on the context stream, instantiate, cache.
+template <typename F>
+int launch_cached_graph(ldso_ba_ctx *c, ldso_ba_ctx::Graph &g, unsigned long long key, F &&body) {
+    const unsigned long long gen = g_alloc_gen.load();
+    if (g.exec && (g.gen != gen || g.key != key)) {
+        (void)hipGraphExecDestroy(g.exec);
+        g.exec = nullptr;
+    }
+    if (!g.exec) {
+        hipGraph_t gr = nullptr;
+        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        const int rcap = body();
+        const hipError_t ecap = hipStreamEndCapture(c->stream, &gr);
+        if (rcap || ecap != hipSuccess) {
+            if (gr) (void)hipGraphDestroy(gr);
+            return rcap ? rcap : fail(-2, std::string("graph capture: ") + hipGetErrorString(ecap));
+        }
+        const hipError_t ei = hipGraphInstantiate(&g.exec, gr, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(gr);
+        if (ei != hipSuccess) {
+            g.exec = nullptr;
+            return fail(-2, std::string("graph instantiate: ") + hipGetErrorString(ei));
+        }
+        g.gen = gen;
+        g.key = key;
+    }
+    const hipError_t el = hipGraphLaunch(g.exec, c->stream);
+    if (el != hipSuccess) return fail(-2, std::string("graph launch: ") + hipGetErrorString(el));
+    return 0;
+}
+}  // namespace
+extern "C" {
+
 int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const double *ns, int32_t n_null, double *x_out,
                     float *point_step_out, double *energy_out) {
-    int rc = ldso_ba_linearize(c, 0, 1);
-    if (rc) return rc;
-    rc = ldso_ba_solve_device(c, iteration, lambda, ns, n_null, nullptr);
+    if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
+    if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc;
+    const bool project = iteration >= 2 && n_null > 0 && (ns || c->ns_resident);
+    if (project && ns) {  // the nullspaces go up before (outside) the captured sequence
+        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
+                               c->stream));
+        c->ns_resident = true;
+    }
+    // pass + solve + resubstitution: one captured graph per (projection, lambda, n_null) without
+    // a communicator or kernel timing; the downloads stay outside it
+    auto body = [&]() -> int {
+        int r;
+        if ((r = ldso_ba_linearize(c, 0, 1))) return r;
+        if ((r = ldso_ba_solve_device(c, project ? 2 : 0, lambda, nullptr, project ? n_null : 0, nullptr))) return r;
+        k_xad<<<c->n_win, 256, 0, c->stream>>>(c->d_wins.p, c->d_x.p, c->d_adH.p, c->d_adT.p, c->d_xad.p);
+        HIP_TRY(hipGetLastError());
+        return c->P_tot > 0 ? launch_resubstitute(c, 0, c->P_tot, lambda) : 0;
+    };
+    if (!c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH")) {
+        unsigned long long lb;
+        std::memcpy(&lb, &lambda, sizeof(lb));
+        rc = launch_cached_graph(c, c->it_graph[project ? 1 : 0], lb ^ ((unsigned long long)n_null << 56), body);
+    } else {
+        rc = body();
+    }
     if (rc) return rc;
     if (x_out)
         HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,
                                c->stream));
-    rc = ldso_ba_resubstitute_device(c, lambda, point_step_out);
-    if (rc) return rc;
+    if (point_step_out) {
+        if (c->pin_step_n < (size_t)c->P_tot) {
+            if (c->pin_step) (void)hipHostFree(c->pin_step);
+            c->pin_step = nullptr;
+            c->pin_step_n = 0;
+            HIP_TRY(hipHostMalloc(&c->pin_step, std::max<size_t>(1, c->P_tot) * sizeof(float), hipHostMallocDefault));
+            c->pin_step_n = c->P_tot;
+        }
+        if (c->P_tot)
+            HIP_TRY(hipMemcpyAsync(c->pin_step, c->d_pt_step.p, c->P_tot * sizeof(float), hipMemcpyDeviceToHost,
+                                   c->stream));
+        if ((rc = ldso_ba_sync(c))) return rc;
+        long long out_base = 0;  // windows back to back, each in its caller point order
+        for (int w = 0; w < c->n_win; w++) {
+            const WinDev &D = c->wd[w];
+            const WinHost &H = c->wh[w];
+            for (int q = 0; q < D.P; q++) point_step_out[out_base + H.pt_orig[q]] = c->pin_step[D.point_base + q];
+            out_base += H.P_all;
+        }
+    }
     if (energy_out) {
         rc = ldso_ba_sync(c);
         if (rc) return rc;
@@ -4337,38 +4422,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     const bool use_graph = !c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH");
     auto variant = [&](int it) { return (it >= 2 ? 1 : 0) + (it + 1 < n_its ? 0 : 2) + (ns ? 4 : 0); };
     for (int it = 0; it < n_its && !rc; it++) {
-        const int v = variant(it);
-        if (!use_graph || it == 0) {
-            rc = gn_iteration(it);
-            continue;
-        }
-        hipGraphExec_t &gx = c->opt_graph[v];
-        const unsigned long long gen = g_alloc_gen.load();
-        if (gx && c->opt_graph_gen[v] != gen) {
-            (void)hipGraphExecDestroy(gx);
-            gx = nullptr;
-        }
-        if (!gx) {
-            hipGraph_t g = nullptr;
-            HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-            const int rcap = gn_iteration(it);
-            const hipError_t ecap = hipStreamEndCapture(c->stream, &g);
-            if (rcap || ecap != hipSuccess) {
-                if (g) (void)hipGraphDestroy(g);
-                rc = rcap ? rcap : fail(-2, std::string("graph capture: ") + hipGetErrorString(ecap));
-                break;
-            }
-            const hipError_t ei = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(g);
-            if (ei != hipSuccess) {
-                gx = nullptr;
-                rc = fail(-2, std::string("graph instantiate: ") + hipGetErrorString(ei));
-                break;
-            }
-            c->opt_graph_gen[v] = gen;
-        }
-        const hipError_t el = hipGraphLaunch(gx, c->stream);
-        if (el != hipSuccess) rc = fail(-2, std::string("graph launch: ") + hipGetErrorString(el));
+        if (!use_graph || it == 0) rc = gn_iteration(it);
+        else rc = launch_cached_graph(c, c->opt_graph[variant(it)], 0, [&] { return gn_iteration(it); });
     }
     c->opt_hist = false;
     if (rc) return rc;
