@@ -846,6 +846,7 @@ struct PointParams {
 };
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
+constexpr int kScBatch = 2;  // residual records per round trip (4 and 8 measured equal, r2)
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int item = P.item_base + blockIdx.x;
     const int4 it = P.items[item];
@@ -870,10 +871,10 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
         float *row = U + tid * KP;
-        for (int k0 = 0; k0 < nres; k0 += 2) {
-            float4 rec[2][4];
+        for (int k0 = 0; k0 < nres; k0 += kScBatch) {
+            float4 rec[kScBatch][4];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < kScBatch; u++) {
                 const int k = min(k0 + u, nres - 1);
                 const int tg = (int)((tgs >> (4 * k)) & 15ull);
                 const float4 *q = rp + (tg < host ? tg : tg - 1) * sstride;
@@ -883,7 +884,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
                 rec[u][3] = q[3];
             }
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < kScBatch; u++) {
                 const int k = k0 + u;
                 if (k >= nres || rec[u][3].z == 0.0f) continue;
                 ngood++;
@@ -938,8 +939,9 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
 
 // ============================================================================================
 // k_stitch: one 256-thread block per frame pair (h,t) of every window, straight from the
-// partial slabs of k_linearize / k_point_sc, accumulating into the packed upper triangles of
-// {HA, bA, Hsc, bsc} with f64 atomics (zeroed before the pass):
+// partial slabs of k_linearize / k_point_sc, writing the pair's contributions to the packed
+// upper triangles of {HA, bA, Hsc, bsc} as one record per (pair, block) that k_stitch_sum adds
+// in a fixed pair order (no atomics: the system is bitwise repeatable):
 //   Top  bucket (h,t): sum the chunk partials, AccumulatorApprox::finish layout, adjoint
 //        sandwiches (AccumulatedTopHessian.cc:213-239), symmetrised as stitchDoubleMT does
 //        (H(a,b) = H(a,b) + H(b,a)^T, H(c,h) = H(h,c)^T; AccumulatedTopHessian.h:91-104)
@@ -949,7 +951,6 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
 //        only it, EnergyFunctional.cc:378) using D_kj = D_jk^T.
 // The diagonal (h == t) blocks have no residuals; block (0,0) of each window instead runs
 // setNewFrameEnergyTH (FullSystem.cc:2078-2109) and the linearizeAll energy sum.
-// Only the f64 summation order of the atomics varies between runs.
 // ============================================================================================
 constexpr int kStThreads = 256;
 constexpr int kStTopLds = 528;  // doubles of k_stitch LDS used by the Top half (521, padded)
