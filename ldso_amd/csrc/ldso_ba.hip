@@ -2106,9 +2106,12 @@ __device__ __forceinline__ void reg_publish(const RegLds &R, int k, int lane, do
 }
 // poll the flag and the column together: a set flag read before the column read means the
 // column read returns the published value; returns the pivot row
+// A bounded wait: after ~2^22 polls (well over 100 ms) it gives up with a NaN column and row 0,
+// so the kernel always drains even if a publication were ever missing (x then reads NaN).
 template <bool kSleep = false>
 __device__ __forceinline__ int reg_wait(const RegLds &R, int k, int lane, double &v) {
     int f;
+    unsigned polls = 0;
     do {
         f = __hip_atomic_load(R.flag + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         LDSO_COMPILER_FENCE();
@@ -2116,6 +2119,10 @@ __device__ __forceinline__ int reg_wait(const RegLds &R, int k, int lane, double
         LDSO_COMPILER_FENCE();
         f = __builtin_amdgcn_readfirstlane(f);
         if (kSleep && f == 0) __builtin_amdgcn_s_sleep(2);
+        if (f == 0 && ++polls > (1u << 22)) {
+            v = __longlong_as_double(0x7ff8000000000000ll);
+            return 0;
+        }
     } while (f == 0);
     return f - 1;
 }
