@@ -8,7 +8,10 @@ first-principles checks are what pin the oracle:
     rebuilt in numpy from the per-residual Jacobians and the adjoints (setAdjointsF);
   * the Schur terms Hsc, bsc (AccumulatedSCHessian.cc) against sum_p h_pd h_pd^T / H_dd;
   * PSD-ness, symmetry, the gauge nullspaces (getNullspaces) of HA - Hsc;
-  * setNewFrameEnergyTH against numpy's partition (nth_element).
+  * setNewFrameEnergyTH against numpy's partition (nth_element);
+  * the photometric residuals, weights, energies and states of linearize (Residuals.cc:48-208)
+    against a float64 numpy restatement written from the reference text;
+  * solveSystemF's LDLT, orthogonalize and resubstituteFPt against numpy.
 """
 import numpy as np
 import pytest
@@ -281,3 +284,103 @@ def test_resubstitute_known_answer(win):
     act = np.array([hdd > 0 for _, hdd, _ in pts])
     assert np.array_equal(step[~act], np.zeros((~act).sum()))
     assert np.linalg.norm(step[act] - exp[act]) <= 1e-5 * np.linalg.norm(exp[act])
+
+
+# pattern 8 of staticPattern (Setting.cc:275); settings from Setting.cc:39-76
+_PATTERN8 = np.array([[0, -2], [-1, -1], [1, -1], [-2, 0], [0, 0], [2, 0], [-1, 1], [0, 2]], np.float64)
+_TH_SUM_COMPONENT, _HUBER_TH = 50.0 * 50.0, 9.0
+
+
+def _photometric_residual(w, p, t):
+    """PointFrameResidual::linearize's photometric part (Residuals.cc:48-208), restated in float64
+    numpy from the reference text alone: the centre projection with the FEJ pose
+    (ResidualProjections.h:57-84), the 8 pattern projections with PRE_KRKiTll / PRE_KtTll
+    (ResidualProjections.h:24-33), bilinear dI (GlobalFuncs.h:90-103), the gradient weight, the
+    Huber weight and the outlier test.  Returns (state, energy_wo, resF[8], JIdx[2,8], JabF[2,8],
+    margin, tol): margin is how far the decisive quantity sits from a branch point (relative), so
+    the caller can skip cases float32 rounding may legitimately flip; tol holds first-order error
+    bounds of a float32 evaluation (energy, resF[8]): a pattern position carries ~1e-4 px of
+    rounding (a few float32 ops at |K u| ~ 1e2), which the image gradient turns into an intensity
+    error of 1e-4 (|dx| + |dy|), plus 1e-4 for I - (a c + b) cancelling two ~1e2 values."""
+    N, W, H = w.n_frames, w.width, w.height
+    h = int(w.point_host[p])
+    pre = w.precalc[h + N * t].astype(np.float64)
+    pd = w.point_data[p].astype(np.float64)
+    fx, fy, cx, cy = w.calib.astype(np.float64)
+    wM3, hM3 = W - 3.0, H - 3.0
+    margins = []
+
+    klip = np.array([(pd[0] - cx) / fx, (pd[1] - cy) / fy, 1.0])
+    ptp = pre[12:21].reshape(3, 3) @ klip + pre[21:24] * pd[3]
+    Ku, Kv = ptp[0] / ptp[2] * fx + cx, ptp[1] / ptp[2] * fy + cy
+    margins += [Ku - 1.1, Kv - 1.1, wM3 - Ku, hM3 - Kv]
+    if not (ptp[2] > 0 and Ku > 1.1 and Kv > 1.1 and Ku < wM3 and Kv < hM3):
+        return 1, -1.0, None, None, None, min(abs(m) for m in margins), None
+
+    KRKi, Kt = pre[0:9].reshape(3, 3), pre[9:12]
+    aff, b0 = pre[24:26], pre[26]
+    dI = w.dI[t].astype(np.float64)
+    e, wJI2 = 0.0, 0.0
+    resF, JIdx, JabF = np.zeros(8), np.zeros((2, 8)), np.zeros((2, 8))
+    tol_e, tol_r = 1e-5, np.zeros(8)
+    for i, (dx, dy) in enumerate(_PATTERN8):
+        q = KRKi @ np.array([pd[0] + dx, pd[1] + dy, 1.0]) + Kt * pd[2]
+        Ku, Kv = q[0] / q[2], q[1] / q[2]
+        margins += [Ku - 1.1, Kv - 1.1, wM3 - Ku, hM3 - Kv]
+        if not (Ku > 1.1 and Kv > 1.1 and Ku < wM3 and Kv < hM3):
+            return 1, -1.0, None, None, None, min(abs(m) for m in margins), None
+        ix, iy = int(Ku), int(Kv)
+        fxr, fyr = Ku - ix, Kv - iy
+        b = ix + iy * W
+        hit = (fxr * fyr * dI[b + 1 + W] + (fyr - fxr * fyr) * dI[b + W] + (fxr - fxr * fyr) * dI[b + 1]
+               + (1 - fxr - fyr + fxr * fyr) * dI[b])
+        color = pd[8 + i]
+        r = hit[0] - (aff[0] * color + aff[1])
+        wg = np.sqrt(_TH_SUM_COMPONENT / (_TH_SUM_COMPONENT + hit[1] ** 2 + hit[2] ** 2))
+        wg = 0.5 * (wg + pd[16 + i])
+        hw = 1.0 if abs(r) < _HUBER_TH else _HUBER_TH / abs(r)
+        margins.append((abs(r) - _HUBER_TH) / _HUBER_TH)
+        e += wg * wg * hw * r * r * (2 - hw)
+        dI_err = 1e-4 * (1 + abs(hit[1]) + abs(hit[2]))
+        tol_e += 4 * wg * wg * abs(r) * dI_err + 1e-5 * wg * wg * hw * r * r
+        hw = (np.sqrt(hw) if hw < 1 else hw) * wg
+        resF[i] = r * hw
+        tol_r[i] = 2 * hw * dI_err + 1e-5 * abs(resF[i])
+        JIdx[:, i] = hit[1:] * hw
+        JabF[:, i] = ((color - b0) * hw, hw)
+        wJI2 += hw * hw * (hit[1] ** 2 + hit[2] ** 2)
+    th = max(float(w.frame_energy_th[h]), float(w.frame_energy_th[t]))
+    margins += [(e - th) / th, (wJI2 - 2) / 2]
+    state = 2 if (e > th or wJI2 < 2) else 0
+    return state, e, resF, JIdx, JabF, min(abs(m) for m in margins), (tol_e, tol_r)
+
+
+def test_photometric_residuals_known_answer(win):
+    """The oracle's linearize (states, NewEnergyWithOutlier, resF, JIdx, JabF) against a float64
+    numpy restatement of Residuals.cc:48-208 on every residual of the window (all three states;
+    the largest error measured is 0.6 of the bound for resF, 0.14 for the energies).
+    Tolerance: float32 arithmetic vs float64 — energies and resF within the first-order float32
+    error bound _photometric_residual derives per residual, JIdx / JabF within 2e-4 of the row's
+    largest entry; cases within 1e-4 of a branch point are skipped."""
+    w, J, res = win["w"], win["J"], win["res"]
+    seen = {0: 0, 1: 0, 2: 0}
+    for k in range(w.n_residuals):
+        p = int(np.searchsorted(w.point_res_begin, k, side="right") - 1)
+        t = int(w.res_target[k])
+        if w.res_state[k] == 1:  # linearize returns at once for a residual already OOB (Residuals.cc:18-22)
+            assert res["new_state"][k] == 1 and res["new_energy_wo"][k] == -1
+            seen[1] += 1
+            continue
+        state, e, resF, JIdx, JabF, margin, tol = _photometric_residual(w, p, t)
+        if margin < 1e-4:
+            continue
+        assert res["new_state"][k] == state, (k, state)
+        seen[state] += 1
+        if state == 1:
+            continue
+        assert abs(res["new_energy_wo"][k] - e) <= tol[0], (k, res["new_energy_wo"][k], e, tol[0])
+        Jk = unpack_J(J[k])
+        assert np.all(np.abs(Jk["resF"] - resF) <= tol[1]), (k, Jk["resF"] - resF, tol[1])
+        np.testing.assert_allclose(Jk["JIdx"], JIdx, rtol=0, atol=2e-4 * max(np.abs(JIdx).max(), 1e-3))
+        np.testing.assert_allclose(Jk["JabF"], JabF, rtol=0, atol=2e-4 * max(np.abs(JabF).max(), 1e-3))
+    assert seen[0] >= 1000 and seen[1] >= 10 and seen[2] >= 10, seen
