@@ -94,28 +94,6 @@ struct WinDev {
     float cdelta[4];         // EnergyFunctional::cDeltaF (marginalisation pass only)
 };
 
-#ifdef LDSO_EXP_STAMPS  // diagnostic builds only: s_memtime stamps of block 0 into LDS (a global
-// store would hold up the next fence), copied out at the end of the kernel
-__device__ unsigned long long g_stamps[64];
-__shared__ unsigned long long g_lds_stamps[64];
-#define LDSO_STAMP(i)                                                                              \
-    do {                                                                                           \
-        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_lds_stamps[i] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#define LDSO_STAMPW(k, i)                                                                          \
-    do {                                                                                           \
-        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && k == 10)                                 \
-            g_lds_stamps[16 + (threadIdx.x >> 6) * 8 + (i)] = __builtin_amdgcn_s_memtime();        \
-    } while (0)
-#define LDSO_STAMP_FLUSH()                                                                         \
-    do {                                                                                           \
-        if (blockIdx.x == 0) g_stamps[threadIdx.x & 63] = g_lds_stamps[threadIdx.x & 63];          \
-    } while (0)
-#else
-#define LDSO_STAMP(i) ((void)0)
-#define LDSO_STAMPW(k, i) ((void)0)
-#define LDSO_STAMP_FLUSH() ((void)0)
-#endif
 // a debugging / A-B switch from the environment: set and not "0"
 inline bool getenv_flag(const char *name) {
     const char *v = std::getenv(name);
@@ -1579,9 +1557,6 @@ __device__ __forceinline__ void solve_assemble(const SolveParams &P, const WinDe
     };
     constexpr int kPer = (int)((kSolveMaxDim * (kSolveMaxDim + 1) / 2 + kThreads - 1) / kThreads);
     static_assert(kSolveMaxDim <= kThreads, "one row per thread for the diagonal terms");
-#ifdef LDSO_EXP_STAMPS
-    if (__builtin_amdgcn_readfirstlane(n) > 0) LDSO_STAMP(14);  // the window descriptor has arrived
-#endif
     // element u of this thread: f = tid + kThreads u in the "folded" order of the packed upper
     // triangle (row p paired with row n-1-p: n/2 rows of n+1 elements, n = 8N+4 is even), decoded
     // without loops; then unconditional loads at clamped positions (a guarded load becomes a
@@ -1604,12 +1579,10 @@ __device__ __forceinline__ void solve_assemble(const SolveParams &P, const WinDe
         ha[u] = HA[q];
         hs[u] = Hs[q];
     }
-    LDSO_STAMP(9);
     const int tr = min(tid, n - 1);
     const long long qd = pk_index(tr, tr, n);
     const double dha = HA[qd], dhs = Hs[qd], dpr = P.prior[2 * (W.vec_base + tr)],
                  bpr = P.prior[2 * (W.vec_base + tr) + 1], ba = bA[tr], bsv = bs[tr];
-    LDSO_STAMP(10);
     double sci = 0, hdiag = 0;
     if (tid < n) {
         hdiag = element(true, dpr, dha, dhs);
@@ -1622,7 +1595,6 @@ __device__ __forceinline__ void solve_assemble(const SolveParams &P, const WinDe
         S.b[tid] = (((bpr + 0.0) + ba) - bsv / (1 + lambda)) * sci;
         S.H[tid * ld + tid] = hdiag * (sci * sci);
     }
-    LDSO_STAMP(11);
 #pragma unroll
     for (int u = 0; u < kPer; u++) {
         const int f = tid + kThreads * u, r = rr[u], c = cc[u];
@@ -1729,7 +1701,6 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
             coef[lane] = 0.0;
         }
         wave_lds_sync();
-        LDSO_STAMP(12);
         if (kk == 7 && S.misc[7] != 0.0) {  // fast path: coef = G^-1 N^T y, one row per lane
             if (lane < 7) {
                 double gr[7], nt[7];
@@ -1825,7 +1796,6 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
             }
         }
         wave_lds_sync();
-        LDSO_STAMP(13);
         for (int i = lane; i < n; i += 64) {
             double t = 0;
 #pragma unroll
@@ -2134,10 +2104,8 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
     const int ld = solve_ld(n);
     const SolveLds S(lds, n);
     const RegLds R(lds, n);
-    LDSO_STAMP(0);
     for (int i = tid; i < kSolveRegDim; i += kSolveRegThreads) R.flag[i] = 0;
     solve_assemble<kSolveRegThreads>(P, W, S, tid);  // its barriers also publish the flags
-    LDSO_STAMP(1);
     if (wave == 4) __builtin_amdgcn_s_setprio(0);  // the factorisation's chain first
     else __builtin_amdgcn_s_setprio(2);
     if (wave == 4) {
@@ -2161,7 +2129,6 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
                 y = fma(-l, yk, y);
             }
         }
-        LDSO_STAMP(5);
         // to the host's order: lane i takes y_i = y of physical row pv[i]; then the diagonal
         if (lane < n) S.col[lane] = y;
         wave_lds_sync();
@@ -2194,10 +2161,7 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
         y = lane < n ? S.b[lane] : 0.0;
         if (lane < n) S.y[lane] = S.sc[lane] * y;  // x = s b, b[perm[i]] = y_i
         wave_lds_sync();
-        LDSO_STAMP(7);
         solve_ortho_apply_store(P, W, S, lane);
-        LDSO_STAMP(8);
-        LDSO_STAMP_FLUSH();
         return;
     }
     typedef double d16 __attribute__((ext_vector_type(16)));
@@ -2211,7 +2175,6 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
     double dg = lane < n ? S.H[lane * ld + lane] : 0.0;
     int pos = lane;
     unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);  // rows not yet pivoted
-    LDSO_STAMP(2);
     int piv = reg_pivot(dg, act, pos, 0, lane);
     double d = readlane_f64(dg, piv);
     double cl = 0.0;
@@ -2221,30 +2184,23 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
     }
     double rd = d != 0 ? 1.0 / d : 0.0;
     for (int k = 0; k < n; k++) {
-        LDSO_STAMPW(k, 0);
         if ((piv >> 4) != wave) (void)reg_wait(R, k, lane, cl);  // column k of the host: A(i, k) after the swap
-        LDSO_STAMPW(k, 1);
         const int kphys = __builtin_ctzll(__ballot(((act >> lane) & 1) && pos == k));
         const int ppos = __builtin_amdgcn_readlane(pos, piv);
         pos = lane == piv ? k : (lane == kphys ? ppos : pos);
         act &= ~(1ull << piv);
         dg = fma(-(cl * cl), rd, dg);
-        LDSO_STAMPW(k, 2);
         int nxt = 0;
         double cn = 0.0, rdn = 0.0;
         if (k + 1 < n) {
             nxt = reg_pivot(dg, act, pos, k + 1, lane);
-            LDSO_STAMPW(k, 3);
             const double dn = readlane_f64(dg, nxt);
             if ((nxt >> 4) == wave) {  // look-ahead: the next pivot's column first
                 cn = fma(-(cl * readlane_f64(cl, nxt)), rd, rv[nxt & 15]);
                 reg_publish(R, k + 1, lane, cn, nxt);
-                LDSO_STAMPW(k, 7);
             }
-            LDSO_STAMPW(k, 4);
             rdn = dn != 0 ? 1.0 / dn : 0.0;
         }
-        LDSO_STAMPW(k, 5);
         // trailing update of this wave's 16 columns, c_q broadcast from the published column
         // (dead columns too: never read again; the look-ahead column gets the same bits again)
         const double2 *cq2 = reinterpret_cast<const double2 *>(R.cb + k * kSolveRegDim + q0);
@@ -2254,12 +2210,9 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
             rv[2 * u] = fma(-(cl * cq.x), rd, rv[2 * u]);
             rv[2 * u + 1] = fma(-(cl * cq.y), rd, rv[2 * u + 1]);
         }
-        LDSO_STAMPW(k, 6);
         piv = nxt;
         cl = cn;
         rd = rdn;
-        if (k == 0) LDSO_STAMP(3);
-        if (k == n / 2) LDSO_STAMP(4);
     }
 }
 
@@ -4164,12 +4117,6 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
     return 0;
 }
 
-#ifdef LDSO_EXP_STAMPS
-extern "C" int ldso_ba_debug_stamps(unsigned long long *out) {
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)));
-    return 0;
-}
-#endif
 // ---- device-side solve / resubstitute ----------------------------------
 int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const double *ns, int32_t n_null,
                          double *x_out) {
