@@ -2739,7 +2739,6 @@ struct PendingEv {
 struct ldso_ba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // ldso_ba_optimize's captured GN iterations: [projection][last pass][nullspaces given]
     bool opt_hist = false;  // inside ldso_ba_optimize: passes also write the energy history
     // captured launch sequences: ldso_ba_optimize's GN iterations [projection][last pass][ns given]
     // and ldso_ba_iterate's pass + solve + resubstitution [projection]
@@ -2813,11 +2812,27 @@ struct ldso_ba_ctx {
     double *pin_sys = nullptr;
     float *pin_xad = nullptr, *pin_step = nullptr;
     size_t pin_sys_n = 0, pin_step_n = 0;
+    // pinned staging for the results of ldso_ba_iterate / ldso_ba_optimize: every download of
+    // one call lands here, behind a single synchronisation
+    char *pin_out = nullptr;
+    size_t pin_out_n = 0;
     std::vector<double> energy_host;
     bool energy_valid = false;
 };
 
 namespace {
+
+// grow-only pinned host staging (the address is kept while it fits)
+int pin_ensure(char *&p, size_t &cap, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 64);
+    if (p && cap >= bytes) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(hipHostMalloc((void **)&p, bytes, hipHostMallocDefault));
+    cap = bytes;
+    return 0;
+}
 
 hipEvent_t get_event(ldso_ba_ctx *c) {
     if (!c->ev_pool.empty()) {
@@ -3162,6 +3177,7 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (c->pin_sys) (void)hipHostFree(c->pin_sys);
     if (c->pin_xad) (void)hipHostFree(c->pin_xad);
     if (c->pin_step) (void)hipHostFree(c->pin_step);
+    if (c->pin_out) (void)hipHostFree(c->pin_out);
     c->d_wins.release();
     c->d_img.release();
     c->d_act_in.release();
@@ -4264,41 +4280,34 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
         rc = body();
     }
     if (rc) return rc;
-    if (x_out)
-        HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,
-                               c->stream));
+    // x, the energies and the point steps into one pinned buffer, one synchronisation
+    const size_t xb = (size_t)c->vec_total * sizeof(double), eb = (size_t)2 * c->n_win * sizeof(double),
+                 sb = (size_t)c->P_tot * sizeof(float);
+    if ((rc = pin_ensure(c->pin_out, c->pin_out_n, xb + eb + sb))) return rc;
+    const double *px = reinterpret_cast<const double *>(c->pin_out), *pe = px + c->vec_total;
+    const float *ps = reinterpret_cast<const float *>(pe + 2 * c->n_win);
+    if (x_out) HIP_TRY(hipMemcpyAsync((void *)px, c->d_x.p, xb, hipMemcpyDeviceToHost, c->stream));
+    if (energy_out) HIP_TRY(hipMemcpyAsync((void *)pe, c->d_win_energy.p, eb, hipMemcpyDeviceToHost, c->stream));
+    if (point_step_out && sb)
+        HIP_TRY(hipMemcpyAsync((void *)ps, c->d_pt_step.p, sb, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = ldso_ba_sync(c))) return rc;
+    if (x_out) std::memcpy(x_out, px, xb);
     if (point_step_out) {
-        if (c->pin_step_n < (size_t)c->P_tot) {
-            if (c->pin_step) (void)hipHostFree(c->pin_step);
-            c->pin_step = nullptr;
-            c->pin_step_n = 0;
-            HIP_TRY(hipHostMalloc(&c->pin_step, std::max<size_t>(1, c->P_tot) * sizeof(float), hipHostMallocDefault));
-            c->pin_step_n = c->P_tot;
-        }
-        if (c->P_tot)
-            HIP_TRY(hipMemcpyAsync(c->pin_step, c->d_pt_step.p, c->P_tot * sizeof(float), hipMemcpyDeviceToHost,
-                                   c->stream));
-        if ((rc = ldso_ba_sync(c))) return rc;
         long long out_base = 0;  // windows back to back, each in its caller point order
         for (int w = 0; w < c->n_win; w++) {
             const WinDev &D = c->wd[w];
             const WinHost &H = c->wh[w];
-            for (int q = 0; q < D.P; q++) point_step_out[out_base + H.pt_orig[q]] = c->pin_step[D.point_base + q];
+            for (int q = 0; q < D.P; q++) point_step_out[out_base + H.pt_orig[q]] = ps[D.point_base + q];
             out_base += H.P_all;
         }
     }
-    if (energy_out) {
-        rc = ldso_ba_sync(c);
-        if (rc) return rc;
-        std::vector<double> e((size_t)2 * c->n_win);
-        HIP_TRY(hipMemcpy(e.data(), c->d_win_energy.p, e.size() * sizeof(double), hipMemcpyDeviceToHost));
+    if (energy_out)
         for (int w = 0; w < c->n_win; w++) {
-            energy_out[3 * w] = e[2 * w];
+            energy_out[3 * w] = pe[2 * w];
             energy_out[3 * w + 1] = 0;
-            energy_out[3 * w + 2] = e[2 * w + 1];
+            energy_out[3 * w + 2] = pe[2 * w + 1];
         }
-    }
-    return ldso_ba_sync(c);
+    return 0;
 }
 
 int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *frames, const double *calib_value,
@@ -4382,10 +4391,28 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     }
     c->opt_hist = false;
     if (rc) return rc;
+    // every result into one pinned buffer (energy history, frame states, calibration, the window
+    // descriptors, the idepth column), one synchronisation
+    const size_t hb = (size_t)2 * nw * (n_its + 1) * sizeof(double),
+                 fb = (size_t)c->n_frames * sizeof(ldso_ba_frame_state), cb = (size_t)4 * nw * sizeof(double),
+                 wb = (size_t)nw * sizeof(WinDev), ib = (size_t)c->P_tot * sizeof(float);
+    auto up16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    const size_t o_f = up16(hb), o_c = o_f + up16(fb), o_w = o_c + up16(cb), o_i = o_w + up16(wb);
+    if ((rc = pin_ensure(c->pin_out, c->pin_out_n, o_i + ib))) return rc;
+    char *po = c->pin_out;
+    if (energy_out) HIP_TRY(hipMemcpyAsync(po, c->d_ehist.p, hb, hipMemcpyDeviceToHost, c->stream));
+    if (frames_out) HIP_TRY(hipMemcpyAsync(po + o_f, c->d_fstate.p, fb, hipMemcpyDeviceToHost, c->stream));
+    if (calib_out) HIP_TRY(hipMemcpyAsync(po + o_c, c->d_calib_val.p, cb, hipMemcpyDeviceToHost, c->stream));
+    // the host mirror of WinDev (calibration, cDeltaF) follows the device
+    HIP_TRY(hipMemcpyAsync(po + o_w, c->d_wins.p, wb, hipMemcpyDeviceToHost, c->stream));
+    if (idepth_out && c->P_tot) {  // the idepth column only
+        k_gather_idepth<<<(c->P_tot + 255) / 256, 256, 0, c->stream>>>(c->d_pt_data.p, c->d_pt_step.p, c->P_tot);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(po + o_i, c->d_pt_step.p, ib, hipMemcpyDeviceToHost, c->stream));
+    }
+    if ((rc = ldso_ba_sync(c))) return rc;
     if (energy_out) {
-        std::vector<double> e((size_t)2 * nw * (n_its + 1));
-        HIP_TRY(hipMemcpyAsync(e.data(), c->d_ehist.p, e.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        if ((rc = ldso_ba_sync(c))) return rc;
+        const double *e = reinterpret_cast<const double *>(po);
         for (int s = 0; s <= n_its; s++)
             for (int w = 0; w < nw; w++) {
                 double *o = energy_out + ((size_t)s * nw + w) * 3;
@@ -4394,37 +4421,19 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
                 o[2] = e[(size_t)2 * (s * nw + w) + 1];
             }
     }
-    if (frames_out)
-        HIP_TRY(hipMemcpyAsync(frames_out, c->d_fstate.p, (size_t)c->n_frames * sizeof(ldso_ba_frame_state),
-                               hipMemcpyDeviceToHost, c->stream));
-    if (calib_out)
-        HIP_TRY(hipMemcpyAsync(calib_out, c->d_calib_val.p, (size_t)4 * nw * sizeof(double), hipMemcpyDeviceToHost,
-                               c->stream));
-    if (idepth_out && c->P_tot) {  // the idepth column only, into the pinned step buffer
-        if (c->pin_step_n < (size_t)c->P_tot) {
-            if (c->pin_step) (void)hipHostFree(c->pin_step);
-            c->pin_step = nullptr;
-            c->pin_step_n = 0;
-            HIP_TRY(hipHostMalloc(&c->pin_step, (size_t)c->P_tot * sizeof(float), hipHostMallocDefault));
-            c->pin_step_n = c->P_tot;
-        }
-        k_gather_idepth<<<(c->P_tot + 255) / 256, 256, 0, c->stream>>>(c->d_pt_data.p, c->d_pt_step.p, c->P_tot);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(c->pin_step, c->d_pt_step.p, (size_t)c->P_tot * sizeof(float), hipMemcpyDeviceToHost,
-                               c->stream));
-    }
-    if ((rc = ldso_ba_sync(c))) return rc;
+    if (frames_out) std::memcpy(frames_out, po + o_f, fb);
+    if (calib_out) std::memcpy(calib_out, po + o_c, cb);
+    std::memcpy(c->wd.data(), po + o_w, wb);
     if (idepth_out) {
+        const float *id = reinterpret_cast<const float *>(po + o_i);
         long long out_base = 0;  // windows back to back, each in its caller point order
         for (int w = 0; w < nw; w++) {
             const WinDev &D = c->wd[w];
             const WinHost &H = c->wh[w];
-            for (int q = 0; q < D.P; q++) idepth_out[out_base + H.pt_orig[q]] = c->pin_step[D.point_base + q];
+            for (int q = 0; q < D.P; q++) idepth_out[out_base + H.pt_orig[q]] = id[D.point_base + q];
             out_base += H.P_all;
         }
     }
-    // the host mirror of WinDev (calibration, cDeltaF) follows the device
-    HIP_TRY(hipMemcpy(c->wd.data(), c->d_wins.p, (size_t)nw * sizeof(WinDev), hipMemcpyDeviceToHost));
     c->sys_host_valid = false;
     c->energy_valid = false;
     return 0;
