@@ -1466,12 +1466,33 @@ constexpr int kSolveThreads = LDSO_SOLVE_THREADS;  // wavefronts share the assem
 __device__ constexpr int kJacobiRounds[7][3][2] = {
     {{1, 6}, {2, 5}, {3, 4}}, {{0, 2}, {3, 6}, {4, 5}}, {{1, 3}, {0, 4}, {5, 6}}, {{2, 4}, {1, 5}, {0, 6}},
     {{3, 5}, {2, 6}, {0, 1}}, {{4, 6}, {0, 3}, {1, 2}}, {{0, 5}, {1, 4}, {2, 3}}};
+constexpr int kXadStride = LDSO_BA_MAX_FRAMES * LDSO_BA_MAX_FRAMES * 8 + 4;  // floats per window
+// xAd[N*h + t] = x_h^T adHostF[h + N t] + x_t^T adTargetF[h + N t] in float (EnergyFunctional.cc:
+// 624-632), then x_c: the statements of the host path of ldso_ba_resubstitute, over threads
+// tid, tid + nthreads, ... of one window
+__device__ __forceinline__ void xad_fill(const WinDev &W, const double *xw, const double *__restrict__ adH,
+                                         const double *__restrict__ adT, float *o, int tid, int nthreads) {
+#pragma clang fp contract(off)
+    const int N = W.N;
+    for (int e = tid; e < N * N * 8; e += nthreads) {
+        const int cc = e & 7, ht = e >> 3, h = ht / N, t = ht % N;
+        const double *AH = adH + (size_t)(W.pair_base + h + N * t) * 64, *AT = adT + (size_t)(W.pair_base + h + N * t) * 64;
+        float s1 = 0, s2 = 0;
+        for (int k = 0; k < 8; k++) s1 += (float)xw[4 + 8 * h + k] * (float)AH[k * 8 + cc];
+        for (int k = 0; k < 8; k++) s2 += (float)xw[4 + 8 * t + k] * (float)AT[k * 8 + cc];
+        o[(size_t)(N * h + t) * 8 + cc] = s1 + s2;
+    }
+    if (tid < 4) o[(size_t)N * N * 8 + tid] = (float)xw[tid];
+}
+
 struct SolveParams {
     const WinDev *__restrict__ wins;
     const double *__restrict__ sys;
     const double *__restrict__ prior;  // [vec][2]: HL diagonal, bL
     const double *__restrict__ ns;     // [win][7][n] nullspaces (iteration >= 2)
     double *x;                         // [vec]
+    const double *adH, *adT;           // k_solve_reg with xad non-null: also the resubstitution's
+    float *xad;                        // xAd from the solution (k_xad fused)
     int iteration, n_null;
 };
 // H's row stride in LDS: odd (in doubles), so a column walk touches 32 distinct bank pairs
@@ -2096,6 +2117,61 @@ __device__ __forceinline__ int reg_wait(const RegLds &R, int k, int lane, double
     } while (f == 0);
     return f - 1;
 }
+// the factorisation waves of k_solve_reg: 16 columns of H in registers per wave
+__device__ __forceinline__ void solve_reg_factor(const RegLds &R, const SolveLds &S, int n, int ld, int wave,
+                                                 int lane) {
+#pragma clang fp contract(off)
+    typedef double d16 __attribute__((ext_vector_type(16)));
+    d16 rv;
+    const int q0 = 16 * wave;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int q = q0 + j, r = lane > q ? lane : q, c = lane > q ? q : lane;
+        rv[j] = q < n && lane < n ? S.H[r * ld + c] : 0.0;
+    }
+    double dg = lane < n ? S.H[lane * ld + lane] : 0.0;
+    int pos = lane;
+    unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);  // rows not yet pivoted
+    int piv = reg_pivot(dg, act, pos, 0, lane);
+    double d = readlane_f64(dg, piv);
+    double cl = 0.0;
+    if ((piv >> 4) == wave) {
+        cl = rv[piv & 15];
+        reg_publish(R, 0, lane, cl, piv);
+    }
+    double rd = d != 0 ? 1.0 / d : 0.0;
+    for (int k = 0; k < n; k++) {
+        if ((piv >> 4) != wave) (void)reg_wait(R, k, lane, cl);  // column k of the host: A(i, k) after the swap
+        const int kphys = __builtin_ctzll(__ballot(((act >> lane) & 1) && pos == k));
+        const int ppos = __builtin_amdgcn_readlane(pos, piv);
+        pos = lane == piv ? k : (lane == kphys ? ppos : pos);
+        act &= ~(1ull << piv);
+        dg = fma(-(cl * cl), rd, dg);
+        int nxt = 0;
+        double cn = 0.0, rdn = 0.0;
+        if (k + 1 < n) {
+            nxt = reg_pivot(dg, act, pos, k + 1, lane);
+            const double dn = readlane_f64(dg, nxt);
+            if ((nxt >> 4) == wave) {  // look-ahead: the next pivot's column first
+                cn = fma(-(cl * readlane_f64(cl, nxt)), rd, rv[nxt & 15]);
+                reg_publish(R, k + 1, lane, cn, nxt);
+            }
+            rdn = dn != 0 ? 1.0 / dn : 0.0;
+        }
+        // trailing update of this wave's 16 columns, c_q broadcast from the published column
+        // (dead columns too: never read again; the look-ahead column gets the same bits again)
+        const double2 *cq2 = reinterpret_cast<const double2 *>(R.cb + k * kSolveRegDim + q0);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const double2 cq = cq2[u];
+            rv[2 * u] = fma(-(cl * cq.x), rd, rv[2 * u]);
+            rv[2 * u + 1] = fma(-(cl * cq.y), rd, rv[2 * u + 1]);
+        }
+        piv = nxt;
+        cl = cn;
+        rd = rdn;
+    }
+}
 __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
@@ -2162,57 +2238,12 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
         if (lane < n) S.y[lane] = S.sc[lane] * y;  // x = s b, b[perm[i]] = y_i
         wave_lds_sync();
         solve_ortho_apply_store(P, W, S, lane);
-        return;
+    } else {
+        solve_reg_factor(R, S, n, ld, wave, lane);
     }
-    typedef double d16 __attribute__((ext_vector_type(16)));
-    d16 rv;
-    const int q0 = 16 * wave;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const int q = q0 + j, r = lane > q ? lane : q, c = lane > q ? q : lane;
-        rv[j] = q < n && lane < n ? S.H[r * ld + c] : 0.0;
-    }
-    double dg = lane < n ? S.H[lane * ld + lane] : 0.0;
-    int pos = lane;
-    unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);  // rows not yet pivoted
-    int piv = reg_pivot(dg, act, pos, 0, lane);
-    double d = readlane_f64(dg, piv);
-    double cl = 0.0;
-    if ((piv >> 4) == wave) {
-        cl = rv[piv & 15];
-        reg_publish(R, 0, lane, cl, piv);
-    }
-    double rd = d != 0 ? 1.0 / d : 0.0;
-    for (int k = 0; k < n; k++) {
-        if ((piv >> 4) != wave) (void)reg_wait(R, k, lane, cl);  // column k of the host: A(i, k) after the swap
-        const int kphys = __builtin_ctzll(__ballot(((act >> lane) & 1) && pos == k));
-        const int ppos = __builtin_amdgcn_readlane(pos, piv);
-        pos = lane == piv ? k : (lane == kphys ? ppos : pos);
-        act &= ~(1ull << piv);
-        dg = fma(-(cl * cl), rd, dg);
-        int nxt = 0;
-        double cn = 0.0, rdn = 0.0;
-        if (k + 1 < n) {
-            nxt = reg_pivot(dg, act, pos, k + 1, lane);
-            const double dn = readlane_f64(dg, nxt);
-            if ((nxt >> 4) == wave) {  // look-ahead: the next pivot's column first
-                cn = fma(-(cl * readlane_f64(cl, nxt)), rd, rv[nxt & 15]);
-                reg_publish(R, k + 1, lane, cn, nxt);
-            }
-            rdn = dn != 0 ? 1.0 / dn : 0.0;
-        }
-        // trailing update of this wave's 16 columns, c_q broadcast from the published column
-        // (dead columns too: never read again; the look-ahead column gets the same bits again)
-        const double2 *cq2 = reinterpret_cast<const double2 *>(R.cb + k * kSolveRegDim + q0);
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const double2 cq = cq2[u];
-            rv[2 * u] = fma(-(cl * cq.x), rd, rv[2 * u]);
-            rv[2 * u + 1] = fma(-(cl * cq.y), rd, rv[2 * u + 1]);
-        }
-        piv = nxt;
-        cl = cn;
-        rd = rdn;
+    if (P.xad) {  // x is in S.y: the resubstitution's xAd by all five waves
+        __syncthreads();
+        xad_fill(W, S.y, P.adH, P.adT, P.xad + (size_t)blockIdx.x * kXadStride, tid, kSolveRegThreads);
     }
 }
 
@@ -2247,7 +2278,6 @@ __global__ __launch_bounds__(kStThreads) void k_frame_th(const WinDev *__restric
         (int)n_cand, keys, kThMaxLds, frame_th + W.frame_base + W.N - 1);
 }
 
-constexpr int kXadStride = LDSO_BA_MAX_FRAMES * LDSO_BA_MAX_FRAMES * 8 + 4;  // floats per window
 struct ResubParams {
     const float *__restrict__ xad;   // [win][kXadStride]: xAd[h*N + t][8], then x_c[4]
     const WinDev *__restrict__ wins;
@@ -2263,25 +2293,12 @@ struct ResubParams {
     float lambda;
 };
 
-// xAd[N*h + t] = x_h^T adHostF[h + N t] + x_t^T adTargetF[h + N t] in float (EnergyFunctional.cc:
-// 624-632), from the device solution; same statements as the host path of ldso_ba_resubstitute
+// xAd from the device solution (windows solved by k_solve, or x set otherwise)
 __global__ __launch_bounds__(256) void k_xad(const WinDev *__restrict__ wins, const double *__restrict__ x,
                                              const double *__restrict__ adH, const double *__restrict__ adT,
                                              float *xad) {
-#pragma clang fp contract(off)
     const WinDev &W = wins[blockIdx.x];
-    const int N = W.N;
-    const double *xw = x + W.vec_base;
-    float *o = xad + (size_t)blockIdx.x * kXadStride;
-    for (int e = threadIdx.x; e < N * N * 8; e += blockDim.x) {
-        const int cc = e & 7, ht = e >> 3, h = ht / N, t = ht % N;
-        const double *AH = adH + (size_t)(W.pair_base + h + N * t) * 64, *AT = adT + (size_t)(W.pair_base + h + N * t) * 64;
-        float s1 = 0, s2 = 0;
-        for (int k = 0; k < 8; k++) s1 += (float)xw[4 + 8 * h + k] * (float)AH[k * 8 + cc];
-        for (int k = 0; k < 8; k++) s2 += (float)xw[4 + 8 * t + k] * (float)AT[k * 8 + cc];
-        o[(size_t)(N * h + t) * 8 + cc] = s1 + s2;
-    }
-    if (threadIdx.x < 4) o[(size_t)N * N * 8 + threadIdx.x] = (float)xw[threadIdx.x];
+    xad_fill(W, x + W.vec_base, adH, adT, xad + (size_t)blockIdx.x * kXadStride, threadIdx.x, blockDim.x);
 }
 
 // ============================================================================================
@@ -2486,9 +2503,8 @@ __global__ __launch_bounds__(256) void k_activate(ActParams P) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
+__device__ __forceinline__ void resubstitute_one(const ResubParams &P, int k) {
 #pragma clang fp contract(off)
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P.count) return;
     const int p = P.begin + k;
     const float *po = P.pt_out + (size_t)p * 12;
@@ -2534,6 +2550,9 @@ __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
     P.pt_step[p] = step;
     apply(step);
 }
+__global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
+    resubstitute_one(P, blockIdx.x * blockDim.x + threadIdx.x);
+}
 
 // image layout 3 (default): the intensity channel only, band-interleaved (band_offset: an 8x4
 // pixel tile per 128-byte line, 1/4 of the float4 texel bytes); k_linearize recomputes the
@@ -2559,31 +2578,16 @@ struct FrameStepParams {
     const double *x;              // [vec]
     float *precalc;               // [pairs][LDSO_BA_PRECALC_STRIDE]
     double *prior;                // [vec][2]: HL diagonal, bL
-    const double *adH, *adT;      // non-null: also k_xad's xAd for the resubstitution (fused)
-    float *xad;
     int *eslot;                   // non-null: the energy-history slot the next pass writes, advanced here
 };
-__global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
+// one window's step: a whole 256-thread block (blk = the window)
+__device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int blk) {
     __shared__ double poses[LDSO_BA_MAX_FRAMES][4][12];  // ev, ev^-1, cur, cur^-1: R (9), t (3)
     __shared__ float calib[4];
-    WinDev &W = P.wins[blockIdx.x];
+    WinDev &W = P.wins[blk];
     const int N = W.N, tid = threadIdx.x;
     const double *xw = P.x + W.vec_base;
-    if (P.eslot && blockIdx.x == 0 && tid == 0) *P.eslot += 1;
-    if (P.xad) {  // k_xad's statements: x is the step's input, so the order does not matter
-#pragma clang fp contract(off)
-        float *o = P.xad + (size_t)blockIdx.x * kXadStride;
-        for (int e = tid; e < N * N * 8; e += blockDim.x) {
-            const int cc = e & 7, ht = e >> 3, h = ht / N, t = ht % N;
-            const double *AH = P.adH + (size_t)(W.pair_base + h + N * t) * 64,
-                         *AT = P.adT + (size_t)(W.pair_base + h + N * t) * 64;
-            float s1 = 0, s2 = 0;
-            for (int k = 0; k < 8; k++) s1 += (float)xw[4 + 8 * h + k] * (float)AH[k * 8 + cc];
-            for (int k = 0; k < 8; k++) s2 += (float)xw[4 + 8 * t + k] * (float)AT[k * 8 + cc];
-            o[(size_t)(N * h + t) * 8 + cc] = s1 + s2;
-        }
-        if (tid < 4) o[(size_t)N * N * 8 + tid] = (float)xw[tid];
-    }
+    if (P.eslot && blk == 0 && tid == 0) *P.eslot += 1;
     ldso_ba_frame_state *fs = P.fstate + W.frame_base;
     if (tid < N) {
         ldso_ba_frame_state o;
@@ -2596,17 +2600,17 @@ __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
             for (int k = 0; k < 3; k++) poses[tid][q][9 + k] = ps[q].t[k];
         }
     } else if (tid == 64) {
-        double *v = P.calib_val + 4 * blockIdx.x;
+        double *v = P.calib_val + 4 * blk;
         float cd[4];
-        calib_step(v, xw, P.calib_zero + 4 * blockIdx.x, calib, cd);
+        calib_step(v, xw, P.calib_zero + 4 * blk, calib, cd);
         for (int k = 0; k < 4; k++) {
             W.calib[k] = calib[k];
             W.cdelta[k] = cd[k];
         }
-        const bool add = P.add_priors[blockIdx.x] != 0;
+        const bool add = P.add_priors[blk] != 0;
         for (int k = 0; k < 4; k++) {  // calibration prior: cPrior, cPrior * cDeltaF (upload_priors)
-            P.prior[2 * (W.vec_base + k)] = add ? P.cprior[4 * blockIdx.x + k] : 0.0;
-            P.prior[2 * (W.vec_base + k) + 1] = add ? P.cprior[4 * blockIdx.x + k] * (double)cd[k] : 0.0;
+            P.prior[2 * (W.vec_base + k)] = add ? P.cprior[4 * blk + k] : 0.0;
+            P.prior[2 * (W.vec_base + k) + 1] = add ? P.cprior[4 * blk + k] * (double)cd[k] : 0.0;
         }
     }
     __syncthreads();
@@ -2624,13 +2628,20 @@ __global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) {
     if (tid < N) {
         double pr[8], dp[8];
         frame_take_data_one(fs[tid], pr, nullptr, dp);
-        const bool add = P.add_priors[blockIdx.x] != 0;
+        const bool add = P.add_priors[blk] != 0;
         for (int i = 0; i < 8; i++) {
             const int q = W.vec_base + 4 + 8 * tid + i;
             P.prior[2 * q] = add ? pr[i] : 0.0;
             P.prior[2 * q + 1] = add ? pr[i] * dp[i] : 0.0;
         }
     }
+}
+__global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) { frame_step_block(P, blockIdx.x); }
+// ldso_ba_optimize: the frame / calibration step (blocks [0, n_win)) and the resubstitution with
+// the point step (the rest) in one launch; both read only x and xAd, which the solve wrote
+__global__ __launch_bounds__(256) void k_step_resub(FrameStepParams F, ResubParams R, int n_win) {
+    if ((int)blockIdx.x < n_win) frame_step_block(F, blockIdx.x);
+    else resubstitute_one(R, ((int)blockIdx.x - n_win) * 256 + threadIdx.x);
 }
 // ldso_ba_optimize's energy history with a communicator (the window blocks of k_stitch write it
 // otherwise): slot *slot <- the all-reduced energies
@@ -2978,7 +2989,7 @@ int upload_priors(ldso_ba_ctx *c, int win) {
     return 0;
 }
 
-int launch_resubstitute(ldso_ba_ctx *c, int begin, int count, double lambda, bool apply_step = false) {
+ResubParams resub_params(ldso_ba_ctx *c, int begin, int count, double lambda, bool apply_step) {
     ResubParams R;
     R.pt_data = apply_step ? c->d_pt_data.p : nullptr;
     R.xad = c->d_xad.p;
@@ -2993,6 +3004,10 @@ int launch_resubstitute(ldso_ba_ctx *c, int begin, int count, double lambda, boo
     R.begin = begin;
     R.count = count;
     R.lambda = (float)lambda;
+    return R;
+}
+int launch_resubstitute(ldso_ba_ctx *c, int begin, int count, double lambda, bool apply_step = false) {
+    const ResubParams R = resub_params(c, begin, count, lambda, apply_step);
     return timed_launch(c, 3, c->stream, [&] { k_resubstitute<<<(count + 255) / 256, 256, 0, c->stream>>>(R); });
 }
 // k_stitch dynamic LDS: max of the Top phase, the SC phase of the largest window, and the
@@ -4154,6 +4169,9 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
     S.prior = c->d_prior.p;
     S.ns = c->d_ns.p;
     S.x = c->d_x.p;
+    S.adH = c->d_adH.p;
+    S.adT = c->d_adT.p;
+    S.xad = c->d_xad.p;  // the resubstitution's xAd comes with x (k_xad after the LDS kernel)
     S.iteration = iteration;
     S.n_null = (iteration >= 2 && (ns || c->ns_resident)) ? n_null : 0;
     static std::once_flag once;
@@ -4173,6 +4191,10 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
             k_solve<<<c->n_win, kSolveThreads, smem, c->stream>>>(S);
     });
     if (rc) return rc;
+    if (!reg) {
+        k_xad<<<c->n_win, 256, 0, c->stream>>>(c->d_wins.p, c->d_x.p, c->d_adH.p, c->d_adT.p, c->d_xad.p);
+        HIP_TRY(hipGetLastError());
+    }
     if (x_out) {
         HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,
                                c->stream));
@@ -4268,8 +4290,6 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
         int r;
         if ((r = ldso_ba_linearize(c, 0, 1))) return r;
         if ((r = ldso_ba_solve_device(c, project ? 2 : 0, lambda, nullptr, project ? n_null : 0, nullptr))) return r;
-        k_xad<<<c->n_win, 256, 0, c->stream>>>(c->d_wins.p, c->d_x.p, c->d_adH.p, c->d_adT.p, c->d_xad.p);
-        HIP_TRY(hipGetLastError());
         return c->P_tot > 0 ? launch_resubstitute(c, 0, c->P_tot, lambda) : 0;
     };
     if (!c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH")) {
@@ -4355,9 +4375,6 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     F.x = c->d_x.p;
     F.precalc = c->d_precalc.p;
     F.prior = c->d_prior.p;
-    F.adH = c->d_adH.p;
-    F.adT = c->d_adT.p;
-    F.xad = c->d_xad.p;
     F.eslot = c->d_eslot.p;
     HIP_TRY(hipMemsetAsync(c->d_eslot.p, 0, sizeof(int), c->stream));
     // one GN iteration: solveSystemF, resubstituteF_MT, doStepFromBackup + setPrecalcValues,
@@ -4365,11 +4382,13 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     auto gn_iteration = [&](int it) -> int {
         int r;
         if ((r = ldso_ba_solve_device(c, it, 1e-5, nullptr, ns ? 7 : 0, nullptr))) return r;
-        // k_xad + the frame / calibration step + FrameFramePrecalc in one launch, then the
-        // resubstitution with the point step applied in place
-        k_frame_step<<<nw, 256, 0, c->stream>>>(F);
-        HIP_TRY(hipGetLastError());
-        if (c->P_tot && (r = launch_resubstitute(c, 0, c->P_tot, 1e-5, true))) return r;
+        // the frame / calibration step + FrameFramePrecalc and the resubstitution with the point
+        // step applied in place, in one launch (the solve wrote x and xAd)
+        const ResubParams R = resub_params(c, 0, c->P_tot, 1e-5, true);
+        if ((r = timed_launch(c, 3, c->stream, [&] {
+                 k_step_resub<<<nw + (c->P_tot + 255) / 256, 256, 0, c->stream>>>(F, R, nw);
+             })))
+            return r;
         return ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0);
     };
     // FullSystem::optimize (FullSystem.cc:853-976) with setting_forceAceptStep: resetOOB, then
