@@ -52,9 +52,9 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kTopVals = 96;    // 55 + 30 + 6 AccumulatorApprox entries, padded to 96
 constexpr int kMaxRes = LDSO_BA_MAX_FRAMES - 1;
-constexpr int kNumKernels = 7;
-const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch", "k_resubstitute", "k_frame_th",
-                                         "k_solve",     "k_activate"};
+constexpr int kNumKernels = 8;
+const char *kKernelNames[kNumKernels] = {"k_linearize", "k_point_sc", "k_stitch",   "k_resubstitute",
+                                         "k_frame_th",  "k_solve",    "k_activate", "k_stitch_sum"};
 
 thread_local std::string g_err;
 int fail(int code, const std::string &msg) {
@@ -3854,7 +3854,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     }
     rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + c->n_pairs, kStThreads, st_smem, st>>>(Sp); });
     if (!rc && accumulate)
-        rc = timed_launch(c, 2, st, [&] {
+        rc = timed_launch(c, 7, st, [&] {
             k_stitch_sum<<<c->n_sum_blocks, 256, 0, st>>>(c->d_wins.p, c->d_sum_blocks.p, c->d_stage.p, c->d_sys.p);
         });
     if (rc || !c->comm) return rc;
