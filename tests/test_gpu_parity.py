@@ -467,3 +467,43 @@ def test_rccl_world1_optimize_keeps_results(built):
         np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
     a.close()
     b.close()
+
+
+def test_degenerate_windows_in_a_batch(built):
+    """A window without points and a window whose residuals all start OOB, batched with a normal
+    one: every window matches the oracle over two passes (the degenerate ones give zero energies
+    and prior-only systems), and ldso_ba_optimize over the batch stays finite and leaves the
+    normal window's result equal to optimising it alone."""
+    cfgs = [dict(n_frames=4, n_points=200, seed=91), dict(n_frames=3, n_points=0, seed=92),
+            dict(n_frames=5, n_points=60, seed=93)]
+
+    def make(i):
+        w = synth.make_window(**cfgs[i])
+        if i == 2:
+            w.res_state[:] = 1  # ResState::OOB: linearize returns the stored energy at once
+        return w
+
+    c = BAContext(0)
+    c.load([make(i) for i in range(3)])
+    ows = [oracle.OracleWindow(make(i), threads=0) for i in range(3)]
+    for _ in range(2):
+        c.linearize()
+        for i, ow in enumerate(ows):
+            e_cpu, s_cpu = ow.iteration()
+            compare_pass(c, ow, i, e_cpu, s_cpu)
+    assert c.energy(1)[2] == 0 and c.energy(2)[2] == 0
+    c.close()
+
+    ws = [make(i) for i in range(3)]
+    both = BAContext(0).load(ws)
+    e3, fr3, co3, id3 = both.optimize(3, nullspaces=[w.nullspaces() for w in ws])
+    assert np.all(np.isfinite(e3)) and np.all(np.isfinite(fr3["state"])) and np.all(np.isfinite(co3))
+    assert len(id3[1]) == 0 and np.all(np.isfinite(id3[2]))
+    w0 = make(0)
+    one = BAContext(0).load([w0])
+    e1, fr1, _, id1 = one.optimize(3, nullspaces=[w0.nullspaces()])
+    np.testing.assert_allclose(e3[:, 0, 0], e1[:, 0, 0], rtol=1e-9)
+    np.testing.assert_allclose(fr3["state"][:w0.n_frames], fr1["state"], rtol=1e-9, atol=1e-15)
+    np.testing.assert_allclose(id3[0], id1[0], rtol=1e-6)
+    one.close()
+    both.close()
