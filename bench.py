@@ -12,9 +12,13 @@ roofline: dominant kernel k_linearize, algorithmic bytes per residual (SURVEY.md
 value  = residuals that gather in the pass (R_active: not OOB going in, OOB being sticky within
           optimize()) of all ranks per step / max-over-ranks step time.
 cpu_baseline: the oracle restatement (oracle/cpu_baseline.py) compiled -O3 -march=native on the
-          box, on one S7 window, median pass over >= 10 s: (ii) one pinned worker per physical
-          core of socket 0 (the "single-socket" figure of SURVEY §8d) and (i) 6 threads as the
-          reference's IndexThreadReduce.
+          box: the headline's own workload (the same 64 S7 windows, one single-threaded window pass
+          per worker process pinned one per physical core of socket 0), the like-for-like figure
+          behind speedup_vs_cpu; beside it one S7 window with (ii) one pinned worker per physical
+          core of socket 0 (SURVEY §8d's "single-socket" figure, compared with the GPU's
+          single-window rate) and (i) 6 threads as the reference's IndexThreadReduce.
+cpp_face: the C++ host face (include/ldso_amd/energy_functional.h) timed as FullSystem drives it
+          (ldso_amd/lib/ldso_face_bench, one S7 window) beside the C ABI's ldso_ba_optimize.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--windows B] [--mode replicas|shard]
 """
@@ -49,6 +53,21 @@ def load_pmc(workload):
     except (OSError, ValueError):
         pass
     return None
+
+
+def cpp_face_leg():
+    """ldso_amd/lib/ldso_face_bench in a child process (its own HIP context): EnergyFunctional::
+    optimize(6) on one S7 window, host clock, beside ldso_ba_optimize(6) on the same window."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "ldso_amd", "lib", "ldso_face_bench")
+    try:
+        p = subprocess.run([exe], cwd=ROOT, capture_output=True, text=True, timeout=300)
+        d = json.loads(p.stdout.strip().splitlines()[-1])
+    except (OSError, subprocess.SubprocessError, ValueError, IndexError) as e:
+        return {"error": str(e)}
+    d["ms_per_gn_iteration"] = d["optimize"]["ms_per_gn_iteration"]
+    return d
 
 
 def cpu_baseline(seconds=10.0):
@@ -449,7 +468,9 @@ def main():
             c1.iterate(2, 1e-5, [ns])
         ms_solve_dev = 1e3 * (time.perf_counter() - t1) / reps
         # GN iteration = pass + solve + resubstitute with x and the point steps on the host
-        single = {"ms_per_pass": sw_ms, "point_residuals_per_s": sw.n_residuals / (sw_ms / 1e3),
+        sw_active = int((c1.residuals(0)["state"] != 1).sum())  # R_active, as the headline counts
+        single = {"ms_per_pass": sw_ms, "residuals": sw.n_residuals, "residuals_active": sw_active,
+                  "point_residuals_per_s": sw_active / (sw_ms / 1e3),
                   "ms_per_gn_iteration_host_solve": ms_solve, "ms_per_gn_iteration_device_solve": ms_solve_dev}
         # FullSystem::optimize(setting_maxOptIterations = 6) entirely on the device (ldso_ba_optimize:
         # resetOOB + linearizeAll, then 6 x {solve, resubstitute, doStepFromBackup + setPrecalcValues,
@@ -467,11 +488,13 @@ def main():
         tracker["trace_new_coarse"] = trace_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
         tracker["activate_points"] = activation_leg(local_rank, with_cpu=(world == 1 and not args.no_cpu))
 
-    cpu = cpu6 = None
+    face = cpp_face_leg() if rank == 0 else None
+
+    cpu = cpu1 = cpu6 = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baseline(args.cpu_seconds)
         if cb:
-            cpu, cpu6 = cb["socket_pinned"], cb["six_threads"]
+            cpu, cpu1, cpu6 = cb.get("batched"), cb["socket_pinned"], cb["six_threads"]
 
     if rank == 0:
         out = {
@@ -514,11 +537,19 @@ def main():
             "single_window": single,
             "s11": s11,
             "tracker": tracker,
+            "cpp_face": face,
             "cpu_baseline": cpu,
+            "cpu_baseline_single_window": cpu1,
             "cpu_baseline_six_threads": cpu6,
         }
-        if cpu is not None:
+        if face and single and "optimize" in face:
+            face["vs_c_abi_single_window_optimize"] = (face["ms_per_gn_iteration"] /
+                                                       single["optimize"]["ms_per_iteration"])
+        if cpu is not None:  # like for like: the same 64-window workload on both sides
             out["speedup_vs_cpu"] = value / cpu["value"]
+            out["speedup_vs_cpu_workload"] = f"{B} x S7 windows: GPU step vs {cpu['workers']} pinned CPU workers"
+        if cpu1 is not None and single is not None:  # one window on each side
+            out["speedup_single_window_vs_cpu"] = single["point_residuals_per_s"] / cpu1["value"]
         if cpu6 is not None:
             out["speedup_vs_cpu_six_threads"] = value / cpu6["value"]
         print(json.dumps(out))

@@ -97,9 +97,20 @@ enum class PointStatus { ACTIVE = 0, OUTLIER, OUT, MARGINALIZED };
 
 struct CalibHessian {
     int wG0 = 0, hG0 = 0;                             // level-0 image size (GlobalCalib wG[0], hG[0])
+    double value[4] = {0, 0, 0, 0};                   // CalibHessian::value (value_scaled = SCALE_F/C * value)
+    double value_zero[4] = {0, 0, 0, 0};              // CalibHessian::value_zero
     float value_scaledf[4] = {0, 0, 0, 0};            // fxl, fyl, cxl, cyl
     double value_minus_value_zero[4] = {0, 0, 0, 0};  // cDeltaF source (setDeltaF)
     double step[4] = {0, 0, 0, 0};                    // resubstituteF_MT: -x.head<CPARS>()
+    // CalibHessian::setValue (CalibHessian.h): value, value_scaledf and value_minus_value_zero
+    void setValue(const double v[4]) {
+        const double sc[4] = {50.0, 50.0, 50.0, 50.0};  // SCALE_F, SCALE_F, SCALE_C, SCALE_C (Settings.h:28-35)
+        for (int i = 0; i < 4; i++) {
+            value[i] = v[i];
+            value_scaledf[i] = (float)(sc[i] * v[i]);
+            value_minus_value_zero[i] = value[i] - value_zero[i];
+        }
+    }
 };
 
 struct FrameHessian {
@@ -152,26 +163,17 @@ struct PointFrameResidual {
         resetOOB();
     }
 
-    // Residuals.cc:15-217.  The device linearises residuals a window at a time: this runs the
-    // linearizeAll pass of the EnergyFunctional the residual was inserted into (applyRes
-    // included, as every reference call site does next) and returns this residual's energy.
+    // Residuals.cc:15-217: this residual's own linearisation.  The device relinearises the
+    // EnergyFunctional's whole window in ONE pass (ldso_ba_linearize_residuals) the first time a
+    // residual asks after the window changed, and every later call until the next change reads
+    // its entry: FullSystem::flagPointsForRemoval's per-residual loop (FullSystem.cc:1390-1398)
+    // costs one device pass, not one per residual.  Sets state_NewState, state_NewEnergy,
+    // state_NewEnergyWithOutlier, centerProjectedTo and the Jacobian applyRes(true) takes; like the
+    // reference it changes neither state_state nor the frame thresholds.
     double linearize(shared_ptr<CalibHessian> &HCalib);
-    // Residuals.h:63-68
-    void resetOOB() {
-        state_NewEnergy = state_energy = 0;
-        state_NewState = OUTLIER;
-        setState(IN);
-    }
-    // Residuals.h:70-88 (the device pass has already taken the Jacobians: JpJdF below)
-    void applyRes(bool copyJacobians) {
-        if (copyJacobians) {
-            if (state_state == OOB) return;
-            isActiveAndIsGoodNEW = state_NewState == IN;
-        }
-        state_state = state_NewState;
-        state_energy = state_NewEnergy;
-    }
-    void setState(ResState s) { state_state = s; }
+    void resetOOB();                       // Residuals.h:63-68
+    void applyRes(bool copyJacobians);     // Residuals.h:70-88 (takeData: JpJdF = J_JpJdF)
+    void setState(ResState s);
     bool isActive() const { return isActiveAndIsGoodNEW; }
     // Residuals.cc:219-245: marks the residual linearised; its res_toZeroF is formed on the
     // device by marginalizePointsF (ldso_ba_marginalize_points), the only consumer.
@@ -190,9 +192,13 @@ struct PointFrameResidual {
     float relBS = 0;                  // linearizeAll_Reductor's maxRelBaseline term (fix pass)
     int hostIDX = 0, targetIDX = 0;
     float JpJdF[8] = {0};
+    // takeData's JpJdF of this residual's last linearisation: what the reference derives from
+    // its RawResidualJacobian J (Residuals.h:120-129); applyRes(true) copies it into JpJdF
+    float J_JpJdF[8] = {0};
     bool isLinearized = false;
     bool isActiveAndIsGoodNEW = false;
-    weak_ptr<EnergyFunctional> ef;    // set by EnergyFunctional::insertResidual
+    EnergyFunctional *ef = nullptr;   // set by EnergyFunctional::insertResidual, cleared on removal
+    int mirrorIdx = -1;               // position in the EnergyFunctional's device mirror
 };
 
 class EnergyFunctional : public std::enable_shared_from_this<EnergyFunctional> {
@@ -238,6 +244,33 @@ public:
     // accumulation of the stitched system for the following solveSystemF.  Returns (E, 0, #IN).
     Vec3 linearizeAll(bool fixLinearization);
 
+    // FullSystem::optimize's Gauss-Newton loop (FullSystem.cc:853-970) with setting_forceAceptStep
+    // on the device (ldso_ba_optimize): resetOOB, linearizeAll, then n_its x {solveSystemF (the
+    // pose / scale nullspaces of getNullspaces from iteration 2), resubstituteF_MT,
+    // doStepFromBackup + setPrecalcValues, linearizeAll}, with no host round trip.  Afterwards the
+    // frames' states, HCalib's value and the points' idepth / idepth_zero hold the stepped values
+    // and setDeltaF has run, as after the reference loop.  The residual fields (state_*, JpJdF,
+    // centerProjectedTo) and the points' HdiF / bdSumF / idepth_hessian are written back lazily:
+    // by the linearizeAll(true) FullSystem::optimize runs next, by syncResiduals(), or before any
+    // PointFrameResidual method call.  Runs exactly n_its iterations (the canbreak exit is the
+    // caller's).  energies (optional): (E, 0, #IN) of the first pass and of every iteration's.
+    // Returns the last one.
+    Vec3 optimize(int n_its, shared_ptr<CalibHessian> HCalib, std::vector<Vec3> *energies = nullptr);
+    // the residual and point fields of the device's last pass, if the host copies are stale
+    void syncResiduals();
+    // device linearisation passes run so far (linearizeAll, the per-residual relinearisation,
+    // every pass of optimize): one per call site
+    long devicePasses() const { return passes_; }
+
+    // called by PointFrameResidual: make the host copy current before a residual method reads
+    // it (device newer -> download), record a host-side edit (uploaded before the next pass),
+    // and serve linearize() from the window's relinearisation pass
+    void residualTouched() {
+        if (resSync_ == ResSync::DeviceNewer) syncResiduals();
+    }
+    void residualEdited() { resSync_ = ResSync::HostNewer; }
+    double linearizeResidual(PointFrameResidual &r);
+
     std::vector<shared_ptr<FrameHessian>> frames;
     int nPoints = 0, nFrames = 0, nResiduals = 0;
     MatXX HM = MatXX::Zero(CPARS, CPARS);  // marginalisation prior H
@@ -262,7 +295,11 @@ public:
     ldso_ba_ctx *context() { return ctx_; }
 
 private:
+    enum class ResSync { Synced, HostNewer, DeviceNewer };
     bool upload();
+    bool uploadFrameTerms();
+    bool runRelinearization();
+    bool readBack(bool points_and_th);
     void fail(const char *what);
     void packFrames(std::vector<ldso_ba_frame_state> &fs) const;
     ldso_ba_ctx *ctx_ = nullptr;
@@ -281,8 +318,20 @@ private:
     std::vector<int8_t> resState_;
     std::vector<uint8_t> resFlags_;
     std::vector<PointFrameResidual *> resPtr_;
-    std::vector<PointHessian *> ptPtr_;
+    std::vector<PointHessian *> ptPtr_, resPoint_;
+    std::vector<float> pointVals_;  // [P][4] uploaded (idepth_scaled, idepth_zero_scaled, priorF, deltaF)
+    std::vector<ldso_ba_frame_state> fsUp_;  // frame states / calibration / thresholds last uploaded
+    float calibUp_[4] = {0, 0, 0, 0};
+    std::vector<float> thUp_;
     int width_ = 0, height_ = 0;
+    ResSync resSync_ = ResSync::Synced;
+    long passes_ = 0;
+    // the per-residual relinearisation (linearizeResidual): valid while epoch_ is unchanged and
+    // the residual's point still has the snapshot's coordinates and inverse depths
+    uint64_t epoch_ = 1, cacheEpoch_ = 0;
+    std::vector<int8_t> cNewState_;
+    std::vector<uint8_t> cCenterOk_;
+    std::vector<float> cNewEnergy_, cEwo_, cCenter_, cJp_, cSnap_;
 };
 
 }  // namespace ldso_amd

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define LDSO_BA_ABI_VERSION 2
+#define LDSO_BA_ABI_VERSION 3
 
 #define LDSO_BA_PATTERN_NUM 8      /* patternNum, Settings.h:225 (staticPattern[8])     */
 #define LDSO_BA_CPARS 4            /* CPARS, NumTypes.h:25                              */
@@ -210,16 +210,45 @@ int ldso_ba_comm_unique_id(uint8_t *id_out);
 int ldso_ba_comm_init(ldso_ba_ctx *ctx, const uint8_t *id, int32_t rank, int32_t world);
 
 /* (Re)build the device mirror of n_windows windows (EnergyFunctional::insertFrame /
- * insertResidual / dropResidual / makeIDX all end here).  shard_count > 1 keeps only the
- * points with (p % shard_count) == shard_rank after host-frame ordering, for multi-GPU
- * sharding (priors are then added by rank 0 only).  Every window must share width/height. */
+ * insertResidual / dropResidual / makeIDX all end here).  shard_count > 1 keeps only run
+ * shard_rank of the host-frame partition (ldso_ba_shard_points: the points in host-frame order
+ * cut into shard_count contiguous runs of equal residual counts), for multi-GPU sharding.  The
+ * priors (HL, bL) are not part of the reduced packed system, so every shard keeps them and every
+ * rank's (redundant) solve sees them.  Every window must share width/height. */
 int ldso_ba_load(ldso_ba_ctx *ctx, int32_t n_windows, const ldso_ba_window *windows,
                  int32_t shard_rank, int32_t shard_count);
 
 /* Refresh per-iteration state of window `win` after doStepFromBackup / setPrecalcValues:
- * precalc, adjoints, priors, cDeltaF, frame_energy_th and point_data (idepth, deltaF).
+ * precalc, adjoints, priors, cDeltaF, frame_energy_th and point_data (all 24 floats per point;
+ * w->point_data == NULL leaves the points as they are, see ldso_ba_update_points).
  * Structure (points, residual lists) must be unchanged. */
 int ldso_ba_update(ldso_ba_ctx *ctx, int32_t win, const ldso_ba_window *w);
+
+/* The per-step point values only (PointHessian::setIdepth / setIdepthZero, priorF, deltaF after
+ * doStepFromBackup / setDeltaF; EnergyFunctional.cc:523-549): vals [P][4] in the caller's point
+ * order = (idepth_scaled, idepth_zero_scaled, priorF, deltaF).  16 B per point instead of the 96-B
+ * record of ldso_ba_update. */
+int ldso_ba_update_points(ldso_ba_ctx *ctx, int32_t win, const float *vals);
+
+/* Residual states edited on the host (PointFrameResidual::resetOOB / applyRes / setState,
+ * Residuals.h:63-88) into the device mirror, caller order [R]: state_state, state_energy,
+ * state_NewEnergy, flags (LDSO_BA_FLAG_*). */
+int ldso_ba_update_residuals(ldso_ba_ctx *ctx, int32_t win, const int8_t *state, const float *state_energy,
+                             const float *new_energy, const uint8_t *flags);
+
+/* PointFrameResidual::linearize (Residuals.cc:15-217) of every residual of window win as it returns
+ * right after the residual's resetOOB() -- FullSystem::flagPointsForRemoval's per-residual
+ * relinearisation (FullSystem.cc:1390-1398) -- in one device pass, without applyRes,
+ * setNewFrameEnergyTH or accumulation: the context's residual states, records and system are left
+ * as they were.  Outputs in caller order (any may be NULL): new_state [R] (state_NewState),
+ * new_energy [R] (state_NewEnergy = the returned energy unless new_state is OOB), new_energy_wo [R]
+ * (state_NewEnergyWithOutlier, -1 when OOB), center [R][3] and center_ok [R] (centerProjectedTo;
+ * 0: the centre projection failed and the reference leaves centerProjectedTo unchanged), jpjdf
+ * [R][8] (the JpJdF applyRes(true)'s takeData forms from this linearisation, where new_state is
+ * IN; 0 elsewhere).  A residual whose state is OOB returns state_energy in the reference without
+ * any computation; the caller keeps that branch. */
+int ldso_ba_linearize_residuals(ldso_ba_ctx *ctx, int32_t win, int8_t *new_state, float *new_energy,
+                                float *new_energy_wo, float *center, uint8_t *center_ok, float *jpjdf);
 
 /* PointFrameResidual::resetOOB for every residual of window win (win < 0: all windows). */
 int ldso_ba_reset_oob(ldso_ba_ctx *ctx, int32_t win);
@@ -324,10 +353,12 @@ int ldso_ba_export_newest(ldso_ba_ctx *ctx, float *dev_buf, int64_t stride);
 int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *ctx, const float *dev_buf, int32_t n_ranks, int64_t stride);
 
 /* Device-side solve and resubstitution, every loaded window at once:
- *   solve_device         EnergyFunctional::solveSystemF on the GPU, one wavefront per window,
- *                        statement for statement ldso_ba_solve (bit-identical x); windows of up to
- *                        11 keyframes.  ns: every window's [n_null][8N+4] nullspaces back to back
- *                        (used at iteration >= 2), x_out: every window's x back to back (or NULL:
+ *   solve_device         EnergyFunctional::solveSystemF on the GPU, one workgroup per window
+ *                        (k_solve_reg: 5 wavefronts, windows of up to 7 keyframes; k_solve: 4
+ *                        wavefronts, up to 11), statement for statement ldso_ba_solve (bit-identical
+ *                        x).  ns: every window's [7][8N+4] nullspaces back to back; the projection
+ *                        (iteration >= 2) uses the nullspaces of THIS call and is skipped when ns is
+ *                        NULL, as in the host solver.  x_out: every window's x back to back (or NULL:
  *                        x stays on the device for resubstitute_device).
  *   resubstitute_device  resubstituteF_MT from the device x; point_step_out (or NULL): every
  *                        window's points back to back, each in its caller order.

@@ -96,6 +96,9 @@ ABI = [
     ("ldso_ba_load", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(LdsoBaWindow), C.c_int32, C.c_int32]),
     ("ldso_ba_update", C.c_int, [C.c_void_p, C.c_int32, C.POINTER(LdsoBaWindow)]),
     ("ldso_ba_reset_oob", C.c_int, [C.c_void_p, C.c_int32]),
+    ("ldso_ba_update_points", C.c_int, [C.c_void_p, C.c_int32, f32p]),
+    ("ldso_ba_update_residuals", C.c_int, [C.c_void_p, C.c_int32, i8p, f32p, f32p, u8p]),
+    ("ldso_ba_linearize_residuals", C.c_int, [C.c_void_p, C.c_int32, i8p, f32p, f32p, f32p, u8p, f32p]),
     ("ldso_ba_linearize", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_sync", C.c_int, [C.c_void_p]),
     ("ldso_ba_get_energy", C.c_int, [C.c_void_p, C.c_int32, f64p]),

@@ -98,7 +98,10 @@ bool read_residuals(ldso_ba_ctx *ctx, const std::vector<PointFrameResidual *> &r
         r.state_NewEnergyWithOutlier = ewo[k];
         std::memcpy(r.centerProjectedTo, &ctr[3 * k], 3 * sizeof(float));
         r.isActiveAndIsGoodNEW = (fl[k] & LDSO_BA_FLAG_ACTIVE) != 0;
-        if (r.isActiveAndIsGoodNEW) std::memcpy(r.JpJdF, &jp[8 * k], 8 * sizeof(float));
+        if (r.isActiveAndIsGoodNEW) {
+            std::memcpy(r.JpJdF, &jp[8 * k], 8 * sizeof(float));
+            std::memcpy(r.J_JpJdF, &jp[8 * k], 8 * sizeof(float));
+        }
         r.relBS = rb[k];
     }
     return true;
@@ -112,12 +115,54 @@ void FrameHessian::takeData() {
     ldso_ba_frame_take_data(1, &S, prior, delta, delta_prior);
 }
 
+// Residuals.cc:15-217 (see the header): the OOB early return here, the rest from the window's
+// relinearisation pass
 double PointFrameResidual::linearize(shared_ptr<CalibHessian> &HCalib) {
     (void)HCalib;  // the window's calibration is its EnergyFunctional's (insertFrame / setAdjointsF)
-    shared_ptr<EnergyFunctional> e = ef.lock();
-    if (!e) return state_energy;
-    e->linearizeAll(false);
-    return state_NewEnergy;
+    if (!ef) return state_energy;
+    ef->residualTouched();
+    state_NewEnergyWithOutlier = -1;
+    if (state_state == OOB) {
+        state_NewState = OOB;
+        return state_energy;
+    }
+    return ef->linearizeResidual(*this);
+}
+
+// Residuals.h:63-68
+void PointFrameResidual::resetOOB() {
+    if (ef) ef->residualTouched();
+    const bool same = state_NewEnergy == 0 && state_energy == 0 && state_NewState == OUTLIER && state_state == IN;
+    state_NewEnergy = state_energy = 0;
+    state_NewState = OUTLIER;
+    state_state = IN;
+    if (ef && !same) ef->residualEdited();
+}
+
+// Residuals.h:70-88; takeData (Residuals.h:120-129) is the JpJdF of the last linearisation
+void PointFrameResidual::applyRes(bool copyJacobians) {
+    if (ef) ef->residualTouched();
+    const ResState s0 = state_state;
+    const double e0 = state_energy;
+    const bool a0 = isActiveAndIsGoodNEW;
+    if (copyJacobians) {
+        if (state_state == OOB) return;
+        if (state_NewState == IN) {
+            isActiveAndIsGoodNEW = true;
+            std::memcpy(JpJdF, J_JpJdF, sizeof(JpJdF));
+        } else {
+            isActiveAndIsGoodNEW = false;
+        }
+    }
+    state_state = state_NewState;
+    state_energy = state_NewEnergy;
+    if (ef && (s0 != state_state || e0 != state_energy || a0 != isActiveAndIsGoodNEW)) ef->residualEdited();
+}
+
+void PointFrameResidual::setState(ResState s) {
+    if (ef) ef->residualTouched();
+    if (ef && s != state_state) ef->residualEdited();
+    state_state = s;
 }
 
 void PointFrameResidual::fixLinearizationF(shared_ptr<EnergyFunctional> e) {
@@ -133,6 +178,9 @@ EnergyFunctional::EnergyFunctional(int device) : device_(device) {
 }
 
 EnergyFunctional::~EnergyFunctional() {
+    for (const shared_ptr<PointHessian> &p : registry_)
+        for (const shared_ptr<PointFrameResidual> &r : p->residuals)
+            if (r->ef == this) r->ef = nullptr;
     if (margCtx_) ldso_ba_destroy(margCtx_);
     if (ctx_) ldso_ba_destroy(ctx_);
 }
@@ -146,14 +194,18 @@ void EnergyFunctional::packFrames(std::vector<ldso_ba_frame_state> &fs) const {
 
 // EnergyFunctional.cc:45-49 (the caller has pushed r into its point's residuals)
 void EnergyFunctional::insertResidual(shared_ptr<PointFrameResidual> r) {
-    r->ef = weak_from_this();
+    residualTouched();  // before any structural change: the mirror's residuals may not outlive it
+    r->ef = this;
+    r->mirrorIdx = -1;
     connectivityMap[conn_key(*r)][0]++;
     nResiduals++;
     dirty_ = true;
+    epoch_++;
 }
 
 // EnergyFunctional.cc:51-98 (the non-VI part): HM, bM grow by the frame's 8 zero rows/columns
 void EnergyFunctional::insertFrame(shared_ptr<FrameHessian> fh, shared_ptr<CalibHessian> Hcalib) {
+    residualTouched();
     fh->takeData();
     frames.push_back(fh);
     fh->idx = (int)frames.size();
@@ -177,19 +229,23 @@ void EnergyFunctional::insertFrame(shared_ptr<FrameHessian> fh, shared_ptr<Calib
         if (fh2 != fh) connectivityMap[((uint64_t)fh2->frameID << 32) + (uint64_t)fh->frameID] = {0, 0};
     }
     dirty_ = true;
+    epoch_++;
 }
 
 void EnergyFunctional::insertPoint(shared_ptr<PointHessian> ph) {
+    residualTouched();
     ph->status = PointStatus::ACTIVE;
     ph->alreadyRemoved = false;
     registry_.push_back(ph);
     allPoints.push_back(ph);
     nPoints++;
     dirty_ = true;
+    epoch_++;
 }
 
 // EnergyFunctional.cc:100-107
 void EnergyFunctional::dropResidual(shared_ptr<PointFrameResidual> r) {
+    residualTouched();
     shared_ptr<PointHessian> p = r->point.lock();
     if (p) {
         auto &v = p->residuals;
@@ -198,12 +254,16 @@ void EnergyFunctional::dropResidual(shared_ptr<PointFrameResidual> r) {
     }
     connectivityMap[conn_key(*r)][0]--;
     nResiduals--;
+    if (r->ef == this) r->ef = nullptr;
+    r->mirrorIdx = -1;
     dirty_ = true;
+    epoch_++;
 }
 
 // EnergyFunctional.cc:109-191: the dense reorder / prior / Schur step on the host
 // (ldso_ba_marginalize_frame), then the frame leaves the window
 void EnergyFunctional::marginalizeFrame(shared_ptr<FrameHessian> fh) {
+    residualTouched();
     const int no = 8 * nFrames + CPARS, nn = no - 8;
     MatXX Ho(nn, nn);
     VecX bo(nn);
@@ -222,22 +282,29 @@ void EnergyFunctional::marginalizeFrame(shared_ptr<FrameHessian> fh) {
     nFrames--;
     makeIDX();
     dirty_ = true;
+    epoch_++;
 }
 
 // EnergyFunctional.cc:193-203
 void EnergyFunctional::removePoint(shared_ptr<PointHessian> ph) {
+    residualTouched();
     for (const shared_ptr<PointFrameResidual> &r : ph->residuals) {
         connectivityMap[conn_key(*r)][0]--;
         nResiduals--;
+        if (r->ef == this) r->ef = nullptr;
+        r->mirrorIdx = -1;
     }
     ph->residuals.clear();
     if (!ph->alreadyRemoved) nPoints--;
     ph->alreadyRemoved = true;
     dirty_ = true;
+    epoch_++;
 }
 
 // EnergyFunctional.cc:205-262 with FullSystem.cc:1384-1404 (see the header)
 void EnergyFunctional::marginalizePointsF() {
+    epoch_++;
+    residualTouched();
     allPointsToMarg.clear();
     for (const shared_ptr<PointHessian> &p : registry_)
         if (p->status == PointStatus::MARGINALIZED && !p->alreadyRemoved) allPointsToMarg.push_back(p);
@@ -279,6 +346,7 @@ void EnergyFunctional::marginalizePointsF() {
         fail("ldso_ba_get_residuals (marginalisation)");
         return;
     }
+    passes_++;
     int nres = 0;
     for (PointFrameResidual *r : pk.res) {
         if (r->isActive()) {
@@ -299,6 +367,7 @@ void EnergyFunctional::marginalizePointsF() {
 
 // EnergyFunctional.cc:264-278
 void EnergyFunctional::dropPointsF() {
+    residualTouched();
     for (const shared_ptr<PointHessian> &p : registry_)
         if ((p->status == PointStatus::OUTLIER || p->status == PointStatus::OUT) && !p->alreadyRemoved) removePoint(p);
     makeIDX();
@@ -307,6 +376,8 @@ void EnergyFunctional::dropPointsF() {
 // EnergyFunctional.cc:500-521: frame indices; the active, not removed points in host-frame order
 // (the reference walks its frames' features; registry_ is that list)
 void EnergyFunctional::makeIDX() {
+    residualTouched();
+    epoch_++;
     for (size_t i = 0; i < frames.size(); i++) frames[i]->idx = (int)i;
     std::vector<shared_ptr<PointHessian>> keep, live;
     for (const shared_ptr<PointHessian> &p : registry_) {
@@ -332,6 +403,7 @@ void EnergyFunctional::makeIDX() {
 // EnergyFunctional.cc:551-609 (ldso_ba_set_adjoints)
 void EnergyFunctional::setAdjointsF(shared_ptr<CalibHessian> Hcalib) {
     (void)Hcalib;
+    epoch_++;
     std::vector<ldso_ba_frame_state> fs;
     packFrames(fs);
     adHost.assign((size_t)nFrames * nFrames * 64, 0.0);
@@ -342,6 +414,7 @@ void EnergyFunctional::setAdjointsF(shared_ptr<CalibHessian> Hcalib) {
 
 // EnergyFunctional.cc:523-549: frames' delta / delta_prior, adHTdeltaF, cDeltaF, points' deltaF
 void EnergyFunctional::setDeltaF(shared_ptr<CalibHessian> HCalib) {
+    epoch_++;
     for (int k = 0; k < 4; k++) cDeltaF[k] = (float)HCalib->value_minus_value_zero[k];
     std::vector<double> delta((size_t)8 * nFrames);
     for (int f = 0; f < nFrames; f++) {
@@ -383,15 +456,17 @@ double EnergyFunctional::calcLEnergyF_MT() {
     return e;
 }
 
-bool EnergyFunctional::upload() {
-    if (!ctx_) return false;
+// Frame-level terms (setPrecalcValues, setAdjointsF, takeData) from the current frame states,
+// uploaded only when a frame state, the calibration or a threshold changed since the last upload
+bool EnergyFunctional::uploadFrameTerms() {
     const int N = nFrames;
-    if (N < 2) {
-        err_ = "need at least two frames";
-        return false;
-    }
-    // frame-level terms from the current states (setPrecalcValues, setAdjointsF, takeData)
     packFrames(fs_);
+    frameTH_.resize(N);
+    for (int f = 0; f < N; f++) frameTH_[f] = frames[f]->frameEnergyTH;
+    const bool same = fsUp_.size() == fs_.size() && thUp_ == frameTH_ &&
+                      std::memcmp(fsUp_.data(), fs_.data(), fs_.size() * sizeof(ldso_ba_frame_state)) == 0 &&
+                      std::memcmp(calibUp_, calib_.value_scaledf, sizeof(calibUp_)) == 0;
+    if (same && !dirty_) return true;
     precalc_.assign((size_t)N * N * LDSO_BA_PRECALC_STRIDE, 0.f);
     adH_.assign((size_t)N * N * 64, 0.0);
     adT_.assign((size_t)N * N * 64, 0.0);
@@ -405,8 +480,86 @@ bool EnergyFunctional::upload() {
         fail("frame terms");
         return false;
     }
-    frameTH_.resize(N);
-    for (int f = 0; f < N; f++) frameTH_[f] = frames[f]->frameEnergyTH;
+    if (!dirty_) {  // structure unchanged: the frame terms alone (ldso_ba_update without point data)
+        ldso_ba_window w;
+        std::memset(&w, 0, sizeof(w));
+        w.n_frames = N;
+        w.n_points = (int32_t)ptPtr_.size();
+        w.n_residuals = (int32_t)resPtr_.size();
+        w.width = width_;
+        w.height = height_;
+        std::memcpy(w.calib, calib_.value_scaledf, sizeof(w.calib));
+        w.frame_energy_th = frameTH_.data();
+        w.precalc = precalc_.data();
+        w.ad_host = adH_.data();
+        w.ad_target = adT_.data();
+        w.c_prior = cPrior_.data();
+        w.c_delta = cDeltaF;
+        w.frame_prior = fPrior_.data();
+        w.frame_delta_prior = fDeltaPrior_.data();
+        if (ldso_ba_update(ctx_, 0, &w)) {
+            fail("ldso_ba_update");
+            return false;
+        }
+    }
+    fsUp_ = fs_;
+    thUp_ = frameTH_;
+    std::memcpy(calibUp_, calib_.value_scaledf, sizeof(calibUp_));
+    return true;
+}
+
+// The persistent SoA mirror of the window (ldso_ba_window).  A structural change (insert / drop /
+// remove / makeIDX / marginalisation) rebuilds and reloads it; otherwise only what changed goes
+// up: the frame terms, the points' four per-step values (ldso_ba_update_points, 16 B a point,
+// read through the mirror's raw pointers) and residual states edited on the host.
+bool EnergyFunctional::upload() {
+    if (!ctx_) return false;
+    const int N = nFrames;
+    if (N < 2) {
+        err_ = "need at least two frames";
+        return false;
+    }
+    if (!dirty_) {
+        if (!uploadFrameTerms()) return false;
+        const size_t P = ptPtr_.size();
+        std::vector<float> pv(4 * P);
+        for (size_t q = 0; q < P; q++) {
+            const PointHessian &p = *ptPtr_[q];
+            pv[4 * q] = p.idepth_scaled;
+            pv[4 * q + 1] = p.idepth_zero_scaled;
+            pv[4 * q + 2] = p.priorF;
+            pv[4 * q + 3] = p.deltaF;
+        }
+        if (P && std::memcmp(pv.data(), pointVals_.data(), pv.size() * sizeof(float)) != 0) {
+            if (ldso_ba_update_points(ctx_, 0, pv.data())) {
+                fail("ldso_ba_update_points");
+                return false;
+            }
+            pointVals_.swap(pv);
+        }
+        if (resSync_ == ResSync::HostNewer) {
+            const size_t R = resPtr_.size();
+            std::vector<int8_t> st(R);
+            std::vector<float> se(R), ne(R);
+            std::vector<uint8_t> fl(R);
+            for (size_t k = 0; k < R; k++) {
+                const PointFrameResidual &r = *resPtr_[k];
+                st[k] = (int8_t)r.state_state;
+                se[k] = (float)r.state_energy;
+                ne[k] = (float)r.state_NewEnergy;
+                fl[k] = (uint8_t)((r.isActiveAndIsGoodNEW ? LDSO_BA_FLAG_ACTIVE : 0u) | (r.isNew ? LDSO_BA_FLAG_NEW : 0u));
+            }
+            if (ldso_ba_update_residuals(ctx_, 0, st.data(), se.data(), ne.data(), fl.data())) {
+                fail("ldso_ba_update_residuals");
+                return false;
+            }
+            resSync_ = ResSync::Synced;
+        }
+        return true;
+    }
+    // structural change: rebuild the mirror (the only place the weak_ptr graph is walked)
+    residualTouched();
+    if (!uploadFrameTerms()) return false;
     ptPtr_.clear();
     for (const shared_ptr<PointHessian> &p : allPoints) ptPtr_.push_back(p.get());
     PointPack pk;
@@ -420,6 +573,19 @@ bool EnergyFunctional::upload() {
     resFlags_ = pk.flags;
     resPtr_ = pk.res;
     nResiduals = (int)resPtr_.size();
+    resPoint_.resize(resPtr_.size());
+    for (size_t q = 0; q < ptPtr_.size(); q++)
+        for (int k = resBegin_[q]; k < resBegin_[q + 1]; k++) {
+            resPtr_[k]->mirrorIdx = k;
+            resPoint_[k] = ptPtr_[q];
+        }
+    pointVals_.resize(4 * ptPtr_.size());
+    for (size_t q = 0; q < ptPtr_.size(); q++) {
+        pointVals_[4 * q] = pointData_[q * LDSO_BA_POINT_STRIDE + 2];
+        pointVals_[4 * q + 1] = pointData_[q * LDSO_BA_POINT_STRIDE + 3];
+        pointVals_[4 * q + 2] = pointData_[q * LDSO_BA_POINT_STRIDE + 4];
+        pointVals_[4 * q + 3] = pointData_[q * LDSO_BA_POINT_STRIDE + 5];
+    }
     ldso_ba_window w;
     std::memset(&w, 0, sizeof(w));
     w.n_frames = N;
@@ -428,12 +594,9 @@ bool EnergyFunctional::upload() {
     w.width = width_;
     w.height = height_;
     std::memcpy(w.calib, calib_.value_scaledf, sizeof(w.calib));
-    if (dirty_) {  // images are only uploaded on a structural change
-        dI_.resize((size_t)N * width_ * height_ * 3);
-        for (int f = 0; f < N; f++)
-            std::memcpy(&dI_[(size_t)f * width_ * height_ * 3], frames[f]->dI,
-                        (size_t)width_ * height_ * 3 * sizeof(float));
-    }
+    dI_.resize((size_t)N * width_ * height_ * 3);
+    for (int f = 0; f < N; f++)
+        std::memcpy(&dI_[(size_t)f * width_ * height_ * 3], frames[f]->dI, (size_t)width_ * height_ * 3 * sizeof(float));
     w.dI = dI_.data();
     w.frame_energy_th = frameTH_.data();
     w.precalc = precalc_.data();
@@ -450,53 +613,188 @@ bool EnergyFunctional::upload() {
     w.res_state = resState_.data();
     w.res_energy = resEnergy_.data();
     w.res_flags = resFlags_.data();
-    const int rc = dirty_ ? ldso_ba_load(ctx_, 1, &w, 0, 1) : ldso_ba_update(ctx_, 0, &w);
-    if (rc) {
-        fail(dirty_ ? "ldso_ba_load" : "ldso_ba_update");
+    if (ldso_ba_load(ctx_, 1, &w, 0, 1)) {
+        fail("ldso_ba_load");
         return false;
     }
+    // the device's state_NewEnergy starts as state_energy (ldso_ba_load); the host's may differ
+    bool ne_differs = false;
+    for (size_t k = 0; k < resPtr_.size() && !ne_differs; k++)
+        ne_differs = (float)resPtr_[k]->state_NewEnergy != resEnergy_[k];
+    resSync_ = ne_differs ? ResSync::HostNewer : ResSync::Synced;
     dirty_ = false;
+    if (resSync_ == ResSync::HostNewer) return upload();
     return true;
 }
 
 void EnergyFunctional::resetOOB() {
+    residualTouched();
     for (const shared_ptr<PointHessian> &p : allPoints)
         for (const shared_ptr<PointFrameResidual> &r : p->residuals)
-            if (!r->isLinearized) r->resetOOB();  // FullSystem.cc:866-869
-    if (!dirty_ && ctx_ && ldso_ba_reset_oob(ctx_, 0)) fail("ldso_ba_reset_oob");
+            if (!r->isLinearized) {  // FullSystem.cc:866-869 (the mirror follows below)
+                r->state_NewEnergy = r->state_energy = 0;
+                r->state_NewState = OUTLIER;
+                r->state_state = IN;
+            }
+    if (!dirty_ && ctx_) {
+        if (ldso_ba_reset_oob(ctx_, 0)) fail("ldso_ba_reset_oob");
+        else if (resSync_ == ResSync::DeviceNewer) resSync_ = ResSync::Synced;
+    }
 }
 
-Vec3 EnergyFunctional::linearizeAll(bool fixLinearization) {
-    Vec3 out = {0, 0, 0};
-    if (!upload()) return out;
-    if (ldso_ba_linearize(ctx_, fixLinearization ? 1 : 0, fixLinearization ? 0 : 1)) {
-        fail("ldso_ba_linearize");
-        return out;
-    }
-    double e[3];
-    if (ldso_ba_get_energy(ctx_, 0, e)) {
-        fail("ldso_ba_get_energy");
-        return out;
-    }
+// every per-residual / per-point result of the device's last pass into the objects
+bool EnergyFunctional::readBack(bool points_and_th) {
     if (!read_residuals(ctx_, resPtr_)) {
         fail("ldso_ba_get_residuals");
-        return out;
+        return false;
     }
+    resSync_ = ResSync::Synced;
+    if (!points_and_th) return true;
     const int P = (int)ptPtr_.size(), N = nFrames;
     std::vector<float> hdi(P), bds(P), ih(P), th(N);
     if (P && ldso_ba_get_points(ctx_, 0, hdi.data(), bds.data(), ih.data(), nullptr, nullptr, nullptr)) {
         fail("ldso_ba_get_points");
-        return out;
+        return false;
     }
     for (int q = 0; q < P; q++) {
         ptPtr_[q]->HdiF = hdi[q];
         ptPtr_[q]->bdSumF = bds[q];
         ptPtr_[q]->idepth_hessian = ih[q];
     }
-    if (ldso_ba_get_frame_energy_th(ctx_, 0, th.data()) == 0)
+    if (ldso_ba_get_frame_energy_th(ctx_, 0, th.data()) == 0) {
         for (int f = 0; f < N; f++) frames[f]->frameEnergyTH = th[f];
+        thUp_ = th;  // the device holds these already
+        frameTH_ = th;
+    }
+    return true;
+}
+
+void EnergyFunctional::syncResiduals() {
+    if (resSync_ != ResSync::DeviceNewer || !ctx_ || dirty_) return;
+    resSync_ = ResSync::Synced;  // before the reads: the residual setters called below see it synced
+    readBack(true);
+}
+
+Vec3 EnergyFunctional::linearizeAll(bool fixLinearization) {
+    Vec3 out = {0, 0, 0};
+    epoch_++;
+    if (!upload()) return out;
+    if (ldso_ba_linearize(ctx_, fixLinearization ? 1 : 0, fixLinearization ? 0 : 1)) {
+        fail("ldso_ba_linearize");
+        return out;
+    }
+    passes_++;
+    double e[3];
+    if (ldso_ba_get_energy(ctx_, 0, e)) {
+        fail("ldso_ba_get_energy");
+        return out;
+    }
+    if (!readBack(true)) return out;
     if (!fixLinearization) resInA = (int)e[2];
     out = {e[0], e[1], e[2]};
+    return out;
+}
+
+// One device pass (ldso_ba_linearize_residuals) relinearising every residual of the window from
+// resetOOB; the entries serve PointFrameResidual::linearize until the next change of the window
+bool EnergyFunctional::runRelinearization() {
+    if (!upload()) return false;
+    const size_t R = resPtr_.size();
+    cNewState_.assign(R, 0);
+    cCenterOk_.assign(R, 0);
+    cNewEnergy_.assign(R, 0.f);
+    cEwo_.assign(R, 0.f);
+    cCenter_.assign(3 * R, 0.f);
+    cJp_.assign(8 * R, 0.f);
+    if (R && ldso_ba_linearize_residuals(ctx_, 0, cNewState_.data(), cNewEnergy_.data(), cEwo_.data(), cCenter_.data(),
+                                         cCenterOk_.data(), cJp_.data())) {
+        fail("ldso_ba_linearize_residuals");
+        return false;
+    }
+    passes_++;
+    cSnap_.resize(4 * R);
+    for (size_t k = 0; k < R; k++) {
+        const PointHessian &p = *resPoint_[k];
+        cSnap_[4 * k] = p.u;
+        cSnap_[4 * k + 1] = p.v;
+        cSnap_[4 * k + 2] = p.idepth_scaled;
+        cSnap_[4 * k + 3] = p.idepth_zero_scaled;
+    }
+    cacheEpoch_ = epoch_;
+    return true;
+}
+
+double EnergyFunctional::linearizeResidual(PointFrameResidual &r) {
+    auto fresh = [&]() {
+        if (dirty_ || cacheEpoch_ != epoch_ || r.mirrorIdx < 0 || (size_t)r.mirrorIdx >= cNewState_.size() ||
+            resPtr_[r.mirrorIdx] != &r)
+            return false;
+        const PointHessian &p = *resPoint_[r.mirrorIdx];
+        const float *sn = &cSnap_[4 * (size_t)r.mirrorIdx];
+        return sn[0] == p.u && sn[1] == p.v && sn[2] == p.idepth_scaled && sn[3] == p.idepth_zero_scaled;
+    };
+    if (!fresh() && (!runRelinearization() || !fresh())) return r.state_energy;
+    const size_t k = (size_t)r.mirrorIdx;
+    const ResState ns = (ResState)cNewState_[k];
+    r.state_NewState = ns;
+    if (cCenterOk_[k]) std::memcpy(r.centerProjectedTo, &cCenter_[3 * k], 3 * sizeof(float));
+    if (ns == OOB) return r.state_energy;  // Residuals.cc:59-63, 131-146: state_energy, NewEnergy kept
+    r.state_NewEnergyWithOutlier = cEwo_[k];
+    if (r.state_NewEnergy != (double)cNewEnergy_[k]) residualEdited();  // the device's NewEnergy follows
+    r.state_NewEnergy = cNewEnergy_[k];
+    if (ns == IN) std::memcpy(r.J_JpJdF, &cJp_[8 * k], sizeof(r.J_JpJdF));
+    return r.state_NewEnergy;
+}
+
+// FullSystem::optimize's loop (FullSystem.cc:853-970) on the device; see the header
+Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std::vector<Vec3> *energies) {
+    Vec3 out = {0, 0, 0};
+    epoch_++;
+    calib_ = *HCalib;
+    if (!upload()) return out;
+    const int N = nFrames, n = 8 * N + CPARS, P = (int)ptPtr_.size();
+    std::vector<double> ns((size_t)7 * n), e((size_t)3 * (n_its + 1));
+    if (ldso_ba_nullspaces(N, fs_.data(), ns.data())) {
+        fail("ldso_ba_nullspaces");
+        return out;
+    }
+    std::vector<ldso_ba_frame_state> fo(N);
+    std::vector<float> idepth(P);
+    double calib_out[4];
+    if (ldso_ba_optimize(ctx_, n_its, fs_.data(), HCalib->value, HCalib->value_zero, ns.data(), e.data(), fo.data(),
+                         calib_out, idepth.data())) {
+        fail("ldso_ba_optimize");
+        return out;
+    }
+    passes_ += n_its + 1;
+    // doStepFromBackup's results (FullSystem.cc:1843-1922) into the objects: frame states, the
+    // calibration, every point's setIdepth / setIdepthZero
+    for (int f = 0; f < N; f++) std::memcpy(frames[f]->state, fo[f].state, sizeof(fo[f].state));
+    HCalib->setValue(calib_out);
+    calib_ = *HCalib;
+    for (int q = 0; q < P; q++) {
+        ptPtr_[q]->setIdepth(idepth[q]);
+        ptPtr_[q]->setIdepthZero(idepth[q]);
+    }
+    // setNewFrameEnergyTH of the loop's passes (the device holds it; the next frame-term upload
+    // must not overwrite it with the old value)
+    std::vector<float> th(N);
+    if (ldso_ba_get_frame_energy_th(ctx_, 0, th.data())) {
+        fail("ldso_ba_get_frame_energy_th");
+        return out;
+    }
+    for (int f = 0; f < N; f++) frames[f]->frameEnergyTH = th[f];
+    setDeltaF(HCalib);  // setPrecalcValues' setDeltaF after the last step: points' deltaF = 0
+    for (int q = 0; q < P; q++) {
+        pointVals_[4 * q] = ptPtr_[q]->idepth_scaled;
+        pointVals_[4 * q + 1] = ptPtr_[q]->idepth_zero_scaled;
+        pointVals_[4 * q + 3] = ptPtr_[q]->deltaF;
+    }
+    resSync_ = ResSync::DeviceNewer;
+    resInA = (int)e[3 * n_its + 2];
+    if (energies)
+        for (int s = 0; s <= n_its; s++) energies->push_back({e[3 * s], e[3 * s + 1], e[3 * s + 2]});
+    out = {e[3 * n_its], e[3 * n_its + 1], e[3 * n_its + 2]};
     return out;
 }
 

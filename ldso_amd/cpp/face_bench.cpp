@@ -1,0 +1,184 @@
+// face_bench.cpp -- times the C++ host face (include/ldso_amd/energy_functional.h) the way LDSO's
+// FullSystem drives it, on one synthetic S7 window (7 keyframes, 2000 points, 640x480), beside
+// the C ABI's ldso_ba_optimize on the same window in the same process.  Run by bench.py
+// (cpp_face); prints one JSON object.
+//
+//   optimize        EnergyFunctional::optimize(6): FullSystem::optimize's GN loop on the device
+//                   plus the face's write-back (frame states, calibration, point idepths,
+//                   setDeltaF), host clock per call
+//   optimize_full   the same + setAdjointsF + setDeltaF + linearizeAll(true) with the complete
+//                   residual / point write-back: everything FullSystem::optimize asks of the
+//                   backend after the frontend's setEvalPT
+//   c_abi_optimize  ldso_ba_optimize(6) on a context loaded with the same window (no face)
+//   flag_loop       FullSystem::flagPointsForRemoval's per-residual resetOOB / linearize /
+//                   applyRes over every residual of 10 % of the points (one device pass)
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/ldso_amd/energy_functional.h"
+#include "../csrc/synth.h"
+
+using namespace ldso_amd;
+using Clock = std::chrono::steady_clock;
+
+static double ms_since(Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+int main(int argc, char **argv) {
+    const int N = 7, P = 2000, W = 640, H = 480, n_its = 6;
+    const int reps = argc > 1 ? std::atoi(argv[1]) : 10;
+    const int R = P * (N - 1);
+    std::vector<ldso_ba_frame_state> fs(N);
+    std::vector<float> dI((size_t)N * W * H * 3), th(N), pd((size_t)P * LDSO_BA_POINT_STRIDE), re(R);
+    std::vector<int32_t> ph(P), rb(P + 1), rt(R);
+    std::vector<int8_t> rs(R);
+    std::vector<uint8_t> rf(R);
+    float calib[4];
+    ldso_synth_params prm = {N, P, W, H, 1, 0.05f, 0.01f, 1e-3f, 0.04f};
+    if (ldso_synth_fill(&prm, fs.data(), dI.data(), calib, th.data(), ph.data(), pd.data(), rb.data(), rt.data(),
+                        rs.data(), re.data(), rf.data())) {
+        std::printf("{\"error\": \"synth\"}\n");
+        return 1;
+    }
+    // the LDSO object graph (shared_ptr ownership, as the reference)
+    auto HCalib = std::make_shared<CalibHessian>();
+    HCalib->wG0 = W;
+    HCalib->hG0 = H;
+    std::memcpy(HCalib->value_scaledf, calib, sizeof(calib));
+    for (int k = 0; k < 4; k++) HCalib->value[k] = HCalib->value_zero[k] = (double)calib[k] * (1.0 / 50.0);
+    std::vector<shared_ptr<FrameHessian>> frames;
+    std::vector<shared_ptr<PointHessian>> points;
+    for (int f = 0; f < N; f++) {
+        auto F = std::make_shared<FrameHessian>();
+        F->frameID = f;
+        std::memcpy(F->worldToCam_evalPT, fs[f].world_to_cam_evalpt, sizeof(F->worldToCam_evalPT));
+        std::memcpy(F->state, fs[f].state, sizeof(F->state));
+        std::memcpy(F->state_zero, fs[f].state_zero, sizeof(F->state_zero));
+        F->ab_exposure = fs[f].ab_exposure;
+        F->dI = &dI[(size_t)f * W * H * 3];
+        F->frameEnergyTH = th[f];
+        frames.push_back(F);
+    }
+    auto ef = std::make_shared<EnergyFunctional>(0);
+    if (!ef->ok()) {
+        std::printf("{\"error\": \"%s\"}\n", ef->lastError().c_str());
+        return 1;
+    }
+    for (auto &F : frames) ef->insertFrame(F, HCalib);
+    for (int p = 0; p < P; p++) {
+        auto Pt = std::make_shared<PointHessian>();
+        const float *d = &pd[(size_t)p * LDSO_BA_POINT_STRIDE];
+        Pt->host = frames[ph[p]];
+        Pt->u = d[0];
+        Pt->v = d[1];
+        Pt->setIdepth(d[2]);
+        Pt->setIdepthZero(d[3]);
+        std::memcpy(Pt->color, d + 8, sizeof(Pt->color));
+        std::memcpy(Pt->weights, d + 16, sizeof(Pt->weights));
+        for (int k = rb[p]; k < rb[p + 1]; k++) {
+            auto r = std::make_shared<PointFrameResidual>(Pt, frames[ph[p]], frames[rt[k]]);
+            r->isNew = true;
+            Pt->residuals.push_back(r);
+        }
+        points.push_back(Pt);
+        ef->insertPoint(Pt);
+        for (auto &r : Pt->residuals) ef->insertResidual(r);
+    }
+    ef->makeIDX();
+    ef->setAdjointsF(HCalib);
+    ef->setDeltaF(HCalib);
+
+    // EnergyFunctional::optimize(6)
+    for (int i = 0; i < 2; i++) ef->optimize(n_its, HCalib);
+    auto t0 = Clock::now();
+    for (int i = 0; i < reps; i++) ef->optimize(n_its, HCalib);
+    const double ms_opt = ms_since(t0) / reps;
+    // + FullSystem::optimize's tail on the backend: setAdjointsF, setDeltaF, linearizeAll(true)
+    auto full = [&] {
+        ef->optimize(n_its, HCalib);
+        ef->setAdjointsF(HCalib);
+        ef->setDeltaF(HCalib);
+        ef->linearizeAll(true);
+    };
+    for (int i = 0; i < 2; i++) full();
+    t0 = Clock::now();
+    for (int i = 0; i < reps; i++) full();
+    const double ms_full = ms_since(t0) / reps;
+    // flagPointsForRemoval's per-residual loop over 10 % of the points
+    const long passes0 = ef->devicePasses();
+    t0 = Clock::now();
+    int nres = 0;
+    for (size_t q = 0; q < ef->allPoints.size(); q += 10)
+        for (auto &r : ef->allPoints[q]->residuals) {
+            r->resetOOB();
+            r->linearize(HCalib);
+            r->applyRes(true);
+            nres++;
+        }
+    const double ms_flag = ms_since(t0);
+    const long flag_passes = ef->devicePasses() - passes0;
+    const bool ok = ef->ok();
+
+    // the C ABI alone on a context of the same window
+    std::vector<float> precalc((size_t)N * N * LDSO_BA_PRECALC_STRIDE);
+    std::vector<double> adH((size_t)N * N * 64), adT((size_t)N * N * 64), cp(4), fp(8 * N), fd(8 * N), fdp(8 * N);
+    ldso_ba_frame_precalc(N, fs.data(), calib, precalc.data());
+    ldso_ba_set_adjoints(N, fs.data(), adH.data(), adT.data(), cp.data());
+    ldso_ba_frame_take_data(N, fs.data(), fp.data(), fd.data(), fdp.data());
+    const float cdelta[4] = {0, 0, 0, 0};
+    ldso_ba_window w;
+    std::memset(&w, 0, sizeof(w));
+    w.n_frames = N;
+    w.n_points = P;
+    w.n_residuals = R;
+    w.width = W;
+    w.height = H;
+    std::memcpy(w.calib, calib, sizeof(calib));
+    w.dI = dI.data();
+    w.frame_energy_th = th.data();
+    w.precalc = precalc.data();
+    w.ad_host = adH.data();
+    w.ad_target = adT.data();
+    w.c_prior = cp.data();
+    w.c_delta = cdelta;
+    w.frame_prior = fp.data();
+    w.frame_delta_prior = fdp.data();
+    w.point_host = ph.data();
+    w.point_data = pd.data();
+    w.point_res_begin = rb.data();
+    w.res_target = rt.data();
+    w.res_state = rs.data();
+    w.res_energy = re.data();
+    w.res_flags = rf.data();
+    ldso_ba_ctx *raw = nullptr;
+    double ms_raw = -1;
+    if (ldso_ba_create(0, &raw) == 0 && ldso_ba_load(raw, 1, &w, 0, 1) == 0) {
+        const int n = 8 * N + 4;
+        std::vector<double> ns((size_t)7 * n), e((size_t)3 * (n_its + 1)), cv(4), co(4);
+        std::vector<ldso_ba_frame_state> fo(N);
+        std::vector<float> id(P);
+        for (int k = 0; k < 4; k++) cv[k] = HCalib->value_zero[k];
+        ldso_ba_nullspaces(N, fs.data(), ns.data());
+        for (int i = 0; i < 2; i++)
+            ldso_ba_optimize(raw, n_its, fs.data(), cv.data(), cv.data(), ns.data(), e.data(), fo.data(), co.data(), id.data());
+        t0 = Clock::now();
+        for (int i = 0; i < reps; i++)
+            ldso_ba_optimize(raw, n_its, fs.data(), cv.data(), cv.data(), ns.data(), e.data(), fo.data(), co.data(), id.data());
+        ms_raw = ms_since(t0) / reps;
+        ldso_ba_destroy(raw);
+    }
+    std::printf(
+        "{\"window\": \"S7 (7 KF, 2000 pts, 640x480, seed 1)\", \"n_its\": %d, \"reps\": %d, \"ok\": %s, "
+        "\"optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f}, "
+        "\"optimize_full\": {\"ms\": %.6f, \"what\": \"optimize(6) + setAdjointsF + setDeltaF + linearizeAll(true) "
+        "with the residual / point write-back\"}, "
+        "\"c_abi_optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f}, "
+        "\"flag_loop\": {\"residuals\": %d, \"ms\": %.6f, \"device_passes\": %ld}}\n",
+        n_its, reps, ok ? "true" : "false", ms_opt, ms_opt / n_its, ms_full, ms_raw, ms_raw / n_its, nres, ms_flag,
+        flag_passes);
+    return ok ? 0 : 1;
+}

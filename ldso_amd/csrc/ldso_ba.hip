@@ -17,9 +17,11 @@
 //                 accD/accE/accEB/accHcc/accbc sums of AccumulatedSCHessian.cc:35-50).
 //   k_stitch      block per (host,target) pair: the Top adjoint sandwiches
 //                 (AccumulatedTopHessian.cc:213-239) and the SC sandwiches for (i=h, j=t)
-//                 (AccumulatedSCHessian.cc:80-114) in double, f64 atomics into the packed upper
-//                 triangles; the (0,0) block also runs setNewFrameEnergyTH (FullSystem.cc:2078-2109)
-//                 as a radix select and sums the linearizeAll energy.
+//                 (AccumulatedSCHessian.cc:80-114) in double, one contribution record per
+//                 (pair, block); one block per window runs setNewFrameEnergyTH
+//                 (FullSystem.cc:2078-2109) as a radix select and sums the linearizeAll energy.
+//   k_stitch_sum  thread per packed output element: its contribution records summed in one fixed
+//                 pair order (no atomics: the stitched system is bitwise repeatable).
 //
 // Outside the pass: k_resubstitute (resubstituteFPt, EnergyFunctional.cc:638-667), k_tile_image
 // (image staging at load/update), k_export_newest + k_frame_th (sharded threshold exchange).
@@ -2649,6 +2651,18 @@ __global__ __launch_bounds__(256) void k_energy_to_history(const double *src, do
     const int s = *slot;
     for (int i = threadIdx.x; i < n2; i += 256) hist[(size_t)s * n2 + i] = src[i];
 }
+// ldso_ba_update_points: [P][4] (idepth_scaled, idepth_zero_scaled, priorF, deltaF) of one window in
+// its sorted point order into the point records (columns 2..5)
+__global__ __launch_bounds__(256) void k_set_point_vals(const float4 *__restrict__ vals, float *pt_data, int n) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const float4 v = vals[q];
+    float *d = pt_data + (size_t)q * LDSO_BA_POINT_STRIDE;
+    d[2] = v.x;
+    d[3] = v.y;
+    d[4] = v.z;
+    d[5] = v.w;
+}
 // idepth of every resident point (point-data column 2), compacted for one small download
 __global__ __launch_bounds__(256) void k_gather_idepth(const float *__restrict__ pt_data, float *out, int n) {
     const int q = blockIdx.x * 256 + threadIdx.x;
@@ -2790,7 +2804,6 @@ struct ldso_ba_ctx {
     int comm_rank = 0, comm_world = 1;
     int64_t x_stride = 0;
     DevBuf<float> d_x_local, d_x_gathered;
-    bool ns_resident = false;  // d_ns holds the nullspaces of the loaded windows (ldso_ba_optimize)
     // device GN loop (ldso_ba_optimize): frame states, CalibHessian::value / value_zero and the
     // prior switches per window, the energy history
     DevBuf<ldso_ba_frame_state> d_fstate;
@@ -2829,6 +2842,13 @@ struct ldso_ba_ctx {
     size_t pin_out_n = 0;
     std::vector<double> energy_host;
     bool energy_valid = false;
+    // ldso_ba_linearize_residuals: k_linearize runs on copies of the residual state so that the
+    // context's own state (and its records, read by resubstitution) stay untouched
+    DevBuf<int8_t> d_sx_state, d_sx_newstate;
+    DevBuf<uint8_t> d_sx_flags;
+    DevBuf<float> d_sx_energy, d_sx_newenergy, d_sx_ewo;
+    DevBuf<float4> d_sx_center, d_sx_rec, d_pt_vals;
+    DevBuf<double> d_sx_item;
 };
 
 namespace {
@@ -3243,6 +3263,16 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_add_priors.release();
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->d_xad.release();
+    c->d_sx_state.release();
+    c->d_sx_newstate.release();
+    c->d_sx_flags.release();
+    c->d_sx_energy.release();
+    c->d_sx_newenergy.release();
+    c->d_sx_ewo.release();
+    c->d_sx_center.release();
+    c->d_sx_rec.release();
+    c->d_pt_vals.release();
+    c->d_sx_item.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -3285,7 +3315,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_win = n_windows;
     c->x_stride = 0;
-    c->ns_resident = false;  // the exchange re-agrees on the newest-frame slot stride
     c->width = ws[0].width;
     c->height = ws[0].height;
     c->npix = c->width * c->height;
@@ -3335,7 +3364,9 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         H.N = N;
         H.P_all = in.n_points;
         H.R_all = in.n_residuals;
-        H.add_priors = (shard_rank == 0);
+        // the priors (HL, bL) are not part of the reduced packed system: every rank adds them in
+        // its own (redundant) solve, so every shard keeps them
+        H.add_priors = true;
         H.c_prior.assign(in.c_prior, in.c_prior + 4);
         H.c_delta.assign(in.c_delta, in.c_delta + 4);
         H.frame_prior.assign(in.frame_prior, in.frame_prior + 8 * N);
@@ -3662,10 +3693,11 @@ int ldso_ba_update(ldso_ba_ctx *c, int32_t win, const ldso_ba_window *w) {
         H.adHF[k] = (float)w->ad_host[k];
         H.adTF[k] = (float)w->ad_target[k];
     }
-    std::vector<float> pd((size_t)H.P * LDSO_BA_POINT_STRIDE);
-    for (int q = 0; q < H.P; q++)
-        std::memcpy(&pd[(size_t)q * LDSO_BA_POINT_STRIDE], w->point_data + (size_t)H.pt_orig[q] * LDSO_BA_POINT_STRIDE,
-                    LDSO_BA_POINT_STRIDE * sizeof(float));
+    std::vector<float> pd(w->point_data ? (size_t)H.P * LDSO_BA_POINT_STRIDE : 0);
+    if (w->point_data)
+        for (int q = 0; q < H.P; q++)
+            std::memcpy(&pd[(size_t)q * LDSO_BA_POINT_STRIDE],
+                        w->point_data + (size_t)H.pt_orig[q] * LDSO_BA_POINT_STRIDE, LDSO_BA_POINT_STRIDE * sizeof(float));
     HIP_TRY(hipMemcpyAsync(c->d_wins.p + win, &D, sizeof(WinDev), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_precalc.p + (size_t)D.pair_base * LDSO_BA_PRECALC_STRIDE, w->precalc,
                            (size_t)N * N * LDSO_BA_PRECALC_STRIDE * sizeof(float), hipMemcpyHostToDevice, c->stream));
@@ -3675,12 +3707,66 @@ int ldso_ba_update(ldso_ba_ctx *c, int32_t win, const ldso_ba_window *w) {
                            hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_frame_th.p + D.frame_base, w->frame_energy_th, N * sizeof(float),
                            hipMemcpyHostToDevice, c->stream));
-    if (H.P)
+    if (H.P && w->point_data)
         HIP_TRY(hipMemcpyAsync(c->d_pt_data.p + (size_t)D.point_base * LDSO_BA_POINT_STRIDE, pd.data(),
                                pd.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->sys_host_valid = false;
     return upload_priors(c, win);
+}
+
+int ldso_ba_update_points(ldso_ba_ctx *c, int32_t win, const float *vals) {
+    if (!c || win < 0 || win >= c->n_win || (!vals && c->wh[win].P_all > 0)) return fail(-1, "bad arguments");
+    const WinHost &H = c->wh[win];
+    const WinDev &D = c->wd[win];
+    if (H.P == 0) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = c->d_pt_vals.ensure((size_t)c->P_tot);
+    if (rc) return rc;
+    if ((rc = pin_ensure(c->pin_out, c->pin_out_n, (size_t)H.P * sizeof(float4)))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));  // pin_out may feed an earlier copy
+    float4 *st = reinterpret_cast<float4 *>(c->pin_out);
+    for (int q = 0; q < H.P; q++) {
+        const float *v = vals + 4 * (size_t)H.pt_orig[q];
+        st[q] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_pt_vals.p + D.point_base, st, (size_t)H.P * sizeof(float4), hipMemcpyHostToDevice,
+                           c->stream));
+    k_set_point_vals<<<(H.P + 255) / 256, 256, 0, c->stream>>>(c->d_pt_vals.p + D.point_base,
+                                                              c->d_pt_data.p + (size_t)D.point_base * LDSO_BA_POINT_STRIDE, H.P);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int ldso_ba_update_residuals(ldso_ba_ctx *c, int32_t win, const int8_t *state, const float *state_energy,
+                             const float *new_energy, const uint8_t *flags) {
+    if (!c || win < 0 || win >= c->n_win) return fail(-1, "bad arguments");
+    const WinHost &H = c->wh[win];
+    const WinDev &D = c->wd[win];
+    if (D.R == 0) return 0;
+    if (!state || !state_energy || !new_energy || !flags) return fail(-1, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t R = (size_t)D.R;
+    int rc = pin_ensure(c->pin_out, c->pin_out_n, R * (2 * sizeof(float) + 2));
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    float *se = reinterpret_cast<float *>(c->pin_out), *ne = se + R;
+    int8_t *st = reinterpret_cast<int8_t *>(ne + R);
+    uint8_t *fl = reinterpret_cast<uint8_t *>(st + R);
+    for (size_t pos = 0; pos < R; pos++) {
+        const int k = H.rs_orig[pos];
+        se[pos] = state_energy[k];
+        ne[pos] = new_energy[k];
+        st[pos] = state[k];
+        fl[pos] = flags[k];
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_rs_energy.p + D.res_base, se, R * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_rs_newenergy.p + D.res_base, ne, R * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_rs_state.p + D.res_base, st, R, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_rs_flags.p + D.res_base, fl, R, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
 }
 
 int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
@@ -3709,8 +3795,8 @@ namespace {
     } while (0)
 
 // SURVEY.md §8e's exchange, stream-ordered after k_stitch on the context stream (no host
-// synchronisation): one fp64 sum all-reduce of every window's packed {HA, bA, Hsc, bsc} (priors
-// are in rank 0's share only), one of the linearizeAll energy / #IN pairs, and an all-gather of
+// synchronisation): one fp64 sum all-reduce of every window's packed {HA, bA, Hsc, bsc} (the priors
+// are not in it: every rank adds its own copy in the solve), one of the linearizeAll energy / #IN pairs, and an all-gather of
 // the newest-frame NewEnergyWithOutlier slots after which k_frame_th re-selects the exact
 // setNewFrameEnergyTH threshold on every rank.
 int comm_exchange(ldso_ba_ctx *c, bool accumulate) {
@@ -3864,6 +3950,103 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         HIP_TRY(hipGetLastError());
     }
     return rc;
+}
+
+int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, float *new_energy,
+                                float *new_energy_wo, float *center, uint8_t *center_ok, float *jpjdf) {
+    if (!c || win < 0 || win >= c->n_win) return fail(-1, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    const WinDev &D = c->wd[win];
+    const WinHost &H = c->wh[win];
+    const size_t R = (size_t)D.R;
+    if (R == 0 || D.n_top_items == 0) return 0;
+    int rc;
+    const size_t Rt = (size_t)c->R_tot, slots = c->d_pt_rec.n;
+    if ((rc = c->d_sx_state.ensure(Rt)) || (rc = c->d_sx_newstate.ensure(Rt)) || (rc = c->d_sx_flags.ensure(Rt)) ||
+        (rc = c->d_sx_energy.ensure(Rt)) || (rc = c->d_sx_newenergy.ensure(Rt)) || (rc = c->d_sx_ewo.ensure(Rt)) ||
+        (rc = c->d_sx_center.ensure(Rt)) || (rc = c->d_sx_rec.ensure(slots)) ||
+        (rc = c->d_sx_item.ensure((size_t)2 * c->n_top_items)))
+        return rc;
+    hipStream_t st = c->stream;
+    const size_t b = (size_t)D.res_base;
+    // resetOOB() of every residual of the window on the copies: state IN, NewState OUTLIER,
+    // energies 0; the centre marked "not projected" (NaN) so a failed centre projection shows
+    HIP_TRY(hipMemsetAsync(c->d_sx_state.p + b, LDSO_BA_RES_IN, R, st));
+    HIP_TRY(hipMemsetAsync(c->d_sx_newstate.p + b, LDSO_BA_RES_OUTLIER, R, st));
+    HIP_TRY(hipMemsetAsync(c->d_sx_energy.p + b, 0, R * sizeof(float), st));
+    HIP_TRY(hipMemsetAsync(c->d_sx_newenergy.p + b, 0, R * sizeof(float), st));
+    HIP_TRY(hipMemsetAsync(c->d_sx_center.p + b, 0xFF, R * sizeof(float4), st));
+    HIP_TRY(hipMemcpyAsync(c->d_sx_flags.p + b, c->d_rs_flags.p + b, R, hipMemcpyDeviceToDevice, st));
+    LinParams L;
+    L.items = c->d_top_items.p;
+    L.wins = c->d_wins.p;
+    L.img = c->img_ext ? c->img_ext : c->d_img.p;
+    L.ad_ht_delta = nullptr;
+    L.precalc = c->d_precalc.p;
+    L.frame_th = c->d_frame_th.p;
+    L.rs_point = c->d_rs_point.p;
+    L.rs_slot = c->d_rs_slot.p;
+    L.pt_data = c->d_pt_data.p;
+    L.rs_state = c->d_sx_state.p;
+    L.rs_newstate = c->d_sx_newstate.p;
+    L.rs_flags = c->d_sx_flags.p;
+    L.rs_energy = c->d_sx_energy.p;
+    L.rs_newenergy = c->d_sx_newenergy.p;
+    L.rs_energy_wo = c->d_sx_ewo.p;
+    L.rs_center = c->d_sx_center.p;
+    L.pt_rec = c->d_sx_rec.p;
+    L.top_slab = nullptr;
+    L.item_energy = c->d_sx_item.p;
+    L.frame_stride = c->frame_stride;
+    L.tiles_per_row = c->tiles_per_row;
+    L.fix = 0;
+    L.accumulate = 0;
+    L.item_base = D.top_item_base;
+    L.n_items = D.n_top_items;
+    L.n_blocks = (L.n_items + 3) / 4;
+    rc = timed_launch(c, 0, st, [&] {
+        if (c->marg) launch_linearize<true>(c->img_mode, L.n_blocks, st, L);
+        else launch_linearize<false>(c->img_mode, L.n_blocks, st, L);
+    });
+    if (rc) return rc;
+    std::vector<int8_t> ns(R);
+    std::vector<float> ne(R), ew(R);
+    std::vector<float4> ce(R), rec;
+    HIP_TRY(hipMemcpyAsync(ns.data(), c->d_sx_newstate.p + b, R, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(ne.data(), c->d_sx_newenergy.p + b, R * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(ew.data(), c->d_sx_ewo.p + b, R * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(ce.data(), c->d_sx_center.p + b, R * sizeof(float4), hipMemcpyDeviceToHost, st));
+    const size_t slot0 = (size_t)D.rec_base;
+    if (jpjdf && D.P > 0) {
+        rec.resize((size_t)D.P * (D.N - 1) * 4);
+        HIP_TRY(hipMemcpyAsync(rec.data(), c->d_sx_rec.p + slot0 * 4, rec.size() * sizeof(float4), hipMemcpyDeviceToHost,
+                               st));
+    }
+    if ((rc = ldso_ba_sync(c))) return rc;
+    for (size_t pos = 0; pos < R; pos++) {
+        const int k = H.rs_orig[pos];
+        const bool cok = !std::isnan(ce[pos].x);
+        if (new_state) new_state[k] = ns[pos];
+        if (new_energy) new_energy[k] = ne[pos];
+        if (new_energy_wo) new_energy_wo[k] = ew[pos];
+        if (center_ok) center_ok[k] = cok ? 1 : 0;
+        if (center) {
+            center[3 * k] = cok ? ce[pos].x : 0.f;
+            center[3 * k + 1] = cok ? ce[pos].y : 0.f;
+            center[3 * k + 2] = cok ? ce[pos].z : 0.f;
+        }
+        if (jpjdf) {
+            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (ns[pos] == LDSO_BA_RES_IN) {
+                const size_t sl = (size_t)H.rs_slot[pos] - slot0;
+                const float4 a = rec[sl * 4], q = rec[sl * 4 + 1];
+                const float t[8] = {a.x, a.y, a.z, a.w, q.x, q.y, q.z, q.w};
+                std::memcpy(v, t, sizeof(v));
+            }
+            std::memcpy(jpjdf + 8 * (size_t)k, v, sizeof(v));
+        }
+    }
+    return 0;
 }
 
 int ldso_ba_activate_points(ldso_ba_ctx *c, int32_t win, int32_t n, const ldso_ct_immature *pts, int32_t min_obs,
@@ -4149,20 +4332,14 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
 }
 
 // ---- device-side solve / resubstitute ----------------------------------
-int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const double *ns, int32_t n_null,
-                         double *x_out) {
-    (void)lambda;  // SOLVER_FIX_LAMBDA, as the host solver
-    if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
-    if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
+}  // extern "C"
+namespace {
+// k_solve_reg / k_solve for every loaded window; n_null > 0 projects with the nullspaces already in
+// d_ns (iteration >= 2), n_null == 0 does not project
+int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
     int dmax = 0;
     for (const WinDev &D : c->wd) dmax = std::max(dmax, D.D);
     if (dmax > kSolveMaxDim) return fail(-1, "device solve supports windows of up to 11 keyframes");
-    HIP_TRY(hipSetDevice(c->device));
-    if (iteration >= 2 && ns && n_null > 0) {
-        // caller layout: every window's [7][D] back to back -> device [7 * vec_total] (same order)
-        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
-                               c->stream));
-    }
     SolveParams S;
     S.wins = c->d_wins.p;
     S.sys = c->d_sys.p;
@@ -4173,7 +4350,7 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
     S.adT = c->d_adT.p;
     S.xad = c->d_xad.p;  // the resubstitution's xAd comes with x (k_xad after the LDS kernel)
     S.iteration = iteration;
-    S.n_null = (iteration >= 2 && (ns || c->ns_resident)) ? n_null : 0;
+    S.n_null = iteration >= 2 ? n_null : 0;
     static std::once_flag once;
     std::call_once(once, [] {
         (void)hipFuncSetAttribute((const void *)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4195,6 +4372,25 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
         k_xad<<<c->n_win, 256, 0, c->stream>>>(c->d_wins.p, c->d_x.p, c->d_adH.p, c->d_adT.p, c->d_xad.p);
         HIP_TRY(hipGetLastError());
     }
+    return 0;
+}
+}  // namespace
+extern "C" {
+
+// The projection (iteration >= 2) uses the nullspaces passed in THIS call; without them the
+// solve does not project, exactly as the host solver (ldso_ba_solve / ldso_ba_solve_system).
+int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const double *ns, int32_t n_null,
+                         double *x_out) {
+    (void)lambda;  // SOLVER_FIX_LAMBDA, as the host solver
+    if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
+    if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
+    HIP_TRY(hipSetDevice(c->device));
+    const bool project = iteration >= 2 && ns && n_null > 0;
+    if (project)  // caller layout: every window's [7][D] back to back -> device [7 * vec_total]
+        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
+                               c->stream));
+    int rc = solve_device_launch(c, iteration, project ? n_null : 0);
+    if (rc) return rc;
     if (x_out) {
         HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,
                                c->stream));
@@ -4267,6 +4463,9 @@ int launch_cached_graph(ldso_ba_ctx *c, ldso_ba_ctx::Graph &g, unsigned long lon
     }
     const hipError_t el = hipGraphLaunch(g.exec, c->stream);
     if (el != hipSuccess) return fail(-2, std::string("graph launch: ") + hipGetErrorString(el));
+    // a replay skips the host side of the captured calls: invalidate what their passes would
+    c->sys_host_valid = false;
+    c->energy_valid = false;
     return 0;
 }
 }  // namespace
@@ -4278,18 +4477,17 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
     if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
     HIP_TRY(hipSetDevice(c->device));
     int rc;
-    const bool project = iteration >= 2 && n_null > 0 && (ns || c->ns_resident);
-    if (project && ns) {  // the nullspaces go up before (outside) the captured sequence
+    // the projection uses the nullspaces of THIS call (as ldso_ba_solve_device)
+    const bool project = iteration >= 2 && n_null > 0 && ns;
+    if (project)  // the nullspaces go up before (outside) the captured sequence
         HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
                                c->stream));
-        c->ns_resident = true;
-    }
     // pass + solve + resubstitution: one captured graph per (projection, lambda, n_null) without
     // a communicator or kernel timing; the downloads stay outside it
     auto body = [&]() -> int {
         int r;
         if ((r = ldso_ba_linearize(c, 0, 1))) return r;
-        if ((r = ldso_ba_solve_device(c, project ? 2 : 0, lambda, nullptr, project ? n_null : 0, nullptr))) return r;
+        if ((r = solve_device_launch(c, project ? 2 : 0, project ? n_null : 0))) return r;
         return c->P_tot > 0 ? launch_resubstitute(c, 0, c->P_tot, lambda) : 0;
     };
     if (!c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH")) {
@@ -4359,12 +4557,9 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
                            hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_cprior.p, cp.data(), cp.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_add_priors.p, ap.data(), ap.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    c->ns_resident = false;
-    if (ns) {
+    if (ns)  // evalPT is fixed during optimize(): getNullspaces stays valid for every iteration
         HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
                                c->stream));
-        c->ns_resident = true;  // evalPT is fixed during optimize(): getNullspaces stays valid
-    }
     FrameStepParams F;
     F.wins = c->d_wins.p;
     F.fstate = c->d_fstate.p;
@@ -4381,7 +4576,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     // linearizeAll + applyRes (+ the accumulation the next solve uses)
     auto gn_iteration = [&](int it) -> int {
         int r;
-        if ((r = ldso_ba_solve_device(c, it, 1e-5, nullptr, ns ? 7 : 0, nullptr))) return r;
+        if ((r = solve_device_launch(c, it, ns ? 7 : 0))) return r;
         // the frame / calibration step + FrameFramePrecalc and the resubstitution with the point
         // step applied in place, in one launch (the solve wrote x and xAd)
         const ResubParams R = resub_params(c, 0, c->P_tot, 1e-5, true);

@@ -7,9 +7,9 @@ are replicated.  Every H/b term is a sum over points, so the exchange per GN ite
 fp64 sum all-reduce of the packed upper triangles {HA, bA, Hsc, bsc} of every window
 (2 * ((8N+4)(8N+5)/2 + 8N+4) doubles: 30 KB at N=7, 70 KB at N=11), one of the energy / #IN
 pairs, and one all-gather of the newest frame's NewEnergyWithOutlier slots after which every
-rank re-selects the exact setNewFrameEnergyTH threshold (nth_element is not additive).  Priors
-(HL, bL) are in rank 0's share only.  Each rank then solves the small system redundantly;
-resubstitution is shard-local.
+rank re-selects the exact setNewFrameEnergyTH threshold (nth_element is not additive).  The
+priors (HL, bL) are not part of the reduced system: every rank adds them in its own solve, which
+it runs redundantly on the reduced system; resubstitution is shard-local.
 
 The product runs this exchange itself over RCCL, stream-ordered inside ldso_ba_linearize, once
 the context is attached to a communicator (attach_rccl: ldso_ba_comm_unique_id on rank 0, the

@@ -5,7 +5,11 @@ the machine that runs it, timed over the same pass the GPU step runs (linearizeA
 setNewFrameEnergyTH + accumulate{AF,LF,SCF} + both stitches) on one S7 window:
   (i)  the reference's own threading: IndexThreadReduce with NUM_THREADS = 6 (Settings.h:11);
   (ii) every physical core of socket 0 that this job may use, pinned (sched_setaffinity, the
-       taskset equivalent), one worker per core.
+       taskset equivalent), one worker per core;
+  (iii) batched, like for like with the GPU headline: the same 64 S7 windows (seeds 1000..1063)
+       with one single-threaded window pass per pinned worker process, one process per physical
+       core of socket 0 (the windows are independent, so this is the CPU's best throughput on
+       the GPU's workload).
 Prints one JSON object.  Usage: python -m oracle.cpu_baseline [--seconds S] [--max-cores C]
 """
 import argparse
@@ -77,11 +81,63 @@ def run(lib_path, threads, seconds, cpus=None):
             "r_total": int(w.n_residuals), "r_active": r_active, "value": r_active / med}
 
 
+def _batched_worker(args):
+    """One pinned process: its share of the windows, single-threaded passes round robin until the
+    shared deadline; returns (residuals processed, seconds)."""
+    lib_path, cpu, seeds, start_at, seconds = args
+    import numpy as np
+
+    import oracle
+    from ldso_amd import synth
+
+    os.sched_setaffinity(0, [cpu])
+    tws, ract = [], []
+    for sd in seeds:
+        w = synth.make_window(**synth.S7, seed=sd)
+        ow = oracle.OracleWindow(synth.make_window(**synth.S7, seed=sd), threads=0)
+        ow.iteration()
+        ract.append(int(np.count_nonzero(ow.residuals()["state"] != 1)))  # R_active (OOB is sticky)
+        ow.close()
+        tw = oracle.TimingWindow(w, 0, lib_path)
+        tw.time_iterations(1)  # warm-up
+        tws.append(tw)
+    while time.time() < start_at:
+        time.sleep(0.001)
+    t0 = time.perf_counter()
+    n = 0
+    done = 0
+    while time.perf_counter() - t0 < seconds or done == 0:
+        for tw, ra in zip(tws, ract):
+            tw.time_iterations(1)
+            n += ra
+        done += 1
+    el = time.perf_counter() - t0
+    for tw in tws:
+        tw.close()
+    return n, el, done
+
+
+def run_batched(lib_path, cpus, n_windows, seconds):
+    import multiprocessing as mp
+
+    seeds = [1000 + i for i in range(n_windows)]  # bench.py's rank-0 windows
+    shares = [seeds[k::len(cpus)] for k in range(len(cpus))]
+    start_at = time.time() + 5.0 + 0.25 * max(len(s) for s in shares)  # every worker built its windows
+    ctx = mp.get_context("fork")
+    with ctx.Pool(len(cpus)) as pool:
+        res = pool.map(_batched_worker, [(lib_path, c, sh, start_at, seconds) for c, sh in zip(cpus, shares) if sh])
+    total = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    return {"value": total / el, "seconds": el, "windows": n_windows, "workers": len(res),
+            "passes_per_window": min(r[2] for r in res), "residuals_processed": total}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--max-cores", type=int, default=16)  # the GPU box's CPU share for one GPU
     ap.add_argument("--mode", default="both")
+    ap.add_argument("--windows", type=int, default=64, help="windows of the batched leg (bench.py's B)")
     a = ap.parse_args()
     info = lscpu()
     tmp = tempfile.mkdtemp(prefix="ldso_cpu_")
@@ -103,6 +159,12 @@ def main():
                                 sample=f"1 S7 window (seed 1), median of {rs['passes']} passes, "
                                        f"{len(sock)} workers pinned one per physical core of socket 0 "
                                        f"(capped at the job's {a.max_cores}-CPU share)")
+    rb = run_batched(lib_path, sock, a.windows, a.seconds)
+    out["batched"] = dict(common, cores=len(sock), pinned_cpus=sock, **rb,
+                          sample=f"{a.windows} S7 windows (seeds 1000..{999 + a.windows}), one single-threaded "
+                                 f"window pass at a time per worker, {rb['workers']} worker processes pinned one per "
+                                 f"physical core of socket 0 (capped at the job's {a.max_cores}-CPU share), "
+                                 f"{rb['passes_per_window']}+ passes per window over {rb['seconds']:.1f} s")
     print(json.dumps(out))
 
 

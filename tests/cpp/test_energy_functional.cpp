@@ -6,10 +6,14 @@
 //   optimize x3: resetOOB, linearizeAll (+applyRes, accumulate), solveSystemF, resubstituteF_MT,
 //                the step (test harness: additive frame states, point setIdepth/setIdepthZero),
 //                setDeltaF, calcLEnergyF_MT / calcMEnergyF
-//   flagPointsForRemoval (frame 0's points + every 7th point MARGINALIZED, some OUT),
+//   flagPointsForRemoval (frame 0's points + every 7th point MARGINALIZED, some OUT) with the
+//   reference's per-residual loop (resetOOB, linearize, applyRes, fixLinearizationF): every
+//   residual against the oracle, and ONE device pass for the whole loop,
 //   marginalizePointsF, dropPointsF, marginalizeFrame(frame 0) + dropResidual of its
 //   observations, setAdjointsF / setDeltaF
 //   optimize x2 with the marginalisation prior HM / bM in the solve
+//   EnergyFunctional::optimize (the device GN loop) against ldso_ba_optimize on the same window,
+//   the lazy write-back of the residual fields, then linearizeAll(true) against the oracle
 //
 //   test_energy_functional --cpu   bookkeeping and the no-device error path
 //   test_energy_functional         the GPU cycle
@@ -17,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ldso_amd/energy_functional.h"
@@ -70,6 +75,7 @@ struct Graph {
         calib->wG0 = S.w;
         calib->hG0 = S.h;
         std::memcpy(calib->value_scaledf, S.calib, sizeof(S.calib));
+        for (int k = 0; k < 4; k++) calib->value[k] = calib->value_zero[k] = (double)S.calib[k] * (1.0 / 50.0);
         for (int f = 0; f < S.N; f++) {
             auto F = std::make_shared<FrameHessian>();
             F->frameID = f;
@@ -410,6 +416,57 @@ static int gpu_tests() {
         k++;
     }
     {
+        // FullSystem::flagPointsForRemoval's per-residual loop (FullSystem.cc:1390-1398) on the
+        // MARGINALIZED points, against the oracle's fresh linearisation of the same window state
+        OracleWin O(S, *ef);
+        oracle_window *ow = oracle_create(&O.w);
+        oracle_reset_oob(ow);
+        double eo[3];
+        oracle_linearize_all(ow, 0, eo);
+        const int R = (int)O.order.size();
+        std::vector<int8_t> ns(R), st(R);
+        std::vector<float> se(R), ewo(R), ctr(3 * R), jp(8 * R), rbs(R);
+        std::vector<uint8_t> fl(R);
+        oracle_get_residuals(ow, ns.data(), st.data(), se.data(), ewo.data(), ctr.data(), fl.data(), jp.data(),
+                             rbs.data());
+        oracle_apply_res(ow);
+        std::vector<float> se2(R), jp2(8 * R);
+        oracle_get_residuals(ow, nullptr, nullptr, se2.data(), nullptr, nullptr, nullptr, jp2.data(), nullptr);
+        oracle_destroy(ow);
+        std::unordered_map<const PointFrameResidual *, int> idx;
+        for (int k = 0; k < R; k++) idx[O.order[k]] = k;
+        const long passes0 = ef->devicePasses();
+        int checked = 0, bad = 0, ngood = 0;
+        for (auto &p : ef->allPoints) {
+            if (p->status != PointStatus::MARGINALIZED) continue;
+            for (auto &r : p->residuals) {
+                r->resetOOB();
+                const double e = r->linearize(G.calib);
+                r->isLinearized = false;
+                r->applyRes(true);
+                if (r->isActive()) {
+                    r->fixLinearizationF(ef);
+                    ngood++;
+                }
+                const int k = idx.at(r.get());
+                const bool oob = ns[k] == LDSO_BA_RES_OOB;
+                const double e_ref = oob ? 0.0 : (double)se2[k];
+                bool ok = r->state_NewState == ns[k] && e == e_ref && (float)r->state_NewEnergyWithOutlier == ewo[k] &&
+                          r->isActiveAndIsGoodNEW == (ns[k] == LDSO_BA_RES_IN);
+                if (!oob) ok = ok && std::memcmp(r->centerProjectedTo, &ctr[3 * k], 12) == 0;
+                if (r->isActive()) ok = ok && std::memcmp(r->JpJdF, &jp2[8 * k], 32) == 0;
+                bad += !ok;
+                checked++;
+            }
+        }
+        CHECK(checked > 0 && bad == 0, "flagPointsForRemoval loop: %d of %d residuals differ from the oracle", bad,
+              checked);
+        CHECK(ngood > 0, "no active residual among the marginalised points");
+        CHECK(ef->devicePasses() == passes0 + 1, "per-residual linearize: %ld device passes for one call site",
+              ef->devicePasses() - passes0);
+        CHECK(ef->ok(), "per-residual linearize: %s", ef->lastError().c_str());
+    }
+    {
         OracleWin O(S, *ef);
         oracle_window *ow = oracle_create(&O.w);  // marginalisation relinearises from resetOOB
         std::vector<int> pts;
@@ -473,10 +530,137 @@ static int gpu_tests() {
     return 0;
 }
 
+// EnergyFunctional::optimize (FullSystem::optimize's loop on the device) against the C ABI's
+// ldso_ba_optimize on the same window, bit for bit; then the lazily written-back residual fields
+// and a FullSystem-style linearizeAll(true) against the oracle
+static int gpu_optimize_tests() {
+    Synth S(6, 800, 320, 240, 22);
+    Graph G(S);
+    auto ef = std::make_shared<EnergyFunctional>(0);
+    CHECK(ef->ok(), "context: %s", ef->lastError().c_str());
+    if (!ef->ok()) return 1;
+    G.insertInto(*ef);
+    // the same window through the C ABI, caller order = the synthetic point order
+    const int N = S.N, n = 8 * N + 4;
+    std::vector<float> precalc((size_t)N * N * LDSO_BA_PRECALC_STRIDE);
+    std::vector<double> adH((size_t)N * N * 64), adT((size_t)N * N * 64), cp(4), fp(8 * N), fd(8 * N), fdp(8 * N);
+    ldso_ba_frame_precalc(N, S.fs.data(), S.calib, precalc.data());
+    ldso_ba_set_adjoints(N, S.fs.data(), adH.data(), adT.data(), cp.data());
+    ldso_ba_frame_take_data(N, S.fs.data(), fp.data(), fd.data(), fdp.data());
+    const float cdelta[4] = {0, 0, 0, 0};
+    ldso_ba_window w;
+    std::memset(&w, 0, sizeof(w));
+    w.n_frames = N;
+    w.n_points = S.P;
+    w.n_residuals = S.R;
+    w.width = S.w;
+    w.height = S.h;
+    std::memcpy(w.calib, S.calib, sizeof(w.calib));
+    w.dI = S.dI.data();
+    w.frame_energy_th = S.th.data();
+    w.precalc = precalc.data();
+    w.ad_host = adH.data();
+    w.ad_target = adT.data();
+    w.c_prior = cp.data();
+    w.c_delta = cdelta;
+    w.frame_prior = fp.data();
+    w.frame_delta_prior = fdp.data();
+    w.point_host = S.ph.data();
+    w.point_data = S.pd.data();
+    w.point_res_begin = S.rb.data();
+    w.res_target = S.rt.data();
+    w.res_state = S.rs.data();
+    w.res_energy = S.re.data();
+    w.res_flags = S.rf.data();
+    ldso_ba_ctx *raw = nullptr;
+    CHECK(ldso_ba_create(0, &raw) == 0 && ldso_ba_load(raw, 1, &w, 0, 1) == 0, "raw context: %s", ldso_ba_last_error());
+    std::vector<double> ns((size_t)7 * n), e_raw(3 * 4), cv(4), cz(4), co(4);
+    ldso_ba_nullspaces(N, S.fs.data(), ns.data());
+    for (int k = 0; k < 4; k++) cv[k] = cz[k] = G.calib->value[k];
+    std::vector<ldso_ba_frame_state> fo(N);
+    std::vector<float> id(S.P);
+    CHECK(ldso_ba_optimize(raw, 3, S.fs.data(), cv.data(), cz.data(), ns.data(), e_raw.data(), fo.data(), co.data(),
+                           id.data()) == 0,
+          "ldso_ba_optimize: %s", ldso_ba_last_error());
+
+    std::vector<Vec3> e_face;
+    const long passes0 = ef->devicePasses();
+    const Vec3 last = ef->optimize(3, G.calib, &e_face);
+    CHECK(ef->ok(), "EnergyFunctional::optimize: %s", ef->lastError().c_str());
+    CHECK(ef->devicePasses() == passes0 + 4, "optimize(3) ran %ld passes", ef->devicePasses() - passes0);
+    CHECK(e_face.size() == 4, "energy history size %zu", e_face.size());
+    for (size_t s2 = 0; s2 < e_face.size() && s2 < 4; s2++)
+        CHECK(e_face[s2][0] == e_raw[3 * s2] && e_face[s2][2] == e_raw[3 * s2 + 2], "optimize energy %zu: %.17g vs %.17g",
+              s2, e_face[s2][0], e_raw[3 * s2]);
+    CHECK(last[0] == e_raw[9] && ef->resInA == (int)e_raw[11], "optimize return value");
+    for (int f = 0; f < N; f++)
+        CHECK(std::memcmp(G.frames[f]->state, fo[f].state, sizeof(fo[f].state)) == 0, "frame %d state after optimize", f);
+    for (int k = 0; k < 4; k++) CHECK(G.calib->value[k] == co[k], "calibration after optimize");
+    int badp = 0;
+    for (int p = 0; p < S.P; p++)
+        badp += !(G.points[p]->idepth == id[p] && G.points[p]->idepth_zero == id[p] && G.points[p]->deltaF == 0.f);
+    CHECK(badp == 0, "%d points' idepth differ after optimize", badp);
+
+    // lazy write-back: the residual fields equal the C ABI context's after the same loop
+    ef->syncResiduals();
+    {
+        std::vector<int8_t> rns(S.R), rst(S.R);
+        std::vector<float> rse(S.R), rew(S.R), rctr(3 * S.R), rjp(8 * S.R);
+        std::vector<uint8_t> rfl(S.R);
+        ldso_ba_get_residuals(raw, 0, rns.data(), rst.data(), rse.data(), rew.data(), rctr.data(), rfl.data(), rjp.data(),
+                              nullptr);
+        int bad = 0, k = 0;
+        for (int p = 0; p < S.P; p++)
+            for (auto &r : G.points[p]->residuals) {
+                bad += !(r->state_state == rst[k] && r->state_NewState == rns[k] && (float)r->state_energy == rse[k] &&
+                         (float)r->state_NewEnergyWithOutlier == rew[k] &&
+                         r->isActiveAndIsGoodNEW == ((rfl[k] & LDSO_BA_FLAG_ACTIVE) != 0) &&
+                         std::memcmp(r->centerProjectedTo, &rctr[3 * k], 12) == 0 &&
+                         (!r->isActiveAndIsGoodNEW || std::memcmp(r->JpJdF, &rjp[8 * k], 32) == 0));
+                k++;
+            }
+        CHECK(bad == 0, "%d residuals differ from ldso_ba_optimize's after syncResiduals", bad);
+        std::vector<float> th(N);
+        ldso_ba_get_frame_energy_th(raw, 0, th.data());
+        for (int f = 0; f < N; f++) CHECK(G.frames[f]->frameEnergyTH == th[f], "frameEnergyTH[%d] after optimize", f);
+    }
+    ldso_ba_destroy(raw);
+
+    // FullSystem::optimize's tail: linearizeAll(true) on the stepped state, against the oracle
+    OracleWin O(S, *ef);
+    oracle_window *ow = oracle_create(&O.w);
+    double eo[3];
+    oracle_linearize_all(ow, 1, eo);
+    const Vec3 ef_fix = ef->linearizeAll(true);
+    CHECK(ef->ok(), "linearizeAll(true): %s", ef->lastError().c_str());
+    CHECK(ef_fix[2] == eo[2] && std::fabs(ef_fix[0] - eo[0]) <= 1e-9 * std::fabs(eo[0]), "fix pass energy %.17g vs %.17g",
+          ef_fix[0], eo[0]);
+    const int R = (int)O.order.size();
+    std::vector<int8_t> ons(R), ost(R);
+    std::vector<float> ose(R), oew(R), octr(3 * R), ojp(8 * R), orb(R);
+    std::vector<uint8_t> ofl(R);
+    oracle_get_residuals(ow, ons.data(), ost.data(), ose.data(), oew.data(), octr.data(), ofl.data(), ojp.data(),
+                         orb.data());
+    int bad = 0;
+    for (int k = 0; k < R; k++) {
+        const PointFrameResidual &r = *O.order[k];
+        bad += !(r.state_NewState == ons[k] && r.state_state == ost[k] && (float)r.state_energy == ose[k] &&
+                 (float)r.state_NewEnergyWithOutlier == oew[k] && r.relBS == orb[k] &&
+                 std::memcmp(r.centerProjectedTo, &octr[3 * k], 12) == 0);
+    }
+    CHECK(bad == 0, "linearizeAll(true) after optimize: %d of %d residuals differ from the oracle", bad, R);
+    oracle_destroy(ow);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const bool cpu = argc > 1 && std::strcmp(argv[1], "--cpu") == 0;
-    if (cpu) cpu_tests();
-    else gpu_tests();
+    if (cpu) {
+        cpu_tests();
+    } else {
+        gpu_tests();
+        gpu_optimize_tests();
+    }
     std::printf("%s: %d failure(s)\n", cpu ? "cpu" : "gpu", g_fail);
     return g_fail ? 1 : 0;
 }
