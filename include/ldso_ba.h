@@ -353,10 +353,11 @@ int ldso_ba_export_newest(ldso_ba_ctx *ctx, float *dev_buf, int64_t stride);
 int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *ctx, const float *dev_buf, int32_t n_ranks, int64_t stride);
 
 /* Device-side solve and resubstitution, every loaded window at once:
- *   solve_device         EnergyFunctional::solveSystemF on the GPU, one workgroup per window
- *                        (k_solve_reg: 5 wavefronts, windows of up to 7 keyframes; k_solve: 4
- *                        wavefronts, up to 11), statement for statement ldso_ba_solve (bit-identical
- *                        x).  ns: every window's [7][8N+4] nullspaces back to back; the projection
+ *   solve_device         EnergyFunctional::solveSystemF on the GPU, one workgroup per window, for
+ *                        windows of up to 11 keyframes: by default the unpivoted blocked LDL^T
+ *                        (k_solve_fast); with LDSO_BA_TUNE_SOLVE_EXACT = 1 statement for statement
+ *                        ldso_ba_solve with its diagonal pivoting (k_solve_reg: 5 wavefronts, up to 7
+ *                        keyframes; k_solve: 4 wavefronts, up to 11; x bit-identical).  ns: every window's [7][8N+4] nullspaces back to back; the projection
  *                        (iteration >= 2) uses the nullspaces of THIS call and is skipped when ns is
  *                        NULL, as in the host solver.  x_out: every window's x back to back (or NULL:
  *                        x stays on the device for resubstitute_device).
@@ -413,12 +414,18 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              (default all; each event pair costs the stream a few us)
  *   LDSO_BA_TUNE_ITEM_ORDER    k_linearize chunk order: 0 (default) target-major, 1 host-major;
  *                              set before ldso_ba_load
+ *   LDSO_BA_TUNE_SOLVE_EXACT   device solve (solve_device / iterate / optimize): 0 (default) the
+ *                              unpivoted blocked LDL^T (k_solve_fast: the Jacobi-scaled, damped system
+ *                              is positive definite; x within rounding of the pivoted solve); 1 the
+ *                              pivoted factorisation of the host solver (k_solve_reg / k_solve,
+ *                              x bit-identical to ldso_ba_solve)
  * Keys 1, 3, 4, 5, 8, 9 and 11 named experiment variants that measured slower and were removed
  * (DESIGN.md §5 keeps their numbers); setting them returns -1. */
 #define LDSO_BA_TUNE_TILED_IMAGES 2
 #define LDSO_BA_TUNE_TOP_CHUNK 6
 #define LDSO_BA_TUNE_TIMING_MASK 7
 #define LDSO_BA_TUNE_ITEM_ORDER 10
+#define LDSO_BA_TUNE_SOLVE_EXACT 12
 int ldso_ba_set_tuning(ldso_ba_ctx *ctx, int32_t key, int32_t value);
 int ldso_ba_get_kernel_times(ldso_ba_ctx *ctx, double *ms, int64_t *counts, int32_t n);
 const char *ldso_ba_kernel_name(int32_t i);

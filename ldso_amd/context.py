@@ -110,6 +110,11 @@ class BAContext:
                                                   out.ctypes.data))
         return out
 
+    def update_points(self, win: int, vals: np.ndarray):
+        """ldso_ba_update_points: [P][4] (idepth_scaled, idepth_zero_scaled, priorF, deltaF), caller order."""
+        v = np.ascontiguousarray(vals, np.float32).reshape(-1, 4)
+        L.check(self._lib.ldso_ba_update_points(self._h, int(win), L.ptr(v, L.f32p)))
+
     def reset_oob(self, win: int = -1):
         L.check(self._lib.ldso_ba_reset_oob(self._h, int(win)))
 

@@ -2250,6 +2250,145 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
 }
 
 // ============================================================================================
+// k_solve_fast: the same solveSystemF without pivoting (LDSO_BA_SOLVE_FAST, the default; windows
+// up to 11 keyframes).  After solve_assemble the scaled matrix is symmetric positive definite
+// (Jacobi-scaled HA + priors + lambda damping - Hsc / (1 + lambda)), so an unpivoted LDL^T is
+// stable; dropping the pivot search removes the serial pivot reduction and the cross-wave
+// hand-off of every step.  Blocked right-looking LDL^T in LDS: wave 0 factorises an 8-column
+// panel out of registers (lane = row, the in-panel columns broadcast with readlane), then all
+// four waves apply the panel's rank-8 update to the trailing matrix (one barrier per panel).
+// Every element sees fma(-(c_i c_j), 1/d, A(i,j)) for the steps in ascending order, as the host
+// solver does, just without the row exchanges; L(i,k) = c_i / d.  Wave 0 then runs the
+// substitutions while wave 1 prepares the nullspace projection.  x differs from the pivoted
+// solve (k_solve_reg / k_solve / ldso_ba_solve) only by rounding (tests: within the system's
+// float sensitivity envelope; optimize energies within 1e-4).
+// ============================================================================================
+constexpr int kSolveFastThreads = 256;
+constexpr int kSolveFastPanel = 8;
+__host__ __device__ inline size_t solve_fast_smem_bytes(int n) {
+    // SolveLds | W [8][128] panel columns | rd [8] | raw [7 n] (projection staging)
+    return solve_smem_bytes(n) + 16 + ((size_t)kSolveFastPanel * 128 + kSolveFastPanel + 7 * (size_t)n) * sizeof(double);
+}
+__global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P) {
+#pragma clang fp contract(off)
+    extern __shared__ double lds[];
+    const WinDev W = P.wins[blockIdx.x];  // a register copy (see k_solve)
+    const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ld = solve_ld(n);
+    const SolveLds S(lds, n);
+    double *H = S.H;
+    double *Wc = lds + (solve_smem_bytes(n) + 16) / sizeof(double);  // [8][128]: c of each panel step
+    double *rdv = Wc + kSolveFastPanel * 128;
+    double *raw = rdv + kSolveFastPanel;
+    solve_assemble<kSolveFastThreads>(P, W, S, tid);
+    for (int p = 0; p < n; p += kSolveFastPanel) {
+        const int w = min(kSolveFastPanel, n - p);
+        if (wave == 0) {
+            // panel columns p .. p+w-1 of rows i = lane, lane + 64 (lower triangle incl. diagonal)
+            double r[2][kSolveFastPanel];
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+                for (int jj = 0; jj < kSolveFastPanel; jj++) {
+                    const int i = lane + 64 * h;
+                    r[h][jj] = i < n && jj < w && i >= p + jj ? H[i * ld + p + jj] : 0.0;
+                }
+#pragma unroll
+            for (int kk = 0; kk < kSolveFastPanel; kk++) {
+                if (kk >= w) break;
+                const int k = p + kk;
+                const double d = k < 64 ? readlane_f64(r[0][kk], k) : readlane_f64(r[1][kk], k - 64);
+                const double rd = d != 0 ? 1.0 / d : 0.0;
+#pragma unroll
+                for (int jj = kk + 1; jj < kSolveFastPanel; jj++) {
+                    if (jj >= w) break;
+                    const int j = p + jj;
+                    const double cj = j < 64 ? readlane_f64(r[0][kk], j) : readlane_f64(r[1][kk], j - 64);  // A(j, k)
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int i = lane + 64 * h;
+                        if (i >= j && i < n) r[h][jj] = fma(-(r[h][kk] * cj), rd, r[h][jj]);
+                    }
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int i = lane + 64 * h;
+                    if (i < n) Wc[kk * 128 + i] = i > k ? r[h][kk] : 0.0;
+                    if (i > k && i < n) H[i * ld + k] = d != 0 ? r[h][kk] / d : 0.0;
+                    if (i == k) H[i * ld + k] = d;
+                }
+                if (lane == 0) rdv[kk] = rd;
+            }
+        }
+        __syncthreads();
+        // rank-w update of the trailing lower triangle (p + w <= j <= i < n), steps in order
+        const int m0 = p + w, nt = n - m0;
+        const int ne = nt * (nt + 1) / 2;
+        for (int e = tid; e < ne; e += kSolveFastThreads) {
+            int ii = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);  // row ii of the nt x nt triangle
+            if (ii * (ii + 1) / 2 > e) ii--;
+            if ((ii + 1) * (ii + 2) / 2 <= e) ii++;
+            const int i = m0 + ii, j = m0 + (e - ii * (ii + 1) / 2);
+            double a = H[i * ld + j];
+            for (int kk = 0; kk < w; kk++) a = fma(-(Wc[kk * 128 + i] * Wc[kk * 128 + j]), rdv[kk], a);
+            H[i * ld + j] = a;
+        }
+        __syncthreads();
+    }
+    if (wave == 1 && P.iteration >= 2 && P.n_null > 0) solve_ortho_prepare(P, W, S, raw, lane);
+    if (wave == 0) {
+        // substitutions (y in lanes i, i + 64), as k_solve without the permutation
+        const int ia = lane, ib = lane + 64, ra = min(ia, n - 1), rb = min(ib, n - 1);
+        double ya = ia < n ? S.b[ia] : 0.0, yb = ib < n ? S.b[ib] : 0.0;
+        constexpr int kSubAhead = 4;
+        for (int j0 = 0; j0 < n; j0 += kSubAhead) {
+            double fa[kSubAhead], fb[kSubAhead];
+#pragma unroll
+            for (int u = 0; u < kSubAhead; u++) {
+                const int j = min(j0 + u, n - 1);
+                fa[u] = H[ra * ld + j];
+                fb[u] = H[rb * ld + j];
+            }
+#pragma unroll
+            for (int u = 0; u < kSubAhead; u++) {
+                const int j = j0 + u;
+                if (j >= n) break;
+                const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+                if (ia > j && ia < n) ya = fma(-fa[u], yj, ya);
+                if (ib > j && ib < n) yb = fma(-fb[u], yj, yb);
+            }
+        }
+        if (ia < n) ya = H[ia * ld + ia] != 0 ? ya / H[ia * ld + ia] : 0.0;
+        if (ib < n) yb = H[ib * ld + ib] != 0 ? yb / H[ib * ld + ib] : 0.0;
+        for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
+            double fa[kSubAhead], fb[kSubAhead];
+#pragma unroll
+            for (int u = 0; u < kSubAhead; u++) {
+                const int j = max(j0 - u, 0);
+                fa[u] = H[j * ld + ra];
+                fb[u] = H[j * ld + rb];
+            }
+#pragma unroll
+            for (int u = 0; u < kSubAhead; u++) {
+                const int j = j0 - u;
+                if (j < 0) break;
+                const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
+                if (ia < j) ya = fma(-fa[u], yj, ya);
+                if (ib < j) yb = fma(-fb[u], yj, yb);
+            }
+        }
+        if (ia < n) S.y[ia] = S.sc[ia] * ya;  // x = s y
+        if (ib < n) S.y[ib] = S.sc[ib] * yb;
+    }
+    __syncthreads();
+    if (wave == 0) solve_ortho_apply_store(P, W, S, lane);
+    if (P.xad) {  // x is in S.y: the resubstitution's xAd by all four waves
+        __syncthreads();
+        xad_fill(W, S.y, P.adH, P.adT, P.xad + (size_t)blockIdx.x * kXadStride, tid, kSolveFastThreads);
+    }
+}
+
+// ============================================================================================
 // k_resubstitute: EnergyFunctional::resubstituteFPt (EnergyFunctional.cc:638-667)
 // ============================================================================================
 // ---- sharded setNewFrameEnergyTH ---------------------------------------
@@ -2823,6 +2962,7 @@ struct ldso_ba_ctx {
     bool timing = false;
     unsigned timing_mask = ~0u;  // kernel slots bracketed by events when timing is on
     int top_chunk = 0;  // residuals per k_linearize wave (0 = automatic); LDSO_BA_TUNE_TOP_CHUNK
+    int solve_exact = 0;  // LDSO_BA_TUNE_SOLVE_EXACT: 1 = the pivoted k_solve_reg / k_solve (bit-identical to the host)
     int img_mode = 3;   // 3 intensity only (band_offset), 1 [I, dx, dy, 0] 2x4 tiles (LDSO_BA_TUNE_TILED_IMAGES)
     std::vector<PendingEv> pending;
     std::vector<hipEvent_t> ev_pool;
@@ -4357,8 +4497,15 @@ int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
                                   (int)solve_smem_bytes(kSolveMaxDim));
         (void)hipFuncSetAttribute((const void *)k_solve_reg, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)solve_reg_smem_bytes(kSolveRegDim));
+        (void)hipFuncSetAttribute((const void *)k_solve_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)solve_fast_smem_bytes(kSolveMaxDim));
     });
-    // windows of up to 7 keyframes (n <= 64): the register factorisation; larger: the LDS one
+    if (!c->solve_exact && !getenv_flag("LDSO_BA_SOLVE_LDS")) {  // the default: unpivoted, xAd fused
+        const size_t smem = solve_fast_smem_bytes(dmax);
+        return timed_launch(c, 5, c->stream,
+                            [&] { k_solve_fast<<<c->n_win, kSolveFastThreads, smem, c->stream>>>(S); });
+    }
+    // exact mode: windows of up to 7 keyframes (n <= 64) the register factorisation, larger the LDS one
     const bool reg = dmax <= kSolveRegDim && !getenv_flag("LDSO_BA_SOLVE_LDS");
     const size_t smem = reg ? solve_reg_smem_bytes(dmax) : solve_smem_bytes(dmax);
     int rc = timed_launch(c, 5, c->stream, [&] {
@@ -4740,6 +4887,11 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
     if (key == LDSO_BA_TUNE_ITEM_ORDER) {
         if (c->n_win) return fail(-1, "item order must be chosen before ldso_ba_load");
         c->item_order = value != 0;
+        return 0;
+    }
+    if (key == LDSO_BA_TUNE_SOLVE_EXACT) {
+        if (value != 0 && value != 1) return fail(-1, "solve mode must be 0 (fast) or 1 (exact)");
+        c->solve_exact = value;
         return 0;
     }
     if (key == LDSO_BA_TUNE_TIMING_MASK) {

@@ -380,7 +380,9 @@ def test_device_solve_and_resubstitute_match_host_path(built, kernel, monkeypatc
         monkeypatch.setenv("LDSO_BA_SOLVE_LDS", "1")
     ws = [synth.make_window(**cf) for cf in cfgs]
     ns = [w.nullspaces() for w in ws]
-    c = BAContext(0).load(ws)
+    c = BAContext(0)
+    c.set_tuning(12, 1)  # LDSO_BA_TUNE_SOLVE_EXACT: the pivoted factorisation
+    c.load(ws)
     c.linearize()
     for it in (0, 2):
         xd = c.solve_device(it, 1e-5, ns)
@@ -410,6 +412,69 @@ def test_device_solve_and_resubstitute_match_host_path(built, kernel, monkeypatc
         np.testing.assert_array_equal(xs[i], xs_ref[i])
         np.testing.assert_array_equal(sts[i], st_ref[i])
         assert e[i][2] == e_ref[i][2] and abs(e[i][0] - e_ref[i][0]) <= 1e-12 * abs(e_ref[i][0])
+    c.close()
+
+
+@pytest.mark.parametrize("it", [0, 2])
+def test_fast_device_solve_matches_host_within_rounding(built, it):
+    """The default device solve (k_solve_fast: unpivoted blocked LDL^T on the Jacobi-scaled,
+    damped, positive definite system) against the host's pivoted solver on the same stitched
+    system: x within 20x the system's float-rounding sensitivity envelope (and 1e-9 relative at
+    worst), for windows of 3 to 11 keyframes batched in one launch; then its resubstitution
+    against the host-staged one from the same x."""
+    cfgs = [dict(n_frames=3, n_points=120, seed=70), dict(n_frames=7, n_points=900, seed=71),
+            dict(n_frames=11, n_points=1200, seed=72), dict(n_frames=5, n_points=400, seed=73),
+            dict(n_frames=7, n_points=300, seed=75, baseline=0.2)]
+    ws = [synth.make_window(**cf) for cf in cfgs]
+    ns = [w.nullspaces() for w in ws]
+    c = BAContext(0).load(ws)
+    c.linearize()
+    xd = c.solve_device(it, 1e-5, ns)
+    for i, w in enumerate(ws):
+        xh = c.solve(i, it, 1e-5, ns[i])
+        env = sensitivity(w.n_frames, it, c.system(i), ns[i], xh)
+        rel = np.linalg.norm(xd[i] - xh) / np.linalg.norm(xh)
+        print(f"window {i} (N={w.n_frames}) it={it}: |x_fast - x_host|/|x_host| = {rel:.3e}, envelope {env:.3e}")
+        assert rel <= max(1e-12, min(1e-9, 20 * env))
+    sd = c.resubstitute_device(1e-5)
+    for i in range(len(ws)):
+        sh = c.resubstitute(i, xd[i], 1e-5)
+        np.testing.assert_array_equal(sd[i], sh)
+    c.close()
+
+
+def test_iterate_replay_refreshes_host_copies_and_projects_only_with_this_calls_nullspaces(built):
+    """A replayed ldso_ba_iterate graph invalidates the host copies of the system / energies (the
+    replay skips the captured calls' host side), and a device solve projects only with the
+    nullspaces passed in THAT call (none: no projection, as the host solver)."""
+    cfg = dict(n_frames=5, n_points=400, seed=61)
+    w = synth.make_window(**cfg)
+    ns = [w.nullspaces()]
+    c = BAContext(0).load([w])
+    c.set_tuning(12, 1)  # exact mode: bit-identical to the host solver
+    c.update_points(0, w.point_data[:, 2:6])  # allocates its staging now, so the graph below stays valid
+    c.iterate(2, 1e-5, ns)  # captures the graph
+    s0 = c.system(0)        # host copy cached
+    vals = np.stack([w.point_data[:, 2] * 1.01, w.point_data[:, 3], w.point_data[:, 4], w.point_data[:, 5]], 1)
+    c.update_points(0, vals)
+    e, _, _ = c.iterate(2, 1e-5, ns)  # replays on the changed points
+    s1 = c.system(0)
+    w2 = synth.make_window(**cfg)
+    w2.point_data[:, 2] = vals[:, 0]
+    fresh = BAContext(0).load([w2])
+    fresh.linearize()
+    sf = fresh.system(0)
+    for k in ("HA", "Hsc", "bA", "bsc"):
+        np.testing.assert_array_equal(s1[k], sf[k], err_msg=k)
+    assert not np.array_equal(s0["HA"], s1["HA"])
+    assert e[0][2] == fresh.energy(0)[2]
+    # projection only with this call's nullspaces
+    x_ns = c.solve_device(2, 1e-5, ns)[0]
+    x_none = c.solve_device(2, 1e-5, None)[0]
+    np.testing.assert_array_equal(x_ns, c.solve(0, 2, 1e-5, ns[0]))
+    np.testing.assert_array_equal(x_none, c.solve(0, 2, 1e-5, None))
+    assert not np.array_equal(x_ns, x_none)
+    fresh.close()
     c.close()
 
 
