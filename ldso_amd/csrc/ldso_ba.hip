@@ -2445,11 +2445,11 @@ __global__ __launch_bounds__(256) void k_xad(const WinDev *__restrict__ wins, co
 // ============================================================================================
 // k_activate: FullSystem::optimizeImmaturePoint (FullSystem.cc:1035-1156) with
 // ImmaturePoint::linearizeResidual (ImmaturePoint.cc:319-389), SURVEY §8f row 4.
-// One wavefront per immature point; lane r owns the temporary residual to the r-th other frame
-// (window order) and evaluates its 8 pattern pixels; the point's Hdd, bd and energy are then
-// summed on every lane in the reference's order (residual by residual, pixel by pixel, with the
-// pixels before an OOB pixel still counted), so the LM steps are wave-uniform and bit-identical
-// to the CPU restatement.
+// One wavefront per immature point; the temporary residual to the r-th other frame (window order)
+// is evaluated by eight lanes, one per pattern pixel (see k_activate); the point's Hdd, bd and
+// energy are summed on every lane in the reference's order (residual by residual, pixel by pixel,
+// with the pixels before an OOB pixel still counted), so the LM steps are wave-uniform and
+// bit-identical to the CPU restatement.
 // ============================================================================================
 struct ActParams {
     const WinDev *__restrict__ wins;
@@ -2481,113 +2481,136 @@ __device__ inline float3 sample33(const float4 *__restrict__ img, int mode, int 
                        w11 * t11.z + w01 * t01.z + w10 * t10.z + w00 * t00.z);
 }
 
+// Lanes per (residual, pattern pixel): lane 8 r' + idx evaluates pattern pixel idx of the
+// temporary residual r = 8 round + r' (up to 8 residuals per round, two rounds for windows above
+// 9 keyframes), so a residual's eight taps are sampled in parallel instead of one after another.
+// The per-pixel terms go through the wave's LDS slot and every lane then folds them in the
+// reference's order -- per residual the pixels up to its first OOB pixel, the residuals in window
+// order -- so the point's energy, Hdd and bd, and every residual state, are wave-uniform and
+// bit-identical to the CPU restatement.
+constexpr int kActRes = 16;  // residual slots per point (N <= 16 -> at most 15)
+struct ActLds {              // one wavefront's slot
+    float e[kActRes][8], h[kActRes][8], b[kActRes][8];
+    int first_oob[kActRes];  // pattern index of the first OOB pixel (8: none)
+    float st_energy[kActRes], st_newenergy[kActRes];
+    int st_state[kActRes], st_new[kActRes];
+};
 __global__ __launch_bounds__(256) void k_activate(ActParams P) {
 #pragma clang fp contract(off)
     constexpr int pat[8][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {0, 0}, {2, 0}, {-1, 1}, {0, 2}};
     constexpr float kMinIdepthHAct = 100;  // setting_minIdepthH_act, Setting.cc:25
     constexpr int kGNItsOnPointActivation = 3;  // Setting.cc:47
+    __shared__ ActLds lds_act[4];
     const int lane = threadIdx.x & 63;
     const int k = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (k >= P.n) return;
+    ActLds &A = lds_act[threadIdx.x >> 6];
     const WinDev &W = P.wins[P.win];
     const ldso_ct_immature &ip = P.pts[k];
-    const int N = W.N, host = ip.host, nres = N - 1;
+    const int N = W.N, host = ip.host, nres = N - 1, rounds = (nres + 7) >> 3;
     const float fxl = W.calib[0], fyl = W.calib[1], cxl = W.calib[2], cyl = W.calib[3];
     const float fxli = 1.0f / fxl, fyli = 1.0f / fyl;
-    const float u0 = ip.u, v0 = ip.v, eth = ip.energy_th;
-    // this lane's temporary residual (ImmaturePointTemporaryResidual, ImmaturePoint.h:18-26)
-    const bool mine = lane < nres;
-    const int tgt = mine ? lane + (lane >= host) : host;
-    int st_state = LDSO_BA_RES_IN, st_new = LDSO_BA_RES_OUTLIER;
-    float st_energy = 0, st_newenergy = 0;  // doubles in the reference holding float values
-    const float *pre = P.precalc + (size_t)(W.pair_base + host + N * tgt) * LDSO_BA_PRECALC_STRIDE;
-    const float4 *img = P.img + (size_t)(W.frame_base + tgt) * P.frame_stride;
-    float R[9], t[3];
-#pragma unroll
-    for (int i = 0; i < 9; i++) R[i] = pre[27 + i];  // PRE_RTll (current poses, ImmaturePoint.cc:336-337)
-#pragma unroll
-    for (int i = 0; i < 3; i++) t[i] = pre[36 + i];  // PRE_tTll
-    const float aff0 = pre[24], aff1 = pre[25];
-    float col[8], wsq[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        col[i] = ip.color[i];
-        wsq[i] = ip.weights[i] * ip.weights[i];
+    const float eth = ip.energy_th;
+    const int idx = lane & 7;
+    // this lane's pattern pixel in the host frame (ImmaturePoint.cc:336-343)
+    const float K0 = (ip.u + pat[idx][0] - cxl) * fxli, K1 = (ip.v + pat[idx][1] - cyl) * fyli;
+    const float col = ip.color[idx], wsq = ip.weights[idx] * ip.weights[idx];
+    if (lane < kActRes) {  // ImmaturePointTemporaryResidual (ImmaturePoint.h:18-26) of slot lane
+        A.st_state[lane] = LDSO_BA_RES_IN;
+        A.st_new[lane] = LDSO_BA_RES_OUTLIER;
+        A.st_energy[lane] = 0;
+        A.st_newenergy[lane] = 0;
     }
+    wave_lds_sync();
 
     // linearizeResidual(HCalib, slack, tmpRes, Hdd, bd, idepth) of every residual, then the
     // point's sums in the reference's order -> (energy, Hdd, bd), identical on every lane
     auto evaluate = [&](float slack, float idepth, float &E, float &Hdd, float &bd) {
-        float tH[8], tb[8];
-        int nvalid = 0;
-        float ret = st_energy;
-        if (mine) {
-            if (st_state == LDSO_BA_RES_OOB) {
-                st_new = LDSO_BA_RES_OOB;
-            } else {
-                float energyLeft = 0;
+        for (int rd = 0; rd < rounds; rd++) {
+            const int r = 8 * rd + (lane >> 3);
+            if (r < nres && A.st_state[r] != LDSO_BA_RES_OOB) {
+                const int tgt = r + (r >= host);
+                const float *pre = P.precalc + (size_t)(W.pair_base + host + N * tgt) * LDSO_BA_PRECALC_STRIDE;
+                const float *R = pre + 27, *t = pre + 36;  // PRE_RTll, PRE_tTll (current poses)
                 bool oob = false;
+                float e = 0, h = 0, b = 0;
+                float ptp[3];
 #pragma unroll
-                for (int idx = 0; idx < 8; idx++) {
-                    tH[idx] = tb[idx] = 0;
-                    if (oob) continue;
-                    const float K0 = (u0 + pat[idx][0] - cxl) * fxli, K1 = (v0 + pat[idx][1] - cyl) * fyli;
-                    float ptp[3];
-#pragma unroll
-                    for (int i = 0; i < 3; i++) ptp[i] = (R[3 * i] * K0 + R[3 * i + 1] * K1 + R[3 * i + 2] * 1.0f) + t[i] * idepth;
-                    const float drescale = 1.0f / ptp[2];
-                    const float uu = ptp[0] * drescale, vv = ptp[1] * drescale;
-                    const float Ku = uu * fxl + cxl, Kv = vv * fyl + cyl;
-                    if (!(drescale > 0) || !(Ku > 1.1f && Kv > 1.1f && Ku < W.wM3 && Kv < W.hM3)) {
-                        oob = true;
-                        continue;
-                    }
+                for (int i = 0; i < 3; i++) ptp[i] = (R[3 * i] * K0 + R[3 * i + 1] * K1 + R[3 * i + 2] * 1.0f) + t[i] * idepth;
+                const float drescale = 1.0f / ptp[2];
+                const float uu = ptp[0] * drescale, vv = ptp[1] * drescale;
+                const float Ku = uu * fxl + cxl, Kv = vv * fyl + cyl;
+                if (!(drescale > 0) || !(Ku > 1.1f && Kv > 1.1f && Ku < W.wM3 && Kv < W.hM3)) {
+                    oob = true;
+                } else {
+                    const float4 *img = P.img + (size_t)(W.frame_base + tgt) * P.frame_stride;
                     const float3 hc = sample33(img, P.img_mode, P.tpr, P.frame_stride, Ku, Kv);
                     if (!isfinite(hc.x)) {
                         oob = true;
-                        continue;
+                    } else {
+                        const float residual = hc.x - (pre[24] * col + pre[25]);
+                        float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
+                        e = wsq * hw * residual * residual * (2 - hw);
+                        const float dxInterp = hc.y * fxl, dyInterp = hc.z * fyl;
+                        const float d_idepth =
+                            (dxInterp * drescale * (t[0] - t[2] * uu) + dyInterp * drescale * (t[1] - t[2] * vv)) *
+                            kScaleIdepth;
+                        hw *= wsq;
+                        h = (hw * d_idepth) * d_idepth;
+                        b = (hw * residual) * d_idepth;
                     }
-                    const float residual = hc.x - (aff0 * col[idx] + aff1);
-                    float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
-                    energyLeft += wsq[idx] * hw * residual * residual * (2 - hw);
-                    const float dxInterp = hc.y * fxl, dyInterp = hc.z * fyl;
-                    const float d_idepth =
-                        (dxInterp * drescale * (t[0] - t[2] * uu) + dyInterp * drescale * (t[1] - t[2] * vv)) * kScaleIdepth;
-                    hw *= wsq[idx];
-                    tH[idx] = (hw * d_idepth) * d_idepth;
-                    tb[idx] = (hw * residual) * d_idepth;
-                    nvalid = idx + 1;
                 }
-                if (oob) {
-                    st_new = LDSO_BA_RES_OOB;
+                A.e[r][idx] = e;
+                A.h[r][idx] = h;
+                A.b[r][idx] = b;
+                const unsigned long long m = __ballot(oob);  // this round's OOB pixels
+                if (idx == 0) {
+                    const unsigned g = (unsigned)(m >> (8 * (lane >> 3))) & 0xFFu;
+                    A.first_oob[r] = g ? __builtin_ctz(g) : 8;
+                }
+            } else {
+                (void)__ballot(false);  // every lane takes part in the ballot
+            }
+        }
+        wave_lds_sync();
+        // the reference's order on every lane: residual by residual, pixel by pixel
+        for (int r = 0; r < nres; r++) {
+            float ret = A.st_energy[r];
+            if (A.st_state[r] == LDSO_BA_RES_OOB) {
+                if (lane == 0) A.st_new[r] = LDSO_BA_RES_OOB;
+            } else {
+                const int fo = A.first_oob[r];
+                float energyLeft = 0;
+                for (int i = 0; i < fo; i++) {
+                    energyLeft += A.e[r][i];
+                    Hdd += A.h[r][i];
+                    bd += A.b[r][i];
+                }
+                int ns;
+                if (fo < 8) {
+                    ns = LDSO_BA_RES_OOB;
                 } else {
                     if (energyLeft > eth * slack) {
                         energyLeft = eth * slack;
-                        st_new = LDSO_BA_RES_OUTLIER;
+                        ns = LDSO_BA_RES_OUTLIER;
                     } else {
-                        st_new = LDSO_BA_RES_IN;
+                        ns = LDSO_BA_RES_IN;
                     }
-                    st_newenergy = energyLeft;
                     ret = energyLeft;
+                    if (lane == 0) A.st_newenergy[r] = energyLeft;
                 }
+                if (lane == 0) A.st_new[r] = ns;
             }
+            E = (float)((double)E + (double)ret);
         }
-        for (int r = 0; r < nres; r++) {
-            const int nv = __shfl(nvalid, r, 64);
-#pragma unroll
-            for (int idx = 0; idx < 8; idx++) {
-                const float h_ = __shfl(tH[idx], r, 64), b_ = __shfl(tb[idx], r, 64);
-                if (idx < nv) {
-                    Hdd += h_;
-                    bd += b_;
-                }
-            }
-            E = (float)((double)E + (double)__shfl(ret, r, 64));
-        }
+        wave_lds_sync();
     };
     auto commit = [&]() {
-        st_state = st_new;
-        st_energy = st_newenergy;
+        if (lane < nres) {
+            A.st_state[lane] = A.st_new[lane];
+            A.st_energy[lane] = A.st_newenergy[lane];
+        }
+        wave_lds_sync();
     };
 
     float lastEnergy = 0, lastHdd = 0, lastbd = 0;
@@ -2626,7 +2649,7 @@ __global__ __launch_bounds__(256) void k_activate(ActParams P) {
     }
     unsigned mask = 0;
     if (status == 0) {
-        const unsigned long long in = __ballot(mine && st_state == LDSO_BA_RES_IN);
+        const unsigned long long in = __ballot(lane < nres && A.st_state[lane] == LDSO_BA_RES_IN);
         if (__popcll(in) < P.min_obs) {
             status = 1;
         } else {

@@ -151,6 +151,11 @@ struct CtResParams {
     int n, wl, hl, lvl, write_warp, n_blocks;
     float fxl, fyl, cxl, cyl, cutoffTH, maxEnergy;
     float Ki[9];
+    // k_ct_calc_res<true> (ldso_ct_calc_res_gs): one pose passed by value, and calcGSSSE's 45
+    // Accumulator9 terms of every warped point summed in the same pass
+    CtPose pose0;
+    float gs_a, gs_b0;
+    double *gs_parts;  // [blocks][kGsParts]
 };
 
 template <int K>
@@ -170,8 +175,35 @@ __device__ __forceinline__ void block_sum_write(double (&v)[K], double *dst) {
     for (int k = threadIdx.x; k < K; k += kCtThreads) dst[k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
 }
 
+// calcGSSSE's Jacobian row of one warped point (CoarseTracker.cc:696-722) from the values the
+// warped buffers hold: id, u, v, dx = dI.y fxl, dy = dI.z fyl, refColor, residual
+__device__ __forceinline__ void ct_gs_terms(float id, float u, float v, float dx, float dy, float a, float b0,
+                                            float refColor, float residual, float w, double *acc) {
+    float J[9];
+    J[0] = id * dx;
+    J[1] = id * dy;
+    J[2] = 0 - id * (u * dx + v * dy);
+    J[3] = 0 - ((u * v) * dx + dy * (1 + v * v));
+    J[4] = (u * v) * dy + dx * (1 + u * u);
+    J[5] = u * dy - v * dx;
+    J[6] = a * (b0 - refColor);
+    J[7] = -1;
+    J[8] = residual;
+    int k = 0;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+        const float Jw = J[r] * w;
+#pragma unroll
+        for (int c = r; c < 9; c++) acc[k++] = (double)(Jw * J[c]);
+    }
+}
+
+template <bool kGS>
 __global__ __launch_bounds__(kCtThreads) void k_ct_calc_res(CtResParams P) {
-    const CtPose &T = P.poses[blockIdx.y];
+    const CtPose &T = kGS ? P.pose0 : P.poses[blockIdx.y];
+    double gs[kGS ? kGsParts : 1];
+#pragma unroll
+    for (int k = 0; k < (kGS ? kGsParts : 1); k++) gs[k] = 0;
     const int i = blockIdx.x * kCtThreads + threadIdx.x;
     double acc[kResParts] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (i < P.n) {
@@ -235,12 +267,18 @@ __global__ __launch_bounds__(kCtThreads) void k_ct_calc_res(CtResParams P) {
                         P.warp[2 * (size_t)i] = make_float4(new_idepth, u, v, h1);
                         P.warp[2 * (size_t)i + 1] = make_float4(h2, residual, hw, refColor);
                     }
+                    if constexpr (kGS)
+                        ct_gs_terms(new_idepth, u, v, h1 * P.fxl, h2 * P.fyl, P.gs_a, P.gs_b0, refColor, residual, hw, gs);
                 }
             }
         }
         if (P.write_warp) P.state[i] = st;
     }
     block_sum_write<kResParts>(acc, P.parts + ((size_t)blockIdx.y * P.n_blocks + blockIdx.x) * kResParts);
+    if constexpr (kGS) {
+        __syncthreads();  // block_sum_write's LDS is reused
+        block_sum_write<kGsParts>(gs, P.gs_parts + (size_t)blockIdx.x * kGsParts);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -262,26 +300,7 @@ __global__ __launch_bounds__(kCtThreads) void k_ct_calc_gs(CtGsParams P) {
     for (int k = 0; k < kGsParts; k++) acc[k] = 0;
     if (i < P.n && P.state[i] == 2) {
         const float4 q0 = P.warp[2 * (size_t)i], q1 = P.warp[2 * (size_t)i + 1];
-        const float id = q0.x, u = q0.y, v = q0.z;
-        const float dx = q0.w * P.fxl, dy = q1.x * P.fyl;
-        float J[9];
-        J[0] = id * dx;
-        J[1] = id * dy;
-        J[2] = 0 - id * (u * dx + v * dy);
-        J[3] = 0 - ((u * v) * dx + dy * (1 + v * v));
-        J[4] = (u * v) * dy + dx * (1 + u * u);
-        J[5] = u * dy - v * dx;
-        J[6] = P.a * (P.b0 - q1.w);
-        J[7] = -1;
-        J[8] = q1.y;
-        const float w = q1.z;
-        int k = 0;
-#pragma unroll
-        for (int r = 0; r < 9; r++) {
-            const float Jw = J[r] * w;
-#pragma unroll
-            for (int c = r; c < 9; c++) acc[k++] = (double)(Jw * J[c]);
-        }
+        ct_gs_terms(q0.x, q0.y, q0.z, q0.w * P.fxl, q1.x * P.fyl, P.a, P.b0, q1.w, q1.y, q1.z, acc);
     }
     block_sum_write<kGsParts>(acc, P.parts + (size_t)blockIdx.x * kGsParts);
 }
@@ -755,12 +774,17 @@ int check_level(const ldso_ct_ctx *c, int lvl) {
 }
 
 // launch calcRes for n_hyp poses already staged in h_poses (partials to d_parts[0, n_hyp*nb*8))
-int launch_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_warp, size_t extra_parts) {
+// gs (n_hyp == 1): the pose by value and calcGSSSE in the same kernel (k_ct_calc_res<true>), its
+// partials at d_parts + n_hyp * nb * kResParts
+int launch_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_warp, size_t extra_parts,
+                    bool gs = false, double aff_a = 0, double aff_b = 0) {
     const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
     const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
     int rc = ensure_parts(c, (size_t)n_hyp * nb * kResParts + extra_parts);
     if (rc) return rc;
-    CT_TRY(hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n_hyp * sizeof(CtPose), hipMemcpyHostToDevice, c->stream));
+    if (!gs)
+        CT_TRY(hipMemcpyAsync(c->d_poses, c->h_poses, (size_t)n_hyp * sizeof(CtPose), hipMemcpyHostToDevice,
+                              c->stream));
     CtResParams P;
     P.pc = c->d_pc + c->pc_off[lvl];
     P.img = c->d_dIp + c->pyr.off[lvl];
@@ -781,7 +805,18 @@ int launch_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool wri
     P.cutoffTH = cutoffTH;
     P.maxEnergy = 2 * kHuberTH * cutoffTH - kHuberTH * kHuberTH;  // CoarseTracker.cc:565-566
     for (int k = 0; k < 9; k++) P.Ki[k] = c->Ki[lvl][k];
-    return ct_launch(c, 2, [&] { k_ct_calc_res<<<dim3(nb, n_hyp), kCtThreads, 0, c->stream>>>(P); });
+    P.pose0 = c->h_poses[0];
+    P.gs_parts = c->d_parts + (size_t)n_hyp * nb * kResParts;
+    P.gs_a = 0;
+    P.gs_b0 = 0;
+    if (gs) {
+        float aLL, bLL;
+        affine_from_to(c->ref_exposure, c->new_exposure, c->ref_a, c->ref_b, (float)aff_a, (float)aff_b, aLL, bLL);
+        P.gs_a = (float)(double)aLL;
+        P.gs_b0 = c->ref_b;
+        return ct_launch(c, 2, [&] { k_ct_calc_res<true><<<dim3(nb, 1), kCtThreads, 0, c->stream>>>(P); });
+    }
+    return ct_launch(c, 2, [&] { k_ct_calc_res<false><<<dim3(nb, n_hyp), kCtThreads, 0, c->stream>>>(P); });
 }
 
 // the Vec6 of every hypothesis from the block partials already on the host
@@ -1117,9 +1152,9 @@ int ldso_ct_calc_res_gs(ldso_ct_ctx *c, int32_t lvl, const double ref_to_new[12]
     const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
     const size_t res_parts = (size_t)nb * kResParts;
     make_pose(c, lvl, ref_to_new, (float)aff_a, (float)aff_b, c->h_poses[0]);
-    rc = launch_calc_res(c, lvl, 1, cutoff_th, true, (size_t)nb * kGsParts);
-    if (rc) return rc;
-    rc = launch_calc_gs(c, lvl, aff_a, aff_b, res_parts);  // same stream: reads the warped buffers just written
+    // calcRes and calcGSSSE in one launch (the GS terms of each warped point from the same values
+    // the warped buffers receive; the block partials are those of k_ct_calc_gs)
+    rc = launch_calc_res(c, lvl, 1, cutoff_th, true, (size_t)nb * kGsParts, true, aff_a, aff_b);
     if (rc) return rc;
     CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (res_parts + (size_t)nb * kGsParts) * sizeof(double),
                           hipMemcpyDeviceToHost, c->stream));

@@ -232,6 +232,51 @@ def test_shards_sum_to_full(built):
     full.close()
 
 
+def test_s11_split_over_four_contexts(built):
+    """BASELINE config 4's split as far as one GPU allows: the S11 window (11 keyframes, 8000
+    points) loaded as 4 contexts with shard_count = 4 (the host-frame partition of SURVEY §8e).
+    The four partial systems sum to the unsharded one within BLOCK_TOL, the four energy / #IN
+    pairs sum to the unsharded ones, and ldso_ba_frame_threshold_gathered over the four exported
+    newest-frame slots re-selects the unsharded setNewFrameEnergyTH threshold on every shard."""
+    import ctypes as C
+
+    import torch
+
+    from ldso_amd import _lib as L
+
+    cfg = dict(synth.S11, seed=2)
+    world = 4
+    full = BAContext(0).load([synth.make_window(**cfg)])
+    full.linearize()
+    s_full, e_full, th_full = full.system(0), full.energy(0), full.frame_energy_th(0)
+    full.close()
+    shards = [BAContext(0).load([synth.make_window(**cfg)], shard_rank=r, shard_count=world) for r in range(world)]
+    parts, strides = [], []
+    for c in shards:
+        c.linearize()
+        parts.append((c.system(0), c.energy(0)))
+        st = C.c_int64()
+        L.check(c._lib.ldso_ba_newest_stride(c._h, C.byref(st)))
+        strides.append(st.value)
+    assert sum(c.stats()["residuals"] for c in shards) == synth.make_window(**cfg).n_residuals
+    N = cfg["n_frames"]
+    for k in ("HA", "Hsc"):
+        assert block_errors(sum(p[0][k] for p in parts), s_full[k], N) < BLOCK_TOL, k
+    for k in ("bA", "bsc"):
+        assert vec_block_errors(sum(p[0][k] for p in parts), s_full[k], N) < BLOCK_TOL, k
+    assert sum(p[1][2] for p in parts) == e_full[2]
+    assert abs(sum(p[1][0] for p in parts) - e_full[0]) <= 1e-9 * abs(e_full[0])
+    stride = max(strides)
+    gathered = torch.empty(world * stride, dtype=torch.float32, device="cuda")
+    for r, c in enumerate(shards):
+        L.check(c._lib.ldso_ba_export_newest(c._h, gathered[r * stride:].data_ptr(), stride))
+    torch.cuda.synchronize()
+    for c in shards:
+        L.check(c._lib.ldso_ba_frame_threshold_gathered(c._h, gathered.data_ptr(), world, stride))
+        np.testing.assert_array_equal(c.frame_energy_th(0)[-1], th_full[-1])
+        c.close()
+
+
 def test_s11_window(ctx):
     cfg = dict(synth.S11, seed=2)
     ctx.load([synth.make_window(**cfg)])
