@@ -191,12 +191,13 @@ class BAContext:
             o += n
         return out
 
-    def solve_device(self, iteration: int = 0, lam: float = 1e-5, nullspaces=None):
-        """x of every window (solveSystemF on the GPU); nullspaces: list of [7][8N+4] arrays."""
+    def solve_device(self, iteration: int = 0, lam: float = 1e-5, nullspaces=None, n_null: int = 7):
+        """x of every window (solveSystemF on the GPU); nullspaces: list of [7][8N+4] arrays, of
+        which the first n_null rows project."""
         ns = self._ns_all(nullspaces)
         x = np.zeros(sum(w.dim for w in self.windows), np.float64)
         L.check(self._lib.ldso_ba_solve_device(self._h, int(iteration), float(lam), L.ptr(ns, L.f64p),
-                                               0 if ns is None else 7, L.ptr(x, L.f64p)))
+                                               0 if ns is None else int(n_null), L.ptr(x, L.f64p)))
         return self._split(x, [w.dim for w in self.windows])
 
     def resubstitute_device(self, lam: float = 1e-5):

@@ -508,6 +508,9 @@ static_assert(32 * kTopRow <= kWaveLds, "the Top operand table (one half) reuses
 // LDS requested per 4-wave workgroup: sets the resident workgroups per CU (= waves per SIMD).
 // 160 KB / 32 KB = 5: measured fastest (64 x S7: 121.6 us; 4 blocks 125.7, 3 blocks 143.5; 6
 // waves/SIMD need <= 80 VGPRs and spill, 145 us).
+#ifndef LDSO_LIN_CW_LDS
+#define LDSO_LIN_CW_LDS 1  // color / weights staged in the sums table (0: gathered per step)
+#endif
 #ifndef LDSO_LIN_BLOCKS_PER_CU
 #define LDSO_LIN_BLOCKS_PER_CU 5
 #endif
@@ -554,6 +557,25 @@ __global__ __launch_bounds__(256, 4) void k_linearize(LinParams P) {
     float new_energy = P.rs_newenergy[rq];
     float4 centre = P.rs_center[rq];
     const float4 my_pd0 = *(const float4 *)(P.pt_data + (size_t)my_point * LDSO_BA_POINT_STRIDE);
+#if LDSO_LIN_CW_LDS
+    // the point's color[8] and weights[8] (record floats 8..23: one 64-B piece per residual)
+    // into this residual's row of the sums table: phase A's pattern lanes read them from LDS at
+    // the step that later overwrites the row with the residual's sums (no per-step gathers)
+    {
+        const float4 *cw = reinterpret_cast<const float4 *>(P.pt_data + (size_t)my_point * LDSO_BA_POINT_STRIDE + 8);
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = cw[u];
+        float *row = lds_sums_w + lane * kSumStride;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            row[4 * u] = v[u].x;
+            row[4 * u + 1] = v[u].y;
+            row[4 * u + 2] = v[u].z;
+            row[4 * u + 3] = v[u].w;
+        }
+    }
+#endif
     if (!valid) my_state = LDSO_BA_RES_OOB;
     // marginalisation pass: Jp * delta of fixLinearizationF (Residuals.cc:221-232) from the centre
     // geometry, per residual, before the pattern pixels need it (dot products left to right)
@@ -584,6 +606,9 @@ __global__ __launch_bounds__(256, 4) void k_linearize(LinParams P) {
     }
 
     // ---------------- phase A: pattern pixels, 8 residuals per step -------------------------
+#if LDSO_LIN_CW_LDS
+    wave_lds_sync();  // every row's color / weights are in before any lane reads another's
+#endif
     {
 #pragma clang fp contract(off)
         const int g = lane >> 3, sl = lane & 7;
@@ -614,9 +639,15 @@ __global__ __launch_bounds__(256, 4) void k_linearize(LinParams P) {
                 q.jx = __shfl(jp_dx, j, kWave);
                 q.jy = __shfl(jp_dy, j, kWave);
             }
+#if LDSO_LIN_CW_LDS
+            (void)p;
+            q.color = S[j * kSumStride + sl];
+            q.weight = S[j * kSumStride + 8 + sl];
+#else
             const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
             q.color = pd[8 + sl];
             q.weight = pd[16 + sl];
+#endif
             const float up = pu + px, vp = pv + py;
             float ptp[3];
 #pragma unroll
@@ -956,6 +987,8 @@ struct StitchParams {
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
     int pair_base;  // first global pair of this launch
+    const int *__restrict__ frame_win;  // k_stitch_host: window of each global frame
+    int frame_base;                     // k_stitch_host: first global host frame of this launch
     int win_base;   // first window of this launch
     int n_win;      // windows of this launch: blocks [0, n_win) run their setNewFrameEnergyTH
 };
@@ -1452,6 +1485,324 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
 }
 
 // ============================================================================================
+// k_stitch_host + k_stitch_host_sum (the default for windows of up to kHostStitchMaxN keyframes):
+// one 256-thread block per host frame i of every window stitches everything host i owns --
+// the Top pairs (i, t) (AccumulatedTopHessian.cc:213-239) and host i's Schur complement
+// (AccumulatedSCHessian.cc:80-114, its targets j, k) -- into a dense packed partial system
+// {HA, bA, Hsc, bsc} of the window, and k_stitch_host_sum adds the N partials of every element in
+// host order (no atomics: the system is bitwise repeatable).  The terms are k_stitch's, grouped
+// by host instead of by pair:
+//   HA  (f,f): f == i: sum_t AH_it A_t AH_it^T; else AT_if A_f AT_if^T
+//       (f1<f2): f1 == i: AH_i,f2 A AT_i,f2^T; f2 == i: (AH_i,f1 A AT_i,f1^T)^T; else 0
+//       (c,f): f == i: sum_t AH_it A_t[8C]; else AT_if A_f[8C]    b(f) likewise, (c,c) / b(c): sum_t
+//   Hsc (f,f): f == i: sum_j AH_ij S_j; else AT_if D_ff AT_if^T   with S_j = sum_k D_jk AH_ik^T
+//       (f1<f2): i not in {f1,f2}: AT_i,f1 D_f1f2 AT_i,f2^T; f2 == i: AT_i,f1 S_f1; f1 == i: (AT_i,f2 S_f2)^T
+//       (c,f) / b(f): f == i: sum_j AH_ij E_j / EB_j; else AT_if E_f / EB_f;  (c,c) / b(c): accHcc / accbc
+// where A_t is pair (i,t)'s 13x13 AccumulatorApprox block and D, E, EB, accHcc, accbc the blocks of
+// G_i = U^T diag(HdiF) U (k_point_sc's chunk partials summed in double).  Everything host i
+// reads is staged in LDS once: G_i (both triangles), the adjoints of the N pairs (i, k), the
+// N-1 Top accumulators; then X_jk = AT_ij D_jk (j <= k), S_j, TH_t = AH_it A_t, TT_t = AT_it A_t;
+// then every element of the partial.  Windows with more keyframes use k_stitch's records.
+// ============================================================================================
+constexpr int kHostStitchMaxN = 12;
+__host__ __device__ inline int hs_k5(int N) { return 8 * (N - 1) + 5; }
+__host__ __device__ inline int hs_ldg(int N) { return hs_k5(N) | 1; }
+__host__ __device__ inline int hs_npair(int N) { return (N - 1) * N / 2; }
+__host__ __device__ inline size_t hs_lds_doubles(int N) {
+    return (size_t)hs_k5(N) * hs_ldg(N) + 2 * 64 * (size_t)N + 96 * (size_t)N + 64 * (size_t)hs_npair(N) +
+           3 * 64 * (size_t)N;
+}
+// tile index t of the upper-tile order (a <= b) over nt tile rows -> (a, b)
+__device__ __forceinline__ void tile_ab(int t, int nt, int &a, int &b) {
+    int r = 0;
+    while (t >= nt - r) {
+        t -= nt - r;
+        r++;
+    }
+    a = r;
+    b = r + t;
+}
+__global__ __launch_bounds__(kStThreads) void k_stitch_host(StitchParams P) {
+    extern __shared__ double sm[];
+    if ((int)blockIdx.x < P.n_win) {  // setNewFrameEnergyTH + the energy sum, as k_stitch
+        const int w = P.win_base + blockIdx.x;
+        frame_threshold_and_energy(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
+        return;
+    }
+    if (!P.accumulate) return;
+    const int fr = P.frame_base + blockIdx.x - P.n_win;
+    const int w = P.frame_win[fr];
+    const WinDev &W = P.wins[w];
+    const int N = W.N, D = W.D, i = fr - W.frame_base, tid = threadIdx.x;
+    const int Kc = 8 * (N - 1), K5 = Kc + 5, ldg = K5 | 1, nt = W.KP / 4, per = W.ntiles * 16;
+    const int Nm1 = N - 1, npair = hs_npair(N);
+    double *Gd = sm;                     // [K5][ldg] G_i, both triangles
+    double *AH = Gd + (size_t)K5 * ldg;  // [N][64] adH of pair (i, k)
+    double *AT = AH + 64 * N;            // [N][64] adT of pair (i, k)
+    double *acc = AT + 64 * N;           // [N][96] Top accumulator of pair (i, t) (t == i unused)
+    double *X = acc + 96 * N;            // [npair][64] X_jk = AT_ij D_jk, target slots sj <= sk
+    double *SS = X + 64 * npair;         // [N][64] S_j = sum_k D_jk AH_ik^T
+    double *TH = SS + 64 * N;            // [N][64] AH_it A_t(88)
+    double *TT = TH + 64 * N;            // [N][64] AT_it A_t(88)
+    auto frame_of = [&](int slot) { return slot < i ? slot : slot + 1; };
+    auto A_t = [&](int t, int r, int c) { return acc[96 * t + top_slot(r, c)]; };
+    // ---- every load of the block in one round trip -------------------------------------
+    {
+        // G_i: each float4 of the host's chunk partials is one row of a 4x4 tile; summed over the
+        // chunks in order (four in flight), then written to both triangles
+        const int2 hi = P.host_items[W.frame_base + i];
+        const float4 *slab = reinterpret_cast<const float4 *>(P.sc_slab + W.sc_slab_base +
+                                                              (size_t)(hi.x - W.sc_item_base) * per);
+        const int per4 = per / 4;
+        for (int q = tid; q < per4; q += kStThreads) {
+            double s[4] = {0, 0, 0, 0};
+            int k = 0;
+            for (; k + 4 <= hi.y; k += 4) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = slab[(size_t)(k + u) * per4 + q];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    s[0] += (double)v[u].x;
+                    s[1] += (double)v[u].y;
+                    s[2] += (double)v[u].z;
+                    s[3] += (double)v[u].w;
+                }
+            }
+            for (; k < hi.y; k++) {
+                const float4 v = slab[(size_t)k * per4 + q];
+                s[0] += (double)v.x;
+                s[1] += (double)v.y;
+                s[2] += (double)v.z;
+                s[3] += (double)v.w;
+            }
+            int a, b;
+            tile_ab(q >> 2, nt, a, b);
+            const int row = 4 * a + (q & 3);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int col = 4 * b + u;
+                if (row < K5 && col < K5 && row <= col) {
+                    Gd[row * ldg + col] = s[u];
+                    Gd[col * ldg + row] = s[u];
+                }
+            }
+        }
+        // the adjoints of the pairs (i, k), k = 0..N-1
+        for (int e = tid; e < 64 * N; e += kStThreads) {
+            const size_t pk = (size_t)(W.pair_base + i + N * (e >> 6)) * 64 + (e & 63);
+            AH[e] = P.adH[pk];
+            AT[e] = P.adT[pk];
+        }
+        // Top accumulators of the pairs (i, t): 24 float4 per item, summed over the pair's items
+        for (int e = tid; e < 24 * Nm1; e += kStThreads) {
+            const int t = frame_of(e / 24), q = e % 24;
+            const int2 pi = P.pair_items[W.pair_base + i + N * t];
+            const float4 *src = reinterpret_cast<const float4 *>(P.top_slab + (size_t)pi.x * kTopVals) + q;
+            double s[4] = {0, 0, 0, 0};
+            int k = 0;
+            for (; k + 4 <= pi.y; k += 4) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = src[(size_t)(k + u) * (kTopVals / 4)];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    s[0] += (double)v[u].x;
+                    s[1] += (double)v[u].y;
+                    s[2] += (double)v[u].z;
+                    s[3] += (double)v[u].w;
+                }
+            }
+            for (; k < pi.y; k++) {
+                const float4 v = src[(size_t)k * (kTopVals / 4)];
+                s[0] += (double)v.x;
+                s[1] += (double)v.y;
+                s[2] += (double)v.z;
+                s[3] += (double)v.w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc[96 * t + 4 * q + u] = s[u];
+        }
+    }
+    __syncthreads();
+    // ---- intermediates: X_jk (sj <= sk), S_j, TH_t, TT_t ---------------------------------
+    {
+        const int nx = 64 * npair, ns = nx + 64 * Nm1, nh = ns + 64 * Nm1, total = nh + 64 * Nm1;
+        for (int u = tid; u < total; u += kStThreads) {
+            const int r = (u >> 3) & 7, c = u & 7;
+            if (u < nx) {  // X_jk[r][c] = sum_q AT_ij[r][q] D_jk[q][c]
+                const int pj = u >> 6;
+                int sj = 0, rem = pj;
+                while (rem >= Nm1 - sj) {
+                    rem -= Nm1 - sj;
+                    sj++;
+                }
+                const int sk = sj + rem, j = frame_of(sj);
+                const double *at = AT + 64 * j + 8 * r, *d = Gd + (8 * sj) * ldg + 8 * sk + c;
+                double v = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++) v += at[q] * d[q * ldg];
+                X[u] = v;
+            } else if (u < ns) {  // S_j[r][c] = sum_k (sum_q D_jk[r][q] AH_ik[c][q]), k in slot order
+                const int sj = (u - nx) >> 6, j = frame_of(sj);
+                double v = 0;
+                for (int sk = 0; sk < Nm1; sk++) {
+                    const double *d = Gd + (8 * sj + r) * ldg + 8 * sk, *ah = AH + 64 * frame_of(sk) + 8 * c;
+                    double t = 0;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) t += d[q] * ah[q];
+                    v += t;
+                }
+                SS[64 * j + 8 * r + c] = v;
+            } else {  // TH_t / TT_t [r][c] = sum_k AH_it / AT_it [r][k] A_t(4+k, 4+c)
+                const bool th = u < nh;
+                const int t = frame_of((u - (th ? ns : nh)) >> 6);
+                const double *ad = (th ? AH : AT) + 64 * t + 8 * r;
+                double v = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) v += ad[k] * A_t(t, 4 + k, 4 + c);
+                (th ? TH : TT)[64 * t + 8 * r + c] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- host i's partial system: every packed element written (zeros included) ------------
+    const long long pl = packed_len(D);
+    double *HAp = P.stage + W.stage_base + (size_t)i * sys_len(D), *bAp = HAp + pl, *Hsp = bAp + D, *bsp = Hsp + pl;
+    auto xblk = [&](int sj, int sk) { return X + 64 * (sj * Nm1 - sj * (sj - 1) / 2 + (sk - sj)); };
+    auto dot8 = [](const double *a, const double *b) {
+        double v = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) v += a[q] * b[q];
+        return v;
+    };
+    auto dot8s = [](const double *a, const double *b, int sb) {  // b strided
+        double v = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) v += a[q] * b[q * sb];
+        return v;
+    };
+    const int nb = N * N * 64;
+    for (int u = tid; u < nb; u += kStThreads) {  // frame blocks (f1 <= f2)
+        const int f1 = u / (N * 64), f2 = (u >> 6) % N, r = (u >> 3) & 7, c = u & 7;
+        if (f2 < f1 || (f1 == f2 && r > c)) continue;
+        double ha = 0, hs = 0;
+        if (f1 == f2) {
+            const int f = f1;
+            if (f == i) {
+                for (int st = 0; st < Nm1; st++) {  // sum over t / j in frame order
+                    const int t = frame_of(st);
+                    ha += dot8(TH + 64 * t + 8 * r, AH + 64 * t + 8 * c);
+                    hs += dot8s(AH + 64 * t + 8 * r, SS + 64 * t + c, 8);
+                }
+            } else {
+                const int sf = f < i ? f : f - 1;
+                ha = dot8(TT + 64 * f + 8 * r, AT + 64 * f + 8 * c);
+                hs = dot8(xblk(sf, sf) + 8 * r, AT + 64 * f + 8 * c);
+            }
+        } else if (f1 == i) {
+            ha = dot8(TH + 64 * f2 + 8 * r, AT + 64 * f2 + 8 * c);
+            hs = dot8s(AT + 64 * f2 + 8 * c, SS + 64 * f2 + r, 8);  // (AT_i,f2 S_f2)^T
+        } else if (f2 == i) {
+            ha = dot8(TH + 64 * f1 + 8 * c, AT + 64 * f1 + 8 * r);  // (AH A AT^T)^T of pair (i, f1)
+            hs = dot8s(AT + 64 * f1 + 8 * r, SS + 64 * f1 + c, 8);  // AT_i,f1 S_f1
+        } else {
+            const int s1 = f1 < i ? f1 : f1 - 1, s2 = f2 < i ? f2 : f2 - 1;
+            hs = dot8(xblk(s1, s2) + 8 * r, AT + 64 * f2 + 8 * c);
+        }
+        const long long q = pk_index(4 + 8 * f1 + r, 4 + 8 * f2 + c, D);
+        HAp[q] = ha;
+        Hsp[q] = hs;
+    }
+    for (int u = tid; u < 32 * N + 8 * N + 20; u += kStThreads) {
+        double ha = 0, hs = 0;
+        long long q;
+        bool bvec = false;
+        if (u < 32 * N) {  // (calib cc, frame f, rr)
+            const int f = u >> 5, rr = (u >> 2) & 7, cc = u & 3;
+            if (f == i) {
+                for (int st = 0; st < Nm1; st++) {
+                    const int t = frame_of(st);
+                    double a = 0, b = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        a += AH[64 * t + 8 * rr + k] * A_t(t, 4 + k, cc);
+                        b += AH[64 * t + 8 * rr + k] * Gd[(8 * st + k) * ldg + Kc + cc];
+                    }
+                    ha += a;
+                    hs += b;
+                }
+            } else {
+                const int sf = f < i ? f : f - 1;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    ha += AT[64 * f + 8 * rr + k] * A_t(f, 4 + k, cc);
+                    hs += AT[64 * f + 8 * rr + k] * Gd[(8 * sf + k) * ldg + Kc + cc];
+                }
+            }
+            q = pk_index(cc, 4 + 8 * f + rr, D);
+        } else if (u < 40 * N) {  // b(f)[rr]
+            const int f = (u - 32 * N) >> 3, rr = u & 7;
+            if (f == i) {
+                for (int st = 0; st < Nm1; st++) {
+                    const int t = frame_of(st);
+                    double a = 0, b = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        a += AH[64 * t + 8 * rr + k] * A_t(t, 4 + k, 12);
+                        b += AH[64 * t + 8 * rr + k] * Gd[(8 * st + k) * ldg + Kc + 4];
+                    }
+                    ha += a;
+                    hs += b;
+                }
+            } else {
+                const int sf = f < i ? f : f - 1;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    ha += AT[64 * f + 8 * rr + k] * A_t(f, 4 + k, 12);
+                    hs += AT[64 * f + 8 * rr + k] * Gd[(8 * sf + k) * ldg + Kc + 4];
+                }
+            }
+            q = 4 + 8 * f + rr;
+            bvec = true;
+        } else {  // the calibration block (16, upper used) and b(calib) (4)
+            const int l = u - 40 * N;
+            const int r = l < 16 ? l >> 2 : l - 16, cI = l < 16 ? (l & 3) : 12, cS = l < 16 ? (l & 3) : 4;
+            if (l < 16 && r > cI) continue;
+            for (int st = 0; st < Nm1; st++) ha += A_t(frame_of(st), r, cI);
+            hs = Gd[(Kc + r) * ldg + Kc + cS];
+            bvec = l >= 16;
+            q = bvec ? r : pk_index(r, cI, D);
+        }
+        if (bvec) {
+            bAp[q] = ha;
+            bsp[q] = hs;
+        } else {
+            HAp[q] = ha;
+            Hsp[q] = hs;
+        }
+    }
+}
+// sys = sum over the window's hosts of their partials, in host order, one thread per element
+__global__ __launch_bounds__(256) void k_stitch_host_sum(const WinDev *__restrict__ wins,
+                                                          const int2 *__restrict__ blocks,
+                                                          const double *__restrict__ stage, double *sys) {
+    const int2 bw = blocks[blockIdx.x];  // {window, first element of this block}
+    const WinDev &W = wins[bw.x];
+    const long long n_el = sys_len(W.D), e = (long long)bw.y + threadIdx.x;
+    if (e >= n_el) return;
+    const double *p = stage + W.stage_base + e;
+    double x[kHostStitchMaxN];
+#pragma unroll
+    for (int h = 0; h < kHostStitchMaxN; h++) x[h] = p[(size_t)min(h, W.N - 1) * n_el];
+    double v = 0;
+#pragma unroll
+    for (int h = 0; h < kHostStitchMaxN; h++)
+        if (h < W.N) v += x[h];
+    sys[W.sys_base + e] = v;
+}
+
+// ============================================================================================
 // k_solve: EnergyFunctional::solveSystemF on the GPU, one workgroup of 4 wavefronts per window
 // (SURVEY §8f row 1).  Statement for statement the host solver (host_math.cpp solve_system:
 // assembly with the FIX_LAMBDA damping, Jacobi scaling, lower-triangle LDL^T with diagonal
@@ -1495,8 +1846,10 @@ struct SolveParams {
     double *x;                         // [vec]
     const double *adH, *adT;           // k_solve_reg with xad non-null: also the resubstitution's
     float *xad;                        // xAd from the solution (k_xad fused)
+    const double *prep_nm, *prep_g;    // k_ortho_prep's results: Nm [vec][n_null], per window G | G^-1 | fast
     int iteration, n_null;
 };
+constexpr int kPrepGStride = 128;  // doubles per window in prep_g: G [49], G^-1 [49], fast flag
 // H's row stride in LDS: odd (in doubles), so a column walk touches 32 distinct bank pairs
 __host__ __device__ inline int solve_ld(int n) { return n | 1; }
 __host__ __device__ inline size_t solve_smem_bytes(int n) {
@@ -1695,7 +2048,40 @@ __device__ __forceinline__ void solve_ortho_prepare(const SolveParams &P, const 
     wave_lds_sync();
 }
 
-// the x-dependent half (one wavefront, after solve_ortho_prepare's results are visible): N^T y,
+// k_ortho_prep runs solve_ortho_prepare once per nullspace upload (the nullspaces, hence Nm, G
+// and G^-1, stay fixed over an optimize() call and usually over consecutive iterate calls); the
+// solve kernels load the results with their assembly loads, every thread, before the assembly's
+// barriers.
+__device__ __forceinline__ void solve_ortho_load(const SolveParams &P, const WinDev &W, const SolveLds &S, int tid,
+                                                 int nthreads) {
+    if (P.iteration < 2 || P.n_null <= 0) return;
+    const int n = W.D, kk = P.n_null;
+    const double *nm = P.prep_nm + (size_t)7 * W.vec_base, *g = P.prep_g + (size_t)kPrepGStride * blockIdx.x;
+    for (int e = tid; e < kk * n; e += nthreads) S.Nm[e] = nm[e];
+    if (tid < 49) {
+        S.G[tid] = g[tid];
+        S.Gi[tid] = g[49 + tid];
+    }
+    if (tid == 0) S.misc[7] = g[98];
+}
+
+__global__ __launch_bounds__(64) void k_ortho_prep(SolveParams P, double *prep_nm, double *prep_g) {
+    extern __shared__ double lds[];
+    const WinDev W = P.wins[blockIdx.x];
+    const int n = W.D, kk = P.n_null, lane = threadIdx.x;
+    const SolveLds S(lds, n);
+    double *raw = lds + (solve_smem_bytes(n) + 15) / 16 * 2;
+    solve_ortho_prepare(P, W, S, raw, lane);  // ends with its results visible to the wave
+    double *nm = prep_nm + (size_t)7 * W.vec_base, *g = prep_g + (size_t)kPrepGStride * blockIdx.x;
+    for (int e = lane; e < kk * n; e += 64) nm[e] = S.Nm[e];
+    if (lane < 49) {
+        g[lane] = S.G[lane];
+        g[49 + lane] = S.Gi[lane];
+    }
+    if (lane == 0) g[98] = S.misc[7];
+}
+
+// the x-dependent half (one wavefront, after solve_ortho_load's results are visible): N^T y,
 // coef = G^-1 N^T y (fast path) or the round-robin Jacobi pseudo-inverse of host_math.cpp
 // project_out, y -= Nm coef; then x (= y) to global memory.
 __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, const WinDev &W, const SolveLds &S,
@@ -1866,6 +2252,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
         tri[t] = e < noff ? ((i * ld + j) | (i << 16) | (j << 23)) : 0;  // padding: (0, 0), never stored
     }
     auto at = [&](int r, int c) -> double & { return H[r * ld + c]; };
+    solve_ortho_load(P, W, S, tid, kSolveThreads);
     solve_assemble<kSolveThreads>(P, W, S, tid);
     // ---- LDL^T with symmetric diagonal pivoting (lower triangle).  Wave 0 runs the serial part
     // of each step (pivot, swap, column k) with the diagonal in its registers (lane i mod 64); all
@@ -1998,7 +2385,6 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
     wave_lds_sync();
     for (int i = lane; i < n; i += 64) y[i] = sc[i] * b[i];  // x
     wave_lds_sync();
-    if (P.iteration >= 2 && P.n_null > 0) solve_ortho_prepare(P, W, S, H, lane);  // H is free now
     solve_ortho_apply_store(P, W, S, lane);
 }
 
@@ -2183,12 +2569,12 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
     const SolveLds S(lds, n);
     const RegLds R(lds, n);
     for (int i = tid; i < kSolveRegDim; i += kSolveRegThreads) R.flag[i] = 0;
+    solve_ortho_load(P, W, S, tid, kSolveRegThreads);
     solve_assemble<kSolveRegThreads>(P, W, S, tid);  // its barriers also publish the flags
     if (wave == 4) __builtin_amdgcn_s_setprio(0);  // the factorisation's chain first
     else __builtin_amdgcn_s_setprio(2);
     if (wave == 4) {
         // ---- the projection's x-independent half, then the substitutions (physical rows)
-        if (P.iteration >= 2 && P.n_null > 0) solve_ortho_prepare(P, W, S, R.raw, lane);
         double y = lane < n ? S.b[lane] : 0.0;
         unsigned long long act = n >= 64 ? ~0ull : ((1ull << n) - 1);
         for (int k = 0; k < n; k++) {  // forward: y_i = fma(-L(i,k), y_k, y_i), k ascending
@@ -2258,16 +2644,128 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
 // panel out of registers (lane = row, the in-panel columns broadcast with readlane), then all
 // four waves apply the panel's rank-8 update to the trailing matrix (one barrier per panel).
 // Every element sees fma(-(c_i c_j), 1/d, A(i,j)) for the steps in ascending order, as the host
-// solver does, just without the row exchanges; L(i,k) = c_i / d.  Wave 0 then runs the
+// solver does, just without the row exchanges; L(i,k) = c_i * (1/d).  Wave 0 then runs the
 // substitutions while wave 1 prepares the nullspace projection.  x differs from the pivoted
 // solve (k_solve_reg / k_solve / ldso_ba_solve) only by rounding (tests: within the system's
 // float sensitivity envelope; optimize energies within 1e-4).
 // ============================================================================================
-constexpr int kSolveFastThreads = 256;
+#ifndef LDSO_SOLVE_FAST_THREADS
+#define LDSO_SOLVE_FAST_THREADS 512
+#endif
+constexpr int kSolveFastThreads = LDSO_SOLVE_FAST_THREADS;  // 8 waves: the trailing updates hide LDS latency
 constexpr int kSolveFastPanel = 8;
+#ifndef LDSO_EXP_SOLVE_SKIP  // timing experiments only (tools/solve_ab.py): 1 panels, 2 trailing, 4 subst, 8 apply
+#define LDSO_EXP_SOLVE_SKIP 0
+#endif
 __host__ __device__ inline size_t solve_fast_smem_bytes(int n) {
-    // SolveLds | W [8][128] panel columns | rd [8] | raw [7 n] (projection staging)
-    return solve_smem_bytes(n) + 16 + ((size_t)kSolveFastPanel * 128 + kSolveFastPanel + 7 * (size_t)n) * sizeof(double);
+    // SolveLds | W [8][128] panel columns | rd [8]
+    return solve_smem_bytes(n) + 16 + ((size_t)kSolveFastPanel * 128 + kSolveFastPanel) * sizeof(double);
+}
+// row k's value of a lane-per-row register pair (rows lane, lane + 64)
+template <int kH>
+__device__ __forceinline__ double fast_row(const double (&v)[kH], int k) {
+    if constexpr (kH == 1)
+        return readlane_f64(v[0], k);
+    else
+        return k < 64 ? readlane_f64(v[0], k) : readlane_f64(v[1], k - 64);
+}
+// Wave 0: LDL^T of panel columns p .. p+w-1 (rows lane + 64 h).  Lane i updates its rows'
+// panel entries unconditionally -- entries above the diagonal and rows past n turn into finite
+// junk that is never stored nor read -- so a step is one readlane pair and one mul + fma per
+// later column and row half, with the h = 1 half compiled out for n <= 64.
+template <int kH>
+__device__ __forceinline__ void fast_panel(double *H, double *Wc, double *rdv, int n, int ld, int p, int w,
+                                           int lane) {
+#pragma clang fp contract(off)
+    double r[kSolveFastPanel][kH];
+#pragma unroll
+    for (int h = 0; h < kH; h++)
+#pragma unroll
+        for (int jj = 0; jj < kSolveFastPanel; jj++) {
+            const int i = lane + 64 * h;
+            r[jj][h] = i < n && jj < w && i >= p + jj ? H[i * ld + p + jj] : 0.0;
+        }
+#pragma unroll
+    for (int kk = 0; kk < kSolveFastPanel; kk++) {
+        if (kk >= w) break;
+        const int k = p + kk;
+        const double d = fast_row<kH>(r[kk], k);
+        const double rd = d != 0 ? 1.0 / d : 0.0;
+#pragma unroll
+        for (int jj = kk + 1; jj < kSolveFastPanel; jj++) {
+            const double cj = fast_row<kH>(r[kk], p + jj);  // A(j, k); columns past n are junk
+#pragma unroll
+            for (int h = 0; h < kH; h++) r[jj][h] = fma(-(r[kk][h] * cj), rd, r[jj][h]);
+        }
+#pragma unroll
+        for (int h = 0; h < kH; h++) {
+            const int i = lane + 64 * h;
+            if (i < n) Wc[kk * 128 + i] = r[kk][h];  // the trailing update reads rows >= p + w only
+            if (i > k && i < n) H[i * ld + k] = r[kk][h] * rd;  // L(i,k) (rd = 0 for d = 0)
+            if (i == k) H[i * ld + k] = d;
+        }
+        if (lane == 0) rdv[kk] = rd;
+    }
+}
+// Wave 0: L y = b, D, L^T x = y (y in lanes i, i + 64), as k_solve without the permutation
+template <int kH>
+__device__ __forceinline__ void fast_subst(const double *H, const SolveLds &S, int n, int ld, int lane) {
+#pragma clang fp contract(off)
+    double y[kH];
+    int ri[kH];
+#pragma unroll
+    for (int h = 0; h < kH; h++) {
+        const int i = lane + 64 * h;
+        y[h] = i < n ? S.b[i] : 0.0;
+        ri[h] = min(i, n - 1);
+    }
+    constexpr int kSubAhead = 4;
+    for (int j0 = 0; j0 < n; j0 += kSubAhead) {
+        double f[kSubAhead][kH];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++)
+#pragma unroll
+            for (int h = 0; h < kH; h++) f[u][h] = H[ri[h] * ld + min(j0 + u, n - 1)];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = j0 + u;
+            if (j >= n) break;
+            const double yj = fast_row<kH>(y, j);
+#pragma unroll
+            for (int h = 0; h < kH; h++) {
+                const int i = lane + 64 * h;
+                if (i > j && i < n) y[h] = fma(-f[u][h], yj, y[h]);
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < kH; h++) {
+        const int i = lane + 64 * h;
+        if (i < n) y[h] = H[i * ld + i] != 0 ? y[h] / H[i * ld + i] : 0.0;
+    }
+    for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
+        double f[kSubAhead][kH];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++)
+#pragma unroll
+            for (int h = 0; h < kH; h++) f[u][h] = H[max(j0 - u, 0) * ld + ri[h]];
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++) {
+            const int j = j0 - u;
+            if (j < 0) break;
+            const double yj = fast_row<kH>(y, j);
+#pragma unroll
+            for (int h = 0; h < kH; h++) {
+                const int i = lane + 64 * h;
+                if (i < j) y[h] = fma(-f[u][h], yj, y[h]);
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < kH; h++) {
+        const int i = lane + 64 * h;
+        if (i < n) S.y[i] = S.sc[i] * y[h];  // x = s y
+    }
 }
 __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P) {
 #pragma clang fp contract(off)
@@ -2279,110 +2777,51 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
     double *H = S.H;
     double *Wc = lds + (solve_smem_bytes(n) + 16) / sizeof(double);  // [8][128]: c of each panel step
     double *rdv = Wc + kSolveFastPanel * 128;
-    double *raw = rdv + kSolveFastPanel;
+    solve_ortho_load(P, W, S, tid, kSolveFastThreads);
     solve_assemble<kSolveFastThreads>(P, W, S, tid);
     for (int p = 0; p < n; p += kSolveFastPanel) {
         const int w = min(kSolveFastPanel, n - p);
-        if (wave == 0) {
-            // panel columns p .. p+w-1 of rows i = lane, lane + 64 (lower triangle incl. diagonal)
-            double r[2][kSolveFastPanel];
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-#pragma unroll
-                for (int jj = 0; jj < kSolveFastPanel; jj++) {
-                    const int i = lane + 64 * h;
-                    r[h][jj] = i < n && jj < w && i >= p + jj ? H[i * ld + p + jj] : 0.0;
-                }
-#pragma unroll
-            for (int kk = 0; kk < kSolveFastPanel; kk++) {
-                if (kk >= w) break;
-                const int k = p + kk;
-                const double d = k < 64 ? readlane_f64(r[0][kk], k) : readlane_f64(r[1][kk], k - 64);
-                const double rd = d != 0 ? 1.0 / d : 0.0;
-#pragma unroll
-                for (int jj = kk + 1; jj < kSolveFastPanel; jj++) {
-                    if (jj >= w) break;
-                    const int j = p + jj;
-                    const double cj = j < 64 ? readlane_f64(r[0][kk], j) : readlane_f64(r[1][kk], j - 64);  // A(j, k)
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const int i = lane + 64 * h;
-                        if (i >= j && i < n) r[h][jj] = fma(-(r[h][kk] * cj), rd, r[h][jj]);
-                    }
-                }
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const int i = lane + 64 * h;
-                    if (i < n) Wc[kk * 128 + i] = i > k ? r[h][kk] : 0.0;
-                    if (i > k && i < n) H[i * ld + k] = d != 0 ? r[h][kk] / d : 0.0;
-                    if (i == k) H[i * ld + k] = d;
-                }
-                if (lane == 0) rdv[kk] = rd;
-            }
+        if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 1)) {
+            if (n > 64)
+                fast_panel<2>(H, Wc, rdv, n, ld, p, w, lane);
+            else
+                fast_panel<1>(H, Wc, rdv, n, ld, p, w, lane);
         }
         __syncthreads();
         // rank-w update of the trailing lower triangle (p + w <= j <= i < n), steps in order
         const int m0 = p + w, nt = n - m0;
         const int ne = nt * (nt + 1) / 2;
-        for (int e = tid; e < ne; e += kSolveFastThreads) {
+        double rdk[kSolveFastPanel];
+#pragma unroll
+        for (int kk = 0; kk < kSolveFastPanel; kk++) rdk[kk] = kk < w ? rdv[kk] : 0.0;
+        for (int e = tid; e < ((LDSO_EXP_SOLVE_SKIP & 2) ? 0 : ne); e += kSolveFastThreads) {
             int ii = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);  // row ii of the nt x nt triangle
             if (ii * (ii + 1) / 2 > e) ii--;
             if ((ii + 1) * (ii + 2) / 2 <= e) ii++;
             const int i = m0 + ii, j = m0 + (e - ii * (ii + 1) / 2);
+            double wi[kSolveFastPanel], wj[kSolveFastPanel];
+#pragma unroll
+            for (int kk = 0; kk < kSolveFastPanel; kk++) {  // every operand in flight before the chain
+                wi[kk] = Wc[kk * 128 + i];
+                wj[kk] = Wc[kk * 128 + j];
+            }
             double a = H[i * ld + j];
-            for (int kk = 0; kk < w; kk++) a = fma(-(Wc[kk * 128 + i] * Wc[kk * 128 + j]), rdv[kk], a);
+#pragma unroll
+            for (int kk = 0; kk < kSolveFastPanel; kk++)
+                if (kk < w) a = fma(-(wi[kk] * wj[kk]), rdk[kk], a);
             H[i * ld + j] = a;
         }
         __syncthreads();
     }
-    if (wave == 1 && P.iteration >= 2 && P.n_null > 0) solve_ortho_prepare(P, W, S, raw, lane);
-    if (wave == 0) {
-        // substitutions (y in lanes i, i + 64), as k_solve without the permutation
-        const int ia = lane, ib = lane + 64, ra = min(ia, n - 1), rb = min(ib, n - 1);
-        double ya = ia < n ? S.b[ia] : 0.0, yb = ib < n ? S.b[ib] : 0.0;
-        constexpr int kSubAhead = 4;
-        for (int j0 = 0; j0 < n; j0 += kSubAhead) {
-            double fa[kSubAhead], fb[kSubAhead];
-#pragma unroll
-            for (int u = 0; u < kSubAhead; u++) {
-                const int j = min(j0 + u, n - 1);
-                fa[u] = H[ra * ld + j];
-                fb[u] = H[rb * ld + j];
-            }
-#pragma unroll
-            for (int u = 0; u < kSubAhead; u++) {
-                const int j = j0 + u;
-                if (j >= n) break;
-                const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
-                if (ia > j && ia < n) ya = fma(-fa[u], yj, ya);
-                if (ib > j && ib < n) yb = fma(-fb[u], yj, yb);
-            }
-        }
-        if (ia < n) ya = H[ia * ld + ia] != 0 ? ya / H[ia * ld + ia] : 0.0;
-        if (ib < n) yb = H[ib * ld + ib] != 0 ? yb / H[ib * ld + ib] : 0.0;
-        for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
-            double fa[kSubAhead], fb[kSubAhead];
-#pragma unroll
-            for (int u = 0; u < kSubAhead; u++) {
-                const int j = max(j0 - u, 0);
-                fa[u] = H[j * ld + ra];
-                fb[u] = H[j * ld + rb];
-            }
-#pragma unroll
-            for (int u = 0; u < kSubAhead; u++) {
-                const int j = j0 - u;
-                if (j < 0) break;
-                const double yj = j < 64 ? readlane_f64(ya, j) : readlane_f64(yb, j - 64);
-                if (ia < j) ya = fma(-fa[u], yj, ya);
-                if (ib < j) yb = fma(-fb[u], yj, yb);
-            }
-        }
-        if (ia < n) S.y[ia] = S.sc[ia] * ya;  // x = s y
-        if (ib < n) S.y[ib] = S.sc[ib] * yb;
+    if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 4)) {
+        if (n > 64)
+            fast_subst<2>(H, S, n, ld, lane);
+        else
+            fast_subst<1>(H, S, n, ld, lane);
     }
     __syncthreads();
-    if (wave == 0) solve_ortho_apply_store(P, W, S, lane);
-    if (P.xad) {  // x is in S.y: the resubstitution's xAd by all four waves
+    if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 8)) solve_ortho_apply_store(P, W, S, lane);
+    if (P.xad) {  // x is in S.y: the resubstitution's xAd by all waves
         __syncthreads();
         xad_fill(W, S.y, P.adH, P.adT, P.xad + (size_t)blockIdx.x * kXadStride, tid, kSolveFastThreads);
     }
@@ -2974,6 +3413,9 @@ struct ldso_ba_ctx {
     DevBuf<int> d_add_priors;
     DevBuf<float> d_xad;            // [win][kXadStride]
     DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
+    DevBuf<double> d_ns_nm, d_ns_g;     // k_ortho_prep's Nm [7 vec] and per-window G | G^-1 | fast
+    std::vector<double> ns_cache;       // the nullspaces k_ortho_prep last prepared (host copy) ...
+    int ns_cache_null = -1;             // ... and their count; -1: nothing prepared
     DevBuf<int> d_pt_win;
     // marginalisation context (ldso_ba_load_marginalization): images borrowed from the parent
     // context's window, addPoint<2> sums, no prior shift in the SC pass
@@ -3744,6 +4186,10 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_prior, (size_t)2 * vec_total);
     ALLOC(c->d_x, (size_t)vec_total);
     ALLOC(c->d_ns, (size_t)7 * vec_total);
+    ALLOC(c->d_ns_nm, (size_t)7 * vec_total);
+    ALLOC(c->d_ns_g, (size_t)kPrepGStride * n_windows);
+    c->ns_cache.clear();
+    c->ns_cache_null = -1;
     ALLOC(c->d_pt_win, std::max<size_t>(1, pt_win.size()));
 #undef ALLOC
     auto up = [&](void *dst, const void *src, size_t bytes) -> int {
@@ -4497,8 +4943,36 @@ int ldso_ba_resubstitute(ldso_ba_ctx *c, int32_t win, const double *x, double la
 // ---- device-side solve / resubstitute ----------------------------------
 }  // extern "C"
 namespace {
-// k_solve_reg / k_solve for every loaded window; n_null > 0 projects with the nullspaces already in
-// d_ns (iteration >= 2), n_null == 0 does not project
+// The caller's nullspaces (every window's [7][D] back to back) to d_ns and k_ortho_prep's
+// normalised Nm, G and G^-1 for n_null of them; skipped when they equal the last prepared ones.
+int upload_nullspaces(ldso_ba_ctx *c, const double *ns, int n_null) {
+    const size_t cnt = (size_t)7 * c->vec_total;
+    if (c->ns_cache_null == n_null && c->ns_cache.size() == cnt &&
+        std::memcmp(c->ns_cache.data(), ns, cnt * sizeof(double)) == 0)
+        return 0;
+    HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, cnt * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    int dmax = 0;
+    for (const WinDev &D : c->wd) dmax = std::max(dmax, D.D);
+    if (dmax > kSolveMaxDim) return fail(-1, "device solve supports windows of up to 11 keyframes");
+    SolveParams S{};
+    S.wins = c->d_wins.p;
+    S.ns = c->d_ns.p;
+    S.iteration = 2;
+    S.n_null = n_null;
+    const size_t smem = solve_smem_bytes(dmax) + 16 + (size_t)7 * dmax * sizeof(double);
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void *)k_ortho_prep, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(solve_smem_bytes(kSolveMaxDim) + 16 + (size_t)7 * kSolveMaxDim * sizeof(double)));
+    });
+    k_ortho_prep<<<c->n_win, 64, smem, c->stream>>>(S, c->d_ns_nm.p, c->d_ns_g.p);
+    HIP_TRY(hipGetLastError());
+    c->ns_cache.assign(ns, ns + cnt);
+    c->ns_cache_null = n_null;
+    return 0;
+}
+// k_solve_fast (or the exact k_solve_reg / k_solve) for every loaded window; n_null > 0 projects
+// with the nullspaces upload_nullspaces prepared (iteration >= 2), n_null == 0 does not project
 int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
     int dmax = 0;
     for (const WinDev &D : c->wd) dmax = std::max(dmax, D.D);
@@ -4512,6 +4986,8 @@ int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
     S.adH = c->d_adH.p;
     S.adT = c->d_adT.p;
     S.xad = c->d_xad.p;  // the resubstitution's xAd comes with x (k_xad after the LDS kernel)
+    S.prep_nm = c->d_ns_nm.p;
+    S.prep_g = c->d_ns_g.p;
     S.iteration = iteration;
     S.n_null = iteration >= 2 ? n_null : 0;
     static std::once_flag once;
@@ -4556,10 +5032,9 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
     if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
     HIP_TRY(hipSetDevice(c->device));
     const bool project = iteration >= 2 && ns && n_null > 0;
-    if (project)  // caller layout: every window's [7][D] back to back -> device [7 * vec_total]
-        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
-                               c->stream));
-    int rc = solve_device_launch(c, iteration, project ? n_null : 0);
+    int rc;
+    if (project && (rc = upload_nullspaces(c, ns, n_null))) return rc;
+    rc = solve_device_launch(c, iteration, project ? n_null : 0);
     if (rc) return rc;
     if (x_out) {
         HIP_TRY(hipMemcpyAsync(x_out, c->d_x.p, (size_t)c->vec_total * sizeof(double), hipMemcpyDeviceToHost,
@@ -4649,9 +5124,8 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
     int rc;
     // the projection uses the nullspaces of THIS call (as ldso_ba_solve_device)
     const bool project = iteration >= 2 && n_null > 0 && ns;
-    if (project)  // the nullspaces go up before (outside) the captured sequence
-        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
-                               c->stream));
+    if (project && (rc = upload_nullspaces(c, ns, n_null)))  // before (outside) the captured sequence
+        return rc;
     // pass + solve + resubstitution: one captured graph per (projection, lambda, n_null) without
     // a communicator or kernel timing; the downloads stay outside it
     auto body = [&]() -> int {
@@ -4727,9 +5201,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
                            hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_cprior.p, cp.data(), cp.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_add_priors.p, ap.data(), ap.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    if (ns)  // evalPT is fixed during optimize(): getNullspaces stays valid for every iteration
-        HIP_TRY(hipMemcpyAsync(c->d_ns.p, ns, (size_t)7 * c->vec_total * sizeof(double), hipMemcpyHostToDevice,
-                               c->stream));
+    if (ns && (rc = upload_nullspaces(c, ns, 7)))  // evalPT is fixed during optimize(): valid for every iteration
+        return rc;
     FrameStepParams F;
     F.wins = c->d_wins.p;
     F.fstate = c->d_fstate.p;

@@ -488,6 +488,24 @@ def test_fast_device_solve_matches_host_within_rounding(built, it):
     c.close()
 
 
+def test_prepared_nullspaces_follow_the_callers_nullspaces(built):
+    """k_ortho_prep's normalised nullspaces and (N^T N)^-1 are kept across calls while the caller
+    passes the same nullspaces, and redone when they change (other values or another count):
+    exact-mode x stays bit-identical to the host solver with the nullspaces of each call."""
+    cfg = dict(n_frames=5, n_points=400, seed=62)
+    w = synth.make_window(**cfg)
+    na = w.nullspaces()
+    rng = np.random.default_rng(5)
+    nb = na + 0.05 * rng.standard_normal(na.shape)
+    c = BAContext(0).load([w])
+    c.set_tuning(12, 1)
+    c.linearize()
+    for ns, k in ((na, 7), (na, 7), (nb, 7), (nb, 5), (na, 7)):
+        xd = c.solve_device(2, 1e-5, [ns], n_null=k)[0]
+        np.testing.assert_array_equal(xd, c.solve(0, 2, 1e-5, ns[:k]))
+    c.close()
+
+
 def test_iterate_replay_refreshes_host_copies_and_projects_only_with_this_calls_nullspaces(built):
     """A replayed ldso_ba_iterate graph invalidates the host copies of the system / energies (the
     replay skips the captured calls' host side), and a device solve projects only with the
