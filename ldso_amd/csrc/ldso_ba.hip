@@ -987,6 +987,7 @@ struct StitchParams {
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
     int pair_base;  // first global pair of this launch
+    int hs_split;   // k_stitch_host: two blocks per host (Top / SC halves)
     const int *__restrict__ frame_win;  // k_stitch_host: window of each global frame
     int frame_base;                     // k_stitch_host: first global host frame of this launch
     int win_base;   // first window of this launch
@@ -1001,11 +1002,17 @@ __device__ __forceinline__ long long pk_index(int row, int col, int D) {  // row
 // nth_element semantics over the candidates get(i), i in [0, n_cand), that are >= 0.
 // Candidates are staged in LDS when they fit; larger sets are re-read from global memory.
 // Every thread of the block must call it; thread 0 writes *th_out.
-template <class Get>
+// LDS behind the candidate keys: a 256-bin histogram per wave, 16 words of shared scalars, and
+// two doubles per wave for the energy sum
+__host__ __device__ constexpr size_t th_fixed_bytes(int threads) {
+    return ((size_t)(threads / 64) * 256 + 16) * sizeof(unsigned) + (size_t)(threads / 64) * 2 * sizeof(double);
+}
+template <int kT, class Get>
 __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, float *th_out) {
-    // LDS: keys[cap] | hist[4 waves][256] | sh[8]
+    // LDS: keys[cap] | hist[kW waves][256] | sh[16]
+    constexpr int kW = kT / 64;
     unsigned *hist = keys + cap;
-    unsigned *sh = hist + 4 * 256;  // [0..3] per-wave valid counts, [4] prefix, [5] rank
+    unsigned *sh = hist + kW * 256;  // [0..kW) per-wave valid counts, [kW] prefix, [kW+1] rank
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const bool in_lds = n_cand <= cap;
     // stage every candidate at its own index (no compaction, so no dependent slot atomics):
@@ -1013,13 +1020,13 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, fl
     // is never selected because the rank is taken among the valid ones only
     constexpr int kU = 8;
     unsigned cnt = 0;
-    for (int i0 = 0; i0 < n_cand; i0 += kStThreads * kU) {
+    for (int i0 = 0; i0 < n_cand; i0 += kT * kU) {
         float x[kU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) x[u] = get(min(i0 + u * kStThreads + tid, n_cand - 1));  // loads in flight
+        for (int u = 0; u < kU; u++) x[u] = get(min(i0 + u * kT + tid, n_cand - 1));  // loads in flight
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-            const int idx = i0 + u * kStThreads + tid;
+            const int idx = i0 + u * kT + tid;
             const bool ok = idx < n_cand && x[u] >= 0;
             cnt += ok ? 1u : 0u;
             if (in_lds && idx < n_cand) keys[idx] = ok ? (__float_as_uint(x[u]) & 0x7FFFFFFFu) : 0xFFFFFFFFu;
@@ -1029,7 +1036,9 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, fl
     for (int m = 32; m >= 1; m >>= 1) cnt += __shfl_xor(cnt, m, kWave);
     if (lane == 0) sh[wid] = cnt;
     __syncthreads();
-    const unsigned n = sh[0] + sh[1] + sh[2] + sh[3];
+    unsigned n = 0;
+#pragma unroll
+    for (int q = 0; q < kW; q++) n += sh[q];
     if (n == 0) {
         if (tid == 0) *th_out = 12 * 12 * LDSO_BA_PATTERN_NUM;
         __syncthreads();
@@ -1043,12 +1052,12 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, fl
         for (int b = lane; b < 256; b += 64) wh[b] = 0;
         __syncthreads();
         if (in_lds) {
-            for (int i = tid; i < n_cand; i += kStThreads) {
+            for (int i = tid; i < n_cand; i += kT) {
                 const unsigned key = keys[i];
                 if ((key & pmask) == (prefix & pmask)) atomicAdd(&wh[(key >> shift) & 255u], 1u);
             }
         } else {
-            for (int i = tid; i < n_cand; i += kStThreads) {
+            for (int i = tid; i < n_cand; i += kT) {
                 const float x = get(i);
                 const unsigned key = x >= 0 ? (__float_as_uint(x) & 0x7FFFFFFFu) : 0xFFFFFFFFu;
                 if ((key & pmask) == (prefix & pmask)) atomicAdd(&wh[(key >> shift) & 255u], 1u);
@@ -1058,8 +1067,11 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, fl
         if (tid < 64) {  // one wave: lane l owns bins 4l..4l+3
             unsigned hb[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                hb[q] = hist[4 * tid + q] + hist[256 + 4 * tid + q] + hist[512 + 4 * tid + q] + hist[768 + 4 * tid + q];
+            for (int q = 0; q < 4; q++) {
+                hb[q] = 0;
+#pragma unroll
+                for (int v = 0; v < kW; v++) hb[q] += hist[256 * v + 4 * tid + q];
+            }
             unsigned incl = hb[0] + hb[1] + hb[2] + hb[3];
 #pragma unroll
             for (int m = 1; m < 64; m <<= 1) {
@@ -1075,13 +1087,13 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, fl
                     if (acc + hb[q] > rank) break;
                     acc += hb[q];
                 }
-                sh[5] = rank - acc;
-                sh[4] = prefix | ((unsigned)d << shift);
+                sh[kW + 1] = rank - acc;
+                sh[kW] = prefix | ((unsigned)d << shift);
             }
         }
         __syncthreads();
-        prefix = sh[4];
-        rank = sh[5];
+        prefix = sh[kW];
+        rank = sh[kW + 1];
     }
     if (tid == 0) {
 #pragma clang fp contract(off)
@@ -1095,16 +1107,18 @@ __device__ void select_frame_th(Get get, int n_cand, unsigned *keys, int cap, fl
     __syncthreads();
 }
 
+template <int kT>
 __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &W, int w, unsigned *keys) {
+    constexpr int kW = kT / 64;
     const int tid = threadIdx.x, N = W.N;
     const float *e_wo = P.e_wo + W.newest_begin;
-    select_frame_th([&](int i) { return e_wo[i]; }, W.newest_end - W.newest_begin, keys, P.th_cap,
-                    P.frame_th + W.frame_base + N - 1);
-    double *red = reinterpret_cast<double *>(keys + P.th_cap + 4 * 256 + 8);
+    select_frame_th<kT>([&](int i) { return e_wo[i]; }, W.newest_end - W.newest_begin, keys, P.th_cap,
+                        P.frame_th + W.frame_base + N - 1);
+    double *red = reinterpret_cast<double *>(keys + P.th_cap + kW * 256 + 16);
     // linearizeAll: sum of returned energies and #IN in a fixed order (strided per thread, then
     // a fixed tree), so repeated passes give identical sums
     double se = 0, sn = 0;
-    for (int k = tid; k < W.n_top_items; k += kStThreads) {
+    for (int k = tid; k < W.n_top_items; k += kT) {
         se += P.item_energy[2 * (W.top_item_base + k)];
         sn += P.item_energy[2 * (W.top_item_base + k) + 1];
     }
@@ -1119,7 +1133,15 @@ __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &
     }
     __syncthreads();
     if (tid == 0) {
-        const double e = (red[0] + red[2]) + (red[4] + red[6]), nin = (red[1] + red[3]) + (red[5] + red[7]);
+        double e = 0, nin = 0;  // the waves in a fixed tree: pairs, then pairs of pairs
+        if constexpr (kW == 4) {
+            e = (red[0] + red[2]) + (red[4] + red[6]);
+            nin = (red[1] + red[3]) + (red[5] + red[7]);
+        } else {
+            static_assert(kW == 8, "4 or 8 waves");
+            e = ((red[0] + red[2]) + (red[4] + red[6])) + ((red[8] + red[10]) + (red[12] + red[14]));
+            nin = ((red[1] + red[3]) + (red[5] + red[7])) + ((red[9] + red[11]) + (red[13] + red[15]));
+        }
         P.win_energy[2 * w] = e;
         P.win_energy[2 * w + 1] = nin;
         if (P.ehist) {  // the optimize() energy history, without a launch of its own
@@ -1170,7 +1192,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     extern __shared__ double sm[];  // sized on the host for the largest window (stitch_smem_bytes)
     if ((int)blockIdx.x < P.n_win) {  // the longest single-block chain goes first in the grid
         const int w = P.win_base + blockIdx.x;
-        frame_threshold_and_energy(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
+        frame_threshold_and_energy<kStThreads>(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
         return;
     }
     const int pair = P.pair_base + blockIdx.x - P.n_win;
@@ -1505,11 +1527,15 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
 // then every element of the partial.  Windows with more keyframes use k_stitch's records.
 // ============================================================================================
 constexpr int kHostStitchMaxN = 12;
+constexpr int kHsThreads = 512;
+#ifndef LDSO_EXP_HS_SKIP  // timing experiments only: 1 outputs, 2 intermediates, 4 G loads, 8 Top loads
+#define LDSO_EXP_HS_SKIP 0
+#endif
 __host__ __device__ inline int hs_k5(int N) { return 8 * (N - 1) + 5; }
-__host__ __device__ inline int hs_ldg(int N) { return hs_k5(N) | 1; }
+__host__ __device__ inline int hs_ldg(int N) { return (hs_k5(N) + 1) & ~1; }  // even: 16-byte aligned rows
 __host__ __device__ inline int hs_npair(int N) { return (N - 1) * N / 2; }
 __host__ __device__ inline size_t hs_lds_doubles(int N) {
-    return (size_t)hs_k5(N) * hs_ldg(N) + 2 * 64 * (size_t)N + 96 * (size_t)N + 64 * (size_t)hs_npair(N) +
+    return (size_t)hs_k5(N) * hs_ldg(N) + 2 * 64 * (size_t)N + 182 * (size_t)N + 64 * (size_t)hs_npair(N) +
            3 * 64 * (size_t)N;
 }
 // tile index t of the upper-tile order (a <= b) over nt tile rows -> (a, b)
@@ -1522,30 +1548,82 @@ __device__ __forceinline__ void tile_ab(int t, int nt, int &a, int &b) {
     a = r;
     b = r + t;
 }
-__global__ __launch_bounds__(kStThreads) void k_stitch_host(StitchParams P) {
-    extern __shared__ double sm[];
+// the (r, c) of top-partial slot s (the inverse of top_slot, r <= c)
+__device__ __forceinline__ void top_slot_rc(int s, int &r, int &c) {
+    if (s < 55) {  // Data[]: upper row-major 10x10
+        int a = 0;
+        while (s >= 10 - a) {
+            s -= 10 - a;
+            a++;
+        }
+        r = a;
+        c = a + s;
+    } else if (s < 85) {  // TopRight 10x3
+        r = (s - 55) / 3;
+        c = 10 + (s - 55) % 3;
+    } else {  // BotRight: (0,0) (0,1) (0,2) (1,1) (1,2) (2,2)
+        const int b = s - 85;
+        r = 10 + (b < 3 ? 0 : b < 5 ? 1 : 2);
+        c = 10 + (b < 3 ? b : b < 5 ? b - 2 : 2);
+    }
+}
+// v[a][b] += sum_q L_a[q] R_b[q] (a, b in {0, 1}): two q-contiguous, 16-byte aligned 8-double
+// rows of each operand; each element's 8 products summed in q order, then added to v
+__device__ __forceinline__ void mm22(const double *L0, const double *L1, const double *R0, const double *R1,
+                                     double (&v)[2][2]) {
+    double l[2][8], r[2][8];
+#pragma unroll
+    for (int q = 0; q < 8; q += 2) {
+        const double2 a0 = *reinterpret_cast<const double2 *>(L0 + q), a1 = *reinterpret_cast<const double2 *>(L1 + q);
+        const double2 b0 = *reinterpret_cast<const double2 *>(R0 + q), b1 = *reinterpret_cast<const double2 *>(R1 + q);
+        l[0][q] = a0.x;
+        l[0][q + 1] = a0.y;
+        l[1][q] = a1.x;
+        l[1][q + 1] = a1.y;
+        r[0][q] = b0.x;
+        r[0][q + 1] = b0.y;
+        r[1][q] = b1.x;
+        r[1][q + 1] = b1.y;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            double t = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) t += l[a][q] * r[b][q];
+            v[a][b] += t;
+        }
+}
+__global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
     if ((int)blockIdx.x < P.n_win) {  // setNewFrameEnergyTH + the energy sum, as k_stitch
         const int w = P.win_base + blockIdx.x;
-        frame_threshold_and_energy(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
+        frame_threshold_and_energy<kHsThreads>(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
         return;
     }
     if (!P.accumulate) return;
-    const int fr = P.frame_base + blockIdx.x - P.n_win;
+    // one block per host, or (hs_split: grids that fit the GPU at once, e.g. one window) two: the
+    // Top half (HA, bA) and the Schur complement (Hsc, bsc) of the host's partial
+    const int hb = blockIdx.x - P.n_win;
+    const int fr = P.frame_base + (P.hs_split ? hb >> 1 : hb);
+    const bool do_top = !P.hs_split || (hb & 1) == 0, do_sc = !P.hs_split || (hb & 1) == 1;
     const int w = P.frame_win[fr];
     const WinDev &W = P.wins[w];
     const int N = W.N, D = W.D, i = fr - W.frame_base, tid = threadIdx.x;
-    const int Kc = 8 * (N - 1), K5 = Kc + 5, ldg = K5 | 1, nt = W.KP / 4, per = W.ntiles * 16;
+    const int Kc = 8 * (N - 1), K5 = Kc + 5, ldg = hs_ldg(N), nt = W.KP / 4, per = W.ntiles * 16;
     const int Nm1 = N - 1, npair = hs_npair(N);
+    // LDS (every region an even number of doubles: 16-byte aligned rows for the b128 reads)
     double *Gd = sm;                     // [K5][ldg] G_i, both triangles
-    double *AH = Gd + (size_t)K5 * ldg;  // [N][64] adH of pair (i, k)
-    double *AT = AH + 64 * N;            // [N][64] adT of pair (i, k)
-    double *acc = AT + 64 * N;           // [N][96] Top accumulator of pair (i, t) (t == i unused)
-    double *X = acc + 96 * N;            // [npair][64] X_jk = AT_ij D_jk, target slots sj <= sk
-    double *SS = X + 64 * npair;         // [N][64] S_j = sum_k D_jk AH_ik^T
-    double *TH = SS + 64 * N;            // [N][64] AH_it A_t(88)
-    double *TT = TH + 64 * N;            // [N][64] AT_it A_t(88)
+    double *AH = Gd + (size_t)K5 * ldg;  // [N][8][8] adH of pair (i, k)
+    double *AT = AH + 64 * N;            // [N][8][8] adT of pair (i, k)
+    double *A14 = AT + 64 * N;           // [N][13][14] pair (i, t)'s 13x13 Top block (t == i unused)
+    double *X = A14 + 182 * N;           // [npair][8][8] X_jk = AT_ij D_jk, target slots sj <= sk
+    double *SSt = X + 64 * npair;        // [N][8][8] S_j^T, S_j = sum_k D_jk AH_ik^T
+    double *TH = SSt + 64 * N;           // [N][8][8] AH_it A_t(88)
+    double *TT = TH + 64 * N;            // [N][8][8] AT_it A_t(88)
     auto frame_of = [&](int slot) { return slot < i ? slot : slot + 1; };
-    auto A_t = [&](int t, int r, int c) { return acc[96 * t + top_slot(r, c)]; };
+    auto A_t = [&](int t, int r, int c) { return A14[182 * t + 14 * r + c]; };
     // ---- every load of the block in one round trip -------------------------------------
     {
         // G_i: each float4 of the host's chunk partials is one row of a 4x4 tile; summed over the
@@ -1554,7 +1632,7 @@ __global__ __launch_bounds__(kStThreads) void k_stitch_host(StitchParams P) {
         const float4 *slab = reinterpret_cast<const float4 *>(P.sc_slab + W.sc_slab_base +
                                                               (size_t)(hi.x - W.sc_item_base) * per);
         const int per4 = per / 4;
-        for (int q = tid; q < per4; q += kStThreads) {
+        for (int q = tid; q < ((LDSO_EXP_HS_SKIP & 4) || !do_sc ? 0 : per4); q += kHsThreads) {
             double s[4] = {0, 0, 0, 0};
             int k = 0;
             for (; k + 4 <= hi.y; k += 4) {
@@ -1589,13 +1667,13 @@ __global__ __launch_bounds__(kStThreads) void k_stitch_host(StitchParams P) {
             }
         }
         // the adjoints of the pairs (i, k), k = 0..N-1
-        for (int e = tid; e < 64 * N; e += kStThreads) {
+        for (int e = tid; e < 64 * N; e += kHsThreads) {
             const size_t pk = (size_t)(W.pair_base + i + N * (e >> 6)) * 64 + (e & 63);
             AH[e] = P.adH[pk];
             AT[e] = P.adT[pk];
         }
         // Top accumulators of the pairs (i, t): 24 float4 per item, summed over the pair's items
-        for (int e = tid; e < 24 * Nm1; e += kStThreads) {
+        for (int e = tid; e < ((LDSO_EXP_HS_SKIP & 8) || !do_top ? 0 : 24 * Nm1); e += kHsThreads) {
             const int t = frame_of(e / 24), q = e % 24;
             const int2 pi = P.pair_items[W.pair_base + i + N * t];
             const float4 *src = reinterpret_cast<const float4 *>(P.top_slab + (size_t)pi.x * kTopVals) + q;
@@ -1621,166 +1699,176 @@ __global__ __launch_bounds__(kStThreads) void k_stitch_host(StitchParams P) {
                 s[3] += (double)v.w;
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) acc[96 * t + 4 * q + u] = s[u];
+            for (int u = 0; u < 4; u++) {  // both triangles of the 13x13 block (slots 91..95: padding)
+                if (4 * q + u >= 91) continue;
+                int r, c;
+                top_slot_rc(4 * q + u, r, c);
+                A14[182 * t + 14 * r + c] = s[u];
+                A14[182 * t + 14 * c + r] = s[u];
+            }
         }
     }
     __syncthreads();
-    // ---- intermediates: X_jk (sj <= sk), S_j, TH_t, TT_t ---------------------------------
+    // ---- intermediates, 2x2 per thread, 16 threads per 8x8 block: S_j^T (N-1 blocks of N-1
+    // terms each, first), X_jk (sj <= sk), TH_t, TT_t ---------------------------------------
     {
-        const int nx = 64 * npair, ns = nx + 64 * Nm1, nh = ns + 64 * Nm1, total = nh + 64 * Nm1;
-        for (int u = tid; u < total; u += kStThreads) {
-            const int r = (u >> 3) & 7, c = u & 7;
-            if (u < nx) {  // X_jk[r][c] = sum_q AT_ij[r][q] D_jk[q][c]
-                const int pj = u >> 6;
-                int sj = 0, rem = pj;
+        const int n_ss = do_sc ? Nm1 : 0, n_x = do_sc ? npair : 0, n_th = do_top ? Nm1 : 0;
+        const int total = 16 * (n_ss + n_x + 2 * n_th);
+        for (int u = tid; u < ((LDSO_EXP_HS_SKIP & 2) ? 0 : total); u += kHsThreads) {
+            int blk = u >> 4;
+            const int r0 = 2 * ((u & 15) >> 2), c0 = 2 * (u & 3);
+            double v[2][2] = {{0, 0}, {0, 0}};
+            if (blk < n_ss) {  // S_j[r][c] = sum_k sum_q D_jk[r][q] AH_ik[c][q], k in slot order
+                const int sj = blk, j = frame_of(sj);
+                for (int sk = 0; sk < Nm1; sk++) {
+                    const double *d = Gd + (size_t)(8 * sj + r0) * ldg + 8 * sk, *ah = AH + 64 * frame_of(sk) + 8 * c0;
+                    mm22(d, d + ldg, ah, ah + 8, v);
+                }
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+#pragma unroll
+                    for (int b = 0; b < 2; b++) SSt[64 * j + 8 * (c0 + b) + r0 + a] = v[a][b];
+                continue;
+            }
+            blk -= n_ss;
+            if (blk < n_x) {  // X_jk[r][c] = sum_q AT_ij[r][q] D_jk[q][c], D_jk[q][c] = G[8sk+c][8sj+q]
+                int sj = 0, rem = blk;
                 while (rem >= Nm1 - sj) {
                     rem -= Nm1 - sj;
                     sj++;
                 }
-                const int sk = sj + rem, j = frame_of(sj);
-                const double *at = AT + 64 * j + 8 * r, *d = Gd + (8 * sj) * ldg + 8 * sk + c;
-                double v = 0;
+                const int sk = sj + rem;
+                const double *at = AT + 64 * frame_of(sj) + 8 * r0, *d = Gd + (size_t)(8 * sk + c0) * ldg + 8 * sj;
+                mm22(at, at + 8, d, d + ldg, v);
+                double *o = X + 64 * blk;
 #pragma unroll
-                for (int q = 0; q < 8; q++) v += at[q] * d[q * ldg];
-                X[u] = v;
-            } else if (u < ns) {  // S_j[r][c] = sum_k (sum_q D_jk[r][q] AH_ik[c][q]), k in slot order
-                const int sj = (u - nx) >> 6, j = frame_of(sj);
-                double v = 0;
-                for (int sk = 0; sk < Nm1; sk++) {
-                    const double *d = Gd + (8 * sj + r) * ldg + 8 * sk, *ah = AH + 64 * frame_of(sk) + 8 * c;
-                    double t = 0;
+                for (int a = 0; a < 2; a++)
 #pragma unroll
-                    for (int q = 0; q < 8; q++) t += d[q] * ah[q];
-                    v += t;
-                }
-                SS[64 * j + 8 * r + c] = v;
-            } else {  // TH_t / TT_t [r][c] = sum_k AH_it / AT_it [r][k] A_t(4+k, 4+c)
-                const bool th = u < nh;
-                const int t = frame_of((u - (th ? ns : nh)) >> 6);
-                const double *ad = (th ? AH : AT) + 64 * t + 8 * r;
-                double v = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) v += ad[k] * A_t(t, 4 + k, 4 + c);
-                (th ? TH : TT)[64 * t + 8 * r + c] = v;
+                    for (int b = 0; b < 2; b++) o[8 * (r0 + a) + c0 + b] = v[a][b];
+                continue;
             }
+            blk -= n_x;  // TH_t / TT_t [r][c] = sum_k AH_it / AT_it [r][k] A_t(4+c, 4+k)
+            const bool th = blk < n_th;
+            const int t = frame_of(th ? blk : blk - n_th);
+            const double *ad = (th ? AH : AT) + 64 * t + 8 * r0, *at = A14 + 182 * t + 14 * (4 + c0) + 4;
+            mm22(ad, ad + 8, at, at + 14, v);
+            double *o = (th ? TH : TT) + 64 * t;
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++) o[8 * (r0 + a) + c0 + b] = v[a][b];
         }
     }
     __syncthreads();
+    if (LDSO_EXP_HS_SKIP & 1) return;
     // ---- host i's partial system: every packed element written (zeros included) ------------
     const long long pl = packed_len(D);
     double *HAp = P.stage + W.stage_base + (size_t)i * sys_len(D), *bAp = HAp + pl, *Hsp = bAp + D, *bsp = Hsp + pl;
     auto xblk = [&](int sj, int sk) { return X + 64 * (sj * Nm1 - sj * (sj - 1) / 2 + (sk - sj)); };
-    auto dot8 = [](const double *a, const double *b) {
-        double v = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) v += a[q] * b[q];
-        return v;
-    };
-    auto dot8s = [](const double *a, const double *b, int sb) {  // b strided
-        double v = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) v += a[q] * b[q * sb];
-        return v;
-    };
-    const int nb = N * N * 64;
-    for (int u = tid; u < nb; u += kStThreads) {  // frame blocks (f1 <= f2)
-        const int f1 = u / (N * 64), f2 = (u >> 6) % N, r = (u >> 3) & 7, c = u & 7;
-        if (f2 < f1 || (f1 == f2 && r > c)) continue;
-        double ha = 0, hs = 0;
-        if (f1 == f2) {
-            const int f = f1;
-            if (f == i) {
+    const int n_fb = 16 * (N * (N + 1) / 2), n_rest = 32 * N + 8 * N + 20, per_part = n_fb + n_rest;
+    for (int uo = tid; uo < (do_top + do_sc) * per_part; uo += kHsThreads) {
+        const bool top = do_top && uo < per_part;  // the Top items first, then the SC ones
+        const int u = uo - (do_top && !top ? per_part : 0);
+        if (u < n_fb) {  // a 2x2 of frame block (f1 <= f2), upper-block order
+            const int r0 = 2 * ((u & 15) >> 2), c0 = 2 * (u & 3);
+            int f1 = 0, rem = u >> 4;
+            while (rem >= N - f1) {
+                rem -= N - f1;
+                f1++;
+            }
+            const int f2 = f1 + rem;
+            if (f1 == f2 && r0 > c0) continue;  // below the diagonal
+            double v[2][2] = {{0, 0}, {0, 0}};
+            if (f1 == f2 && f1 == i) {
                 for (int st = 0; st < Nm1; st++) {  // sum over t / j in frame order
                     const int t = frame_of(st);
-                    ha += dot8(TH + 64 * t + 8 * r, AH + 64 * t + 8 * c);
-                    hs += dot8s(AH + 64 * t + 8 * r, SS + 64 * t + c, 8);
+                    const double *th = TH + 64 * t + 8 * r0, *ah = AH + 64 * t, *ss = SSt + 64 * t + 8 * c0;
+                    if (top)
+                        mm22(th, th + 8, ah + 8 * c0, ah + 8 * c0 + 8, v);
+                    else
+                        mm22(ah + 8 * r0, ah + 8 * r0 + 8, ss, ss + 8, v);
                 }
-            } else {
-                const int sf = f < i ? f : f - 1;
-                ha = dot8(TT + 64 * f + 8 * r, AT + 64 * f + 8 * c);
-                hs = dot8(xblk(sf, sf) + 8 * r, AT + 64 * f + 8 * c);
+            } else if (f1 == f2) {
+                const int f = f1, sf = f < i ? f : f - 1;
+                const double *tt = TT + 64 * f + 8 * r0, *at = AT + 64 * f + 8 * c0;
+                const double *x = top ? tt : xblk(sf, sf) + 8 * r0;
+                mm22(top ? tt : x, (top ? tt : x) + 8, at, at + 8, v);
+            } else if (f1 == i) {
+                const double *th = TH + 64 * f2 + 8 * r0, *at = AT + 64 * f2 + 8 * c0, *ss = SSt + 64 * f2 + 8 * r0;
+                const double *l = top ? th : ss;  // (AT_i,f2 S_f2)^T on the SC side
+                mm22(l, l + 8, at, at + 8, v);
+            } else if (f2 == i) {
+                const double *at = AT + 64 * f1 + 8 * r0, *th = TH + 64 * f1 + 8 * c0, *ss = SSt + 64 * f1 + 8 * c0;
+                const double *rr = top ? th : ss;  // (AH A AT^T)^T of pair (i, f1) / AT_i,f1 S_f1
+                mm22(at, at + 8, rr, rr + 8, v);
+            } else if (!top) {
+                const int s1 = f1 < i ? f1 : f1 - 1, s2 = f2 < i ? f2 : f2 - 1;
+                const double *x = xblk(s1, s2) + 8 * r0, *at = AT + 64 * f2 + 8 * c0;
+                mm22(x, x + 8, at, at + 8, v);
             }
-        } else if (f1 == i) {
-            ha = dot8(TH + 64 * f2 + 8 * r, AT + 64 * f2 + 8 * c);
-            hs = dot8s(AT + 64 * f2 + 8 * c, SS + 64 * f2 + r, 8);  // (AT_i,f2 S_f2)^T
-        } else if (f2 == i) {
-            ha = dot8(TH + 64 * f1 + 8 * c, AT + 64 * f1 + 8 * r);  // (AH A AT^T)^T of pair (i, f1)
-            hs = dot8s(AT + 64 * f1 + 8 * r, SS + 64 * f1 + c, 8);  // AT_i,f1 S_f1
-        } else {
-            const int s1 = f1 < i ? f1 : f1 - 1, s2 = f2 < i ? f2 : f2 - 1;
-            hs = dot8(xblk(s1, s2) + 8 * r, AT + 64 * f2 + 8 * c);
+            double *o = top ? HAp : Hsp;
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++) {
+                    if (f1 == f2 && r0 + a > c0 + b) continue;
+                    o[pk_index(4 + 8 * f1 + r0 + a, 4 + 8 * f2 + c0 + b, D)] = v[a][b];
+                }
+            continue;
         }
-        const long long q = pk_index(4 + 8 * f1 + r, 4 + 8 * f2 + c, D);
-        HAp[q] = ha;
-        Hsp[q] = hs;
-    }
-    for (int u = tid; u < 32 * N + 8 * N + 20; u += kStThreads) {
-        double ha = 0, hs = 0;
+        const int l0 = u - n_fb;
+        double ha = 0;  // this part's value: HA / bA (top) or Hsc / bsc
         long long q;
         bool bvec = false;
-        if (u < 32 * N) {  // (calib cc, frame f, rr)
-            const int f = u >> 5, rr = (u >> 2) & 7, cc = u & 3;
+        if (l0 < 32 * N) {  // (calib cc, frame f, rr)
+            const int f = l0 >> 5, rr = (l0 >> 2) & 7, cc = l0 & 3;
             if (f == i) {
                 for (int st = 0; st < Nm1; st++) {
                     const int t = frame_of(st);
-                    double a = 0, b = 0;
+                    double a = 0;
 #pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        a += AH[64 * t + 8 * rr + k] * A_t(t, 4 + k, cc);
-                        b += AH[64 * t + 8 * rr + k] * Gd[(8 * st + k) * ldg + Kc + cc];
-                    }
+                    for (int k = 0; k < 8; k++)
+                        a += AH[64 * t + 8 * rr + k] * (top ? A_t(t, 4 + k, cc) : Gd[(8 * st + k) * ldg + Kc + cc]);
                     ha += a;
-                    hs += b;
                 }
             } else {
                 const int sf = f < i ? f : f - 1;
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    ha += AT[64 * f + 8 * rr + k] * A_t(f, 4 + k, cc);
-                    hs += AT[64 * f + 8 * rr + k] * Gd[(8 * sf + k) * ldg + Kc + cc];
-                }
+                for (int k = 0; k < 8; k++)
+                    ha += AT[64 * f + 8 * rr + k] * (top ? A_t(f, 4 + k, cc) : Gd[(8 * sf + k) * ldg + Kc + cc]);
             }
             q = pk_index(cc, 4 + 8 * f + rr, D);
-        } else if (u < 40 * N) {  // b(f)[rr]
-            const int f = (u - 32 * N) >> 3, rr = u & 7;
+        } else if (l0 < 40 * N) {  // b(f)[rr]
+            const int f = (l0 - 32 * N) >> 3, rr = l0 & 7;
             if (f == i) {
                 for (int st = 0; st < Nm1; st++) {
                     const int t = frame_of(st);
-                    double a = 0, b = 0;
+                    double a = 0;
 #pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        a += AH[64 * t + 8 * rr + k] * A_t(t, 4 + k, 12);
-                        b += AH[64 * t + 8 * rr + k] * Gd[(8 * st + k) * ldg + Kc + 4];
-                    }
+                    for (int k = 0; k < 8; k++)
+                        a += AH[64 * t + 8 * rr + k] * (top ? A_t(t, 4 + k, 12) : Gd[(8 * st + k) * ldg + Kc + 4]);
                     ha += a;
-                    hs += b;
                 }
             } else {
                 const int sf = f < i ? f : f - 1;
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    ha += AT[64 * f + 8 * rr + k] * A_t(f, 4 + k, 12);
-                    hs += AT[64 * f + 8 * rr + k] * Gd[(8 * sf + k) * ldg + Kc + 4];
-                }
+                for (int k = 0; k < 8; k++)
+                    ha += AT[64 * f + 8 * rr + k] * (top ? A_t(f, 4 + k, 12) : Gd[(8 * sf + k) * ldg + Kc + 4]);
             }
             q = 4 + 8 * f + rr;
             bvec = true;
         } else {  // the calibration block (16, upper used) and b(calib) (4)
-            const int l = u - 40 * N;
+            const int l = l0 - 40 * N;
             const int r = l < 16 ? l >> 2 : l - 16, cI = l < 16 ? (l & 3) : 12, cS = l < 16 ? (l & 3) : 4;
             if (l < 16 && r > cI) continue;
-            for (int st = 0; st < Nm1; st++) ha += A_t(frame_of(st), r, cI);
-            hs = Gd[(Kc + r) * ldg + Kc + cS];
+            if (top)
+                for (int st = 0; st < Nm1; st++) ha += A_t(frame_of(st), r, cI);
+            else
+                ha = Gd[(Kc + r) * ldg + Kc + cS];
             bvec = l >= 16;
             q = bvec ? r : pk_index(r, cI, D);
         }
-        if (bvec) {
-            bAp[q] = ha;
-            bsp[q] = hs;
-        } else {
-            HAp[q] = ha;
-            Hsp[q] = hs;
-        }
+        (bvec ? (top ? bAp : bsp) : (top ? HAp : Hsp))[q] = ha;
     }
 }
 // sys = sum over the window's hosts of their partials, in host order, one thread per element
@@ -2846,11 +2934,11 @@ __global__ __launch_bounds__(256) void k_export_newest(const WinDev *__restrict_
 
 __global__ __launch_bounds__(kStThreads) void k_frame_th(const WinDev *__restrict__ wins, const float *__restrict__ buf,
                                                          int n_ranks, int n_win, long long stride, float *frame_th) {
-    __shared__ unsigned keys[kThMaxLds + 4 * 256 + 8];
+    __shared__ unsigned keys[kThMaxLds + th_fixed_bytes(kStThreads) / sizeof(unsigned)];
     const int w = blockIdx.x;
     const WinDev &W = wins[w];
     const long long n_cand = (long long)n_ranks * stride;
-    select_frame_th(
+    select_frame_th<kStThreads>(
         [&](int i) {
             const int r = (int)(i / stride);
             return buf[((size_t)r * n_win + w) * stride + (i - (long long)r * stride)];
@@ -3420,6 +3508,8 @@ struct ldso_ba_ctx {
     // marginalisation context (ldso_ba_load_marginalization): images borrowed from the parent
     // context's window, addPoint<2> sums, no prior shift in the SC pass
     bool marg = false;
+    bool host_stitch = false;
+    int n_cu = 256;  // compute units (k_stitch_host splits its blocks when the grid fits at once)  // k_stitch_host + k_stitch_host_sum (every window <= kHostStitchMaxN keyframes)
     const float4 *img_ext = nullptr;
     DevBuf<float> d_adhtd;  // [pairs][8] adHTdeltaF
     int vec_total = 0;
@@ -3640,9 +3730,19 @@ int launch_resubstitute(ldso_ba_ctx *c, int begin, int count, double lambda, boo
 size_t stitch_smem_bytes(int KP, int N, int *th_cap) {
     const size_t top = (96 + 169 + 4 * 64) * sizeof(double);
     const size_t sc = (size_t)(kStTopLds + 8 * KP + 4 * (N - 1) * 64 + 20) * sizeof(double);
-    const size_t th_fixed = (4 * 256 + 8) * sizeof(unsigned) + 8 * sizeof(double);
+    const size_t th_fixed = th_fixed_bytes(kStThreads);
     size_t bytes = std::max(top, sc);
     bytes = std::max(bytes, th_fixed + 1024 * sizeof(unsigned));
+    bytes = (bytes + 15) & ~(size_t)15;
+    *th_cap = (int)((bytes - th_fixed) / sizeof(unsigned)) & ~3;
+    return bytes;
+}
+
+// k_stitch_host dynamic LDS: the host block's staging for the largest window, at least the
+// frame-threshold staging of 1024 candidates (more if the host phase leaves room)
+size_t stitch_host_smem_bytes(int N, int *th_cap) {
+    const size_t th_fixed = th_fixed_bytes(kHsThreads);
+    size_t bytes = std::max(hs_lds_doubles(N) * sizeof(double), th_fixed + 1024 * sizeof(unsigned));
     bytes = (bytes + 15) & ~(size_t)15;
     *th_cap = (int)((bytes - th_fixed) / sizeof(unsigned)) & ~3;
     return bytes;
@@ -3795,6 +3895,8 @@ int ldso_ba_create(int32_t device, ldso_ba_ctx **out) {
     HIP_TRY(hipSetDevice(device));
     ldso_ba_ctx *c = new ldso_ba_ctx();
     c->device = device;
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->n_cu <= 0)
+        c->n_cu = 256;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -4100,7 +4202,8 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         D.sys_base = sys_total;
         sys_total += sys_len(D.D);
         D.stage_base = stage_total;
-        stage_total += (long long)N * N * stage_rec(N);
+        // k_stitch's per-pair records, or k_stitch_host's per-host partial systems
+        stage_total += std::max<long long>((long long)N * N * stage_rec(N), (long long)N * sys_len(D.D));
         D.newest_begin = res_base + bucket_start[N * (N - 1)];
         D.newest_end = res_base + bucket_start[N * N];
         D.rec_base = rec_base;
@@ -4124,6 +4227,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     c->n_frames = frame_base;
     c->max_frames = 0;
     for (int w = 0; w < n_windows; w++) c->max_frames = std::max(c->max_frames, ws[w].n_frames);
+    c->host_stitch = c->max_frames <= kHostStitchMaxN && !getenv_flag("LDSO_BA_STITCH_RECORDS");
     c->P_tot = point_base;
     c->vec_total = vec_total;
     c->R_tot = res_base;
@@ -4534,7 +4638,12 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         kp_max = std::max(kp_max, D.KP);
         n_max = std::max(n_max, D.N);
     }
-    const size_t st_smem = stitch_smem_bytes(kp_max, n_max, &Sp.th_cap);
+    Sp.frame_win = c->d_frame_win.p;
+    Sp.frame_base = 0;
+    // two 512-thread blocks fit a CU: split the host blocks when the doubled grid still runs at once
+    Sp.hs_split = Sp.n_win + 2 * c->n_frames <= 2 * c->n_cu ? 1 : 0;
+    const size_t st_smem = c->host_stitch ? stitch_host_smem_bytes(n_max, &Sp.th_cap)
+                                          : stitch_smem_bytes(kp_max, n_max, &Sp.th_cap);
     hipStream_t st = c->stream;
     if (L.n_items > 0) {
         rc = timed_launch(c, 0, st, [&] {
@@ -4547,11 +4656,27 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
         if (rc) return rc;
     }
-    rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + c->n_pairs, kStThreads, st_smem, st>>>(Sp); });
-    if (!rc && accumulate)
-        rc = timed_launch(c, 7, st, [&] {
-            k_stitch_sum<<<c->n_sum_blocks, 256, 0, st>>>(c->d_wins.p, c->d_sum_blocks.p, c->d_stage.p, c->d_sys.p);
+    if (c->host_stitch) {
+        static std::once_flag once;
+        std::call_once(once, [] {
+            int th;
+            (void)hipFuncSetAttribute((const void *)k_stitch_host, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)stitch_host_smem_bytes(kHostStitchMaxN, &th));
         });
+        rc = timed_launch(c, 2, st, [&] { k_stitch_host<<<Sp.n_win + (Sp.hs_split ? 2 : 1) * c->n_frames, kHsThreads, st_smem, st>>>(Sp);
+        });
+        if (!rc && accumulate)
+            rc = timed_launch(c, 7, st, [&] {
+                k_stitch_host_sum<<<c->n_sum_blocks, 256, 0, st>>>(c->d_wins.p, c->d_sum_blocks.p, c->d_stage.p,
+                                                                   c->d_sys.p);
+            });
+    } else {
+        rc = timed_launch(c, 2, st, [&] { k_stitch<<<Sp.n_win + c->n_pairs, kStThreads, st_smem, st>>>(Sp); });
+        if (!rc && accumulate)
+            rc = timed_launch(c, 7, st, [&] {
+                k_stitch_sum<<<c->n_sum_blocks, 256, 0, st>>>(c->d_wins.p, c->d_sum_blocks.p, c->d_stage.p, c->d_sys.p);
+            });
+    }
     if (rc || !c->comm) return rc;
     rc = comm_exchange(c, accumulate != 0);
     if (!rc && c->opt_hist) {  // the reduced energies into the optimize() history
