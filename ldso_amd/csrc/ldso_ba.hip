@@ -1925,6 +1925,41 @@ __device__ __forceinline__ void xad_fill(const WinDev &W, const double *xw, cons
     }
     if (tid < 4) o[(size_t)N * N * 8 + tid] = (float)xw[tid];
 }
+// xad_fill with the adjoint columns of item tid loaded at kernel start (their load latency hides
+// behind the factorisation); items tid + nthreads, ... as xad_fill
+struct XadPre {
+    float ah[8], at[8];
+    __device__ void load(const WinDev &W, const double *__restrict__ adH, const double *__restrict__ adT, int tid) {
+        const int N = W.N, e = min(tid, N * N * 8 - 1), cc = e & 7, ht = e >> 3, h = ht / N, t = ht % N;
+        const double *AH = adH + (size_t)(W.pair_base + h + N * t) * 64, *AT = adT + (size_t)(W.pair_base + h + N * t) * 64;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            ah[k] = (float)AH[k * 8 + cc];
+            at[k] = (float)AT[k * 8 + cc];
+        }
+    }
+    __device__ void fill(const WinDev &W, const double *xw, const double *__restrict__ adH,
+                         const double *__restrict__ adT, float *o, int tid, int nthreads) const {
+#pragma clang fp contract(off)
+        const int N = W.N;
+        if (tid < N * N * 8) {
+            const int cc = tid & 7, ht = tid >> 3, h = ht / N, t = ht % N;
+            float s1 = 0, s2 = 0;
+            for (int k = 0; k < 8; k++) s1 += (float)xw[4 + 8 * h + k] * ah[k];
+            for (int k = 0; k < 8; k++) s2 += (float)xw[4 + 8 * t + k] * at[k];
+            o[(size_t)(N * h + t) * 8 + cc] = s1 + s2;
+        }
+        for (int e = tid + nthreads; e < N * N * 8; e += nthreads) {
+            const int cc = e & 7, ht = e >> 3, h = ht / N, t = ht % N;
+            const double *AH = adH + (size_t)(W.pair_base + h + N * t) * 64, *AT = adT + (size_t)(W.pair_base + h + N * t) * 64;
+            float s1 = 0, s2 = 0;
+            for (int k = 0; k < 8; k++) s1 += (float)xw[4 + 8 * h + k] * (float)AH[k * 8 + cc];
+            for (int k = 0; k < 8; k++) s2 += (float)xw[4 + 8 * t + k] * (float)AT[k * 8 + cc];
+            o[(size_t)(N * h + t) * 8 + cc] = s1 + s2;
+        }
+        if (tid < 4) o[(size_t)N * N * 8 + tid] = (float)xw[tid];
+    }
+};
 
 struct SolveParams {
     const WinDev *__restrict__ wins;
@@ -1937,7 +1972,7 @@ struct SolveParams {
     const double *prep_nm, *prep_g;    // k_ortho_prep's results: Nm [vec][n_null], per window G | G^-1 | fast
     int iteration, n_null;
 };
-constexpr int kPrepGStride = 128;  // doubles per window in prep_g: G [49], G^-1 [49], fast flag
+constexpr int kPrepGStride = 192;  // doubles per window in prep_g: G [49], G^-1 [49], fast flag, V [49], ev [7], keep [7]
 // H's row stride in LDS: odd (in doubles), so a column walk touches 32 distinct bank pairs
 __host__ __device__ inline int solve_ld(int n) { return n | 1; }
 __host__ __device__ inline size_t solve_smem_bytes(int n) {
@@ -2133,6 +2168,67 @@ __device__ __forceinline__ void solve_ortho_prepare(const SolveParams &P, const 
                 for (int q = 0; q < 7; q++) S.Gi[r * 7 + q] = gi[r][q];
     }
     if (lane == 0) S.misc[7] = fast ? 1.0 : 0.0;
+    if (!fast) {  // the round-robin Jacobi eigen-decomposition of host_math.cpp project_out (lane 0)
+        if (lane == 0) {
+            double g[7][7], v[7][7];
+#pragma unroll
+            for (int r = 0; r < 7; r++)
+#pragma unroll
+                for (int q = 0; q < 7; q++) {
+                    g[r][q] = r < kk && q < kk ? G[r * kk + q] : 0.0;
+                    v[r][q] = r == q ? 1.0 : 0.0;
+                }
+            for (int sweep = 0; sweep < 64; sweep++) {
+                double off = 0;
+                for (int p = 0; p < 7; p++)
+                    for (int q = p + 1; q < 7; q++)
+                        if (q < kk) off += g[p][q] * g[p][q];
+                if (off < 1e-30) break;
+                for (int rd = 0; rd < 7; rd++) {
+                    double c[3], sn[3];
+                    bool on[3];
+                    for (int e = 0; e < 3; e++) {
+                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
+                        const double apq = g[p][q];
+                        on[e] = q < kk && apq != 0;
+                        const double th = (g[q][q] - g[p][p]) / (2 * apq);
+                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+                        c[e] = 1 / sqrt(t * t + 1);
+                        sn[e] = t * c[e];
+                    }
+                    for (int e = 0; e < 3; e++) {  // column phase
+                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
+                        if (!on[e]) continue;
+                        for (int r = 0; r < 7; r++) {
+                            const double gp = g[r][p], gq = g[r][q];
+                            g[r][p] = c[e] * gp - sn[e] * gq;
+                            g[r][q] = sn[e] * gp + c[e] * gq;
+                        }
+                    }
+                    for (int e = 0; e < 3; e++) {  // row phase, then V
+                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
+                        if (!on[e]) continue;
+                        for (int r = 0; r < 7; r++) {
+                            const double gp = g[p][r], gq = g[q][r];
+                            g[p][r] = c[e] * gp - sn[e] * gq;
+                            g[q][r] = sn[e] * gp + c[e] * gq;
+                            const double vp = v[r][p], vq = v[r][q];
+                            v[r][p] = c[e] * vp - sn[e] * vq;
+                            v[r][q] = sn[e] * vp + c[e] * vq;
+                        }
+                    }
+                }
+            }
+            double smax = 0;
+            for (int e = 0; e < 7; e++)
+                if (e < kk) smax = fmax(smax, sqrt(fmax(0.0, g[e][e])));
+            for (int e = 0; e < 7; e++) {
+                S.lr[e] = g[e][e];  // eigenvalue
+                S.lr[7 + e] = e < kk && sqrt(fmax(0.0, g[e][e])) > kSolverModeDelta * smax ? 1.0 : 0.0;
+                for (int a = 0; a < 7; a++) V[a * 7 + e] = v[a][e];
+            }
+        }
+    }
     wave_lds_sync();
 }
 
@@ -2149,7 +2245,9 @@ __device__ __forceinline__ void solve_ortho_load(const SolveParams &P, const Win
     if (tid < 49) {
         S.G[tid] = g[tid];
         S.Gi[tid] = g[49 + tid];
+        S.V[tid] = g[99 + tid];
     }
+    if (tid < 14) S.lr[tid] = g[148 + tid];  // eigenvalues, kept modes (the Jacobi fallback)
     if (tid == 0) S.misc[7] = g[98];
 }
 
@@ -2165,7 +2263,9 @@ __global__ __launch_bounds__(64) void k_ortho_prep(SolveParams P, double *prep_n
     if (lane < 49) {
         g[lane] = S.G[lane];
         g[49 + lane] = S.Gi[lane];
+        g[99 + lane] = S.V[lane];
     }
+    if (lane < 14) g[148 + lane] = S.lr[lane];
     if (lane == 0) g[98] = S.misc[7];
 }
 
@@ -2176,7 +2276,7 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
                                                         int lane) {
 #pragma clang fp contract(off)
     const int n = W.D;
-    double *y = S.y, *Nm = S.Nm, *G = S.G;
+    double *y = S.y, *Nm = S.Nm;
     const int kk = P.n_null;
     if (P.iteration >= 2 && kk > 0) {
         double *ntx = S.misc, *coef = S.misc + 8;
@@ -2208,88 +2308,22 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
                 }
                 coef[lane] = gram_apply7_row(gr, nt);
             }
-        } else {  // (NtN)^+ NtX in registers, every lane redundantly (no LDS traffic, no synchronisation)
-            double g[7][7], v[7][7], nt[7], cf[7] = {0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int r = 0; r < 7; r++)
-#pragma unroll
-                for (int q = 0; q < 7; q++) {
-                    g[r][q] = r < kk && q < kk ? G[r * kk + q] : 0.0;
-                    v[r][q] = r == q ? 1.0 : 0.0;
-                }
-#pragma unroll
-            for (int a = 0; a < 7; a++) nt[a] = a < kk ? ntx[a] : 0.0;
-            for (int sweep = 0; sweep < 64; sweep++) {
-                double off = 0;
-#pragma unroll
-                for (int p = 0; p < 7; p++)
-#pragma unroll
-                    for (int q = p + 1; q < 7; q++)
-                        if (q < kk) off += g[p][q] * g[p][q];
-                if (off < 1e-30) break;
-#pragma unroll
-                for (int rd = 0; rd < 7; rd++) {
-                    double c[3], sn[3];
-                    bool on[3];
-#pragma unroll
-                    for (int e = 0; e < 3; e++) {
-                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
-                        const double apq = g[p][q];
-                        on[e] = q < kk && apq != 0;
-                        const double th = (g[q][q] - g[p][p]) / (2 * apq);
-                        const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
-                        c[e] = 1 / sqrt(t * t + 1);
-                        sn[e] = t * c[e];
-                    }
-#pragma unroll
-                    for (int e = 0; e < 3; e++) {  // column phase
-                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
-                        if (!on[e]) continue;
-#pragma unroll
-                        for (int r = 0; r < 7; r++) {
-                            const double gp = g[r][p], gq = g[r][q];
-                            g[r][p] = c[e] * gp - sn[e] * gq;
-                            g[r][q] = sn[e] * gp + c[e] * gq;
-                        }
-                    }
-#pragma unroll
-                    for (int e = 0; e < 3; e++) {  // row phase, then V
-                        const int p = kJacobiRounds[rd][e][0], q = kJacobiRounds[rd][e][1];
-                        if (!on[e]) continue;
-#pragma unroll
-                        for (int r = 0; r < 7; r++) {
-                            const double gp = g[p][r], gq = g[q][r];
-                            g[p][r] = c[e] * gp - sn[e] * gq;
-                            g[q][r] = sn[e] * gp + c[e] * gq;
-                            const double vp = v[r][p], vq = v[r][q];
-                            v[r][p] = c[e] * vp - sn[e] * vq;
-                            v[r][q] = sn[e] * vp + c[e] * vq;
-                        }
-                    }
-                }
-            }
-            double smax = 0;
-#pragma unroll
-            for (int e = 0; e < 7; e++)
-                if (e < kk) smax = fmax(smax, sqrt(fmax(0.0, g[e][e])));
-#pragma unroll
-            for (int e = 0; e < 7; e++) {
-                if (e >= kk) continue;
-                const double ev = g[e][e];
-                if (!(sqrt(fmax(0.0, ev)) > kSolverModeDelta * smax)) continue;
-                double proj = 0;
-#pragma unroll
-                for (int a = 0; a < 7; a++)
-                    if (a < kk) proj += v[a][e] * nt[a];
-#pragma unroll
-                for (int a = 0; a < 7; a++)
-                    if (a < kk) cf[a] += v[a][e] * proj / ev;
-            }
+        } else {  // (NtN)^+ NtX from k_ortho_prep's eigen-decomposition (V, eigenvalues, kept modes)
             if (lane < kk) {
-                double mine = 0;
+                const double *V = S.V, *ev = S.lr, *keep = S.lr + 7;
+                double cf = 0, nt[7];
 #pragma unroll
-                for (int a = 0; a < 7; a++) mine = a == lane ? cf[a] : mine;
-                coef[lane] = mine;
+                for (int a = 0; a < 7; a++) nt[a] = a < kk ? ntx[a] : 0.0;
+#pragma unroll
+                for (int e = 0; e < 7; e++) {  // host_math.cpp project_out's accumulation, row `lane`
+                    if (e >= kk || keep[e] == 0.0) continue;
+                    double proj = 0;
+#pragma unroll
+                    for (int a = 0; a < 7; a++)
+                        if (a < kk) proj += V[a * 7 + e] * nt[a];
+                    cf += V[lane * 7 + e] * proj / ev[e];
+                }
+                coef[lane] = cf;
             }
         }
         wave_lds_sync();
@@ -2729,11 +2763,12 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
 // (Jacobi-scaled HA + priors + lambda damping - Hsc / (1 + lambda)), so an unpivoted LDL^T is
 // stable; dropping the pivot search removes the serial pivot reduction and the cross-wave
 // hand-off of every step.  Blocked right-looking LDL^T in LDS: wave 0 factorises an 8-column
-// panel out of registers (lane = row, the in-panel columns broadcast with readlane), then all
-// four waves apply the panel's rank-8 update to the trailing matrix (one barrier per panel).
-// Every element sees fma(-(c_i c_j), 1/d, A(i,j)) for the steps in ascending order, as the host
-// solver does, just without the row exchanges; L(i,k) = c_i * (1/d).  Wave 0 then runs the
-// substitutions while wave 1 prepares the nullspace projection.  x differs from the pivoted
+// panel out of registers (lane = row, the in-panel columns broadcast with readlane) together with
+// the forward substitution, while the other waves apply the previous panel's rank-8 update to
+// the trailing matrix (look-ahead, two barriers per panel).  Trailing elements see
+// fma(-(c_i c_j), 1/d, A(i,j)) for the steps in ascending order, as the host solver, just without
+// the row exchanges; in-panel ones fma(-c_i, c_j / d, A(i,j)); L(i,k) = c_i * (1/d).  Wave 0
+// then runs the backward substitution and the projection (prepared by k_ortho_prep).  x differs from the pivoted
 // solve (k_solve_reg / k_solve / ldso_ba_solve) only by rounding (tests: within the system's
 // float sensitivity envelope; optimize energies within 1e-4).
 // ============================================================================================
@@ -2742,28 +2777,29 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
 #endif
 constexpr int kSolveFastThreads = LDSO_SOLVE_FAST_THREADS;  // 8 waves: the trailing updates hide LDS latency
 constexpr int kSolveFastPanel = 8;
-#ifndef LDSO_EXP_SOLVE_SKIP  // timing experiments only (tools/solve_ab.py): 1 panels, 2 trailing, 4 subst, 8 apply
+#ifndef LDSO_EXP_SOLVE_SKIP  // timing experiments only (tools/solve_ab.py): 1 panels, 2 trailing, 4 back subst, 8 store, 16 xad
 #define LDSO_EXP_SOLVE_SKIP 0
 #endif
 __host__ __device__ inline size_t solve_fast_smem_bytes(int n) {
-    // SolveLds | W [8][128] panel columns | rd [8]
-    return solve_smem_bytes(n) + 16 + ((size_t)kSolveFastPanel * 128 + kSolveFastPanel) * sizeof(double);
+    // SolveLds | W [2][8][128] panel columns (double-buffered) | rd [2][8]
+    return solve_smem_bytes(n) + 16 + 2 * ((size_t)kSolveFastPanel * 128 + kSolveFastPanel) * sizeof(double);
 }
 // row k's value of a lane-per-row register pair (rows lane, lane + 64)
 template <int kH>
-__device__ __forceinline__ double fast_row(const double (&v)[kH], int k) {
+__device__ __forceinline__ double fast_row(const double *v, int k) {
     if constexpr (kH == 1)
         return readlane_f64(v[0], k);
     else
         return k < 64 ? readlane_f64(v[0], k) : readlane_f64(v[1], k - 64);
 }
-// Wave 0: LDL^T of panel columns p .. p+w-1 (rows lane + 64 h).  Lane i updates its rows'
-// panel entries unconditionally -- entries above the diagonal and rows past n turn into finite
-// junk that is never stored nor read -- so a step is one readlane pair and one mul + fma per
-// later column and row half, with the h = 1 half compiled out for n <= 64.
+// Wave 0: LDL^T of panel columns p .. p+w-1 (rows lane + 64 h) and the forward substitution
+// L y = b over the same columns (y in wave 0's registers across panels).  Lane i updates its
+// rows' panel entries unconditionally -- entries above the diagonal and rows past n turn into
+// finite junk that is never stored nor read -- so a step is one readlane pair, one product
+// cj / d and one fma per later column and row half, with the h = 1 half compiled out for n <= 64.
 template <int kH>
-__device__ __forceinline__ void fast_panel(double *H, double *Wc, double *rdv, int n, int ld, int p, int w,
-                                           int lane) {
+__device__ __forceinline__ void fast_panel(double *H, double *Wc, double *rdv, double *y, int n, int ld, int p,
+                                           int w, int lane) {
 #pragma clang fp contract(off)
     double r[kSolveFastPanel][kH];
 #pragma unroll
@@ -2778,59 +2814,44 @@ __device__ __forceinline__ void fast_panel(double *H, double *Wc, double *rdv, i
         if (kk >= w) break;
         const int k = p + kk;
         const double d = fast_row<kH>(r[kk], k);
-        const double rd = d != 0 ? 1.0 / d : 0.0;
+        // 1/d: v_rcp_f64 and two Newton steps (the IEEE divide's 10-deep chain sits on every step)
+        double rd = __builtin_amdgcn_rcp(d);
+        rd = fma(rd, fma(-d, rd, 1.0), rd);
+        rd = fma(rd, fma(-d, rd, 1.0), rd);
+        rd = d != 0 ? rd : 0.0;
 #pragma unroll
         for (int jj = kk + 1; jj < kSolveFastPanel; jj++) {
-            const double cj = fast_row<kH>(r[kk], p + jj);  // A(j, k); columns past n are junk
+            const double wj = fast_row<kH>(r[kk], p + jj) * rd;  // A(j, k) / d; columns past n are junk
 #pragma unroll
-            for (int h = 0; h < kH; h++) r[jj][h] = fma(-(r[kk][h] * cj), rd, r[jj][h]);
+            for (int h = 0; h < kH; h++) r[jj][h] = fma(-r[kk][h], wj, r[jj][h]);
         }
+        const double yk = fast_row<kH>(y, k);  // final: every earlier column already applied
 #pragma unroll
         for (int h = 0; h < kH; h++) {
             const int i = lane + 64 * h;
-            if (i < n) Wc[kk * 128 + i] = r[kk][h];  // the trailing update reads rows >= p + w only
-            if (i > k && i < n) H[i * ld + k] = r[kk][h] * rd;  // L(i,k) (rd = 0 for d = 0)
-            if (i == k) H[i * ld + k] = d;
+            const double l = i > k ? r[kk][h] * rd : 0.0;  // L(i,k) (rd = 0 for d = 0)
+            y[h] = fma(-l, yk, y[h]);
+            Wc[kk * 128 + i] = r[kk][h];  // 128 rows a column; the trailing updates read rows >= p + w only
+            // L below the diagonal, d on it; rows above it hold junk (nothing reads H's upper
+            // triangle after the assembly)
+            if (i < n) H[i * ld + k] = i > k ? l : d;
         }
         if (lane == 0) rdv[kk] = rd;
     }
 }
-// Wave 0: L y = b, D, L^T x = y (y in lanes i, i + 64), as k_solve without the permutation
+// Wave 0, after the last panel: D, L^T x = y (y in lanes i, i + 64), x = s y into S.y
 template <int kH>
-__device__ __forceinline__ void fast_subst(const double *H, const SolveLds &S, int n, int ld, int lane) {
+__device__ __forceinline__ void fast_back_subst(const double *H, const SolveLds &S, double *y, int n, int ld,
+                                                int lane) {
 #pragma clang fp contract(off)
-    double y[kH];
     int ri[kH];
 #pragma unroll
     for (int h = 0; h < kH; h++) {
         const int i = lane + 64 * h;
-        y[h] = i < n ? S.b[i] : 0.0;
         ri[h] = min(i, n - 1);
-    }
-    constexpr int kSubAhead = 4;
-    for (int j0 = 0; j0 < n; j0 += kSubAhead) {
-        double f[kSubAhead][kH];
-#pragma unroll
-        for (int u = 0; u < kSubAhead; u++)
-#pragma unroll
-            for (int h = 0; h < kH; h++) f[u][h] = H[ri[h] * ld + min(j0 + u, n - 1)];
-#pragma unroll
-        for (int u = 0; u < kSubAhead; u++) {
-            const int j = j0 + u;
-            if (j >= n) break;
-            const double yj = fast_row<kH>(y, j);
-#pragma unroll
-            for (int h = 0; h < kH; h++) {
-                const int i = lane + 64 * h;
-                if (i > j && i < n) y[h] = fma(-f[u][h], yj, y[h]);
-            }
-        }
-    }
-#pragma unroll
-    for (int h = 0; h < kH; h++) {
-        const int i = lane + 64 * h;
         if (i < n) y[h] = H[i * ld + i] != 0 ? y[h] / H[i * ld + i] : 0.0;
     }
+    constexpr int kSubAhead = 4;
     for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
         double f[kSubAhead][kH];
 #pragma unroll
@@ -2855,6 +2876,21 @@ __device__ __forceinline__ void fast_subst(const double *H, const SolveLds &S, i
         if (i < n) S.y[i] = S.sc[i] * y[h];  // x = s y
     }
 }
+// panel (Wp, rp: its c columns and 1/d, w steps) applied to A(i, j), steps in order
+__device__ __forceinline__ double fast_update(const double *Wp, const double *rp, int w, int i, int j, double a) {
+#pragma clang fp contract(off)
+    double wi[kSolveFastPanel], wj[kSolveFastPanel], rk[kSolveFastPanel];
+#pragma unroll
+    for (int kk = 0; kk < kSolveFastPanel; kk++) {  // every operand in flight before the chain
+        wi[kk] = Wp[kk * 128 + i];
+        wj[kk] = Wp[kk * 128 + j];
+        rk[kk] = rp[kk];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kSolveFastPanel; kk++)
+        if (kk < w) a = fma(-(wi[kk] * wj[kk]), rk[kk], a);
+    return a;
+}
 __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
@@ -2863,55 +2899,63 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
     const int ld = solve_ld(n);
     const SolveLds S(lds, n);
     double *H = S.H;
-    double *Wc = lds + (solve_smem_bytes(n) + 16) / sizeof(double);  // [8][128]: c of each panel step
-    double *rdv = Wc + kSolveFastPanel * 128;
+    double *Wc = lds + (solve_smem_bytes(n) + 16) / sizeof(double);  // [2][8][128]: c of each panel step
+    double *rdv = Wc + 2 * kSolveFastPanel * 128;                     // [2][8]: 1/d of each panel step
+    XadPre xp;
+    if (P.xad) xp.load(W, P.adH, P.adT, tid);
     solve_ortho_load(P, W, S, tid, kSolveFastThreads);
     solve_assemble<kSolveFastThreads>(P, W, S, tid);
-    for (int p = 0; p < n; p += kSolveFastPanel) {
-        const int w = min(kSolveFastPanel, n - p);
-        if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 1)) {
-            if (n > 64)
-                fast_panel<2>(H, Wc, rdv, n, ld, p, w, lane);
-            else
-                fast_panel<1>(H, Wc, rdv, n, ld, p, w, lane);
+    double y[2] = {0.0, 0.0};  // wave 0: the forward substitution's y (rows lane, lane + 64)
+    if (wave == 0) {
+        y[0] = lane < n ? S.b[lane] : 0.0;
+        y[1] = lane + 64 < n ? S.b[lane + 64] : 0.0;
+    }
+    auto panel = [&](int p, int w, int buf) {
+        double *Wb = Wc + buf * kSolveFastPanel * 128, *rb = rdv + buf * kSolveFastPanel;
+        if (LDSO_EXP_SOLVE_SKIP & 1) return;
+        if (n > 64)
+            fast_panel<2>(H, Wb, rb, y, n, ld, p, w, lane);
+        else
+            fast_panel<1>(H, Wb, rb, y, n, ld, p, w, lane);
+    };
+    // Blocked right-looking LDL^T with look-ahead: after panel p is factorised, all waves apply
+    // it to the next panel's columns; then wave 0 factorises the next panel while the other
+    // waves apply panel p to the rest of the trailing triangle (double-buffered panel columns).
+    if (wave == 0) panel(0, min(kSolveFastPanel, n), 0);
+    __syncthreads();
+    for (int p = 0, buf = 0; p + kSolveFastPanel < n; p += kSolveFastPanel, buf ^= 1) {
+        const int w = kSolveFastPanel, m0 = p + w, w1 = min(kSolveFastPanel, n - m0), m1 = m0 + w1;
+        const double *Wp = Wc + buf * kSolveFastPanel * 128, *rp = rdv + buf * kSolveFastPanel;
+        for (int e = tid; e < ((LDSO_EXP_SOLVE_SKIP & 2) ? 0 : (n - m0) * w1); e += kSolveFastThreads) {  // the next panel's columns
+            const int i = m0 + e / w1, j = m0 + e % w1;
+            if (i >= j) H[i * ld + j] = fast_update(Wp, rp, w, i, j, H[i * ld + j]);
         }
         __syncthreads();
-        // rank-w update of the trailing lower triangle (p + w <= j <= i < n), steps in order
-        const int m0 = p + w, nt = n - m0;
-        const int ne = nt * (nt + 1) / 2;
-        double rdk[kSolveFastPanel];
-#pragma unroll
-        for (int kk = 0; kk < kSolveFastPanel; kk++) rdk[kk] = kk < w ? rdv[kk] : 0.0;
-        for (int e = tid; e < ((LDSO_EXP_SOLVE_SKIP & 2) ? 0 : ne); e += kSolveFastThreads) {
-            int ii = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);  // row ii of the nt x nt triangle
-            if (ii * (ii + 1) / 2 > e) ii--;
-            if ((ii + 1) * (ii + 2) / 2 <= e) ii++;
-            const int i = m0 + ii, j = m0 + (e - ii * (ii + 1) / 2);
-            double wi[kSolveFastPanel], wj[kSolveFastPanel];
-#pragma unroll
-            for (int kk = 0; kk < kSolveFastPanel; kk++) {  // every operand in flight before the chain
-                wi[kk] = Wc[kk * 128 + i];
-                wj[kk] = Wc[kk * 128 + j];
+        if (wave == 0) {
+            panel(m0, w1, buf ^ 1);
+        } else {  // the rest of the trailing triangle (m1 <= j <= i < n)
+            const int nt = n - m1, ne = (LDSO_EXP_SOLVE_SKIP & 2) ? 0 : nt * (nt + 1) / 2;
+            for (int e = tid - 64; e < ne; e += kSolveFastThreads - 64) {
+                int ii = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);  // row ii of the nt x nt triangle
+                if (ii * (ii + 1) / 2 > e) ii--;
+                if ((ii + 1) * (ii + 2) / 2 <= e) ii++;
+                const int i = m1 + ii, j = m1 + (e - ii * (ii + 1) / 2);
+                H[i * ld + j] = fast_update(Wp, rp, w, i, j, H[i * ld + j]);
             }
-            double a = H[i * ld + j];
-#pragma unroll
-            for (int kk = 0; kk < kSolveFastPanel; kk++)
-                if (kk < w) a = fma(-(wi[kk] * wj[kk]), rdk[kk], a);
-            H[i * ld + j] = a;
         }
         __syncthreads();
     }
     if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 4)) {
         if (n > 64)
-            fast_subst<2>(H, S, n, ld, lane);
+            fast_back_subst<2>(H, S, y, n, ld, lane);
         else
-            fast_subst<1>(H, S, n, ld, lane);
+            fast_back_subst<1>(H, S, y, n, ld, lane);
     }
     __syncthreads();
     if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 8)) solve_ortho_apply_store(P, W, S, lane);
-    if (P.xad) {  // x is in S.y: the resubstitution's xAd by all waves
+    if (P.xad && !(LDSO_EXP_SOLVE_SKIP & 16)) {  // x is in S.y: the resubstitution's xAd by all waves
         __syncthreads();
-        xad_fill(W, S.y, P.adH, P.adT, P.xad + (size_t)blockIdx.x * kXadStride, tid, kSolveFastThreads);
+        xp.fill(W, S.y, P.adH, P.adT, P.xad + (size_t)blockIdx.x * kXadStride, tid, kSolveFastThreads);
     }
 }
 
