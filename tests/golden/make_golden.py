@@ -23,11 +23,14 @@ from ldso_amd import synth  # noqa: E402
 CASES = {
     "w3_p64": dict(n_frames=3, n_points=64, width=160, height=120, seed=101),
     "w5_p160": dict(n_frames=5, n_points=160, width=160, height=120, seed=102, baseline=0.08),
+    "w7_p256": dict(n_frames=7, n_points=256, width=160, height=120, seed=103),  # SURVEY §7 step 2's N=7, P=256
 }
 
 
-def main():
+def main(names=None):
     for name, cfg in CASES.items():
+        if names and name not in names:
+            continue
         w = synth.make_window(**cfg)
         ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
         e, s = ow.iteration()
@@ -50,4 +53,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

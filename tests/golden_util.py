@@ -36,4 +36,4 @@ def load(name):
     return w, {k[4:]: z[k] for k in z.files if k.startswith("out_")}, z
 
 
-NAMES = ["w3_p64", "w5_p160"]
+NAMES = ["w3_p64", "w5_p160", "w7_p256"]
