@@ -3397,6 +3397,25 @@ __global__ __launch_bounds__(256) void k_set_point_vals(const float4 *__restrict
     d[5] = v.w;
 }
 // idepth of every resident point (point-data column 2), compacted for one small download
+// up to kPackSegs device arrays (4-byte words) and optionally the idepth column of the point
+// records into the mapped results buffer, one launch
+constexpr int kPackSegs = 5;
+struct PackOut {
+    const unsigned *src[kPackSegs];
+    unsigned *dst[kPackSegs];
+    int words[kPackSegs];
+    int n_seg;
+    const float *pt_data;  // non-null: idepth of every point record into idepth_dst
+    float *idepth_dst;
+    int n_points;
+};
+__global__ __launch_bounds__(256) void k_pack_out(PackOut P) {
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    for (int s = 0; s < P.n_seg; s++)
+        for (int e = tid; e < P.words[s]; e += nth) P.dst[s][e] = P.src[s][e];
+    if (P.pt_data)
+        for (int q = tid; q < P.n_points; q += nth) P.idepth_dst[q] = P.pt_data[(size_t)q * LDSO_BA_POINT_STRIDE + 2];
+}
 __global__ __launch_bounds__(256) void k_gather_idepth(const float *__restrict__ pt_data, float *out, int n) {
     const int q = blockIdx.x * 256 + threadIdx.x;
     if (q < n) out[q] = pt_data[(size_t)q * LDSO_BA_POINT_STRIDE + 2];
@@ -3504,7 +3523,8 @@ struct ldso_ba_ctx {
         hipGraphExec_t exec = nullptr;
         unsigned long long gen = 0, key = 0;
     };
-    Graph opt_graph[8], it_graph[2];
+    Graph opt_graph[2], it_graph[2];  // ldso_ba_optimize's whole call (without / with nullspaces)
+    bool opt_warm = false;            // an optimize call ran directly on this context
     int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
@@ -3579,6 +3599,8 @@ struct ldso_ba_ctx {
     // one call lands here, behind a single synchronisation
     char *pin_out = nullptr;
     size_t pin_out_n = 0;
+    char *pin_map = nullptr, *pin_map_dev = nullptr;  // fine-grained pinned results buffer, written by k_pack_out
+    size_t pin_map_n = 0;
     std::vector<double> energy_host;
     bool energy_valid = false;
     // ldso_ba_linearize_residuals: k_linearize runs on copies of the residual state so that the
@@ -3601,6 +3623,26 @@ int pin_ensure(char *&p, size_t &cap, size_t bytes) {
     cap = 0;
     HIP_TRY(hipHostMalloc((void **)&p, bytes, hipHostMallocDefault));
     cap = bytes;
+    return 0;
+}
+
+// the results buffer the device writes directly (coherent host memory: k_pack_out's stores are
+// visible to the host once the stream has synchronised), so a call's results come back in one
+// launch instead of one blit per array
+int pin_map_ensure(ldso_ba_ctx *c, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 64);
+    if (c->pin_map && c->pin_map_n >= bytes) return 0;
+    if (c->pin_map) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        (void)hipHostFree(c->pin_map);
+    }
+    c->pin_map = c->pin_map_dev = nullptr;
+    c->pin_map_n = 0;
+    HIP_TRY(hipHostMalloc((void **)&c->pin_map, bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    void *d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, c->pin_map, 0));
+    c->pin_map_dev = static_cast<char *>(d);
+    c->pin_map_n = bytes;
     return 0;
 }
 
@@ -3964,6 +4006,7 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (c->pin_xad) (void)hipHostFree(c->pin_xad);
     if (c->pin_step) (void)hipHostFree(c->pin_step);
     if (c->pin_out) (void)hipHostFree(c->pin_out);
+    if (c->pin_map) (void)hipHostFree(c->pin_map);
     c->d_wins.release();
     c->d_img.release();
     c->d_act_in.release();
@@ -5295,15 +5338,17 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
     const bool project = iteration >= 2 && n_null > 0 && ns;
     if (project && (rc = upload_nullspaces(c, ns, n_null)))  // before (outside) the captured sequence
         return rc;
-    // pass + solve + resubstitution: one captured graph per (projection, lambda, n_null) without
-    // a communicator or kernel timing; the downloads stay outside it
+    // pass + solve + resubstitution (LDSO_BA_ITERATE_GRAPH=1: one captured graph per (projection,
+    // lambda, n_null) without a communicator or kernel timing); the downloads stay outside it
     auto body = [&]() -> int {
         int r;
         if ((r = ldso_ba_linearize(c, 0, 1))) return r;
         if ((r = solve_device_launch(c, project ? 2 : 0, project ? n_null : 0))) return r;
         return c->P_tot > 0 ? launch_resubstitute(c, 0, c->P_tot, lambda) : 0;
     };
-    if (!c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH")) {
+    // direct launches by default: for this six-launch sequence hipGraphLaunch costs more host
+    // time than it saves (one S7 window: 89 vs 95 us per call, tools/iter_probe.py)
+    if (!c->comm && !c->timing && getenv_flag("LDSO_BA_ITERATE_GRAPH") && !getenv_flag("LDSO_BA_NO_GRAPH")) {
         unsigned long long lb;
         std::memcpy(&lb, &lambda, sizeof(lb));
         rc = launch_cached_graph(c, c->it_graph[project ? 1 : 0], lb ^ ((unsigned long long)n_null << 56), body);
@@ -5311,16 +5356,28 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
         rc = body();
     }
     if (rc) return rc;
-    // x, the energies and the point steps into one pinned buffer, one synchronisation
+    // x, the energies and the point steps into the mapped results buffer (one launch), one
+    // synchronisation
     const size_t xb = (size_t)c->vec_total * sizeof(double), eb = (size_t)2 * c->n_win * sizeof(double),
                  sb = (size_t)c->P_tot * sizeof(float);
-    if ((rc = pin_ensure(c->pin_out, c->pin_out_n, xb + eb + sb))) return rc;
-    const double *px = reinterpret_cast<const double *>(c->pin_out), *pe = px + c->vec_total;
+    if ((rc = pin_map_ensure(c, xb + eb + sb))) return rc;
+    const double *px = reinterpret_cast<const double *>(c->pin_map), *pe = px + c->vec_total;
     const float *ps = reinterpret_cast<const float *>(pe + 2 * c->n_win);
-    if (x_out) HIP_TRY(hipMemcpyAsync((void *)px, c->d_x.p, xb, hipMemcpyDeviceToHost, c->stream));
-    if (energy_out) HIP_TRY(hipMemcpyAsync((void *)pe, c->d_win_energy.p, eb, hipMemcpyDeviceToHost, c->stream));
-    if (point_step_out && sb)
-        HIP_TRY(hipMemcpyAsync((void *)ps, c->d_pt_step.p, sb, hipMemcpyDeviceToHost, c->stream));
+    {
+        PackOut K{};
+        auto seg = [&](const void *src, size_t off, size_t bytes) {
+            K.src[K.n_seg] = static_cast<const unsigned *>(src);
+            K.dst[K.n_seg] = reinterpret_cast<unsigned *>(c->pin_map_dev + off);
+            K.words[K.n_seg++] = (int)(bytes / 4);
+        };
+        if (x_out) seg(c->d_x.p, 0, xb);
+        if (energy_out) seg(c->d_win_energy.p, xb, eb);
+        if (point_step_out && sb) seg(c->d_pt_step.p, xb + eb, sb);
+        if (K.n_seg) {
+            k_pack_out<<<std::min(64, (int)((xb + eb + sb) / 1024) + 1), 256, 0, c->stream>>>(K);
+            HIP_TRY(hipGetLastError());
+        }
+    }
     if ((rc = ldso_ba_sync(c))) return rc;
     if (x_out) std::memcpy(x_out, px, xb);
     if (point_step_out) {
@@ -5399,21 +5456,25 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         return ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0);
     };
     // FullSystem::optimize (FullSystem.cc:853-976) with setting_forceAceptStep: resetOOB, then
-    // linearizeAll + applyRes, then the GN iterations.  Without a communicator or kernel timing,
-    // iterations after the first replay a captured HIP graph of one iteration: every launch
-    // argument of an iteration is the same except the solve's projection (iteration >= 2) and the
-    // last pass's accumulate flag, so at most three graphs; they are cached in the context and
-    // re-captured only after a device (re)allocation.
+    // linearizeAll + applyRes, then the GN iterations.  Every launch argument of the whole
+    // sequence is fixed by (n_its, nullspaces or not), so without a communicator or kernel timing
+    // the calls after the first replay ONE captured HIP graph of it (graph launches are
+    // separated by ~9 us on the GPU; one per call instead of one per iteration), cached in the
+    // context and re-captured only after a device (re)allocation or for another n_its.
     c->opt_hist = true;  // every pass of this call writes its energies into the history too
-    if ((rc = ldso_ba_reset_oob(c, -1)) || (rc = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0))) {
-        c->opt_hist = false;
-        return rc;
-    }
+    auto body = [&]() -> int {
+        int r;
+        if ((r = ldso_ba_reset_oob(c, -1)) || (r = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0))) return r;
+        for (int it = 0; it < n_its; it++)
+            if ((r = gn_iteration(it))) return r;
+        return 0;
+    };
     const bool use_graph = !c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH");
-    auto variant = [&](int it) { return (it >= 2 ? 1 : 0) + (it + 1 < n_its ? 0 : 2) + (ns ? 4 : 0); };
-    for (int it = 0; it < n_its && !rc; it++) {
-        if (!use_graph || it == 0) rc = gn_iteration(it);
-        else rc = launch_cached_graph(c, c->opt_graph[variant(it)], 0, [&] { return gn_iteration(it); });
+    if (use_graph && c->opt_warm) {
+        rc = launch_cached_graph(c, c->opt_graph[ns ? 1 : 0], (unsigned long long)n_its, body);
+    } else {
+        rc = body();  // the first call runs directly (one-time setup stays out of any capture)
+        c->opt_warm = rc == 0;
     }
     c->opt_hist = false;
     if (rc) return rc;
@@ -5424,17 +5485,26 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
                  wb = (size_t)nw * sizeof(WinDev), ib = (size_t)c->P_tot * sizeof(float);
     auto up16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
     const size_t o_f = up16(hb), o_c = o_f + up16(fb), o_w = o_c + up16(cb), o_i = o_w + up16(wb);
-    if ((rc = pin_ensure(c->pin_out, c->pin_out_n, o_i + ib))) return rc;
-    char *po = c->pin_out;
-    if (energy_out) HIP_TRY(hipMemcpyAsync(po, c->d_ehist.p, hb, hipMemcpyDeviceToHost, c->stream));
-    if (frames_out) HIP_TRY(hipMemcpyAsync(po + o_f, c->d_fstate.p, fb, hipMemcpyDeviceToHost, c->stream));
-    if (calib_out) HIP_TRY(hipMemcpyAsync(po + o_c, c->d_calib_val.p, cb, hipMemcpyDeviceToHost, c->stream));
-    // the host mirror of WinDev (calibration, cDeltaF) follows the device
-    HIP_TRY(hipMemcpyAsync(po + o_w, c->d_wins.p, wb, hipMemcpyDeviceToHost, c->stream));
-    if (idepth_out && c->P_tot) {  // the idepth column only
-        k_gather_idepth<<<(c->P_tot + 255) / 256, 256, 0, c->stream>>>(c->d_pt_data.p, c->d_pt_step.p, c->P_tot);
+    if ((rc = pin_map_ensure(c, o_i + ib))) return rc;
+    char *po = c->pin_map, *pd = c->pin_map_dev;
+    {  // one launch writes every result into the mapped buffer (the idepth column only)
+        PackOut K{};
+        auto seg = [&](const void *src, size_t off, size_t bytes) {
+            K.src[K.n_seg] = static_cast<const unsigned *>(src);
+            K.dst[K.n_seg] = reinterpret_cast<unsigned *>(pd + off);
+            K.words[K.n_seg++] = (int)(bytes / 4);
+        };
+        if (energy_out) seg(c->d_ehist.p, 0, hb);
+        if (frames_out) seg(c->d_fstate.p, o_f, fb);
+        if (calib_out) seg(c->d_calib_val.p, o_c, cb);
+        seg(c->d_wins.p, o_w, wb);  // the host mirror of WinDev (calibration, cDeltaF) follows the device
+        if (idepth_out && c->P_tot) {
+            K.pt_data = c->d_pt_data.p;
+            K.idepth_dst = reinterpret_cast<float *>(pd + o_i);
+            K.n_points = c->P_tot;
+        }
+        k_pack_out<<<std::min(64, (int)((o_i + ib) / 1024) + 1), 256, 0, c->stream>>>(K);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(po + o_i, c->d_pt_step.p, ib, hipMemcpyDeviceToHost, c->stream));
     }
     if ((rc = ldso_ba_sync(c))) return rc;
     if (energy_out) {

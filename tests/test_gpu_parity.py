@@ -506,10 +506,12 @@ def test_prepared_nullspaces_follow_the_callers_nullspaces(built):
     c.close()
 
 
-def test_iterate_replay_refreshes_host_copies_and_projects_only_with_this_calls_nullspaces(built):
-    """A replayed ldso_ba_iterate graph invalidates the host copies of the system / energies (the
-    replay skips the captured calls' host side), and a device solve projects only with the
-    nullspaces passed in THAT call (none: no projection, as the host solver)."""
+def test_iterate_replay_refreshes_host_copies_and_projects_only_with_this_calls_nullspaces(built, monkeypatch):
+    """A replayed ldso_ba_iterate graph (LDSO_BA_ITERATE_GRAPH=1; direct launches are the default)
+    invalidates the host copies of the system / energies (the replay skips the captured calls'
+    host side), and a device solve projects only with the nullspaces passed in THAT call (none:
+    no projection, as the host solver)."""
+    monkeypatch.setenv("LDSO_BA_ITERATE_GRAPH", "1")
     cfg = dict(n_frames=5, n_points=400, seed=61)
     w = synth.make_window(**cfg)
     ns = [w.nullspaces()]
