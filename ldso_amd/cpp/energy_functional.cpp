@@ -785,6 +785,9 @@ Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std:
     }
     for (int f = 0; f < N; f++) frames[f]->frameEnergyTH = th[f];
     setDeltaF(HCalib);  // setPrecalcValues' setDeltaF after the last step: points' deltaF = 0
+    // The frame terms are NOT marked uploaded: the next pass uses the host's FrameFramePrecalc /
+    // takeData of the stepped states (the reference's setPrecalcValues), which differ from the
+    // device's in libm's last ulp; upload() re-sends them in one staged launch.
     for (int q = 0; q < P; q++) {
         pointVals_[4 * q] = ptPtr_[q]->idepth_scaled;
         pointVals_[4 * q + 1] = ptPtr_[q]->idepth_zero_scaled;

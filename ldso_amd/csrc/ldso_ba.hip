@@ -3399,7 +3399,7 @@ __global__ __launch_bounds__(256) void k_set_point_vals(const float4 *__restrict
 // idepth of every resident point (point-data column 2), compacted for one small download
 // up to kPackSegs device arrays (4-byte words) and optionally the idepth column of the point
 // records into the mapped results buffer, one launch
-constexpr int kPackSegs = 5;
+constexpr int kPackSegs = 8;
 struct PackOut {
     const unsigned *src[kPackSegs];
     unsigned *dst[kPackSegs];
@@ -3601,8 +3601,14 @@ struct ldso_ba_ctx {
     size_t pin_out_n = 0;
     char *pin_map = nullptr, *pin_map_dev = nullptr;  // fine-grained pinned results buffer, written by k_pack_out
     size_t pin_map_n = 0;
+    char *pin_in = nullptr, *pin_in_dev = nullptr;  // mapped staging of small uploads, read by k_pack_out
+    size_t pin_in_n = 0;
+    hipEvent_t pin_in_ev = nullptr;  // the last launch reading pin_in
+    bool pin_in_busy = false;
     std::vector<double> energy_host;
     bool energy_valid = false;
+    std::vector<float> th_host;  // d_frame_th as of the end of the last ldso_ba_optimize ...
+    bool th_host_valid = false;  // ... until the next pass, update or threshold exchange
     // ldso_ba_linearize_residuals: k_linearize runs on copies of the residual state so that the
     // context's own state (and its records, read by resubstitution) stay untouched
     DevBuf<int8_t> d_sx_state, d_sx_newstate;
@@ -3643,6 +3649,60 @@ int pin_map_ensure(ldso_ba_ctx *c, size_t bytes) {
     HIP_TRY(hipHostGetDevicePointer(&d, c->pin_map, 0));
     c->pin_map_dev = static_cast<char *>(d);
     c->pin_map_n = bytes;
+    return 0;
+}
+
+// Small host -> device uploads of one call gathered into the mapped staging buffer and written
+// by ONE k_pack_out launch (pageable hipMemcpyAsync costs ~10 us of host time per array)
+struct InBatch {
+    struct Item {
+        void *dst;
+        const void *src;
+        size_t bytes;
+    };
+    std::vector<Item> items;
+    void add(void *dst, const void *src, size_t bytes) {
+        if (bytes) items.push_back({dst, src, bytes});
+    }
+    int flush(ldso_ba_ctx *c);
+};
+int InBatch::flush(ldso_ba_ctx *c) {
+    if (items.empty()) return 0;
+    size_t total = 0;
+    for (const Item &it : items) total += (it.bytes + 15) & ~(size_t)15;
+    if (c->pin_in_busy) {  // the previous launch must have read the staging buffer
+        HIP_TRY(hipEventSynchronize(c->pin_in_ev));
+        c->pin_in_busy = false;
+    }
+    if (!c->pin_in || c->pin_in_n < total) {
+        if (c->pin_in) (void)hipHostFree(c->pin_in);
+        c->pin_in = c->pin_in_dev = nullptr;
+        c->pin_in_n = 0;
+        HIP_TRY(hipHostMalloc((void **)&c->pin_in, std::max<size_t>(total, 4096), hipHostMallocCoherent | hipHostMallocMapped));
+        void *d = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&d, c->pin_in, 0));
+        c->pin_in_dev = static_cast<char *>(d);
+        c->pin_in_n = std::max<size_t>(total, 4096);
+    }
+    if (!c->pin_in_ev) HIP_TRY(hipEventCreateWithFlags(&c->pin_in_ev, hipEventDisableTiming));
+    size_t off = 0;
+    PackOut K{};
+    for (size_t k = 0; k < items.size(); k++) {
+        const Item &it = items[k];
+        std::memcpy(c->pin_in + off, it.src, it.bytes);
+        K.src[K.n_seg] = reinterpret_cast<const unsigned *>(c->pin_in_dev + off);
+        K.dst[K.n_seg] = static_cast<unsigned *>(it.dst);
+        K.words[K.n_seg++] = (int)(it.bytes / 4);
+        off += (it.bytes + 15) & ~(size_t)15;
+        if (K.n_seg == kPackSegs || k + 1 == items.size()) {
+            k_pack_out<<<std::min(64, (int)(total / 1024) + 1), 256, 0, c->stream>>>(K);
+            HIP_TRY(hipGetLastError());
+            K = PackOut{};
+        }
+    }
+    HIP_TRY(hipEventRecord(c->pin_in_ev, c->stream));
+    c->pin_in_busy = true;
+    items.clear();
     return 0;
 }
 
@@ -3768,10 +3828,10 @@ int stage_images(ldso_ba_ctx *c, const ldso_ba_window *ws, int n_windows, int *m
 
 // HL diagonal and bL of one window (the priors accumulateLF_MT stitches, AccumulatedTopHessian.cc:
 // 241-250) as the device solver reads them; zero on ranks other than 0 of a sharded window
-int upload_priors(ldso_ba_ctx *c, int win) {
+void priors_vector(const ldso_ba_ctx *c, int win, std::vector<double> &pr) {
     const WinHost &H = c->wh[win];
     const WinDev &D = c->wd[win];
-    std::vector<double> pr((size_t)2 * D.D, 0.0);
+    pr.assign((size_t)2 * D.D, 0.0);
     if (H.add_priors) {
         for (int i = 0; i < 4; i++) {
             pr[2 * i] = H.c_prior[i];
@@ -3784,7 +3844,11 @@ int upload_priors(ldso_ba_ctx *c, int win) {
                 pr[2 * q + 1] = H.frame_prior[8 * f + i] * H.frame_delta_prior[8 * f + i];
             }
     }
-    HIP_TRY(hipMemcpyAsync(c->d_prior.p + (size_t)2 * D.vec_base, pr.data(), pr.size() * sizeof(double),
+}
+int upload_priors(ldso_ba_ctx *c, int win) {
+    std::vector<double> pr;
+    priors_vector(c, win, pr);
+    HIP_TRY(hipMemcpyAsync(c->d_prior.p + (size_t)2 * c->wd[win].vec_base, pr.data(), pr.size() * sizeof(double),
                            hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
@@ -4007,6 +4071,8 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     if (c->pin_step) (void)hipHostFree(c->pin_step);
     if (c->pin_out) (void)hipHostFree(c->pin_out);
     if (c->pin_map) (void)hipHostFree(c->pin_map);
+    if (c->pin_in) (void)hipHostFree(c->pin_in);
+    if (c->pin_in_ev) (void)hipEventDestroy(c->pin_in_ev);
     c->d_wins.release();
     c->d_img.release();
     c->d_act_in.release();
@@ -4099,6 +4165,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
               const ldso_ba_ctx *parent, int parent_win) {
     if (!c || n_windows < 1 || !ws) return fail(-1, "bad arguments");
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(-1, "bad shard");
+    c->th_host_valid = false;
     for (int w = 0; w < n_windows; w++) {
         int rc = check_window(ws[w], parent == nullptr);
         if (rc) return rc;
@@ -4477,13 +4544,13 @@ int ldso_ba_load_marginalization(ldso_ba_ctx *marg, const ldso_ba_ctx *parent, i
 
 int ldso_ba_update(ldso_ba_ctx *c, int32_t win, const ldso_ba_window *w) {
     if (!c || !w || win < 0 || win >= c->n_win) return fail(-1, "bad arguments");
+    c->th_host_valid = false;
     WinHost &H = c->wh[win];
     WinDev &D = c->wd[win];
     if (w->n_frames != H.N || w->n_points != H.P_all || w->n_residuals != H.R_all)
         return fail(-1, "update() cannot change the window structure; call ldso_ba_load");
     const int N = H.N;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
     for (int i = 0; i < 4; i++) D.calib[i] = w->calib[i];
     H.c_prior.assign(w->c_prior, w->c_prior + 4);
     H.c_delta.assign(w->c_delta, w->c_delta + 4);
@@ -4498,21 +4565,22 @@ int ldso_ba_update(ldso_ba_ctx *c, int32_t win, const ldso_ba_window *w) {
         for (int q = 0; q < H.P; q++)
             std::memcpy(&pd[(size_t)q * LDSO_BA_POINT_STRIDE],
                         w->point_data + (size_t)H.pt_orig[q] * LDSO_BA_POINT_STRIDE, LDSO_BA_POINT_STRIDE * sizeof(float));
-    HIP_TRY(hipMemcpyAsync(c->d_wins.p + win, &D, sizeof(WinDev), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_precalc.p + (size_t)D.pair_base * LDSO_BA_PRECALC_STRIDE, w->precalc,
-                           (size_t)N * N * LDSO_BA_PRECALC_STRIDE * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_adH.p + (size_t)D.pair_base * 64, w->ad_host, (size_t)N * N * 64 * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_adT.p + (size_t)D.pair_base * 64, w->ad_target, (size_t)N * N * 64 * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_frame_th.p + D.frame_base, w->frame_energy_th, N * sizeof(float),
-                           hipMemcpyHostToDevice, c->stream));
+    std::vector<double> pr;
+    priors_vector(c, win, pr);
+    // every array of the update through the mapped staging buffer in one launch, stream-ordered
+    // (the caller's arrays are copied before this returns; no synchronisation)
+    InBatch B;
+    B.add(c->d_wins.p + win, &D, sizeof(WinDev));
+    B.add(c->d_precalc.p + (size_t)D.pair_base * LDSO_BA_PRECALC_STRIDE, w->precalc,
+          (size_t)N * N * LDSO_BA_PRECALC_STRIDE * sizeof(float));
+    B.add(c->d_adH.p + (size_t)D.pair_base * 64, w->ad_host, (size_t)N * N * 64 * sizeof(double));
+    B.add(c->d_adT.p + (size_t)D.pair_base * 64, w->ad_target, (size_t)N * N * 64 * sizeof(double));
+    B.add(c->d_frame_th.p + D.frame_base, w->frame_energy_th, N * sizeof(float));
+    B.add(c->d_prior.p + (size_t)2 * D.vec_base, pr.data(), pr.size() * sizeof(double));
     if (H.P && w->point_data)
-        HIP_TRY(hipMemcpyAsync(c->d_pt_data.p + (size_t)D.point_base * LDSO_BA_POINT_STRIDE, pd.data(),
-                               pd.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+        B.add(c->d_pt_data.p + (size_t)D.point_base * LDSO_BA_POINT_STRIDE, pd.data(), pd.size() * sizeof(float));
     c->sys_host_valid = false;
-    return upload_priors(c, win);
+    return B.flush(c);
 }
 
 int ldso_ba_update_points(ldso_ba_ctx *c, int32_t win, const float *vals) {
@@ -4659,6 +4727,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     HIP_TRY(hipSetDevice(c->device));
     c->sys_host_valid = false;
     c->energy_valid = false;
+    c->th_host_valid = false;
     int rc;
     LinParams L;
     L.items = c->d_top_items.p;
@@ -5097,6 +5166,10 @@ int ldso_ba_get_points(ldso_ba_ctx *c, int32_t win, float *HdiF, float *bdSumF, 
 
 int ldso_ba_get_frame_energy_th(ldso_ba_ctx *c, int32_t win, float *th) {
     if (!c || !th || win < 0 || win >= c->n_win) return fail(-1, "bad arguments");
+    if (c->th_host_valid) {  // ldso_ba_optimize brought it back with its other results
+        std::memcpy(th, c->th_host.data() + c->wd[win].frame_base, c->wd[win].N * sizeof(float));
+        return 0;
+    }
     int rc = ldso_ba_sync(c);
     if (rc) return rc;
     HIP_TRY(hipMemcpy(th, c->d_frame_th.p + c->wd[win].frame_base, c->wd[win].N * sizeof(float), hipMemcpyDeviceToHost));
@@ -5323,6 +5396,7 @@ int launch_cached_graph(ldso_ba_ctx *c, ldso_ba_ctx::Graph &g, unsigned long lon
     // a replay skips the host side of the captured calls: invalidate what their passes would
     c->sys_host_valid = false;
     c->energy_valid = false;
+    c->th_host_valid = false;
     return 0;
 }
 }  // namespace
@@ -5419,14 +5493,15 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         for (int k = 0; k < 4; k++) cp[4 * w + k] = c->wh[w].c_prior[k];
         ap[w] = c->wh[w].add_priors ? 1 : 0;
     }
-    HIP_TRY(hipMemcpyAsync(c->d_fstate.p, frames, (size_t)c->n_frames * sizeof(ldso_ba_frame_state),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_calib_val.p, calib_value, (size_t)4 * nw * sizeof(double), hipMemcpyHostToDevice,
-                           c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_calib_zero.p, calib_value_zero, (size_t)4 * nw * sizeof(double),
-                           hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_cprior.p, cp.data(), cp.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_add_priors.p, ap.data(), ap.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    {  // the call's inputs in one staged launch
+        InBatch B;
+        B.add(c->d_fstate.p, frames, (size_t)c->n_frames * sizeof(ldso_ba_frame_state));
+        B.add(c->d_calib_val.p, calib_value, (size_t)4 * nw * sizeof(double));
+        B.add(c->d_calib_zero.p, calib_value_zero, (size_t)4 * nw * sizeof(double));
+        B.add(c->d_cprior.p, cp.data(), cp.size() * sizeof(double));
+        B.add(c->d_add_priors.p, ap.data(), ap.size() * sizeof(int));
+        if ((rc = B.flush(c))) return rc;
+    }
     if (ns && (rc = upload_nullspaces(c, ns, 7)))  // evalPT is fixed during optimize(): valid for every iteration
         return rc;
     FrameStepParams F;
@@ -5482,9 +5557,10 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     // descriptors, the idepth column), one synchronisation
     const size_t hb = (size_t)2 * nw * (n_its + 1) * sizeof(double),
                  fb = (size_t)c->n_frames * sizeof(ldso_ba_frame_state), cb = (size_t)4 * nw * sizeof(double),
-                 wb = (size_t)nw * sizeof(WinDev), ib = (size_t)c->P_tot * sizeof(float);
+                 wb = (size_t)nw * sizeof(WinDev), ib = (size_t)c->P_tot * sizeof(float),
+                 tb = (size_t)c->n_frames * sizeof(float);
     auto up16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
-    const size_t o_f = up16(hb), o_c = o_f + up16(fb), o_w = o_c + up16(cb), o_i = o_w + up16(wb);
+    const size_t o_f = up16(hb), o_c = o_f + up16(fb), o_w = o_c + up16(cb), o_t = o_w + up16(wb), o_i = o_t + up16(tb);
     if ((rc = pin_map_ensure(c, o_i + ib))) return rc;
     char *po = c->pin_map, *pd = c->pin_map_dev;
     {  // one launch writes every result into the mapped buffer (the idepth column only)
@@ -5498,6 +5574,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         if (frames_out) seg(c->d_fstate.p, o_f, fb);
         if (calib_out) seg(c->d_calib_val.p, o_c, cb);
         seg(c->d_wins.p, o_w, wb);  // the host mirror of WinDev (calibration, cDeltaF) follows the device
+        seg(c->d_frame_th.p, o_t, tb);  // setNewFrameEnergyTH of the last pass (ldso_ba_get_frame_energy_th)
         if (idepth_out && c->P_tot) {
             K.pt_data = c->d_pt_data.p;
             K.idepth_dst = reinterpret_cast<float *>(pd + o_i);
@@ -5520,6 +5597,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     if (frames_out) std::memcpy(frames_out, po + o_f, fb);
     if (calib_out) std::memcpy(calib_out, po + o_c, cb);
     std::memcpy(c->wd.data(), po + o_w, wb);
+    c->th_host.assign(reinterpret_cast<const float *>(po + o_t), reinterpret_cast<const float *>(po + o_t) + c->n_frames);
+    c->th_host_valid = true;
     if (idepth_out) {
         const float *id = reinterpret_cast<const float *>(po + o_i);
         long long out_base = 0;  // windows back to back, each in its caller point order
@@ -5602,6 +5681,7 @@ int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *c, const float *dev_buf, int32
     if (!c || !dev_buf || c->n_win == 0 || n_ranks < 1 || stride < 1) return fail(-1, "bad arguments");
     if ((int64_t)n_ranks * stride > INT32_MAX) return fail(-1, "too many candidates");
     HIP_TRY(hipSetDevice(c->device));
+    c->th_host_valid = false;
     int rc = timed_launch(c, 4, c->stream, [&] {
         k_frame_th<<<c->n_win, kStThreads, 0, c->stream>>>(c->d_wins.p, dev_buf, n_ranks, c->n_win, (long long)stride,
                                                            c->d_frame_th.p);
