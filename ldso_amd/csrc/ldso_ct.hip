@@ -735,15 +735,22 @@ int ct_launch(ldso_ct_ctx *c, int slot, F &&launch) {
     return 0;
 }
 
+// The block partials live in coherent mapped host memory: the kernels write them straight to the
+// host (a few KB), so a call needs no copy launch, only the synchronisation (d_parts is the
+// device address of h_parts)
 int ensure_parts(ldso_ct_ctx *c, size_t n) {
     if (n <= c->parts_cap) return 0;
-    if (c->d_parts) (void)hipFree(c->d_parts);
-    if (c->h_parts) (void)hipHostFree(c->h_parts);
+    if (c->h_parts) {
+        CT_TRY(hipStreamSynchronize(c->stream));
+        (void)hipHostFree(c->h_parts);
+    }
     c->d_parts = nullptr;
     c->h_parts = nullptr;
     c->parts_cap = 0;
-    CT_TRY(hipMalloc(&c->d_parts, n * sizeof(double)));
-    CT_TRY(hipHostMalloc(&c->h_parts, n * sizeof(double), hipHostMallocDefault));
+    CT_TRY(hipHostMalloc(&c->h_parts, n * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
+    void *d = nullptr;
+    CT_TRY(hipHostGetDevicePointer(&d, c->h_parts, 0));
+    c->d_parts = static_cast<double *>(d);
     c->parts_cap = n;
     return 0;
 }
@@ -847,9 +854,8 @@ int run_calc_res(ldso_ct_ctx *c, int lvl, int n_hyp, float cutoffTH, bool write_
     if (rc) return rc;
     const int n = c->pc_off[lvl + 1] - c->pc_off[lvl];
     const int nb = std::max(1, (n + kCtThreads - 1) / kCtThreads);
-    CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (size_t)n_hyp * nb * kResParts * sizeof(double),
-                          hipMemcpyDeviceToHost, c->stream));
-    CT_TRY(hipStreamSynchronize(c->stream));
+    (void)nb;
+    CT_TRY(hipStreamSynchronize(c->stream));  // the partials are in h_parts already
     finish_calc_res(c, lvl, n_hyp, write_warp, rs_out);
     return 0;
 }
@@ -956,7 +962,7 @@ void ldso_ct_destroy(ldso_ct_ctx *c) {
         (void)hipEventDestroy(p.second.second);
     }
     void *dev[] = {c->d_color, c->d_inten, c->d_B,  c->d_dIp, c->d_pc,  c->d_state,  c->d_warp,
-                   c->d_poses, c->d_parts, c->d_ip, c->d_hosts, c->d_uv, c->d_mk, c->d_counts};
+                   c->d_poses, c->d_ip, c->d_hosts, c->d_uv, c->d_mk, c->d_counts};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_poses) (void)hipHostFree(c->h_poses);
@@ -1135,9 +1141,7 @@ int ldso_ct_calc_gs(ldso_ct_ctx *c, int32_t lvl, const double ref_to_new[12], do
     if (rc) return rc;
     rc = launch_calc_gs(c, lvl, aff_a, aff_b, 0);
     if (rc) return rc;
-    CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (size_t)nb * kGsParts * sizeof(double), hipMemcpyDeviceToHost,
-                          c->stream));
-    CT_TRY(hipStreamSynchronize(c->stream));
+    CT_TRY(hipStreamSynchronize(c->stream));  // the partials are in h_parts already
     finish_calc_gs(c, lvl, c->h_parts, H_out, b_out);
     return 0;
 }
@@ -1156,9 +1160,7 @@ int ldso_ct_calc_res_gs(ldso_ct_ctx *c, int32_t lvl, const double ref_to_new[12]
     // the warped buffers receive; the block partials are those of k_ct_calc_gs)
     rc = launch_calc_res(c, lvl, 1, cutoff_th, true, (size_t)nb * kGsParts, true, aff_a, aff_b);
     if (rc) return rc;
-    CT_TRY(hipMemcpyAsync(c->h_parts, c->d_parts, (res_parts + (size_t)nb * kGsParts) * sizeof(double),
-                          hipMemcpyDeviceToHost, c->stream));
-    CT_TRY(hipStreamSynchronize(c->stream));
+    CT_TRY(hipStreamSynchronize(c->stream));  // the partials are in h_parts already
     finish_calc_res(c, lvl, 1, true, rs_out);
     c->last_lvl = lvl;
     finish_calc_gs(c, lvl, c->h_parts + res_parts, H_out, b_out);

@@ -112,14 +112,17 @@ class CoarseTracker:
         return H, b
 
     def calc_res_gs(self, lvl: int, ref_to_new, aff_ab=(0.0, 0.0), cutoff_th: float = 20.0):
-        """calcRes + calcGSSSE at the same pose in one round trip -> (rs[6], H 8x8, b 8)."""
-        T = np.ascontiguousarray(np.asarray(ref_to_new, np.float64)[:3, :4])
-        rs = np.zeros(6, np.float64)
-        H = np.zeros((8, 8), np.float64)
-        b = np.zeros(8, np.float64)
-        L.check(L.lib().ldso_ct_calc_res_gs(self._h, int(lvl), L.ptr(T, L.f64p), float(aff_ab[0]), float(aff_ab[1]),
-                                            float(cutoff_th), L.ptr(rs, L.f64p), L.ptr(H, L.f64p), L.ptr(b, L.f64p)))
-        return rs, H, b
+        """calcRes + calcGSSSE at the same pose in one round trip -> (rs[6], H 8x8, b 8).
+        The LM loop calls this once per iteration: the pose and result buffers and their ctypes
+        pointers are made once per tracker, the results returned as copies."""
+        if not hasattr(self, "_lm"):
+            bufs = (np.zeros((3, 4), np.float64), np.zeros(6, np.float64), np.zeros((8, 8), np.float64),
+                    np.zeros(8, np.float64))
+            self._lm = (bufs, tuple(L.ptr(x, L.f64p) for x in bufs), L.lib().ldso_ct_calc_res_gs)
+        (T, rs, H, b), (pT, prs, pH, pb), fn = self._lm
+        T[...] = np.asarray(ref_to_new, np.float64)[:3, :4]
+        L.check(fn(self._h, int(lvl), pT, float(aff_ab[0]), float(aff_ab[1]), float(cutoff_th), prs, pH, pb))
+        return rs.copy(), H.copy(), b.copy()
 
     def warped(self) -> np.ndarray:
         """buf_warped_* of the last calc_res as [n][8] {idepth, u, v, dx, dy, residual, weight, refColor}."""
