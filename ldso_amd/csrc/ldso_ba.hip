@@ -857,6 +857,9 @@ struct PointParams {
 };
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
+#ifndef LDSO_EXP_SC_SKIP  // timing experiments only: 1 the SYRK, 2 the record gather
+#define LDSO_EXP_SC_SKIP 0
+#endif
 constexpr int kScBatch = 2;  // residual records per round trip (4 and 8 measured equal, r2)
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int item = P.item_base + blockIdx.x;
@@ -870,7 +873,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int tid = threadIdx.x;
     for (int i = tid; i < 64 * KP; i += blockDim.x) U[i] = 0;
     __syncthreads();
-    if (tid < it.y) {
+    if (tid < it.y && !(LDSO_EXP_SC_SKIP & 2)) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
         const int nres = P.pt_nres[p];
@@ -944,6 +947,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     }
     __syncthreads();
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
+    if (LDSO_EXP_SC_SKIP & 1) return;
     syrk_tiles(U, Wt, KP, nt, ntiles, it.y,
                P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16, tid, blockDim.x);
 }
