@@ -1530,7 +1530,7 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
 // N-1 Top accumulators; then X_jk = AT_ij D_jk (j <= k), S_j, TH_t = AH_it A_t, TT_t = AT_it A_t;
 // then every element of the partial.  Windows with more keyframes use k_stitch's records.
 // ============================================================================================
-constexpr int kHostStitchMaxN = 12;
+constexpr int kHostStitchMaxN = 11;
 constexpr int kHsThreads = 512;
 #ifndef LDSO_EXP_HS_SKIP  // timing experiments only: 1 outputs, 2 intermediates, 4 G loads, 8 Top loads
 #define LDSO_EXP_HS_SKIP 0
@@ -1540,7 +1540,7 @@ __host__ __device__ inline int hs_ldg(int N) { return (hs_k5(N) + 1) & ~1; }  //
 __host__ __device__ inline int hs_npair(int N) { return (N - 1) * N / 2; }
 __host__ __device__ inline size_t hs_lds_doubles(int N) {
     return (size_t)hs_k5(N) * hs_ldg(N) + 2 * 64 * (size_t)N + 182 * (size_t)N + 64 * (size_t)hs_npair(N) +
-           3 * 64 * (size_t)N;
+           3 * 64 * (size_t)N + 208 * (size_t)(N - 1);
 }
 // tile index t of the upper-tile order (a <= b) over nt tile rows -> (a, b)
 __device__ __forceinline__ void tile_ab(int t, int nt, int &a, int &b) {
@@ -1626,6 +1626,8 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
     double *SSt = X + 64 * npair;        // [N][8][8] S_j^T, S_j = sum_k D_jk AH_ik^T
     double *TH = SSt + 64 * N;           // [N][8][8] AH_it A_t(88)
     double *TT = TH + 64 * N;            // [N][8][8] AT_it A_t(88)
+    double *HP = TT + 64 * N;            // [2 parts][16 2x2s][N-1][4] the (i,i) block's per-term 2x2s
+    double *CP = HP + 128 * (N - 1);     // [2 parts][40 items][N-1] the (calib, i) / b(i) per-term dots
     auto frame_of = [&](int slot) { return slot < i ? slot : slot + 1; };
     auto A_t = [&](int t, int r, int c) { return A14[182 * t + 14 * r + c]; };
     // ---- every load of the block in one round trip -------------------------------------
@@ -1770,7 +1772,40 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
     double *HAp = P.stage + W.stage_base + (size_t)i * sys_len(D), *bAp = HAp + pl, *Hsp = bAp + D, *bsp = Hsp + pl;
     auto xblk = [&](int sj, int sk) { return X + 64 * (sj * Nm1 - sj * (sj - 1) / 2 + (sk - sj)); };
     const int n_fb = 16 * (N * (N + 1) / 2), n_rest = 32 * N + 8 * N + 20, per_part = n_fb + n_rest;
-    for (int uo = tid; uo < (do_top + do_sc) * per_part; uo += kHsThreads) {
+    // The sums over t / j of the (i, i) block and of the (calib, i) / b(i) items are split into
+    // one task per term (partials to HP / CP, summed after a barrier in the same order as one
+    // task would: (0 + t_0) + t_1 + ...), so no thread carries N-1 terms of them alone.
+    const int nH = 56 * Nm1, nparts = do_top + do_sc, pbase = do_top ? 0 : 1;
+    for (int uh = tid; uh < nparts * nH; uh += kHsThreads) {
+        const int part = pbase + uh / nH, hu = uh % nH;
+        const bool top = part == 0;
+        if (hu < 16 * Nm1) {  // (i, i) 2x2 sub-block `sub`, term st
+            const int sub = hu / Nm1, st = hu % Nm1, r0 = 2 * (sub >> 2), c0 = 2 * (sub & 3);
+            if (r0 > c0) continue;
+            const int t = frame_of(st);
+            const double *th = TH + 64 * t + 8 * r0, *ah = AH + 64 * t, *ss = SSt + 64 * t + 8 * c0;
+            double v[2][2] = {{0, 0}, {0, 0}};
+            if (top)
+                mm22(th, th + 8, ah + 8 * c0, ah + 8 * c0 + 8, v);
+            else
+                mm22(ah + 8 * r0, ah + 8 * r0 + 8, ss, ss + 8, v);
+            double *o = HP + ((part * 16 + sub) * Nm1 + st) * 4;
+            o[0] = v[0][0];
+            o[1] = v[0][1];
+            o[2] = v[1][0];
+            o[3] = v[1][1];
+        } else {  // (calib cc, frame i, rr) item < 32 / b(i)[rr] item >= 32, term st
+            const int item = (hu - 16 * Nm1) / Nm1, st = (hu - 16 * Nm1) % Nm1;
+            const int rr = item < 32 ? item >> 2 : item - 32, cI = item < 32 ? (item & 3) : 12, cS = item < 32 ? (item & 3) : 4;
+            const int t = frame_of(st);
+            double a = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                a += AH[64 * t + 8 * rr + k] * (top ? A_t(t, 4 + k, cI) : Gd[(8 * st + k) * ldg + Kc + cS]);
+            CP[(part * 40 + item) * Nm1 + st] = a;
+        }
+    }
+    for (int uo = tid; uo < nparts * per_part; uo += kHsThreads) {
         const bool top = do_top && uo < per_part;  // the Top items first, then the SC ones
         const int u = uo - (do_top && !top ? per_part : 0);
         if (u < n_fb) {  // a 2x2 of frame block (f1 <= f2), upper-block order
@@ -1782,17 +1817,9 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             }
             const int f2 = f1 + rem;
             if (f1 == f2 && r0 > c0) continue;  // below the diagonal
+            if (f1 == f2 && f1 == i) continue;  // the (i, i) block: per-term tasks above
             double v[2][2] = {{0, 0}, {0, 0}};
-            if (f1 == f2 && f1 == i) {
-                for (int st = 0; st < Nm1; st++) {  // sum over t / j in frame order
-                    const int t = frame_of(st);
-                    const double *th = TH + 64 * t + 8 * r0, *ah = AH + 64 * t, *ss = SSt + 64 * t + 8 * c0;
-                    if (top)
-                        mm22(th, th + 8, ah + 8 * c0, ah + 8 * c0 + 8, v);
-                    else
-                        mm22(ah + 8 * r0, ah + 8 * r0 + 8, ss, ss + 8, v);
-                }
-            } else if (f1 == f2) {
+            if (f1 == f2) {
                 const int f = f1, sf = f < i ? f : f - 1;
                 const double *tt = TT + 64 * f + 8 * r0, *at = AT + 64 * f + 8 * c0;
                 const double *x = top ? tt : xblk(sf, sf) + 8 * r0;
@@ -1826,16 +1853,8 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
         bool bvec = false;
         if (l0 < 32 * N) {  // (calib cc, frame f, rr)
             const int f = l0 >> 5, rr = (l0 >> 2) & 7, cc = l0 & 3;
-            if (f == i) {
-                for (int st = 0; st < Nm1; st++) {
-                    const int t = frame_of(st);
-                    double a = 0;
-#pragma unroll
-                    for (int k = 0; k < 8; k++)
-                        a += AH[64 * t + 8 * rr + k] * (top ? A_t(t, 4 + k, cc) : Gd[(8 * st + k) * ldg + Kc + cc]);
-                    ha += a;
-                }
-            } else {
+            if (f == i) continue;  // per-term tasks above
+            {
                 const int sf = f < i ? f : f - 1;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
@@ -1844,16 +1863,8 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             q = pk_index(cc, 4 + 8 * f + rr, D);
         } else if (l0 < 40 * N) {  // b(f)[rr]
             const int f = (l0 - 32 * N) >> 3, rr = l0 & 7;
-            if (f == i) {
-                for (int st = 0; st < Nm1; st++) {
-                    const int t = frame_of(st);
-                    double a = 0;
-#pragma unroll
-                    for (int k = 0; k < 8; k++)
-                        a += AH[64 * t + 8 * rr + k] * (top ? A_t(t, 4 + k, 12) : Gd[(8 * st + k) * ldg + Kc + 4]);
-                    ha += a;
-                }
-            } else {
+            if (f == i) continue;  // per-term tasks above
+            {
                 const int sf = f < i ? f : f - 1;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
@@ -1873,6 +1884,37 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             q = bvec ? r : pk_index(r, cI, D);
         }
         (bvec ? (top ? bAp : bsp) : (top ? HAp : Hsp))[q] = ha;
+    }
+    __syncthreads();
+    for (int uf = tid; uf < nparts * 56; uf += kHsThreads) {  // the split sums, terms in order
+        const int part = pbase + uf / 56, fu = uf % 56;
+        const bool top = part == 0;
+        if (fu < 16) {
+            const int r0 = 2 * (fu >> 2), c0 = 2 * (fu & 3);
+            if (r0 > c0) continue;
+            double v[4] = {0, 0, 0, 0};
+            for (int st = 0; st < Nm1; st++) {
+                const double *hp = HP + ((part * 16 + fu) * Nm1 + st) * 4;
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] += hp[e];
+            }
+            double *o = top ? HAp : Hsp;
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++) {
+                    if (r0 + a > c0 + b) continue;
+                    o[pk_index(4 + 8 * i + r0 + a, 4 + 8 * i + c0 + b, D)] = v[2 * a + b];
+                }
+        } else {
+            const int item = fu - 16, rr = item < 32 ? item >> 2 : item - 32, cc = item & 3;
+            double ha = 0;
+            for (int st = 0; st < Nm1; st++) ha += CP[(part * 40 + item) * Nm1 + st];
+            if (item < 32)
+                (top ? HAp : Hsp)[pk_index(cc, 4 + 8 * i + rr, D)] = ha;
+            else
+                (top ? bAp : bsp)[4 + 8 * i + rr] = ha;
+        }
     }
 }
 // sys = sum over the window's hosts of their partials, in host order, one thread per element

@@ -13,7 +13,10 @@ import torch
 torch.cuda.init()
 import numpy as np
 from ldso_amd import BAContext, synth
-ws = [synth.make_window(**synth.S7, seed=900 + i) for i in range(3)] + [synth.make_window(n_frames=12, n_points=700, seed=950)]
+import os
+ws = [synth.make_window(**synth.S7, seed=900 + i) for i in range(3)]
+if not os.environ.get("SYS_COMPARE_S7_ONLY"):
+    ws.append(synth.make_window(n_frames=12, n_points=700, seed=950))
 c = BAContext(0).load(ws)
 c.linearize()
 h = hashlib.sha256()
