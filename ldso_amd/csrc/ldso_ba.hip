@@ -857,9 +857,6 @@ struct PointParams {
 };
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
-#ifndef LDSO_EXP_SC_SKIP  // timing experiments only: 1 the SYRK, 2 the record gather
-#define LDSO_EXP_SC_SKIP 0
-#endif
 constexpr int kScBatch = 2;  // residual records per round trip (4 and 8 measured equal, r2)
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int item = P.item_base + blockIdx.x;
@@ -873,7 +870,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int tid = threadIdx.x;
     for (int i = tid; i < 64 * KP; i += blockDim.x) U[i] = 0;
     __syncthreads();
-    if (tid < it.y && !(LDSO_EXP_SC_SKIP & 2)) {
+    if (tid < it.y) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
         const int nres = P.pt_nres[p];
@@ -947,7 +944,6 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     }
     __syncthreads();
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
-    if (LDSO_EXP_SC_SKIP & 1) return;
     syrk_tiles(U, Wt, KP, nt, ntiles, it.y,
                P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16, tid, blockDim.x);
 }
@@ -1532,9 +1528,6 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
 // ============================================================================================
 constexpr int kHostStitchMaxN = 11;
 constexpr int kHsThreads = 512;
-#ifndef LDSO_EXP_HS_SKIP  // timing experiments only: 1 outputs, 2 intermediates, 4 G loads, 8 Top loads
-#define LDSO_EXP_HS_SKIP 0
-#endif
 __host__ __device__ inline int hs_k5(int N) { return 8 * (N - 1) + 5; }
 __host__ __device__ inline int hs_ldg(int N) { return (hs_k5(N) + 1) & ~1; }  // even: 16-byte aligned rows
 __host__ __device__ inline int hs_npair(int N) { return (N - 1) * N / 2; }
@@ -1638,7 +1631,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
         const float4 *slab = reinterpret_cast<const float4 *>(P.sc_slab + W.sc_slab_base +
                                                               (size_t)(hi.x - W.sc_item_base) * per);
         const int per4 = per / 4;
-        for (int q = tid; q < ((LDSO_EXP_HS_SKIP & 4) || !do_sc ? 0 : per4); q += kHsThreads) {
+        for (int q = tid; q < (do_sc ? per4 : 0); q += kHsThreads) {
             double s[4] = {0, 0, 0, 0};
             int k = 0;
             for (; k + 4 <= hi.y; k += 4) {
@@ -1679,7 +1672,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             AT[e] = P.adT[pk];
         }
         // Top accumulators of the pairs (i, t): 24 float4 per item, summed over the pair's items
-        for (int e = tid; e < ((LDSO_EXP_HS_SKIP & 8) || !do_top ? 0 : 24 * Nm1); e += kHsThreads) {
+        for (int e = tid; e < (do_top ? 24 * Nm1 : 0); e += kHsThreads) {
             const int t = frame_of(e / 24), q = e % 24;
             const int2 pi = P.pair_items[W.pair_base + i + N * t];
             const float4 *src = reinterpret_cast<const float4 *>(P.top_slab + (size_t)pi.x * kTopVals) + q;
@@ -1720,7 +1713,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
     {
         const int n_ss = do_sc ? Nm1 : 0, n_x = do_sc ? npair : 0, n_th = do_top ? Nm1 : 0;
         const int total = 16 * (n_ss + n_x + 2 * n_th);
-        for (int u = tid; u < ((LDSO_EXP_HS_SKIP & 2) ? 0 : total); u += kHsThreads) {
+        for (int u = tid; u < total; u += kHsThreads) {
             int blk = u >> 4;
             const int r0 = 2 * ((u & 15) >> 2), c0 = 2 * (u & 3);
             double v[2][2] = {{0, 0}, {0, 0}};
@@ -1766,7 +1759,6 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
         }
     }
     __syncthreads();
-    if (LDSO_EXP_HS_SKIP & 1) return;
     // ---- host i's partial system: every packed element written (zeros included) ------------
     const long long pl = packed_len(D);
     double *HAp = P.stage + W.stage_base + (size_t)i * sys_len(D), *bAp = HAp + pl, *Hsp = bAp + D, *bsp = Hsp + pl;
@@ -2823,9 +2815,6 @@ __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
 #endif
 constexpr int kSolveFastThreads = LDSO_SOLVE_FAST_THREADS;  // 8 waves: the trailing updates hide LDS latency
 constexpr int kSolveFastPanel = 8;
-#ifndef LDSO_EXP_SOLVE_SKIP  // timing experiments only (tools/solve_ab.py): 1 panels, 2 trailing, 4 back subst, 8 store, 16 xad
-#define LDSO_EXP_SOLVE_SKIP 0
-#endif
 __host__ __device__ inline size_t solve_fast_smem_bytes(int n) {
     // SolveLds | W [2][8][128] panel columns (double-buffered) | rd [2][8]
     return solve_smem_bytes(n) + 16 + 2 * ((size_t)kSolveFastPanel * 128 + kSolveFastPanel) * sizeof(double);
@@ -2958,7 +2947,6 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
     }
     auto panel = [&](int p, int w, int buf) {
         double *Wb = Wc + buf * kSolveFastPanel * 128, *rb = rdv + buf * kSolveFastPanel;
-        if (LDSO_EXP_SOLVE_SKIP & 1) return;
         if (n > 64)
             fast_panel<2>(H, Wb, rb, y, n, ld, p, w, lane);
         else
@@ -2972,7 +2960,7 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
     for (int p = 0, buf = 0; p + kSolveFastPanel < n; p += kSolveFastPanel, buf ^= 1) {
         const int w = kSolveFastPanel, m0 = p + w, w1 = min(kSolveFastPanel, n - m0), m1 = m0 + w1;
         const double *Wp = Wc + buf * kSolveFastPanel * 128, *rp = rdv + buf * kSolveFastPanel;
-        for (int e = tid; e < ((LDSO_EXP_SOLVE_SKIP & 2) ? 0 : (n - m0) * w1); e += kSolveFastThreads) {  // the next panel's columns
+        for (int e = tid; e < (n - m0) * w1; e += kSolveFastThreads) {  // the next panel's columns
             const int i = m0 + e / w1, j = m0 + e % w1;
             if (i >= j) H[i * ld + j] = fast_update(Wp, rp, w, i, j, H[i * ld + j]);
         }
@@ -2980,7 +2968,7 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
         if (wave == 0) {
             panel(m0, w1, buf ^ 1);
         } else {  // the rest of the trailing triangle (m1 <= j <= i < n)
-            const int nt = n - m1, ne = (LDSO_EXP_SOLVE_SKIP & 2) ? 0 : nt * (nt + 1) / 2;
+            const int nt = n - m1, ne = nt * (nt + 1) / 2;
             for (int e = tid - 64; e < ne; e += kSolveFastThreads - 64) {
                 int ii = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);  // row ii of the nt x nt triangle
                 if (ii * (ii + 1) / 2 > e) ii--;
@@ -2991,15 +2979,15 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
         }
         __syncthreads();
     }
-    if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 4)) {
+    if (wave == 0) {
         if (n > 64)
             fast_back_subst<2>(H, S, y, n, ld, lane);
         else
             fast_back_subst<1>(H, S, y, n, ld, lane);
     }
     __syncthreads();
-    if (wave == 0 && !(LDSO_EXP_SOLVE_SKIP & 8)) solve_ortho_apply_store(P, W, S, lane);
-    if (P.xad && !(LDSO_EXP_SOLVE_SKIP & 16)) {  // x is in S.y: the resubstitution's xAd by all waves
+    if (wave == 0) solve_ortho_apply_store(P, W, S, lane);
+    if (P.xad) {  // x is in S.y: the resubstitution's xAd by all waves
         __syncthreads();
         xp.fill(W, S.y, P.adH, P.adT, P.xad + (size_t)blockIdx.x * kXadStride, tid, kSolveFastThreads);
     }
