@@ -4832,6 +4832,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.frame_base = 0;
     // two 512-thread blocks fit a CU: split the host blocks when the doubled grid still runs at once
     Sp.hs_split = Sp.n_win + 2 * c->n_frames <= 2 * c->n_cu ? 1 : 0;
+    if (const char *e = std::getenv("LDSO_BA_HS_SPLIT")) Sp.hs_split = e[0] == '1';  // tests: force either
     const size_t st_smem = c->host_stitch ? stitch_host_smem_bytes(n_max, &Sp.th_cap)
                                           : stitch_smem_bytes(kp_max, n_max, &Sp.th_cap);
     hipStream_t st = c->stream;

@@ -137,6 +137,37 @@ def test_single_pass_parity(ctx, cfg):
     assert np.linalg.norm(stg - stc) <= 1e-3 * np.linalg.norm(stc) + 1e-12
 
 
+@pytest.mark.parametrize("stitch", ["split", "whole", "records"])
+def test_stitch_paths_agree(built, monkeypatch, stitch):
+    """The three stitch paths -- k_stitch_host with the Top / Schur halves in separate blocks
+    (small grids), with one block per host (large grids: the bench's 64 windows), and k_stitch's
+    per-pair records (windows over 11 keyframes) -- against the oracle on the same windows; the
+    two host-stitch modes are the same arithmetic, so their systems are bitwise equal."""
+    cfgs = [dict(n_frames=7, n_points=600, seed=81), dict(n_frames=4, n_points=200, seed=82),
+            dict(n_frames=11, n_points=900, seed=83)]
+    if stitch == "records":
+        monkeypatch.setenv("LDSO_BA_STITCH_RECORDS", "1")
+    else:
+        monkeypatch.setenv("LDSO_BA_HS_SPLIT", "1" if stitch == "split" else "0")
+    c = BAContext(0).load([synth.make_window(**cf) for cf in cfgs])
+    c.linearize(fix=False, accumulate=True)
+    systems = [c.system(i) for i in range(len(cfgs))]
+    for i, cf in enumerate(cfgs):
+        ow = oracle.OracleWindow(synth.make_window(**cf), threads=0)
+        e_cpu, s_cpu = ow.iteration()
+        compare_pass(c, ow, i, e_cpu, s_cpu)
+    c.close()
+    if stitch != "records":
+        monkeypatch.setenv("LDSO_BA_HS_SPLIT", "0" if stitch == "split" else "1")
+        c2 = BAContext(0).load([synth.make_window(**cf) for cf in cfgs])
+        c2.linearize(fix=False, accumulate=True)
+        for i in range(len(cfgs)):
+            s2 = c2.system(i)
+            for k in ("HA", "Hsc", "bA", "bsc"):
+                np.testing.assert_array_equal(systems[i][k], s2[k], err_msg=k)
+        c2.close()
+
+
 def test_repeated_passes_and_oob_stickiness(ctx):
     """OOB is sticky inside optimize(): later passes return the stored state_energy."""
     cfg = dict(n_frames=6, n_points=800, seed=5, baseline=0.12)
