@@ -52,7 +52,8 @@ def main():
     args = ap.parse_args()
     res = {}
     n_gather = None
-    for i, ctrs in enumerate([["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]]):
+    for i, ctrs in enumerate([["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"],
+                              ["TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TCP_PENDING_STALL_CYCLES_sum"]]):
         vals, ng = run_pass(ctrs, os.path.join(args.out, f"pass{i}"), args)
         n_gather = n_gather or ng
         for k, v in vals.items():
@@ -75,6 +76,10 @@ def main():
         "hbm_bytes_per_gather_residual": (2 * fetch_kib * 1024 + write_kib * 1024) / n_gather if n_gather else None,
         "TCC_hit_rate": res["TCC_HIT_sum"] / (res["TCC_HIT_sum"] + res["TCC_MISS_sum"])
         if res.get("TCC_HIT_sum") is not None else None,
+        "TCP_accesses_per_gather_residual": res["TCP_TOTAL_CACHE_ACCESSES_sum"] / n_gather
+        if n_gather and res.get("TCP_TOTAL_CACHE_ACCESSES_sum") is not None else None,
+        "TCP_TCC_read_requests_per_gather_residual": res["TCP_TCC_READ_REQ_sum"] / n_gather
+        if n_gather and res.get("TCP_TCC_READ_REQ_sum") is not None else None,
         "counters": res,
     }
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
