@@ -3450,6 +3450,23 @@ __global__ __launch_bounds__(256) void k_pack_out(PackOut P) {
     if (P.pt_data)
         for (int q = tid; q < P.n_points; q += nth) P.idepth_dst[q] = P.pt_data[(size_t)q * LDSO_BA_POINT_STRIDE + 2];
 }
+// resetOOB() over a residual range; optionally also the scratch copies of
+// ldso_ba_linearize_residuals: centre "not projected" (all-ones NaN) and the flags copied
+__global__ __launch_bounds__(256) void k_reset_oob(int8_t *state, int8_t *newstate, float *energy, float *newenergy,
+                                                    int n, float4 *center = nullptr, uint8_t *flags = nullptr,
+                                                    const uint8_t *flags_src = nullptr) {
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        state[r] = LDSO_BA_RES_IN;
+        newstate[r] = LDSO_BA_RES_OUTLIER;
+        energy[r] = 0.f;
+        newenergy[r] = 0.f;
+        if (center) {
+            const float q = __uint_as_float(0xFFFFFFFFu);
+            center[r] = make_float4(q, q, q, q);
+            flags[r] = flags_src[r];
+        }
+    }
+}
 __global__ __launch_bounds__(256) void k_gather_idepth(const float *__restrict__ pt_data, float *out, int n) {
     const int q = blockIdx.x * 256 + threadIdx.x;
     if (q < n) out[q] = pt_data[(size_t)q * LDSO_BA_POINT_STRIDE + 2];
@@ -4674,16 +4691,16 @@ int ldso_ba_update_residuals(ldso_ba_ctx *c, int32_t win, const int8_t *state, c
 int ldso_ba_reset_oob(ldso_ba_ctx *c, int32_t win) {
     if (!c || win >= c->n_win) return fail(-1, "bad arguments");
     HIP_TRY(hipSetDevice(c->device));
+    // resetOOB(): state_NewEnergy = state_energy = 0; state_NewState = OUTLIER; state_state = IN,
+    // for the windows' residual range (contiguous: windows back to back) in one launch instead of
+    // four fills per window
     const int w0 = win < 0 ? 0 : win, w1 = win < 0 ? c->n_win : win + 1;
-    for (int w = w0; w < w1; w++) {
-        const WinDev &D = c->wd[w];
-        if (!D.R) continue;
-        // resetOOB(): state_NewEnergy = state_energy = 0; state_NewState = OUTLIER; state_state = IN
-        HIP_TRY(hipMemsetAsync(c->d_rs_state.p + D.res_base, LDSO_BA_RES_IN, D.R, c->stream));
-        HIP_TRY(hipMemsetAsync(c->d_rs_newstate.p + D.res_base, LDSO_BA_RES_OUTLIER, D.R, c->stream));
-        HIP_TRY(hipMemsetAsync(c->d_rs_energy.p + D.res_base, 0, (size_t)D.R * sizeof(float), c->stream));
-        HIP_TRY(hipMemsetAsync(c->d_rs_newenergy.p + D.res_base, 0, (size_t)D.R * sizeof(float), c->stream));
-    }
+    const long long r0 = c->wd[w0].res_base, r1 = c->wd[w1 - 1].res_base + c->wd[w1 - 1].R;
+    if (r1 <= r0) return 0;
+    const int n = (int)(r1 - r0);
+    k_reset_oob<<<std::min(1024, (n + 255) / 256), 256, 0, c->stream>>>(
+        c->d_rs_state.p + r0, c->d_rs_newstate.p + r0, c->d_rs_energy.p + r0, c->d_rs_newenergy.p + r0, n);
+    HIP_TRY(hipGetLastError());
     return 0;
 }
 
@@ -4896,12 +4913,12 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     const size_t b = (size_t)D.res_base;
     // resetOOB() of every residual of the window on the copies: state IN, NewState OUTLIER,
     // energies 0; the centre marked "not projected" (NaN) so a failed centre projection shows
-    HIP_TRY(hipMemsetAsync(c->d_sx_state.p + b, LDSO_BA_RES_IN, R, st));
-    HIP_TRY(hipMemsetAsync(c->d_sx_newstate.p + b, LDSO_BA_RES_OUTLIER, R, st));
-    HIP_TRY(hipMemsetAsync(c->d_sx_energy.p + b, 0, R * sizeof(float), st));
-    HIP_TRY(hipMemsetAsync(c->d_sx_newenergy.p + b, 0, R * sizeof(float), st));
-    HIP_TRY(hipMemsetAsync(c->d_sx_center.p + b, 0xFF, R * sizeof(float4), st));
-    HIP_TRY(hipMemcpyAsync(c->d_sx_flags.p + b, c->d_rs_flags.p + b, R, hipMemcpyDeviceToDevice, st));
+    if (R) {  // one launch for the five fills and the flag copy
+        k_reset_oob<<<std::min<int>(1024, (int)((R + 255) / 256)), 256, 0, st>>>(
+            c->d_sx_state.p + b, c->d_sx_newstate.p + b, c->d_sx_energy.p + b, c->d_sx_newenergy.p + b, (int)R,
+            c->d_sx_center.p + b, c->d_sx_flags.p + b, c->d_rs_flags.p + b);
+        HIP_TRY(hipGetLastError());
+    }
     LinParams L;
     L.items = c->d_top_items.p;
     L.wins = c->d_wins.p;
