@@ -327,15 +327,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: LDSO_BENCH_SHARE_GPU=1 puts every rank on
+    # device 0 and the timing collectives on gloo (the driver's multi-GPU runs use neither)
+    share_gpu = os.environ.get("LDSO_BENCH_SHARE_GPU") == "1"
+    if share_gpu:
+        local_rank = 0
+    backend = "gloo" if share_gpu else "nccl"
     dist = None
     if world > 1:
         import torch
         import torch.distributed as tdist
 
         torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(backend)
         dist = tdist
     import torch
+    coll_dev = "cpu" if backend == "gloo" else "cuda"
 
     # torch's bundled HIP runtime must initialise before the one libldso_ba.so links
     torch.cuda.set_device(local_rank)
@@ -410,10 +417,10 @@ def main():
         gn["optimize"] = time_optimize(ctx, nss, n_its=6, reps=3)
 
     if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        tot = torch.tensor([R_rank, n_gather], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([R_rank, n_gather], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tot)
         R_total, G_total = float(tot[0].item()), float(tot[1].item())
     else:
