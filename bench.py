@@ -309,6 +309,119 @@ def trace_leg(device, reps=50, cpu_seconds=2.0, with_cpu=True):
     return out
 
 
+def sharded_window_leg(dist, rank, world, device, coll_dev, steps=20):
+    """BASELINE config[3]'s split on the job's ranks: ONE S11 window (11 KF, 8000
+    points) with its points sharded by host frame over the ranks, every pass ending with the
+    library's own RCCL exchange (ldso_ba_comm_init: all-reduce of the packed systems and energies,
+    all-gather of the newest-frame slots, the threshold re-selected on every rank).  Timed like
+    the headline (barriers, max over ranks); rank 0 checks the reduced system against the same
+    window unsharded on its own GPU (worst block ||G - O||_F / ||O||_F, energies, the newest
+    frame's threshold bit for bit) and times that unsharded pass beside it.  Every phase ends
+    with a status all-reduce, so a rank that fails is reported instead of leaving the others
+    waiting inside a collective."""
+    import torch
+
+    from ldso_amd import BAContext, synth
+    from ldso_amd import dist as ldist
+
+    out = {"workload": "1 x S11 synthetic window (11 KF, 8000 pts, 640x480), points sharded over the ranks",
+           "ranks": world, "exchange": "in-library RCCL (ldso_ba_comm_init)"}
+    cfg = dict(synth.S11, seed=7001)
+    state = {"err": None}
+
+    def phase(fn):
+        if state["err"] is None:
+            try:
+                fn()
+            except Exception as ex:  # reported, the other ranks told below
+                state["err"] = f"rank {rank}: {ex!r}"[:400]
+        t = torch.tensor([0.0 if state["err"] is None else 1.0], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t)
+        if t.item() != 0 and state["err"] is None:
+            state["err"] = "another rank failed"
+        return state["err"] is None
+
+    ctxs = {}
+
+    def build():
+        ctxs["w"] = synth.make_window(**cfg)
+        ctxs["c"] = BAContext(device)
+
+    def attach():
+        ldist.attach_rccl(ctxs["c"], dist)
+        ctxs["c"].load([ctxs["w"]], shard_rank=rank, shard_count=world)
+
+    times = {}
+
+    def run():
+        c = ctxs["c"]
+        for _ in range(3):
+            c.linearize()
+        c.sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            c.linearize()
+        c.sync()
+        dist.barrier()
+        times["el"] = time.perf_counter() - t0
+        times["points"] = c.stats()["points"]
+
+    ok = phase(build) and phase(attach) and phase(run)
+    if ok:
+        t = torch.tensor([times["el"], times["points"]], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0].item())
+        pts = torch.tensor([times["points"]], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(pts)
+        out["ms_per_pass"] = 1e3 * el / steps
+        out["points_total"] = int(pts.item())
+        if rank == 0:
+            c = ctxs["c"]
+            f = BAContext(device).load([synth.make_window(**cfg)])
+            for _ in range(3 + steps):  # the sharded context's pass count
+                f.linearize()
+            s, sf = c.system(0), f.system(0)
+            N = cfg["n_frames"]
+            edges = [0, 4] + [4 + 8 * (k + 1) for k in range(N)]
+            worst = 0.0
+            for key in ("HA", "Hsc"):
+                G, O = s[key], sf[key]
+                scale = np.linalg.norm(O)
+                for a in range(len(edges) - 1):
+                    for b in range(a, len(edges) - 1):
+                        g = G[edges[a]:edges[a + 1], edges[b]:edges[b + 1]]
+                        o = O[edges[a]:edges[a + 1], edges[b]:edges[b + 1]]
+                        if a == b:
+                            g, o = np.triu(g), np.triu(o)
+                        den = max(np.linalg.norm(o), 1e-12 * scale, 1e-300)
+                        worst = max(worst, float(np.linalg.norm(g - o) / den))
+            e, ef = c.energy(0), f.energy(0)
+            th_equal = bool(np.array_equal(c.frame_energy_th(0)[-1], f.frame_energy_th(0)[-1]))
+            f.sync()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                f.linearize()
+            f.sync()
+            out["ms_per_pass_unsharded_one_gpu"] = 1e3 * (time.perf_counter() - t0) / steps
+            out["parity"] = {
+                "max_block_rel_err": worst,
+                "block_tol": 1e-4,
+                "energy_rel_err": float(abs(e[0] - ef[0]) / max(abs(ef[0]), 1e-300)),
+                "n_in_equal": bool(e[2] == ef[2]),
+                "newest_threshold_bitwise": th_equal,
+            }
+            out["parity"]["ok"] = bool(worst < 1e-4 and out["parity"]["energy_rel_err"] <= 1e-9
+                                       and out["parity"]["n_in_equal"] and out["parity"]["newest_threshold_bitwise"])
+            f.close()
+    if state["err"] is not None:
+        out["error"] = state["err"]
+    if "c" in ctxs:
+        ctxs["c"].close()
+    dist.barrier()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -322,6 +435,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-tracker", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the S11 line")
+    ap.add_argument("--no-shard-leg", action="store_true", help="N > 1: skip the sharded S11 window")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -440,6 +554,11 @@ def main():
         f"{B} x synthetic windows/GPU ({N} KF, {P} pts, 640x480)"
     traffic = load_pmc(workload)
 
+    # N > 1: one S11 window sharded over every rank, the library's RCCL exchange in each pass
+    sharded = None
+    if dist is not None and not args.no_shard_leg:
+        sharded = sharded_window_leg(dist, rank, world, local_rank, coll_dev, steps=min(args.steps, 20))
+
     # one window: pass alone, and a GN iteration with the solve on the host (stitched-system
     # download + LDLT + resubstitute) or on the device (ldso_ba_iterate), host clock
     single = None
@@ -543,6 +662,7 @@ def main():
             "gn_iteration_batched": gn,
             "single_window": single,
             "s11": s11,
+            "sharded_window": sharded,
             "tracker": tracker,
             "cpp_face": face,
             "cpu_baseline": cpu,
