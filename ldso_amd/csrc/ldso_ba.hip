@@ -1528,12 +1528,19 @@ __global__ __launch_bounds__(256) void k_stitch_sum(const WinDev *__restrict__ w
 // ============================================================================================
 constexpr int kHostStitchMaxN = 11;
 constexpr int kHsThreads = 512;
+// the 8x8 blocks in LDS: row r at hs_row(r) (rows 4..7 shifted by two doubles), blocks kHsB = 72
+// doubles apart, so the rows {0, 2, 4, 6} a 2x2 task group reads, in a block and in its
+// neighbour, fall on distinct bank quads of ds_read_b128's 16-lane groups (dense 8x8 blocks put
+// rows r and r + 4, and neighbouring blocks, on the same banks).  Rows r0, r0 + 1 (r0 even) stay
+// 8 doubles apart.
+constexpr int kHsB = 72;
+__device__ __forceinline__ int hs_row(int r) { return 8 * r + ((r & 4) >> 1); }
 __host__ __device__ inline int hs_k5(int N) { return 8 * (N - 1) + 5; }
 __host__ __device__ inline int hs_ldg(int N) { return (hs_k5(N) + 1) & ~1; }  // even: 16-byte aligned rows
 __host__ __device__ inline int hs_npair(int N) { return (N - 1) * N / 2; }
 __host__ __device__ inline size_t hs_lds_doubles(int N) {
-    return (size_t)hs_k5(N) * hs_ldg(N) + 2 * 64 * (size_t)N + 182 * (size_t)N + 64 * (size_t)hs_npair(N) +
-           3 * 64 * (size_t)N + 208 * (size_t)(N - 1);
+    return (size_t)hs_k5(N) * hs_ldg(N) + 2 * kHsB * (size_t)N + 182 * (size_t)N + kHsB * (size_t)hs_npair(N) +
+           3 * kHsB * (size_t)N + 208 * (size_t)(N - 1);
 }
 // tile index t of the upper-tile order (a <= b) over nt tile rows -> (a, b)
 __device__ __forceinline__ void tile_ab(int t, int nt, int &a, int &b) {
@@ -1613,13 +1620,13 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
     // LDS (every region an even number of doubles: 16-byte aligned rows for the b128 reads)
     double *Gd = sm;                     // [K5][ldg] G_i, both triangles
     double *AH = Gd + (size_t)K5 * ldg;  // [N][8][8] adH of pair (i, k)
-    double *AT = AH + 64 * N;            // [N][8][8] adT of pair (i, k)
-    double *A14 = AT + 64 * N;           // [N][13][14] pair (i, t)'s 13x13 Top block (t == i unused)
+    double *AT = AH + kHsB * N;          // [N][8][8] adT of pair (i, k)
+    double *A14 = AT + kHsB * N;         // [N][13][14] pair (i, t)'s 13x13 Top block (t == i unused)
     double *X = A14 + 182 * N;           // [npair][8][8] X_jk = AT_ij D_jk, target slots sj <= sk
-    double *SSt = X + 64 * npair;        // [N][8][8] S_j^T, S_j = sum_k D_jk AH_ik^T
-    double *TH = SSt + 64 * N;           // [N][8][8] AH_it A_t(88)
-    double *TT = TH + 64 * N;            // [N][8][8] AT_it A_t(88)
-    double *HP = TT + 64 * N;            // [2 parts][16 2x2s][N-1][4] the (i,i) block's per-term 2x2s
+    double *SSt = X + kHsB * npair;      // [N][8][8] S_j^T, S_j = sum_k D_jk AH_ik^T
+    double *TH = SSt + kHsB * N;         // [N][8][8] AH_it A_t(88)
+    double *TT = TH + kHsB * N;          // [N][8][8] AT_it A_t(88)
+    double *HP = TT + kHsB * N;          // [2 parts][16 2x2s][N-1][4] the (i,i) block's per-term 2x2s
     double *CP = HP + 128 * (N - 1);     // [2 parts][40 items][N-1] the (calib, i) / b(i) per-term dots
     auto frame_of = [&](int slot) { return slot < i ? slot : slot + 1; };
     auto A_t = [&](int t, int r, int c) { return A14[182 * t + 14 * r + c]; };
@@ -1668,8 +1675,9 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
         // the adjoints of the pairs (i, k), k = 0..N-1
         for (int e = tid; e < 64 * N; e += kHsThreads) {
             const size_t pk = (size_t)(W.pair_base + i + N * (e >> 6)) * 64 + (e & 63);
-            AH[e] = P.adH[pk];
-            AT[e] = P.adT[pk];
+            const int eb = kHsB * (e >> 6) + hs_row((e >> 3) & 7) + (e & 7);
+            AH[eb] = P.adH[pk];
+            AT[eb] = P.adT[pk];
         }
         // Top accumulators of the pairs (i, t): 24 float4 per item, summed over the pair's items
         for (int e = tid; e < (do_top ? 24 * Nm1 : 0); e += kHsThreads) {
@@ -1720,13 +1728,13 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             if (blk < n_ss) {  // S_j[r][c] = sum_k sum_q D_jk[r][q] AH_ik[c][q], k in slot order
                 const int sj = blk, j = frame_of(sj);
                 for (int sk = 0; sk < Nm1; sk++) {
-                    const double *d = Gd + (size_t)(8 * sj + r0) * ldg + 8 * sk, *ah = AH + 64 * frame_of(sk) + 8 * c0;
+                    const double *d = Gd + (size_t)(8 * sj + r0) * ldg + 8 * sk, *ah = AH + kHsB * frame_of(sk) + hs_row(c0);
                     mm22(d, d + ldg, ah, ah + 8, v);
                 }
 #pragma unroll
                 for (int a = 0; a < 2; a++)
 #pragma unroll
-                    for (int b = 0; b < 2; b++) SSt[64 * j + 8 * (c0 + b) + r0 + a] = v[a][b];
+                    for (int b = 0; b < 2; b++) SSt[kHsB * j + hs_row(c0 + b) + r0 + a] = v[a][b];
                 continue;
             }
             blk -= n_ss;
@@ -1737,32 +1745,32 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
                     sj++;
                 }
                 const int sk = sj + rem;
-                const double *at = AT + 64 * frame_of(sj) + 8 * r0, *d = Gd + (size_t)(8 * sk + c0) * ldg + 8 * sj;
+                const double *at = AT + kHsB * frame_of(sj) + hs_row(r0), *d = Gd + (size_t)(8 * sk + c0) * ldg + 8 * sj;
                 mm22(at, at + 8, d, d + ldg, v);
-                double *o = X + 64 * blk;
+                double *o = X + kHsB * blk;
 #pragma unroll
                 for (int a = 0; a < 2; a++)
 #pragma unroll
-                    for (int b = 0; b < 2; b++) o[8 * (r0 + a) + c0 + b] = v[a][b];
+                    for (int b = 0; b < 2; b++) o[hs_row(r0 + a) + c0 + b] = v[a][b];
                 continue;
             }
             blk -= n_x;  // TH_t / TT_t [r][c] = sum_k AH_it / AT_it [r][k] A_t(4+c, 4+k)
             const bool th = blk < n_th;
             const int t = frame_of(th ? blk : blk - n_th);
-            const double *ad = (th ? AH : AT) + 64 * t + 8 * r0, *at = A14 + 182 * t + 14 * (4 + c0) + 4;
+            const double *ad = (th ? AH : AT) + kHsB * t + hs_row(r0), *at = A14 + 182 * t + 14 * (4 + c0) + 4;
             mm22(ad, ad + 8, at, at + 14, v);
-            double *o = (th ? TH : TT) + 64 * t;
+            double *o = (th ? TH : TT) + kHsB * t;
 #pragma unroll
             for (int a = 0; a < 2; a++)
 #pragma unroll
-                for (int b = 0; b < 2; b++) o[8 * (r0 + a) + c0 + b] = v[a][b];
+                for (int b = 0; b < 2; b++) o[hs_row(r0 + a) + c0 + b] = v[a][b];
         }
     }
     __syncthreads();
     // ---- host i's partial system: every packed element written (zeros included) ------------
     const long long pl = packed_len(D);
     double *HAp = P.stage + W.stage_base + (size_t)i * sys_len(D), *bAp = HAp + pl, *Hsp = bAp + D, *bsp = Hsp + pl;
-    auto xblk = [&](int sj, int sk) { return X + 64 * (sj * Nm1 - sj * (sj - 1) / 2 + (sk - sj)); };
+    auto xblk = [&](int sj, int sk) { return X + kHsB * (sj * Nm1 - sj * (sj - 1) / 2 + (sk - sj)); };
     const int n_fb = 16 * (N * (N + 1) / 2), n_rest = 32 * N + 8 * N + 20, per_part = n_fb + n_rest;
     // The sums over t / j of the (i, i) block and of the (calib, i) / b(i) items are split into
     // one task per term (partials to HP / CP, summed after a barrier in the same order as one
@@ -1775,12 +1783,12 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             const int sub = hu / Nm1, st = hu % Nm1, r0 = 2 * (sub >> 2), c0 = 2 * (sub & 3);
             if (r0 > c0) continue;
             const int t = frame_of(st);
-            const double *th = TH + 64 * t + 8 * r0, *ah = AH + 64 * t, *ss = SSt + 64 * t + 8 * c0;
+            const double *th = TH + kHsB * t + hs_row(r0), *ah = AH + kHsB * t, *ss = SSt + kHsB * t + hs_row(c0);
             double v[2][2] = {{0, 0}, {0, 0}};
             if (top)
-                mm22(th, th + 8, ah + 8 * c0, ah + 8 * c0 + 8, v);
+                mm22(th, th + 8, ah + hs_row(c0), ah + hs_row(c0) + 8, v);
             else
-                mm22(ah + 8 * r0, ah + 8 * r0 + 8, ss, ss + 8, v);
+                mm22(ah + hs_row(r0), ah + hs_row(r0) + 8, ss, ss + 8, v);
             double *o = HP + ((part * 16 + sub) * Nm1 + st) * 4;
             o[0] = v[0][0];
             o[1] = v[0][1];
@@ -1793,7 +1801,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             double a = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++)
-                a += AH[64 * t + 8 * rr + k] * (top ? A_t(t, 4 + k, cI) : Gd[(8 * st + k) * ldg + Kc + cS]);
+                a += AH[kHsB * t + hs_row(rr) + k] * (top ? A_t(t, 4 + k, cI) : Gd[(8 * st + k) * ldg + Kc + cS]);
             CP[(part * 40 + item) * Nm1 + st] = a;
         }
     }
@@ -1813,20 +1821,20 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
             double v[2][2] = {{0, 0}, {0, 0}};
             if (f1 == f2) {
                 const int f = f1, sf = f < i ? f : f - 1;
-                const double *tt = TT + 64 * f + 8 * r0, *at = AT + 64 * f + 8 * c0;
-                const double *x = top ? tt : xblk(sf, sf) + 8 * r0;
+                const double *tt = TT + kHsB * f + hs_row(r0), *at = AT + kHsB * f + hs_row(c0);
+                const double *x = top ? tt : xblk(sf, sf) + hs_row(r0);
                 mm22(top ? tt : x, (top ? tt : x) + 8, at, at + 8, v);
             } else if (f1 == i) {
-                const double *th = TH + 64 * f2 + 8 * r0, *at = AT + 64 * f2 + 8 * c0, *ss = SSt + 64 * f2 + 8 * r0;
+                const double *th = TH + kHsB * f2 + hs_row(r0), *at = AT + kHsB * f2 + hs_row(c0), *ss = SSt + kHsB * f2 + hs_row(r0);
                 const double *l = top ? th : ss;  // (AT_i,f2 S_f2)^T on the SC side
                 mm22(l, l + 8, at, at + 8, v);
             } else if (f2 == i) {
-                const double *at = AT + 64 * f1 + 8 * r0, *th = TH + 64 * f1 + 8 * c0, *ss = SSt + 64 * f1 + 8 * c0;
+                const double *at = AT + kHsB * f1 + hs_row(r0), *th = TH + kHsB * f1 + hs_row(c0), *ss = SSt + kHsB * f1 + hs_row(c0);
                 const double *rr = top ? th : ss;  // (AH A AT^T)^T of pair (i, f1) / AT_i,f1 S_f1
                 mm22(at, at + 8, rr, rr + 8, v);
             } else if (!top) {
                 const int s1 = f1 < i ? f1 : f1 - 1, s2 = f2 < i ? f2 : f2 - 1;
-                const double *x = xblk(s1, s2) + 8 * r0, *at = AT + 64 * f2 + 8 * c0;
+                const double *x = xblk(s1, s2) + hs_row(r0), *at = AT + kHsB * f2 + hs_row(c0);
                 mm22(x, x + 8, at, at + 8, v);
             }
             double *o = top ? HAp : Hsp;
@@ -1850,7 +1858,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
                 const int sf = f < i ? f : f - 1;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
-                    ha += AT[64 * f + 8 * rr + k] * (top ? A_t(f, 4 + k, cc) : Gd[(8 * sf + k) * ldg + Kc + cc]);
+                    ha += AT[kHsB * f + hs_row(rr) + k] * (top ? A_t(f, 4 + k, cc) : Gd[(8 * sf + k) * ldg + Kc + cc]);
             }
             q = pk_index(cc, 4 + 8 * f + rr, D);
         } else if (l0 < 40 * N) {  // b(f)[rr]
@@ -1860,7 +1868,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
                 const int sf = f < i ? f : f - 1;
 #pragma unroll
                 for (int k = 0; k < 8; k++)
-                    ha += AT[64 * f + 8 * rr + k] * (top ? A_t(f, 4 + k, 12) : Gd[(8 * sf + k) * ldg + Kc + 4]);
+                    ha += AT[kHsB * f + hs_row(rr) + k] * (top ? A_t(f, 4 + k, 12) : Gd[(8 * sf + k) * ldg + Kc + 4]);
             }
             q = 4 + 8 * f + rr;
             bvec = true;
