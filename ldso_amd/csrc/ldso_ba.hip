@@ -431,7 +431,22 @@ __device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kTopRow = 36;
 constexpr int kTermQ = 9;                      // quantities per transposition round (17 = 9 + 8)
-constexpr int kTermsPerWave = 8 * kTermQ * 8;   // per-pixel addends of one round [8 residuals][9][8]
+#ifndef LDSO_LIN_PIECE8_SKIP
+#define LDSO_LIN_PIECE8_SKIP 1  // skip the 9th-column load when no residual of the step needs it
+#endif
+#ifndef LDSO_LIN_PIECES
+#define LDSO_LIN_PIECES 1  // layout 3: tap footprints loaded as 16-B band columns through LDS (0: 12 gathers per lane)
+#endif
+// k_linearize footprint box of one residual (layout 3, LDSO_LIN_PIECES): 3 bands x 9 columns of
+// 16-B band-column pieces (4 rows each) + one dummy slot, in floats
+#ifndef LDSO_LIN_BOX_STRIDE
+#define LDSO_LIN_BOX_STRIDE 112
+#endif
+constexpr int kBoxCols = 9, kBoxBands = 3, kBoxFloats = LDSO_LIN_BOX_STRIDE;
+static_assert(kBoxFloats >= (kBoxCols * kBoxBands + 1) * 4, "box");
+constexpr int kTermsOnly = 8 * kTermQ * 8;       // per-pixel addends of one round [8 residuals][9][8]
+// the terms region also holds the 8 residuals' footprint boxes of a step (used before the terms)
+constexpr int kTermsPerWave = LDSO_LIN_PIECES ? (8 * kBoxFloats > kTermsOnly ? 8 * kBoxFloats : kTermsOnly) : kTermsOnly;
 constexpr int kSumsPerWave = 64 * kSumStride;   // per-residual sums [64][17]
 
 __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, const Geo &g, const PhotoSums &s,
@@ -514,11 +529,231 @@ static_assert(32 * kTopRow <= kWaveLds, "the Top operand table (one half) reuses
 #ifndef LDSO_LIN_BLOCKS_PER_CU
 #define LDSO_LIN_BLOCKS_PER_CU 5
 #endif
+#ifndef LDSO_LIN_MIN_BLOCKS
+#define LDSO_LIN_MIN_BLOCKS 4  // register budget: 4 waves / SIMD (106 VGPRs; 5 waves spill 44 B: 127.5 vs 117.4 us)
+#endif
 constexpr size_t kLinLdsBytes = (160 * 1024 / LDSO_LIN_BLOCKS_PER_CU) & ~(size_t)511;
 static_assert(kLinLdsBytes >= 4 * kWaveLds * sizeof(float), "k_linearize LDS");
+static_assert(!LDSO_LIN_PIECES || LDSO_LIN_CW_LDS, "the footprint path reads color / weights from the sums table");
+
+// 8-lane group reductions (lanes 8g .. 8g+7) on DPP: quad swaps, then the half-row mirror
+// (lane i <-> 7 - i) joins the two quads.
+__device__ __forceinline__ int grp8_min(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    return min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+}
+__device__ __forceinline__ int grp8_or(int v) {
+    v |= __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);
+    v |= __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);
+    return v | __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float4 ldb4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 v = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+    return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
+}
+
+// Phase A of k_linearize on image layout 3 with footprint pieces (LDSO_LIN_PIECES).  The 8 pattern
+// pixels of a residual read their 96 taps (12 each, load12's stencil) from the residual's tap
+// footprint: the 16-B band columns (4 rows of one column) that hold at least one of the taps,
+// i.e. exactly the 128-B lines the per-lane gathers touch.  The residual's 8 lanes load them with
+// one buffer_load_dwordx4 per box band (lane = column) plus one for a 9th column, into a box of
+// 3 bands x 9 columns in the wave's LDS (aliasing the terms table of the same step), and the
+// pattern lanes read their taps from there: 4 wide loads per lane instead of 12 scalar ones
+// (TCP accesses per launch 64.9 M -> 12.4 M on 64 x S7).  The pieces of step k+1 are in flight
+// while step k reads its box and sums its terms.  A residual whose footprint does not fit the box
+// (pattern spread > 5 pixels) is left out of the pipelined loop and gathered per lane in a second
+// loop over the steps that hold one (a gather inside the pipelined loop would make the compiler
+// wait for every load in flight, the next step's pieces included).  Taps bit-identical to load12's.
+template <bool kMarg>
+__device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, float *S, const float *pre, int jlimit,
+                                               int my_state, float4 my_pd0, float jp_dx, float jp_dy, float da,
+                                               float db, __amdgpu_buffer_rsrc_t rsrc, unsigned band, float wM3,
+                                               float hM3) {
+#pragma clang fp contract(off)
+    const int g = lane >> 3, sl = lane & 7;
+    // staticPattern[8] (Setting.cc:275) offset of this lane's pixel
+    const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
+    const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
+    const float aff0 = pre[24], aff1 = pre[25], b0a = pre[26];
+    float *T = lds_terms_w + g * (kTermQ * 8);
+    float *box = lds_terms_w + g * kBoxFloats;
+    const int nsteps = (jlimit + 7) >> 3;
+    constexpr unsigned kOOB = 0x7FFFFFF0u;  // beyond the frame's buffer range: the load returns 0, no access
+
+    struct Geo8 {
+        float Ku, Kv, jx, jy;
+        int cx0, b0, m;  // box origin (column, band); needed pieces, bit 9 band + column
+        bool gok, wide;
+    };
+    // projection of the lane's pattern pixel of residual 8k + g (Residuals.cc:128-135) and the box
+    auto geo = [&](int k, Geo8 &q) {
+        const int j = 8 * k + g;
+        const int st = __shfl(my_state, j, kWave);
+        const float pu = __shfl(my_pd0.x, j, kWave), pv = __shfl(my_pd0.y, j, kWave),
+                    pz = __shfl(my_pd0.z, j, kWave);
+        const bool go = j < jlimit && st != LDSO_BA_RES_OOB;
+        if constexpr (kMarg) {
+            q.jx = __shfl(jp_dx, j, kWave);
+            q.jy = __shfl(jp_dy, j, kWave);
+        }
+        const float up = pu + px, vp = pv + py;
+        float ptp[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) ptp[i] = (pre[3 * i] * up + pre[3 * i + 1] * vp + pre[3 * i + 2] * 1.0f) + pre[9 + i] * pz;
+        q.Ku = ptp[0] / ptp[2];
+        q.Kv = ptp[1] / ptp[2];
+        const bool pok = go && q.Ku > 1.1f && q.Kv > 1.1f && q.Ku < wM3 && q.Kv < hM3;
+        const unsigned long long m1 = __ballot(pok);
+        q.gok = ((m1 >> (8 * g)) & 0xFFull) == 0xFFull;
+        const int ix = pok ? (int)q.Ku : 1, iy = pok ? (int)q.Kv : 1;
+        // the box: columns from min(ix) - 1, bands from that of min(iy) - 1
+        const int cx0 = grp8_min(ix) - 1, b0 = (grp8_min(iy) - 1) >> 2;
+        const int rx = ix - cx0;
+        const int bA = ((iy - 1) >> 2) - b0, bB = (iy >> 2) - b0, bC = ((iy + 1) >> 2) - b0,
+                  bD = ((iy + 2) >> 2) - b0;
+        const bool wide_l = rx + 2 >= kBoxCols || bD >= kBoxBands;
+        // rows iy-1 / iy+2 use columns ix, ix+1, rows iy, iy+1 columns ix-1 .. ix+2
+        int m = wide_l ? 0
+                       : (3 << (bA * kBoxCols + rx)) | (15 << (bB * kBoxCols + rx - 1)) |
+                             (15 << (bC * kBoxCols + rx - 1)) | (3 << (bD * kBoxCols + rx));
+        m = grp8_or(m);
+        const unsigned long long mw = __ballot(wide_l);
+        q.wide = ((mw >> (8 * g)) & 0xFFull) != 0;
+        q.m = (q.gok && !q.wide) ? m : 0;
+        q.cx0 = cx0;
+        q.b0 = b0;
+    };
+    float4 pc[4];
+    bool any8 = true;  // some residual of the step in flight needs the 9th column
+    auto issue = [&](int k, Geo8 &q) {
+        geo(k, q);
+        const int m = q.m;
+        const unsigned col = (unsigned)(q.cx0 + sl) << 4, base = (unsigned)q.b0 * band;
+#pragma unroll
+        for (int b = 0; b < kBoxBands; b++)
+            pc[b] = ldb4(rsrc, (m >> (b * kBoxCols + sl)) & 1 ? base + b * band + col : kOOB);
+        const bool n8 = sl < kBoxBands && ((m >> (sl * kBoxCols + 8)) & 1);
+#if LDSO_LIN_PIECE8_SKIP
+        any8 = __ballot(n8) != 0;
+        if (any8)
+#endif
+            pc[3] = ldb4(rsrc, n8 ? base + sl * band + ((unsigned)(q.cx0 + 8) << 4) : kOOB);
+    };
+    auto store = [&]() {
+        float4 *bx = reinterpret_cast<float4 *>(box);
+#pragma unroll
+        for (int b = 0; b < kBoxBands; b++) bx[b * kBoxCols + sl] = pc[b];
+#if LDSO_LIN_PIECE8_SKIP
+        if (any8)
+#endif
+            bx[sl < kBoxBands ? sl * kBoxCols + 8 : kBoxBands * kBoxCols] = pc[3];
+    };
+    // the 12 taps of the lane's pixel from the residual's box
+    auto box_taps = [&](const Geo8 &q, float *iv) {
+        const int ix = (int)q.Ku, iy = (int)q.Kv;
+        // row y of column ix - 1: box float (((y >> 2) - b0) * 9 + ix - 1 - cx0) * 4 + (y & 3); the next
+        // columns are 4 floats apart
+        const int c = ix - 1 - q.cx0;
+        const float *r0 = box + ((((iy - 1) >> 2) - q.b0) * kBoxCols + c) * 4 + ((iy - 1) & 3);
+        const float *r1 = box + (((iy >> 2) - q.b0) * kBoxCols + c) * 4 + (iy & 3);
+        const float *r2 = box + ((((iy + 1) >> 2) - q.b0) * kBoxCols + c) * 4 + ((iy + 1) & 3);
+        const float *r3 = box + ((((iy + 2) >> 2) - q.b0) * kBoxCols + c) * 4 + ((iy + 2) & 3);
+        iv[0] = r0[4];
+        iv[1] = r0[8];
+        iv[2] = r1[0];
+        iv[3] = r1[4];
+        iv[4] = r1[8];
+        iv[5] = r1[12];
+        iv[6] = r2[0];
+        iv[7] = r2[4];
+        iv[8] = r2[8];
+        iv[9] = r2[12];
+        iv[10] = r3[4];
+        iv[11] = r3[8];
+    };
+    // the 17 addends of the residuals this pass owns (kWide: the wide ones), summed in pattern order
+    // into their sums rows; an owned residual with a pixel out of bounds or not finite gets the
+    // "pattern not ok" mark.  Residuals the pass does not own are left untouched.
+    auto terms = [&](int k, const Geo8 &q, bool owner, const float *iv) {
+        const int j = 8 * k + g;
+        const bool part = owner && q.gok;
+        bool fin = false;
+        float tt[kSums];
+        if (part) {
+            const float color = S[j * kSumStride + sl], weight = S[j * kSumStride + 8 + sl];
+            const int ix = (int)q.Ku, iy = (int)q.Kv;
+            const float3 s3 = bilin12(iv, q.Ku - ix, q.Kv - iy);
+            fin = isfinite(s3.x);
+            pixel_terms<kMarg>(s3.x, s3.y, s3.z, color, weight, aff0, aff1, b0a, tt, kMarg ? q.jx : 0.f,
+                               kMarg ? q.jy : 0.f, da, db);
+        }
+        const unsigned long long m2 = __ballot(fin);
+        const bool rok = part && ((m2 >> (8 * g)) & 0xFFull) == 0xFFull;
+        auto sum8 = [&](int qq, int e) {
+            const float4 a = *(const float4 *)&T[e * 8], b = *(const float4 *)&T[e * 8 + 4];
+            float sum = 0.0f;
+            sum += a.x;
+            sum += a.y;
+            sum += a.z;
+            sum += a.w;
+            sum += b.x;
+            sum += b.y;
+            sum += b.z;
+            sum += b.w;
+            S[j * kSumStride + qq] = sum;
+        };
+        wave_lds_sync();  // every box read is done before the terms overwrite the boxes
+        if (part) {
+#pragma unroll
+            for (int e = 0; e < kTermQ; e++) T[e * 8 + sl] = tt[e];
+        }
+        wave_lds_sync();
+        if (rok) {
+            sum8(sl, sl);
+            if (sl == 0) sum8(8, 8);
+        } else if (owner && sl == 0 && j < jlimit) {
+            S[j * kSumStride] = -1.0f;  // energy slot: pattern not ok
+        }
+        wave_lds_sync();
+        if (part) {
+#pragma unroll
+            for (int e = 0; e < kSums - kTermQ; e++) T[e * 8 + sl] = tt[kTermQ + e];
+        }
+        wave_lds_sync();
+        if (rok) sum8(kTermQ + sl, sl);
+        wave_lds_sync();
+    };
+    Geo8 cur, nxt;
+    pc[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    unsigned wide_steps = 0;
+    issue(0, cur);
+    for (int k = 0; k < nsteps; k++) {
+        store();            // waits for step k's pieces
+        issue(k + 1, nxt);  // step k+1's pieces in flight during step k's arithmetic
+        wave_lds_sync();
+        const bool wide = cur.gok && cur.wide;
+        if (__ballot(wide)) wide_steps |= 1u << k;
+        float iv[12];
+        if (cur.gok && !wide) box_taps(cur, iv);
+        terms(k, cur, !wide, iv);
+        cur = nxt;
+    }
+    // residuals whose footprint exceeds the box: per-lane gathers, step by step
+    while (wide_steps) {
+        const int k = __builtin_ctz(wide_steps);
+        wide_steps &= wide_steps - 1;
+        geo(k, cur);
+        const bool wide = cur.gok && cur.wide;
+        float iv[12];
+        if (wide) load12(rsrc, band, (int)cur.Ku, (int)cur.Kv, iv);
+        terms(k, cur, wide, iv);
+    }
+}
 
 template <int kImg, bool kMarg>
-__global__ __launch_bounds__(256, 4) void k_linearize(LinParams P) {
+__global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParams P) {
     static_assert(kImg == 1 || kImg == 3, "image layouts 1 and 3");
     extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
     const int lane = threadIdx.x & 63;
@@ -609,7 +844,10 @@ __global__ __launch_bounds__(256, 4) void k_linearize(LinParams P) {
 #if LDSO_LIN_CW_LDS
     wave_lds_sync();  // every row's color / weights are in before any lane reads another's
 #endif
-    {
+    if constexpr (kImg == 3 && LDSO_LIN_PIECES) {
+        phase_a_pieces<kMarg>(lane, lds_terms_w, lds_sums_w, pre, jlimit, my_state, my_pd0, jp_dx, jp_dy, da, db,
+                              rsrc, band, wM3, hM3);
+    } else {
 #pragma clang fp contract(off)
         const int g = lane >> 3, sl = lane & 7;
         // staticPattern[8] (Setting.cc:275) offset of this lane's pixel

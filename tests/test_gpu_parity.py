@@ -317,6 +317,57 @@ def test_s11_window(ctx):
     compare_pass(ctx, ow, 0, e_cpu, s_cpu)
 
 
+def _zoomed_window(seed, dz, angle):
+    """A synthetic window whose newest keyframe moved dz toward the plane and rolled by angle
+    (radians) about its optical axis: patterns projected into it spread over more pixels."""
+    w = synth.make_window(n_frames=4, n_points=600, seed=seed, finalize=False)
+    T = w.frames["world_to_cam_evalpt"][-1]
+    R, t = T[:9].reshape(3, 3), T[9:].copy()
+    c, s = np.cos(angle), np.sin(angle)
+    Rz = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1.0]])
+    T[:9] = (Rz @ R).reshape(-1)
+    T[9:] = Rz @ t - np.array([0, 0, dz])
+    w.frames["world_to_cam_evalpt"][-1] = T
+    return w.refresh_frame_terms()
+
+
+def _pattern_spreads(w):
+    """max - min of floor(projected x) and of floor(y) over each residual's 8 pattern pixels
+    (float64 host projection with the window's precalc), for residuals with all pixels in view."""
+    pat = np.array([[0, -2], [-1, -1], [1, -1], [-2, 0], [0, 0], [2, 0], [-1, 1], [0, 2]], np.float64)
+    N, out = w.n_frames, []
+    for p in range(w.point_data.shape[0]):
+        h = w.point_host[p]
+        u, v, idz = w.point_data[p, 0], w.point_data[p, 1], w.point_data[p, 2]
+        for r in range(w.point_res_begin[p], w.point_res_begin[p + 1]):
+            pre = w.precalc[w.res_target[r] * N + h].astype(np.float64)
+            q = np.stack([u + pat[:, 0], v + pat[:, 1], np.ones(8)], 1) @ pre[:9].reshape(3, 3).T + pre[9:12] * idz
+            if np.any(q[:, 2] <= 0):
+                continue
+            x, y = q[:, 0] / q[:, 2], q[:, 1] / q[:, 2]
+            if x.min() > 2 and y.min() > 2 and x.max() < w.width - 4 and y.max() < w.height - 4:
+                out.append((np.ptp(np.floor(x)), np.ptp(np.floor(y))))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("dz,angle", [(0.0, 0.0), (0.6, 0.3), (1.0, 0.8)], ids=["plain", "zoom1.4", "zoom2"])
+def test_wide_pattern_footprints(ctx, dz, angle):
+    """k_linearize loads each residual's tap footprint into a 3-band x 9-column box; residuals
+    whose projected pattern spreads more (zoom, roll) gather per lane.  Both paths, in one
+    window, are bit-exact against the oracle."""
+    w = _zoomed_window(5, dz, angle)
+    sp = _pattern_spreads(w)
+    wide = np.mean((sp[:, 0] > 5) | (sp[:, 1] > 5))
+    print(f"dz={dz} angle={angle}: {len(sp)} residuals in view, {wide:.1%} with spread > 5")
+    if dz > 0:
+        assert 0.03 < wide < 0.5  # both paths exercised in one pass
+    ctx.load([w])
+    ctx.linearize()
+    ow = oracle.OracleWindow(_zoomed_window(5, dz, angle), threads=0)
+    e_cpu, s_cpu = ow.iteration()
+    compare_pass(ctx, ow, 0, e_cpu, s_cpu)
+
+
 def test_sharded_frame_threshold_exchange(built):
     """ldso_ba_export_newest + ldso_ba_frame_threshold_gathered: three shards' newest-frame
     slots concatenated as an all-gather would lay them out re-select the unsharded threshold,
