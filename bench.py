@@ -110,7 +110,6 @@ def secondary_s11(device, windows=8, steps=20):
     for _ in range(3):
         ctx.linearize()
     ctx.sync()
-    n_gather = sum(int((ctx.residuals(i)["state"] != 1).sum()) for i in range(len(ws)))
     ctx.set_tuning(7, 1)
     ctx.set_kernel_timing(True)
     t0 = time.perf_counter()
@@ -120,6 +119,7 @@ def secondary_s11(device, windows=8, steps=20):
     el = time.perf_counter() - t0
     kt = ctx.kernel_times()
     ctx.set_kernel_timing(False)
+    n_gather = sum(int((ctx.residuals(i)["state"] != 1).sum()) for i in range(len(ws)))  # same every pass
     ctx.close()
     k_ms, k_n = kt["k_linearize"]
     k_s = k_ms / max(1, k_n) / 1e3
@@ -487,8 +487,6 @@ def main():
         step()
     ctx.sync()
     torch.cuda.synchronize()
-    # residuals that gather texels this pass (OOB is sticky within optimize())
-    n_gather = sum(int((ctx.residuals(i)["state"] != 1).sum()) for i in range(len(windows)))
 
     # HIP events bracket only the dominant kernel inside the timed region (each event pair
     # costs the stream a few us); the per-kernel breakdown is taken afterwards
@@ -507,6 +505,10 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     ktimes = ctx.kernel_times()
+    # residuals that gather texels in a pass (the same in every pass after the first: the inputs do
+    # not change between the passes and OOB is sticky), counted after the timed region so that no
+    # host-side download leaves the GPU idle between the warmup and the timed steps
+    n_gather = sum(int((ctx.residuals(i)["state"] != 1).sum()) for i in range(len(windows)))
     ctx.set_kernel_timing(False)
     ctx.set_tuning(7, -1)
     ctx.set_kernel_timing(True)  # breakdown of every kernel, outside the timed region

@@ -444,6 +444,13 @@ constexpr int kTermQ = 9;                      // quantities per transposition r
 #endif
 constexpr int kBoxCols = 9, kBoxBands = 3, kBoxFloats = LDSO_LIN_BOX_STRIDE;
 static_assert(kBoxFloats >= (kBoxCols * kBoxBands + 1) * 4, "box");
+#ifndef LDSO_LIN_T_STRIDE
+#define LDSO_LIN_T_STRIDE 72
+#endif
+// floats between the 8 residuals' term tables of a step (72 = dense; 76 halves the bank conflicts of
+// the pattern-order sums' 16-B reads)
+constexpr int kTermStride = LDSO_LIN_T_STRIDE;
+static_assert(kTermStride >= kTermQ * 8 && 8 * kTermStride <= 8 * kBoxFloats, "term tables");
 constexpr int kTermsOnly = 8 * kTermQ * 8;       // per-pixel addends of one round [8 residuals][9][8]
 // the terms region also holds the 8 residuals' footprint boxes of a step (used before the terms)
 constexpr int kTermsPerWave = LDSO_LIN_PIECES ? (8 * kBoxFloats > kTermsOnly ? 8 * kBoxFloats : kTermsOnly) : kTermsOnly;
@@ -577,7 +584,7 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
     const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
     const float aff0 = pre[24], aff1 = pre[25], b0a = pre[26];
-    float *T = lds_terms_w + g * (kTermQ * 8);
+    float *T = lds_terms_w + g * kTermStride;
     float *box = lds_terms_w + g * kBoxFloats;
     const int nsteps = (jlimit + 7) >> 3;
     constexpr unsigned kOOB = 0x7FFFFFF0u;  // beyond the frame's buffer range: the load returns 0, no access
@@ -683,11 +690,17 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
         float tt[kSums];
         if (part) {
             const float color = S[j * kSumStride + sl], weight = S[j * kSumStride + 8 + sl];
+#ifdef LDSO_LIN_ABL_NOMATH  // diagnostic ablation only: no bilinear / pixel arithmetic
+            fin = true;
+#pragma unroll
+            for (int e = 0; e < kSums; e++) tt[e] = iv[e % 12] * color + weight;
+#else
             const int ix = (int)q.Ku, iy = (int)q.Kv;
             const float3 s3 = bilin12(iv, q.Ku - ix, q.Kv - iy);
             fin = isfinite(s3.x);
             pixel_terms<kMarg>(s3.x, s3.y, s3.z, color, weight, aff0, aff1, b0a, tt, kMarg ? q.jx : 0.f,
                                kMarg ? q.jy : 0.f, da, db);
+#endif
         }
         const unsigned long long m2 = __ballot(fin);
         const bool rok = part && ((m2 >> (8 * g)) & 0xFFull) == 0xFFull;
