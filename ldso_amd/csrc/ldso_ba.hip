@@ -525,7 +525,11 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
 //   Top      the chunk's AccumulatorApprox block on the matrix cores (top_mfma).
 // kMarg: the marginalisation pass (addPoint<2> sums with fixLinearizationF's res_toZeroF).
 // ============================================================================================
-constexpr int kWaveLds = kTermsPerWave + kSumsPerWave;  // floats of LDS per wavefront (6.5 KB: 6 waves/SIMD)
+#ifndef LDSO_LIN_PT_TABLE
+#define LDSO_LIN_PT_TABLE 1  // phase A reads each residual's (u, v, idepth, state) from a per-wave LDS table
+#endif
+constexpr int kPtTable = LDSO_LIN_PT_TABLE ? 64 * 4 : 0;  // floats: [64 residuals][u, v, idepth, state]
+constexpr int kWaveLds = kTermsPerWave + kSumsPerWave + kPtTable;  // floats of LDS per wavefront
 static_assert(32 * kTopRow <= kWaveLds, "the Top operand table (one half) reuses the wave's LDS");
 // LDS requested per 4-wave workgroup: sets the resident workgroups per CU (= waves per SIMD).
 // 160 KB / 32 KB = 5: measured fastest (64 x S7: 121.6 us; 4 blocks 125.7, 3 blocks 143.5; 6
@@ -534,7 +538,7 @@ static_assert(32 * kTopRow <= kWaveLds, "the Top operand table (one half) reuses
 #define LDSO_LIN_CW_LDS 1  // color / weights staged in the sums table (0: gathered per step)
 #endif
 #ifndef LDSO_LIN_BLOCKS_PER_CU
-#define LDSO_LIN_BLOCKS_PER_CU 5
+#define LDSO_LIN_BLOCKS_PER_CU 4
 #endif
 #ifndef LDSO_LIN_MIN_BLOCKS
 #define LDSO_LIN_MIN_BLOCKS 4  // register budget: 4 waves / SIMD (106 VGPRs; 5 waves spill 44 B: 127.5 vs 117.4 us)
@@ -545,15 +549,25 @@ static_assert(!LDSO_LIN_PIECES || LDSO_LIN_CW_LDS, "the footprint path reads col
 
 // 8-lane group reductions (lanes 8g .. 8g+7) on DPP: quad swaps, then the half-row mirror
 // (lane i <-> 7 - i) joins the two quads.
+#ifndef LDSO_LIN_DPP_MOV
+#define LDSO_LIN_DPP_MOV 1
+#endif
+#if LDSO_LIN_DPP_MOV
+// every lane active, full row / bank masks: no "old" value, so the DPP move can fold into the
+// min / or (one DPP-modified VALU op per stage instead of a copy, a DPP move and the op)
+#define LDSO_DPP(v, ctrl) __builtin_amdgcn_mov_dpp(v, ctrl, 0xF, 0xF, true)
+#else
+#define LDSO_DPP(v, ctrl) __builtin_amdgcn_update_dpp(v, v, ctrl, 0xF, 0xF, false)
+#endif
 __device__ __forceinline__ int grp8_min(int v) {
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-    return min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = min(v, LDSO_DPP(v, 0xB1));    // quad_perm [1,0,3,2]
+    v = min(v, LDSO_DPP(v, 0x4E));    // quad_perm [2,3,0,1]
+    return min(v, LDSO_DPP(v, 0x141));  // row_half_mirror
 }
 __device__ __forceinline__ int grp8_or(int v) {
-    v |= __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);
-    v |= __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);
-    return v | __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
+    v |= LDSO_DPP(v, 0xB1);
+    v |= LDSO_DPP(v, 0x4E);
+    return v | LDSO_DPP(v, 0x141);
 }
 __device__ __forceinline__ float4 ldb4(__amdgpu_buffer_rsrc_t r, unsigned off) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -597,9 +611,15 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     // projection of the lane's pattern pixel of residual 8k + g (Residuals.cc:128-135) and the box
     auto geo = [&](int k, Geo8 &q) {
         const int j = 8 * k + g;
+#if LDSO_LIN_PT_TABLE
+        const float4 pt = *reinterpret_cast<const float4 *>(S + kSumsPerWave + 4 * (j & 63));
+        const float pu = pt.x, pv = pt.y, pz = pt.z;
+        const int st = __float_as_int(pt.w);
+#else
         const int st = __shfl(my_state, j, kWave);
         const float pu = __shfl(my_pd0.x, j, kWave), pv = __shfl(my_pd0.y, j, kWave),
                     pz = __shfl(my_pd0.z, j, kWave);
+#endif
         const bool go = j < jlimit && st != LDSO_BA_RES_OOB;
         if constexpr (kMarg) {
             q.jx = __shfl(jp_dx, j, kWave);
@@ -858,6 +878,11 @@ __global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParam
     wave_lds_sync();  // every row's color / weights are in before any lane reads another's
 #endif
     if constexpr (kImg == 3 && LDSO_LIN_PIECES) {
+#if LDSO_LIN_PT_TABLE
+        *reinterpret_cast<float4 *>(lds_sums_w + kSumsPerWave + 4 * lane) =
+            make_float4(my_pd0.x, my_pd0.y, my_pd0.z, __int_as_float(my_state));
+        wave_lds_sync();
+#endif
         phase_a_pieces<kMarg>(lane, lds_terms_w, lds_sums_w, pre, jlimit, my_state, my_pd0, jp_dx, jp_dy, da, db,
                               rsrc, band, wM3, hM3);
     } else {
