@@ -477,8 +477,17 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
     const bool geo = i < 10, ind = i >= 13;
     const float a0c = i == 13 ? 1.f : 0.f, a1c = i == 14 ? 1.f : 0.f;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#if LDSO_LIN_TOP_FULL
+    {  // every residual's row at once; K rows (residual 32 half + 8 kk + m, c), half by half as below
+        float4 *row = reinterpret_cast<float4 *>(tab + lane * kTopRow);
+#pragma unroll
+        for (int k = 0; k < 9; k++) row[k] = v[k];
+    }
+    wave_lds_sync();
+#endif
 #pragma unroll
     for (int half = 0; half < 2; half++) {
+#if !LDSO_LIN_TOP_FULL
         if ((lane >> 5) == half) {
             float4 *row = reinterpret_cast<float4 *>(tab + (lane & 31) * kTopRow);
 #pragma unroll
@@ -486,6 +495,9 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
         }
         wave_lds_sync();
         const float *base = tab + kk * 8 * kTopRow;  // K rows (residual kk*8 + m, c)
+#else
+        const float *base = tab + (32 * half + kk * 8) * kTopRow;
+#endif
 #pragma unroll 4
         for (int m = 0; m < 8; m++) {
             const float *rr = base + m * kTopRow;
@@ -497,7 +509,9 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A0, B0, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A1, B1, acc, 0, 0, 0);
         }
+#if !LDSO_LIN_TOP_FULL
         wave_lds_sync();
+#endif
     }
     // lane holds D[4 kk + v][i]; scatter into the 96-slot partial layout read by k_stitch
 #pragma unroll
@@ -529,8 +543,13 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
 #define LDSO_LIN_PT_TABLE 1  // phase A reads each residual's (u, v, idepth, state) from a per-wave LDS table
 #endif
 constexpr int kPtTable = LDSO_LIN_PT_TABLE ? 64 * 4 : 0;  // floats: [64 residuals][u, v, idepth, state]
-constexpr int kWaveLds = kTermsPerWave + kSumsPerWave + kPtTable;  // floats of LDS per wavefront
-static_assert(32 * kTopRow <= kWaveLds, "the Top operand table (one half) reuses the wave's LDS");
+#ifndef LDSO_LIN_TOP_FULL
+#define LDSO_LIN_TOP_FULL 1  // the Top operand table holds all 64 residuals (one staging round, not two)
+#endif
+constexpr int kTopRows = LDSO_LIN_TOP_FULL ? 64 : 32;
+constexpr int kWaveLdsA = kTermsPerWave + kSumsPerWave + kPtTable;
+// floats of LDS per wavefront (the Top operand table reuses the wave's region after phase B)
+constexpr int kWaveLds = kWaveLdsA > kTopRows * kTopRow ? kWaveLdsA : kTopRows * kTopRow;
 // LDS requested per 4-wave workgroup: sets the resident workgroups per CU (= waves per SIMD).
 // 160 KB / 32 KB = 5: measured fastest (64 x S7: 121.6 us; 4 blocks 125.7, 3 blocks 143.5; 6
 // waves/SIMD need <= 80 VGPRs and spill, 145 us).
@@ -4048,7 +4067,9 @@ hipEvent_t get_event(ldso_ba_ctx *c) {
         return e;
     }
     hipEvent_t e;
-    (void)hipEventCreate(&e);
+    // timing-only events: no system-scope fence (its L2 write-back and invalidate would be timed,
+    // and would slow the kernel after the start event)
+    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     return e;
 }
 
