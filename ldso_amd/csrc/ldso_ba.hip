@@ -729,17 +729,11 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
         float tt[kSums];
         if (part) {
             const float color = S[j * kSumStride + sl], weight = S[j * kSumStride + 8 + sl];
-#ifdef LDSO_LIN_ABL_NOMATH  // diagnostic ablation only: no bilinear / pixel arithmetic
-            fin = true;
-#pragma unroll
-            for (int e = 0; e < kSums; e++) tt[e] = iv[e % 12] * color + weight;
-#else
             const int ix = (int)q.Ku, iy = (int)q.Kv;
             const float3 s3 = bilin12(iv, q.Ku - ix, q.Kv - iy);
             fin = isfinite(s3.x);
             pixel_terms<kMarg>(s3.x, s3.y, s3.z, color, weight, aff0, aff1, b0a, tt, kMarg ? q.jx : 0.f,
                                kMarg ? q.jy : 0.f, da, db);
-#endif
         }
         const unsigned long long m2 = __ballot(fin);
         const bool rok = part && ((m2 >> (8 * g)) & 0xFFull) == 0xFFull;
