@@ -594,21 +594,6 @@ __device__ __forceinline__ float4 ldb4(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
 }
 
-#ifndef LDSO_LIN_LIGHT_SYNC
-#define LDSO_LIN_LIGHT_SYNC 0
-#endif
-// ordering of phase A's LDS traffic between the lanes of one wave: the LDS serves a wave's
-// requests in issue order, so a compiler barrier suffices (LIGHT) where wave_lds_sync also waits
-// for every outstanding LDS access
-__device__ __forceinline__ void lin_sync() {
-#if LDSO_LIN_LIGHT_SYNC
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-#else
-    wave_lds_sync();
-#endif
-}
-
 // Phase A of k_linearize on image layout 3 with footprint pieces (LDSO_LIN_PIECES).  The 8 pattern
 // pixels of a residual read their 96 taps (12 each, load12's stencil) from the residual's tap
 // footprint: the 16-B band columns (4 rows of one column) that hold at least one of the taps,
@@ -765,26 +750,26 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
             sum += b.w;
             S[j * kSumStride + qq] = sum;
         };
-        lin_sync();  // every box read is done before the terms overwrite the boxes
+        wave_lds_sync();  // every box read is done before the terms overwrite the boxes
         if (part) {
 #pragma unroll
             for (int e = 0; e < kTermQ; e++) T[e * 8 + sl] = tt[e];
         }
-        lin_sync();
+        wave_lds_sync();
         if (rok) {
             sum8(sl, sl);
             if (sl == 0) sum8(8, 8);
         } else if (owner && sl == 0 && j < jlimit) {
             S[j * kSumStride] = -1.0f;  // energy slot: pattern not ok
         }
-        lin_sync();
+        wave_lds_sync();
         if (part) {
 #pragma unroll
             for (int e = 0; e < kSums - kTermQ; e++) T[e * 8 + sl] = tt[kTermQ + e];
         }
-        lin_sync();
+        wave_lds_sync();
         if (rok) sum8(kTermQ + sl, sl);
-        lin_sync();
+        wave_lds_sync();
     };
     Geo8 cur, nxt;
     pc[3] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -793,7 +778,7 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     for (int k = 0; k < nsteps; k++) {
         store();            // waits for step k's pieces
         issue(k + 1, nxt);  // step k+1's pieces in flight during step k's arithmetic
-        lin_sync();
+        wave_lds_sync();
         const bool wide = cur.gok && cur.wide;
         if (__ballot(wide)) wide_steps |= 1u << k;
         float iv[12];
