@@ -41,6 +41,65 @@ def algo_bytes_per_residual(n_frames):
     return 276.0 + 8.0 + 88.0 / (n_frames - 1)
 
 
+def world_from_env(gpus, env=None):
+    """(world, launched_by_a_launcher).  Under torchrun (WORLD_SIZE set) --gpus must equal
+    WORLD_SIZE: a mismatch is an error, not a silently different measurement."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world} (the launcher started {world} ranks)")
+        return world, True
+    return 1, False
+
+
+def free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, cmd, env=None, poll_s=0.5):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes of `cmd` (one per
+    GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free MASTER_PORT)
+    before this process touches the GPU, forward rank 0's stdout (the JSON line), and return
+    the first non-zero exit code (0 when every rank succeeded).  If a rank fails the others are
+    stopped (they would wait in a collective forever)."""
+    import subprocess
+
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n))
+        # rank 0's stdout is this process's (the one JSON line); the others' goes to stderr
+        procs.append(subprocess.Popen(cmd, env=e, stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def load_pmc(workload):
     """HBM traffic per k_linearize launch from a committed rocprofv3 --pmc summary, if one
     exists for this exact workload (written by tools/pmc_traffic.py); else None."""
@@ -67,6 +126,8 @@ def cpp_face_leg():
     except (OSError, subprocess.SubprocessError, ValueError, IndexError) as e:
         return {"error": str(e)}
     d["ms_per_gn_iteration"] = d["optimize"]["ms_per_gn_iteration"]
+    if "shim" in d:  # INTEGRATION.md §3's forwarding loops per GN iteration (index vectors)
+        d["shim_ms_per_gn_iteration"] = d["shim"]["shim_ms_per_gn_iteration"]
     return d
 
 
@@ -84,15 +145,24 @@ def cpu_baseline(seconds=10.0):
         return None
 
 
-def time_optimize(ctx, nss, n_its=6, reps=10):
-    """ms per ldso_ba_optimize(n_its) call (host clock) and per GN iteration of it."""
+def time_optimize(ctx, nss, n_its=6, reps=10, settings=None):
+    """ms per ldso_ba_optimize(n_its) call (host clock) and per GN iteration it ran.  With the
+    default settings every window leaves the loop on the reference's exits (canbreak after
+    setting_minOptIterations, FullSystem.cc:968-969), so the iterations run are reported;
+    settings with th_opt_iterations = 0 never break and run all n_its."""
     for _ in range(2):
-        ctx.optimize(n_its, nullspaces=nss)
+        r = ctx.optimize(n_its, nullspaces=nss, settings=settings)
     t = time.perf_counter()
     for _ in range(reps):
-        ctx.optimize(n_its, nullspaces=nss)
+        ctx.optimize(n_its, nullspaces=nss, settings=settings)
     ms = 1e3 * (time.perf_counter() - t) / reps
-    return {"n_its": n_its, "ms_per_optimize": ms, "ms_per_iteration": ms / n_its, "windows": len(nss)}
+    its, status = np.asarray(r[4]), np.asarray(r[5])
+    out = {"n_its": n_its, "ms_per_optimize": ms, "windows": len(nss),
+           "iterations_run": int(its[0]) if len(its) == 1 else
+           {"min": int(its.min()), "max": int(its.max()), "mean": float(its.mean())},
+           "converged_windows": int((status == 1).sum()), "lost_windows": int((status == 2).sum())}
+    out["ms_per_iteration"] = ms / max(1, int(its.max()))
+    return out
 
 
 def secondary_s11(device, windows=8, steps=20):
@@ -438,7 +508,9 @@ def main():
     ap.add_argument("--no-shard-leg", action="store_true", help="N > 1: skip the sharded S11 window")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, launched = world_from_env(args.gpus)
+    if not launched and args.gpus > 1:  # no launcher: start the ranks here, before any GPU call
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N > 1 path on a one-GPU box: LDSO_BENCH_SHARE_GPU=1 puts every rank on
@@ -460,6 +532,7 @@ def main():
 
     # torch's bundled HIP runtime must initialise before the one libldso_ba.so links
     torch.cuda.set_device(local_rank)
+    from ldso_amd import _lib as L
     from ldso_amd import BAContext, synth
 
     B, N, P = args.windows, args.frames, args.points
@@ -531,6 +604,8 @@ def main():
         gn_ms = 1e3 * (time.perf_counter() - t1) / it_reps
         gn = {"ms_per_iteration": gn_ms, "windows": B, "windows_per_s": B / (gn_ms / 1e3)}
         gn["optimize"] = time_optimize(ctx, nss, n_its=6, reps=3)
+        gn["optimize_all_its"] = time_optimize(ctx, nss, n_its=6, reps=3,
+                                               settings=L.OptSettings.default(th_opt_iterations=0.0))
 
     if dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
@@ -604,6 +679,8 @@ def main():
         # resetOOB + linearizeAll, then 6 x {solve, resubstitute, doStepFromBackup + setPrecalcValues,
         # linearizeAll}; one synchronisation), host clock around the call
         single["optimize"] = time_optimize(c1, [ns], n_its=6)
+        # the same call with the early exit disabled (th_opt_iterations = 0): all 6 iterations
+        single["optimize_all_its"] = time_optimize(c1, [ns], n_its=6, settings=L.OptSettings.default(th_opt_iterations=0.0))
         c1.close()
 
     s11 = None
@@ -671,9 +748,9 @@ def main():
             "cpu_baseline_single_window": cpu1,
             "cpu_baseline_six_threads": cpu6,
         }
-        if face and single and "optimize" in face:
+        if face and single and "optimize" in face:  # both with all 6 iterations
             face["vs_c_abi_single_window_optimize"] = (face["ms_per_gn_iteration"] /
-                                                       single["optimize"]["ms_per_iteration"])
+                                                       single["optimize_all_its"]["ms_per_iteration"])
         if cpu is not None:  # like for like: the same 64-window workload on both sides
             out["speedup_vs_cpu"] = value / cpu["value"]
             out["speedup_vs_cpu_workload"] = f"{B} x S7 windows: GPU step vs {cpu['workers']} pinned CPU workers"

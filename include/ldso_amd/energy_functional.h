@@ -244,18 +244,23 @@ public:
     // accumulation of the stitched system for the following solveSystemF.  Returns (E, 0, #IN).
     Vec3 linearizeAll(bool fixLinearization);
 
-    // FullSystem::optimize's Gauss-Newton loop (FullSystem.cc:853-970) with setting_forceAceptStep
-    // on the device (ldso_ba_optimize): resetOOB, linearizeAll, then n_its x {solveSystemF (the
-    // pose / scale nullspaces of getNullspaces from iteration 2), resubstituteF_MT,
-    // doStepFromBackup + setPrecalcValues, linearizeAll}, with no host round trip.  Afterwards the
-    // frames' states, HCalib's value and the points' idepth / idepth_zero hold the stepped values
-    // and setDeltaF has run, as after the reference loop.  The residual fields (state_*, JpJdF,
+    // FullSystem::optimize(mnumOptIts) (FullSystem.cc:844-970) with setting_forceAceptStep on the
+    // device (ldso_ba_optimize): the iteration-count override for 2-3 frames (:846-851), resetOOB,
+    // linearizeAll, then up to n_its x {solveSystemF (the pose / scale nullspaces of getNullspaces
+    // from iteration 2), resubstituteF_MT, doStepFromBackup + setPrecalcValues, linearizeAll},
+    // with no host round trip, leaving the loop on the reference's exits: canbreak once
+    // iteration >= setting_minOptIterations (:968-969), or *isLost = true when the solution has a
+    // NaN norm (:907-911; the reference then returns DBL_MAX).  Afterwards the frames' states,
+    // HCalib's value and the points' idepth / idepth_zero hold the stepped values and setDeltaF
+    // has run, as after the reference loop.  The residual fields (state_*, JpJdF,
     // centerProjectedTo) and the points' HdiF / bdSumF / idepth_hessian are written back lazily:
     // by the linearizeAll(true) FullSystem::optimize runs next, by syncResiduals(), or before any
-    // PointFrameResidual method call.  Runs exactly n_its iterations (the canbreak exit is the
-    // caller's).  energies (optional): (E, 0, #IN) of the first pass and of every iteration's.
-    // Returns the last one.
-    Vec3 optimize(int n_its, shared_ptr<CalibHessian> HCalib, std::vector<Vec3> *energies = nullptr);
+    // PointFrameResidual method call.  energies (optional): (E, 0, #IN) of the first pass and of
+    // every iteration's (after an exit: repeats of the last); iterations: the iterations entered;
+    // settings: NULL = the reference's defaults (ldso_ba_check_settings rejects the rest).
+    // Returns the last pass's energies.
+    Vec3 optimize(int n_its, shared_ptr<CalibHessian> HCalib, std::vector<Vec3> *energies = nullptr,
+                  bool *isLost = nullptr, int *iterations = nullptr, const ldso_ba_opt_settings *settings = nullptr);
     // the residual and point fields of the device's last pass, if the host copies are stale
     void syncResiduals();
     // device linearisation passes run so far (linearizeAll, the per-residual relinearisation,
@@ -322,6 +327,7 @@ private:
     std::vector<float> pointVals_;  // [P][4] uploaded (idepth_scaled, idepth_zero_scaled, priorF, deltaF)
     std::vector<ldso_ba_frame_state> fsUp_;  // frame states / calibration / thresholds last uploaded
     float calibUp_[4] = {0, 0, 0, 0};
+    float cDeltaUp_[4] = {0, 0, 0, 0};  // cDeltaF as last uploaded (it feeds the bL prior)
     std::vector<float> thUp_;
     int width_ = 0, height_ = 0;
     ResSync resSync_ = ResSync::Synced;

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define LDSO_BA_ABI_VERSION 3
+#define LDSO_BA_ABI_VERSION 4
 
 #define LDSO_BA_PATTERN_NUM 8      /* patternNum, Settings.h:225 (staticPattern[8])     */
 #define LDSO_BA_CPARS 4            /* CPARS, NumTypes.h:25                              */
@@ -246,7 +246,8 @@ int ldso_ba_update_residuals(ldso_ba_ctx *ctx, int32_t win, const int8_t *state,
  * 0: the centre projection failed and the reference leaves centerProjectedTo unchanged), jpjdf
  * [R][8] (the JpJdF applyRes(true)'s takeData forms from this linearisation, where new_state is
  * IN; 0 elsewhere).  A residual whose state is OOB returns state_energy in the reference without
- * any computation; the caller keeps that branch. */
+ * any computation; the caller keeps that branch.  Single-shard windows only (a sharded window
+ * holds only its run of the residuals: -1), not on a marginalisation context (-1). */
 int ldso_ba_linearize_residuals(ldso_ba_ctx *ctx, int32_t win, int8_t *new_state, float *new_energy,
                                 float *new_energy_wo, float *center, uint8_t *center_ok, float *jpjdf);
 
@@ -371,24 +372,75 @@ int ldso_ba_resubstitute_device(ldso_ba_ctx *ctx, double lambda, float *point_st
 int ldso_ba_iterate(ldso_ba_ctx *ctx, int32_t iteration, double lambda, const double *ns, int32_t n_null,
                     double *x_out, float *point_step_out, double *energy_out);
 
-/* FullSystem::optimize (FullSystem.cc:844-976) on the device for every loaded window, with
+/* setting_solverMode bits (Settings.h:14-25).  The library implements the reference's default
+ * mode, SOLVER_FIX_LAMBDA | SOLVER_ORTHOGONALIZE_X_LATER (Setting.cc:23); every other bit is
+ * rejected (ldso_ba_check_settings) rather than silently run as the default. */
+#define LDSO_BA_SOLVER_SVD 1
+#define LDSO_BA_SOLVER_ORTHOGONALIZE_SYSTEM 2
+#define LDSO_BA_SOLVER_ORTHOGONALIZE_POINTMARG 4
+#define LDSO_BA_SOLVER_ORTHOGONALIZE_FULL 8
+#define LDSO_BA_SOLVER_SVD_CUT7 16
+#define LDSO_BA_SOLVER_REMOVE_POSEPRIOR 32
+#define LDSO_BA_SOLVER_USE_GN 64
+#define LDSO_BA_SOLVER_FIX_LAMBDA 128
+#define LDSO_BA_SOLVER_ORTHOGONALIZE_X 256
+#define LDSO_BA_SOLVER_MOMENTUM 512
+#define LDSO_BA_SOLVER_STEPMOMENTUM 1024
+#define LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER 2048
+#define LDSO_BA_SOLVER_DEFAULT (LDSO_BA_SOLVER_FIX_LAMBDA | LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER)
+
+/* The FullSystem::optimize settings the device loop reads (Setting.cc:23, 36-38, 73). */
+typedef struct ldso_ba_opt_settings {
+    int32_t solver_mode;         /* setting_solverMode (LDSO_BA_SOLVER_DEFAULT)                  */
+    int32_t force_accept_step;   /* setting_forceAceptStep (1); 0 is rejected                      */
+    int32_t min_opt_iterations;  /* setting_minOptIterations (1)                                   */
+    float th_opt_iterations;     /* setting_thOptIterations (1.2f)                                 */
+} ldso_ba_opt_settings;
+
+/* 0 when the settings are what this library runs, else -1 with a message naming the first
+ * unsupported setting (SVD / SVD_CUT7 / ORTHOGONALIZE_SYSTEM / USE_GN / MOMENTUM / STEPMOMENTUM /
+ * ... or force_accept_step == 0, whose accept / reject branch FullSystem.cc:935-966 is absent).
+ * NULL means the defaults (accepted). */
+int ldso_ba_check_settings(const ldso_ba_opt_settings *s);
+
+/* Per-window outcome of ldso_ba_optimize (status_out). */
+#define LDSO_BA_OPT_RAN_ALL 0      /* n_its iterations, no early exit                            */
+#define LDSO_BA_OPT_CONVERGED 1    /* doStepFromBackup's canbreak after >= min_opt_iterations    */
+#define LDSO_BA_OPT_LOST 2         /* lastX had a NaN norm: FullSystem.cc:907-911 isLost = true  */
+
+/* FullSystem::optimize (FullSystem.cc:844-970) on the device for every loaded window, with
  * setting_forceAceptStep (the default) and the non-momentum doStepFromBackup: resetOOB, one
- * linearizeAll + applyRes, then n_its times {solveSystemF (k_solve; orthogonalize with ns from
- * iteration 2), resubstituteF_MT, doStepFromBackup (FullSystem.cc:1843-1922: frame states by
+ * linearizeAll + applyRes, then up to n_its times {solveSystemF (k_solve; orthogonalize with ns
+ * from iteration 2), resubstituteF_MT, doStepFromBackup (FullSystem.cc:1826-1931: frame states by
  * log(exp(step) exp(state)), CalibHessian::setValue, point setIdepth / setIdepthZero) +
  * setPrecalcValues (FrameFramePrecalc::Set for every pair, the prior vector), linearizeAll +
  * applyRes}, all on the context stream with no host round trip; one synchronisation at the end.
+ * Each window leaves the loop on its own, as the reference's loop does:
+ *   - lost (FullSystem.cc:907-911): the solve's x has a NaN element (isnan(lastX.norm())): no
+ *     step is applied in that iteration and the window stops (status LDSO_BA_OPT_LOST; the
+ *     reference returns DBL_MAX and sets isLost);
+ *   - converged (FullSystem.cc:968-969): doStepFromBackup's canbreak -- sqrtf of the frame-averaged
+ *     squared a, b, rotation and translation steps (the translation term times the mean
+ *     |idepth_backup| of the window's points, summed in the window's point order, hosts in
+ *     window order) below 5e-4 / 5e-5 x th_opt_iterations (FullSystem.cc:1914-1931) -- once
+ *     iteration >= min_opt_iterations: the pass after that step still runs, then the window stops.
+ * A stopped window's later launches are no-ops inside the same (captured) sequence.
+ *   settings: NULL = the defaults; anything ldso_ba_check_settings rejects returns -1.
  *   frames [sum N]: the windows' frame states back to back; calib_value / calib_value_zero
  *   [n_windows][4]: CalibHessian::value / value_zero (unscaled: value_scaled = 50 value);
  *   ns: [7][sum (8N+4)] nullspaces (ldso_ba_nullspaces per window, back to back) or NULL.
  * Outputs (any may be NULL): energy_out [n_its + 1][n_windows][3] = (E, 0, #IN) of the initial
- * and every iteration's linearizeAll; frames_out / calib_out the stepped states; idepth_out
- * [sum P] the points' idepth, caller order.  The reference's early exit (canbreak) is the
- * caller's: it runs exactly n_its iterations.  Afterwards the context's precalc, calibration,
- * priors and point data are the stepped ones (ldso_ba_update overrides them as before). */
-int ldso_ba_optimize(ldso_ba_ctx *ctx, int32_t n_its, const ldso_ba_frame_state *frames, const double *calib_value,
-                     const double *calib_value_zero, const double *ns, double *energy_out,
-                     ldso_ba_frame_state *frames_out, double *calib_out, float *idepth_out);
+ * and every iteration's linearizeAll (rows after a window stopped repeat its last pass, the
+ * reference's lastEnergy); frames_out / calib_out the stepped states; idepth_out [sum P] the
+ * points' idepth, caller order; iterations_out [n_windows] the loop iterations entered (solves
+ * run); status_out [n_windows] LDSO_BA_OPT_*.  Afterwards the context's precalc, calibration,
+ * priors and point data are the stepped ones (ldso_ba_update overrides them as before).  The
+ * reference's iteration-count override for windows of 2-3 frames (FullSystem.cc:846-851) is the
+ * caller's (the C++ face applies it). */
+int ldso_ba_optimize(ldso_ba_ctx *ctx, int32_t n_its, const ldso_ba_opt_settings *settings,
+                     const ldso_ba_frame_state *frames, const double *calib_value, const double *calib_value_zero,
+                     const double *ns, double *energy_out, ldso_ba_frame_state *frames_out, double *calib_out,
+                     float *idepth_out, int32_t *iterations_out, int32_t *status_out);
 
 /* doStepFromBackup's frame and calibration step on the host (the same se3.h statements as the
  * device loop): out[f] = in[f] stepped by -x[4 + 8f ..]; calib_value (if not NULL) += -x[0..3],

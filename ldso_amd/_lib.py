@@ -45,6 +45,30 @@ FRAME_STATE_DTYPE = np.dtype(
 assert FRAME_STATE_DTYPE.itemsize == 272
 
 
+ABI_VERSION = 4
+
+# setting_solverMode bits (Settings.h:14-25) and ldso_ba_optimize's per-window outcome
+SOLVER_SVD, SOLVER_ORTHOGONALIZE_SYSTEM, SOLVER_ORTHOGONALIZE_POINTMARG, SOLVER_ORTHOGONALIZE_FULL = 1, 2, 4, 8
+SOLVER_SVD_CUT7, SOLVER_REMOVE_POSEPRIOR, SOLVER_USE_GN, SOLVER_FIX_LAMBDA = 16, 32, 64, 128
+SOLVER_ORTHOGONALIZE_X, SOLVER_MOMENTUM, SOLVER_STEPMOMENTUM, SOLVER_ORTHOGONALIZE_X_LATER = 256, 512, 1024, 2048
+SOLVER_DEFAULT = SOLVER_FIX_LAMBDA | SOLVER_ORTHOGONALIZE_X_LATER
+OPT_RAN_ALL, OPT_CONVERGED, OPT_LOST = 0, 1, 2
+
+
+class OptSettings(C.Structure):
+    """ldso_ba_opt_settings: setting_solverMode, setting_forceAceptStep, setting_minOptIterations,
+    setting_thOptIterations (Setting.cc:23, 36-38, 73)."""
+    _fields_ = [("solver_mode", C.c_int32), ("force_accept_step", C.c_int32), ("min_opt_iterations", C.c_int32),
+                ("th_opt_iterations", C.c_float)]
+
+    @classmethod
+    def default(cls, **kw):
+        s = cls(SOLVER_DEFAULT, 1, 1, 1.2)
+        for k, v in kw.items():
+            setattr(s, k, v)
+        return s
+
+
 class LdsoBaWindow(C.Structure):
     _fields_ = [
         ("n_frames", C.c_int32),
@@ -123,8 +147,9 @@ ABI = [
     ("ldso_ba_frame_threshold", C.c_int, [f32p, C.c_int64, f32p]),
     ("ldso_ba_comm_unique_id", C.c_int, [C.c_void_p]),
     ("ldso_ba_comm_init", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
-    ("ldso_ba_optimize", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, f64p, f64p, f64p, f64p, C.c_void_p, f64p,
-                                   f32p]),
+    ("ldso_ba_check_settings", C.c_int, [C.c_void_p]),
+    ("ldso_ba_optimize", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, f64p, f64p, f64p, f64p, C.c_void_p,
+                                   f64p, f32p, i32p, i32p]),
     ("ldso_ba_frame_step", C.c_int, [C.c_int32, C.c_void_p, f64p, C.c_void_p, f64p, f64p, f32p, f32p]),
     ("ldso_ba_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("ldso_ba_set_tuning", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
@@ -196,6 +221,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        if L.ldso_ba_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH} has ABI {L.ldso_ba_abi_version()}, these bindings expect {ABI_VERSION}: "
+                               "rebuild it (make -C ldso_amd/csrc)")
         _lib = L
     return _lib
 

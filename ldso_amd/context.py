@@ -49,11 +49,14 @@ class BAContext:
             w._keep = []  # host copies are no longer referenced by the device
         return self
 
-    def optimize(self, n_its: int, calib_value=None, calib_value_zero=None, nullspaces=None):
-        """FullSystem::optimize on the device (ldso_ba_optimize): n_its GN iterations of every
-        loaded window with no host round trip.  calib_value / calib_value_zero: [n_windows][4]
-        CalibHessian::value / value_zero (default: each window's calib / 50, i.e. no calibration
-        delta).  Returns (energies [n_its + 1][n_windows][3], frames, calib_value, idepths)."""
+    def optimize(self, n_its: int, calib_value=None, calib_value_zero=None, nullspaces=None, settings=None):
+        """FullSystem::optimize on the device (ldso_ba_optimize): up to n_its GN iterations of every
+        loaded window with no host round trip; each window leaves the loop on the reference's
+        exits (canbreak after setting_minOptIterations, or lost on a NaN solution).
+        calib_value / calib_value_zero: [n_windows][4] CalibHessian::value / value_zero (default:
+        each window's calib / 50, i.e. no calibration delta); settings: an L.OptSettings (None =
+        the reference's defaults).  Returns (energies [n_its + 1][n_windows][3], frames,
+        calib_value, idepths, iterations [n_windows], status [n_windows] (L.OPT_*))."""
         nw = len(self.windows)
         frames = np.ascontiguousarray(np.concatenate([np.ascontiguousarray(w.frames) for w in self.windows]))
         if calib_value is None:
@@ -65,10 +68,14 @@ class BAContext:
         fo = np.zeros_like(frames)
         co = np.zeros((nw, 4), np.float64)
         idep = np.zeros(sum(w.n_points for w in self.windows), np.float32)
-        L.check(self._lib.ldso_ba_optimize(self._h, int(n_its), frames.ctypes.data, L.ptr(calib_value, L.f64p),
+        its = np.zeros(nw, np.int32)
+        status = np.zeros(nw, np.int32)
+        sp = C.byref(settings) if settings is not None else None
+        L.check(self._lib.ldso_ba_optimize(self._h, int(n_its), sp, frames.ctypes.data, L.ptr(calib_value, L.f64p),
                                            L.ptr(cz, L.f64p), L.ptr(ns, L.f64p), L.ptr(e, L.f64p), fo.ctypes.data,
-                                           L.ptr(co, L.f64p), L.ptr(idep, L.f32p)))
-        return e, fo, co, self._split(idep, [w.n_points for w in self.windows])
+                                           L.ptr(co, L.f64p), L.ptr(idep, L.f32p), L.ptr(its, L.i32p),
+                                           L.ptr(status, L.i32p)))
+        return e, fo, co, self._split(idep, [w.n_points for w in self.windows]), its, status
 
     def comm_init(self, unique_id, rank: int, world: int):
         """Attach to an RCCL communicator (ldso_ba_comm_init); unique_id: 128 bytes from

@@ -465,7 +465,8 @@ bool EnergyFunctional::uploadFrameTerms() {
     for (int f = 0; f < N; f++) frameTH_[f] = frames[f]->frameEnergyTH;
     const bool same = fsUp_.size() == fs_.size() && thUp_ == frameTH_ &&
                       std::memcmp(fsUp_.data(), fs_.data(), fs_.size() * sizeof(ldso_ba_frame_state)) == 0 &&
-                      std::memcmp(calibUp_, calib_.value_scaledf, sizeof(calibUp_)) == 0;
+                      std::memcmp(calibUp_, calib_.value_scaledf, sizeof(calibUp_)) == 0 &&
+                      std::memcmp(cDeltaUp_, cDeltaF, sizeof(cDeltaUp_)) == 0;  // the bL calibration prior
     if (same && !dirty_) return true;
     precalc_.assign((size_t)N * N * LDSO_BA_PRECALC_STRIDE, 0.f);
     adH_.assign((size_t)N * N * 64, 0.0);
@@ -505,6 +506,7 @@ bool EnergyFunctional::uploadFrameTerms() {
     fsUp_ = fs_;
     thUp_ = frameTH_;
     std::memcpy(calibUp_, calib_.value_scaledf, sizeof(calibUp_));
+    std::memcpy(cDeltaUp_, cDeltaF, sizeof(cDeltaUp_));
     return true;
 }
 
@@ -731,7 +733,21 @@ double EnergyFunctional::linearizeResidual(PointFrameResidual &r) {
             return false;
         const PointHessian &p = *resPoint_[r.mirrorIdx];
         const float *sn = &cSnap_[4 * (size_t)r.mirrorIdx];
-        return sn[0] == p.u && sn[1] == p.v && sn[2] == p.idepth_scaled && sn[3] == p.idepth_zero_scaled;
+        if (!(sn[0] == p.u && sn[1] == p.v && sn[2] == p.idepth_scaled && sn[3] == p.idepth_zero_scaled)) return false;
+        // the frame terms the pass used: the residual's host and target as uploaded (state,
+        // evaluation point, exposure, threshold) and the calibration -- a direct edit of either
+        // without setDeltaF / setAdjointsF / linearizeAll in between is seen here
+        if (std::memcmp(calibUp_, calib_.value_scaledf, sizeof(calibUp_)) != 0) return false;
+        for (const auto &wf : {r.host, r.target}) {
+            const auto f = wf.lock();
+            if (!f) return false;
+            const size_t i = (size_t)f->idx;
+            if (i >= fsUp_.size() || i >= frames.size() || frames[i].get() != f.get()) return false;
+            ldso_ba_frame_state fsn;
+            frame_state(*f, fsn);
+            if (std::memcmp(&fsn, &fsUp_[i], sizeof(fsn)) != 0 || f->frameEnergyTH != thUp_[i]) return false;
+        }
+        return true;
     };
     if (!fresh() && (!runRelinearization() || !fresh())) return r.state_energy;
     const size_t k = (size_t)r.mirrorIdx;
@@ -746,9 +762,15 @@ double EnergyFunctional::linearizeResidual(PointFrameResidual &r) {
     return r.state_NewEnergy;
 }
 
-// FullSystem::optimize's loop (FullSystem.cc:853-970) on the device; see the header
-Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std::vector<Vec3> *energies) {
+// FullSystem::optimize's loop (FullSystem.cc:844-970) on the device; see the header
+Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std::vector<Vec3> *energies,
+                                bool *isLost, int *iterations, const ldso_ba_opt_settings *settings) {
     Vec3 out = {0, 0, 0};
+    if (isLost) *isLost = false;
+    if (iterations) *iterations = 0;
+    if (nFrames < 2) return out;   // FullSystem.cc:846-851
+    if (nFrames < 3) n_its = 20;
+    if (nFrames < 4) n_its = 15;
     epoch_++;
     calib_ = *HCalib;
     if (!upload()) return out;
@@ -761,12 +783,17 @@ Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std:
     std::vector<ldso_ba_frame_state> fo(N);
     std::vector<float> idepth(P);
     double calib_out[4];
-    if (ldso_ba_optimize(ctx_, n_its, fs_.data(), HCalib->value, HCalib->value_zero, ns.data(), e.data(), fo.data(),
-                         calib_out, idepth.data())) {
+    int32_t its = 0, status = 0;
+    if (ldso_ba_optimize(ctx_, n_its, settings, fs_.data(), HCalib->value, HCalib->value_zero, ns.data(), e.data(),
+                         fo.data(), calib_out, idepth.data(), &its, &status)) {
         fail("ldso_ba_optimize");
         return out;
     }
-    passes_ += n_its + 1;
+    // the loop's exits: lost (FullSystem.cc:907-911) after its iterations (the state is that of
+    // the step before), canbreak (:968-969); the passes the device ran: the first + one per step
+    passes_ += 1 + (status == LDSO_BA_OPT_LOST ? its - 1 : its);
+    if (isLost) *isLost = status == LDSO_BA_OPT_LOST;
+    if (iterations) *iterations = its;
     // doStepFromBackup's results (FullSystem.cc:1843-1922) into the objects: frame states, the
     // calibration, every point's setIdepth / setIdepthZero
     for (int f = 0; f < N; f++) std::memcpy(frames[f]->state, fo[f].state, sizeof(fo[f].state));

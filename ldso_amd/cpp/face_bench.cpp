@@ -3,9 +3,15 @@
 // the C ABI's ldso_ba_optimize on the same window in the same process.  Run by bench.py
 // (cpp_face); prints one JSON object.
 //
-//   optimize        EnergyFunctional::optimize(6): FullSystem::optimize's GN loop on the device
-//                   plus the face's write-back (frame states, calibration, point idepths,
-//                   setDeltaF), host clock per call
+//   optimize        EnergyFunctional::optimize(6) with the early exit off (th_opt_iterations = 0:
+//                   all 6 iterations, so per-iteration times compare across calls and with the C
+//                   ABI): FullSystem::optimize's GN loop on the device plus the face's write-back
+//                   (frame states, calibration, point idepths, setDeltaF), host clock per call;
+//                   iterations_default: what the reference's exits (canbreak) leave of the 6
+//   shim            INTEGRATION.md §3's reference-side forwarding around one FullSystem::optimize
+//                   (copy-in, optimize, copy-back, linearizeAll(true), residual / point copy-out)
+//                   on stand-ins for the reference's heap objects: the copy loops alone, through
+//                   std::unordered_map (as §3 writes it) and through index vectors
 //   optimize_full   the same + setAdjointsF + setDeltaF + linearizeAll(true) with the complete
 //                   residual / point write-back: everything FullSystem::optimize asks of the
 //                   backend after the frontend's setEvalPT
@@ -16,6 +22,8 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <random>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ldso_amd/energy_functional.h"
@@ -92,14 +100,21 @@ int main(int argc, char **argv) {
     ef->setAdjointsF(HCalib);
     ef->setDeltaF(HCalib);
 
-    // EnergyFunctional::optimize(6)
-    for (int i = 0; i < 2; i++) ef->optimize(n_its, HCalib);
+    // the reference's exits on the first call (the window as synthesised)
+    int its_default = 0;
+    {
+        bool lost = false;
+        ef->optimize(n_its, HCalib, nullptr, &lost, &its_default);
+    }
+    // EnergyFunctional::optimize(6), all iterations
+    ldso_ba_opt_settings all_its = {LDSO_BA_SOLVER_DEFAULT, 1, 1, 0.0f};
+    for (int i = 0; i < 2; i++) ef->optimize(n_its, HCalib, nullptr, nullptr, nullptr, &all_its);
     auto t0 = Clock::now();
-    for (int i = 0; i < reps; i++) ef->optimize(n_its, HCalib);
+    for (int i = 0; i < reps; i++) ef->optimize(n_its, HCalib, nullptr, nullptr, nullptr, &all_its);
     const double ms_opt = ms_since(t0) / reps;
     // + FullSystem::optimize's tail on the backend: setAdjointsF, setDeltaF, linearizeAll(true)
     auto full = [&] {
-        ef->optimize(n_its, HCalib);
+        ef->optimize(n_its, HCalib, nullptr, nullptr, nullptr, &all_its);
         ef->setAdjointsF(HCalib);
         ef->setDeltaF(HCalib);
         ef->linearizeAll(true);
@@ -121,6 +136,102 @@ int main(int argc, char **argv) {
         }
     const double ms_flag = ms_since(t0);
     const long flag_passes = ef->devicePasses() - passes0;
+
+    // INTEGRATION.md §3's forwarding shim, timed: stand-ins for the reference's objects, each its
+    // own heap allocation in the reference's creation order (frames, then per point the point and
+    // its residuals), mapped to the face's objects either by std::unordered_map keyed by the
+    // reference pointer (mf / mp / mr, as §3 writes it) or by index vectors filled in the same
+    // order (the replacement)
+    struct RefFrame {
+        double state[10], state_zero[10], ab_exposure;
+        float frameEnergyTH;
+        char other[512];  // the rest of a FrameHessian
+    };
+    struct RefPoint {
+        float idepth, idepth_zero, HdiF, bdSumF, idepth_hessian, step;
+        char other[160];
+    };
+    struct RefResidual {
+        int state_state, state_NewState;
+        double state_energy, state_NewEnergy, state_NewEnergyWithOutlier;
+        float centerProjectedTo[3], JpJdF[8];
+        bool isActiveAndIsGoodNEW;
+        char other[96];
+    };
+    std::vector<std::unique_ptr<RefFrame>> rframes;
+    std::vector<std::unique_ptr<RefPoint>> rpoints;
+    std::vector<std::unique_ptr<RefResidual>> rres;
+    std::unordered_map<RefFrame *, FrameHessian *> mf;
+    std::unordered_map<RefPoint *, PointHessian *> mp;
+    std::unordered_map<RefResidual *, PointFrameResidual *> mr;
+    std::vector<std::pair<RefFrame *, FrameHessian *>> vf;
+    std::vector<std::pair<RefPoint *, PointHessian *>> vp;
+    std::vector<std::pair<RefResidual *, PointFrameResidual *>> vr;
+    for (auto &F : ef->frames) {
+        rframes.emplace_back(new RefFrame());
+        mf[rframes.back().get()] = F.get();
+        vf.emplace_back(rframes.back().get(), F.get());
+    }
+    for (auto &Pt : ef->allPoints) {
+        rpoints.emplace_back(new RefPoint());
+        mp[rpoints.back().get()] = Pt.get();
+        vp.emplace_back(rpoints.back().get(), Pt.get());
+        for (auto &r : Pt->residuals) {
+            rres.emplace_back(new RefResidual());
+            mr[rres.back().get()] = r.get();
+            vr.emplace_back(rres.back().get(), r.get());
+        }
+    }
+    // the copy loops of one FullSystem::optimize through the shim (§3: "replaces
+    // FullSystem.cc:853-970" and FullSystem::linearizeAll), without the face calls themselves
+    auto shim_loops = [&](auto &F, auto &Pm, auto &Rm) {
+        for (auto &kv : F) std::memcpy(kv.second->state, kv.first->state, sizeof(kv.first->state));  // copyIn
+        for (auto &kv : Pm) {
+            kv.second->setIdepth(kv.first->idepth);
+            kv.second->setIdepthZero(kv.first->idepth_zero);
+        }
+        // ... gpu->optimize(...) ...
+        for (auto &kv : F) std::memcpy(kv.first->state, kv.second->state, sizeof(kv.first->state));
+        for (auto &kv : Pm) {
+            kv.first->idepth = kv.second->idepth;
+            kv.first->idepth_zero = kv.second->idepth_zero;
+        }
+        // FullSystem::linearizeAll(true): copy-in, gpu->linearizeAll, copy-out
+        for (auto &kv : F) std::memcpy(kv.second->state, kv.first->state, sizeof(kv.first->state));
+        for (auto &kv : Pm) kv.second->setIdepth(kv.first->idepth);
+        for (auto &kv : Rm) {
+            RefResidual &r = *kv.first;
+            const PointFrameResidual &g = *kv.second;
+            r.state_state = (int)g.state_state;
+            r.state_NewState = (int)g.state_NewState;
+            r.state_energy = g.state_energy;
+            r.state_NewEnergy = g.state_NewEnergy;
+            r.state_NewEnergyWithOutlier = g.state_NewEnergyWithOutlier;
+            std::memcpy(r.centerProjectedTo, g.centerProjectedTo, sizeof(r.centerProjectedTo));
+            r.isActiveAndIsGoodNEW = g.isActiveAndIsGoodNEW;
+            std::memcpy(r.JpJdF, g.JpJdF, sizeof(r.JpJdF));
+        }
+        for (auto &kv : Pm) {
+            kv.first->HdiF = kv.second->HdiF;
+            kv.first->bdSumF = kv.second->bdSumF;
+            kv.first->idepth_hessian = kv.second->idepth_hessian;
+        }
+    };
+    ef->syncResiduals();
+    auto time_shim = [&](auto &F, auto &Pm, auto &Rm) {
+        // between calls the frontend touches other memory (tracking, images): evict the caches
+        std::vector<char> evict((size_t)64 << 20, 1);
+        double tot = 0;
+        for (int i = 0; i < reps; i++) {
+            for (size_t k = 0; k < evict.size(); k += 64) evict[k]++;
+            auto t1 = Clock::now();
+            shim_loops(F, Pm, Rm);
+            tot += ms_since(t1);
+        }
+        return tot / reps;
+    };
+    const double ms_shim_map = time_shim(mf, mp, mr);
+    const double ms_shim_vec = time_shim(vf, vp, vr);
     const bool ok = ef->ok();
 
     // the C ABI alone on a context of the same window
@@ -164,21 +275,29 @@ int main(int argc, char **argv) {
         for (int k = 0; k < 4; k++) cv[k] = HCalib->value_zero[k];
         ldso_ba_nullspaces(N, fs.data(), ns.data());
         for (int i = 0; i < 2; i++)
-            ldso_ba_optimize(raw, n_its, fs.data(), cv.data(), cv.data(), ns.data(), e.data(), fo.data(), co.data(), id.data());
+            ldso_ba_optimize(raw, n_its, &all_its, fs.data(), cv.data(), cv.data(), ns.data(), e.data(), fo.data(),
+                             co.data(), id.data(), nullptr, nullptr);
         t0 = Clock::now();
         for (int i = 0; i < reps; i++)
-            ldso_ba_optimize(raw, n_its, fs.data(), cv.data(), cv.data(), ns.data(), e.data(), fo.data(), co.data(), id.data());
+            ldso_ba_optimize(raw, n_its, &all_its, fs.data(), cv.data(), cv.data(), ns.data(), e.data(), fo.data(),
+                             co.data(), id.data(), nullptr, nullptr);
         ms_raw = ms_since(t0) / reps;
         ldso_ba_destroy(raw);
     }
     std::printf(
         "{\"window\": \"S7 (7 KF, 2000 pts, 640x480, seed 1)\", \"n_its\": %d, \"reps\": %d, \"ok\": %s, "
-        "\"optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f}, "
+        "\"optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f, \"iterations\": %d, "
+        "\"iterations_default\": %d}, "
+        "\"shim\": {\"what\": \"INTEGRATION.md 3 copy loops of one FullSystem::optimize, %d residuals, %d points, "
+        "caches evicted between calls\", \"unordered_map_ms\": %.6f, \"index_vector_ms\": %.6f, "
+        "\"shim_ms_per_gn_iteration\": %.6f, \"unordered_map_ms_per_gn_iteration\": %.6f, "
+        "\"frac_of_face_gn_iteration\": %.4f, \"unordered_map_frac_of_face_gn_iteration\": %.4f}, "
         "\"optimize_full\": {\"ms\": %.6f, \"what\": \"optimize(6) + setAdjointsF + setDeltaF + linearizeAll(true) "
         "with the residual / point write-back\"}, "
         "\"c_abi_optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f}, "
         "\"flag_loop\": {\"residuals\": %d, \"ms\": %.6f, \"device_passes\": %ld}}\n",
-        n_its, reps, ok ? "true" : "false", ms_opt, ms_opt / n_its, ms_full, ms_raw, ms_raw / n_its, nres, ms_flag,
-        flag_passes);
+        n_its, reps, ok ? "true" : "false", ms_opt, ms_opt / n_its, n_its, its_default, (int)vr.size(), (int)vp.size(),
+        ms_shim_map, ms_shim_vec, ms_shim_vec / n_its, ms_shim_map / n_its, ms_shim_vec / ms_opt, ms_shim_map / ms_opt,
+        ms_full, ms_raw, ms_raw / n_its, nres, ms_flag, flag_passes);
     return ok ? 0 : 1;
 }

@@ -148,6 +148,8 @@ struct LinParams {
     int fix;
     int accumulate;
     const float *ad_ht_delta;  // [pair_global][8] EnergyFunctional::adHTdeltaF (marginalisation pass)
+    const int *stop;           // ldso_ba_optimize: [win] first pass index a window skips - 1 (see opt_pass)
+    int pass;                  // ldso_ba_optimize: this pass's index (0 = the initial linearizeAll)
 };
 
 struct Geo {
@@ -814,6 +816,7 @@ __global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParam
     if (lblock * 4 + wave >= P.n_items) return;
     const int itemL = P.item_base + lblock * 4 + wave;  // global chunk index
     const int4 it = P.items[itemL];                     // {res_begin, count, pair_global, win}
+    if (P.stop && P.pass > P.stop[__builtin_amdgcn_readfirstlane(it.w)]) return;  // window left the GN loop
     const bool valid = lane < it.y;
     const int pair = __builtin_amdgcn_readfirstlane(it.z), jlimit = __builtin_amdgcn_readfirstlane(it.y);
     const WinDev &W = P.wins[__builtin_amdgcn_readfirstlane(it.w)];
@@ -1143,6 +1146,8 @@ struct PointParams {
     int n_items;
     int item_base;
     int shift_prior;  // AccumulatedSCHessianSSE::addPoint's shiftPriorToZero (false when marginalising)
+    const int *stop;  // ldso_ba_optimize (LinParams::stop)
+    int pass;
 };
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
@@ -1150,6 +1155,7 @@ constexpr int kScBatch = 2;  // residual records per round trip (4 and 8 measure
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int item = P.item_base + blockIdx.x;
     const int4 it = P.items[item];
+    if (P.stop && P.pass > P.stop[it.w]) return;  // window left the GN loop
     const WinDev &W = P.wins[it.w];
     const int host = it.z, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
     const int Kj = 8 * (W.N - 1);
@@ -1271,8 +1277,11 @@ struct StitchParams {
     double *sys;
     double *stage;  // k_stitch -> k_stitch_sum contribution records (WinDev::stage_base)
     double *win_energy;
-    double *ehist;         // non-null (ldso_ba_optimize): also win_energy into slot *eslot of the history
-    const int *eslot;      // (k_frame_step advances it once per GN iteration)
+    double *ehist;         // non-null (ldso_ba_optimize): also win_energy into row `pass` of the history
+    const int *stop;       // ldso_ba_optimize (LinParams::stop): host / pair blocks of stopped windows skip
+    int pass;
+    const float *pt_data;  // with win_nid: doStepFromBackup's sumNID / numID of every window
+    float *win_nid;
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
     int pair_base;  // first global pair of this launch
@@ -1434,10 +1443,35 @@ __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &
         P.win_energy[2 * w] = e;
         P.win_energy[2 * w + 1] = nin;
         if (P.ehist) {  // the optimize() energy history, without a launch of its own
-            double *hs = P.ehist + (size_t)(*P.eslot) * 2 * P.n_win;
+            double *hs = P.ehist + (size_t)P.pass * 2 * P.n_win;
             hs[2 * w] = e;
             hs[2 * w + 1] = nin;
         }
+    }
+}
+
+// doStepFromBackup's sumNID and numID (FullSystem.cc:1899-1909) for the step that follows this pass:
+// the float sum of fabsf(idepth_backup) over the window's points in frames -> features order (host
+// frames in window order, each host's points in the caller's order: the device point order), i.e.
+// over the idepths this pass linearised at.  One wavefront; 64 idepths per load, added lane by
+// lane (readlane) so the sum rounds exactly as the reference's sequential loop.  With sharded
+// points each rank sums its own run; the exchange adds the ranks' partials.
+__device__ void window_nid(const StitchParams &P, const WinDev &W, int w) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x, n = W.P;
+    const float *pd = P.pt_data + (size_t)W.point_base * LDSO_BA_POINT_STRIDE + 2;
+    auto load = [&](int q0) { return q0 + lane < n ? fabsf(pd[(size_t)(q0 + lane) * LDSO_BA_POINT_STRIDE]) : 0.0f; };
+    float s = 0.0f, v = load(0);
+    for (int q0 = 0; q0 < n; q0 += 64) {
+        const float nv = load(q0 + 64);  // the next round's loads in flight during this round's adds
+#pragma unroll
+        for (int l = 0; l < 64; l++)  // padding lanes add +0: s is unchanged
+            s += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+        v = nv;
+    }
+    if (lane == 0) {
+        P.win_nid[2 * w] = s;
+        P.win_nid[2 * w + 1] = (float)n;  // numID++ per point: exact below 2^24
     }
 }
 
@@ -1482,10 +1516,12 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     if ((int)blockIdx.x < P.n_win) {  // the longest single-block chain goes first in the grid
         const int w = P.win_base + blockIdx.x;
         frame_threshold_and_energy<kStThreads>(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
+        if (P.win_nid) window_nid(P, P.wins[w], w);
         return;
     }
     const int pair = P.pair_base + blockIdx.x - P.n_win;
     const int w = P.pair_win[pair];
+    if (P.stop && P.pass > P.stop[w]) return;  // window left the GN loop: its records stay as they are
     const WinDev &W = P.wins[w];
     const int N = W.N, D = W.D, aidx = pair - W.pair_base, h = aidx % N, t = aidx / N;
     const int tid = threadIdx.x;
@@ -1893,6 +1929,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
     if ((int)blockIdx.x < P.n_win) {  // setNewFrameEnergyTH + the energy sum, as k_stitch
         const int w = P.win_base + blockIdx.x;
         frame_threshold_and_energy<kHsThreads>(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
+        if (P.win_nid) window_nid(P, P.wins[w], w);
         return;
     }
     if (!P.accumulate) return;
@@ -1902,6 +1939,7 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
     const int fr = P.frame_base + (P.hs_split ? hb >> 1 : hb);
     const bool do_top = !P.hs_split || (hb & 1) == 0, do_sc = !P.hs_split || (hb & 1) == 1;
     const int w = P.frame_win[fr];
+    if (P.stop && P.pass > P.stop[w]) return;  // window left the GN loop: its partials stay as they are
     const WinDev &W = P.wins[w];
     const int N = W.N, D = W.D, i = fr - W.frame_base, tid = threadIdx.x;
     const int Kc = 8 * (N - 1), K5 = Kc + 5, ldg = hs_ldg(N), nt = W.KP / 4, per = W.ntiles * 16;
@@ -2306,6 +2344,7 @@ struct SolveParams {
     float *xad;                        // xAd from the solution (k_xad fused)
     const double *prep_nm, *prep_g;    // k_ortho_prep's results: Nm [vec][n_null], per window G | G^-1 | fast
     int iteration, n_null;
+    int *stop, *status;  // ldso_ba_optimize: windows with iteration >= stop skip; a NaN x marks the window lost
 };
 constexpr int kPrepGStride = 192;  // doubles per window in prep_g: G [49], G^-1 [49], fast flag, V [49], ev [7], keep [7]
 // H's row stride in LDS: odd (in doubles), so a column walk touches 32 distinct bank pairs
@@ -2674,7 +2713,17 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
         }
         wave_lds_sync();
     }
-    for (int i = lane; i < n; i += 64) P.x[W.vec_base + i] = y[i];
+    bool nan = false;
+    for (int i = lane; i < n; i += 64) {
+        P.x[W.vec_base + i] = y[i];
+        nan |= isnan(y[i]);
+    }
+    // FullSystem::optimize (FullSystem.cc:907-911): isnan(lastX.norm()) -- a NaN element (inf
+    // elements give an inf norm, not NaN) -- is isLost: no step in this iteration, the loop ends
+    if (P.stop && __any(nan) && lane == 0) {
+        P.stop[blockIdx.x] = P.iteration;
+        P.status[blockIdx.x] = LDSO_BA_OPT_LOST;
+    }
 }
 
 // The trailing update of step k is A(i,j) = fma(-(c_i c_j), 1/d, A(i,j)) with c = column k and
@@ -2683,6 +2732,7 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
 __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveParams P) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
+    if (P.stop && P.iteration >= P.stop[blockIdx.x]) return;  // the window left the GN loop
     const WinDev W = P.wins[blockIdx.x];  // a register copy: the helpers would re-read global memory after every LDS store
     const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ld = solve_ld(n);
@@ -3020,6 +3070,7 @@ __device__ __forceinline__ void solve_reg_factor(const RegLds &R, const SolveLds
 __global__ __launch_bounds__(kSolveRegThreads) void k_solve_reg(SolveParams P) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
+    if (P.stop && P.iteration >= P.stop[blockIdx.x]) return;  // the window left the GN loop
     const WinDev W = P.wins[blockIdx.x];  // a register copy (see k_solve)
     const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ld = solve_ld(n);
@@ -3226,6 +3277,7 @@ __device__ __forceinline__ double fast_update(const double *Wp, const double *rp
 __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
+    if (P.stop && P.iteration >= P.stop[blockIdx.x]) return;  // the window left the GN loop
     const WinDev W = P.wins[blockIdx.x];  // a register copy (see k_solve)
     const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ld = solve_ld(n);
@@ -3334,6 +3386,8 @@ struct ResubParams {
     float *pt_data;  // non-null: apply doStepFromBackup's point step in place (ldso_ba_optimize)
     int begin, count;
     float lambda;
+    const int *stop;  // ldso_ba_optimize: points of windows with it >= stop[w] skip
+    int it;
 };
 
 // xAd from the device solution (windows solved by k_solve, or x set otherwise)
@@ -3573,6 +3627,7 @@ __device__ __forceinline__ void resubstitute_one(const ResubParams &P, int k) {
 #pragma clang fp contract(off)
     if (k >= P.count) return;
     const int p = P.begin + k;
+    if (P.stop && P.it >= P.stop[P.pt_win[p]]) return;
     const float *po = P.pt_out + (size_t)p * 12;
     // doStepFromBackup's point step (setIdepth / setIdepthZero / setDeltaF)
     auto apply = [&](float step) {
@@ -3644,16 +3699,26 @@ struct FrameStepParams {
     const double *x;              // [vec]
     float *precalc;               // [pairs][LDSO_BA_PRECALC_STRIDE]
     double *prior;                // [vec][2]: HL diagonal, bL
-    int *eslot;                   // non-null: the energy-history slot the next pass writes, advanced here
+    // ldso_ba_optimize's loop exits (FullSystem.cc:922, 968-969): windows with it >= stop[w] skip;
+    // canbreak at it >= min_its sets stop[w] = it + 1 (the pass after this step still runs)
+    int *stop, *status;
+    const float *win_nid;  // [win][2]: sumNID, numID of the idepths the step starts from (window_nid)
+    int it, min_its;
+    float th;  // setting_thOptIterations
 };
 // one window's step: a whole 256-thread block (blk = the window)
 __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int blk) {
     __shared__ double poses[LDSO_BA_MAX_FRAMES][4][12];  // ev, ev^-1, cur, cur^-1: R (9), t (3)
     __shared__ float calib[4];
+    if (P.stop && P.it >= P.stop[blk]) return;  // lost in this iteration's solve, or stopped earlier
     WinDev &W = P.wins[blk];
     const int N = W.N, tid = threadIdx.x;
     const double *xw = P.x + W.vec_base;
-    if (P.eslot && blk == 0 && tid == 0) *P.eslot += 1;
+    if (P.stop && tid == 128 && P.it >= P.min_its &&
+        step_canbreak(N, xw, P.win_nid[2 * blk], P.win_nid[2 * blk + 1], P.th)) {
+        P.stop[blk] = P.it + 1;
+        P.status[blk] = LDSO_BA_OPT_CONVERGED;
+    }
     ldso_ba_frame_state *fs = P.fstate + W.frame_base;
     if (tid < N) {
         ldso_ba_frame_state o;
@@ -3702,7 +3767,6 @@ __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int b
         }
     }
 }
-__global__ __launch_bounds__(256) void k_frame_step(FrameStepParams P) { frame_step_block(P, blockIdx.x); }
 // ldso_ba_optimize: the frame / calibration step (blocks [0, n_win)) and the resubstitution with
 // the point step (the rest) in one launch; both read only x and xAd, which the solve wrote
 __global__ __launch_bounds__(256) void k_step_resub(FrameStepParams F, ResubParams R, int n_win) {
@@ -3710,9 +3774,8 @@ __global__ __launch_bounds__(256) void k_step_resub(FrameStepParams F, ResubPara
     else resubstitute_one(R, ((int)blockIdx.x - n_win) * 256 + threadIdx.x);
 }
 // ldso_ba_optimize's energy history with a communicator (the window blocks of k_stitch write it
-// otherwise): slot *slot <- the all-reduced energies
-__global__ __launch_bounds__(256) void k_energy_to_history(const double *src, double *hist, const int *slot, int n2) {
-    const int s = *slot;
+// otherwise): row s <- the all-reduced energies
+__global__ __launch_bounds__(256) void k_energy_to_history(const double *src, double *hist, int s, int n2) {
     for (int i = threadIdx.x; i < n2; i += 256) hist[(size_t)s * n2 + i] = src[i];
 }
 // ldso_ba_update_points: [P][4] (idepth_scaled, idepth_zero_scaled, priorF, deltaF) of one window in
@@ -3864,7 +3927,11 @@ struct PendingEv {
 struct ldso_ba_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    bool opt_hist = false;  // inside ldso_ba_optimize: passes also write the energy history
+    // inside ldso_ba_optimize: the index of the pass being issued (0 = the initial linearizeAll,
+    // k = the pass after step k-1), else -1.  Passes then write row opt_pass of the energy history,
+    // the window blocks sumNID / numID, and every launch honours the per-window loop exits (d_stop)
+    int opt_pass = -1;
+    int opt_it = 0;
     // captured launch sequences: ldso_ba_optimize's GN iterations [projection][last pass][ns given]
     // and ldso_ba_iterate's pass + solve + resubstitution [projection]
     struct Graph {
@@ -3909,7 +3976,8 @@ struct ldso_ba_ctx {
     // prior switches per window, the energy history
     DevBuf<ldso_ba_frame_state> d_fstate;
     DevBuf<double> d_calib_val, d_calib_zero, d_cprior, d_ehist;
-    DevBuf<int> d_eslot;
+    DevBuf<int> d_stop, d_status;  // ldso_ba_optimize: per window, see FrameStepParams
+    DevBuf<float> d_win_nid;       // [win][2] sumNID, numID of the last pass (window_nid)
     DevBuf<int> d_add_priors;
     DevBuf<float> d_xad;            // [win][kXadStride]
     DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
@@ -4205,7 +4273,7 @@ int upload_priors(ldso_ba_ctx *c, int win) {
 }
 
 ResubParams resub_params(ldso_ba_ctx *c, int begin, int count, double lambda, bool apply_step) {
-    ResubParams R;
+    ResubParams R{};
     R.pt_data = apply_step ? c->d_pt_data.p : nullptr;
     R.xad = c->d_xad.p;
     R.wins = c->d_wins.p;
@@ -4469,7 +4537,9 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_calib_zero.release();
     c->d_cprior.release();
     c->d_ehist.release();
-    c->d_eslot.release();
+    c->d_stop.release();
+    c->d_status.release();
+    c->d_win_nid.release();
     c->d_add_priors.release();
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->d_xad.release();
@@ -5036,6 +5106,8 @@ int comm_exchange(ldso_ba_ctx *c, bool accumulate) {
     if (accumulate) NCCL_TRY(ncclAllReduce(c->d_sys.p, c->d_sys.p, c->d_sys.n, ncclFloat64, ncclSum, c->comm, st));
     NCCL_TRY(ncclAllReduce(c->d_win_energy.p, c->d_win_energy.p, (size_t)2 * c->n_win, ncclFloat64, ncclSum, c->comm,
                            st));
+    if (c->opt_pass >= 0)  // optimize(): doStepFromBackup's sumNID / numID over every rank's points
+        NCCL_TRY(ncclAllReduce(c->d_win_nid.p, c->d_win_nid.p, (size_t)2 * c->n_win, ncclFloat32, ncclSum, c->comm, st));
     const long long stride = c->x_stride;
     const dim3 grid((unsigned)std::min<long long>((stride + 255) / 256, 64), (unsigned)c->n_win);
     k_export_newest<<<grid, 256, 0, st>>>(c->d_wins.p, c->d_rs_energy_wo.p, c->d_x_local.p, stride);
@@ -5079,7 +5151,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     c->energy_valid = false;
     c->th_host_valid = false;
     int rc;
-    LinParams L;
+    LinParams L{};
     L.items = c->d_top_items.p;
     L.wins = c->d_wins.p;
     L.img = c->img_ext ? c->img_ext : c->d_img.p;
@@ -5106,7 +5178,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     L.item_base = 0;
     L.n_items = c->n_top_items;
     L.n_blocks = (L.n_items + 3) / 4;
-    PointParams Pp;
+    PointParams Pp{};
     Pp.items = c->d_sc_items.p;
     Pp.wins = c->d_wins.p;
     Pp.pt_data = c->d_pt_data.p;
@@ -5118,7 +5190,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.shift_prior = c->marg ? 0 : 1;
     Pp.item_base = 0;
     Pp.n_items = c->n_sc_items;
-    StitchParams Sp;
+    StitchParams Sp{};
     Sp.wins = c->d_wins.p;
     Sp.pair_win = c->d_pair_win.p;
     Sp.e_wo = c->d_rs_energy_wo.p;
@@ -5133,8 +5205,16 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.sys = c->d_sys.p;
     Sp.stage = c->d_stage.p;
     Sp.win_energy = c->d_win_energy.p;
-    Sp.ehist = c->opt_hist && !c->comm ? c->d_ehist.p : nullptr;  // with RCCL: after the exchange
-    Sp.eslot = c->d_eslot.p;
+    const bool in_opt = c->opt_pass >= 0;
+    Sp.ehist = in_opt && !c->comm ? c->d_ehist.p : nullptr;  // with RCCL: after the exchange
+    Sp.pass = c->opt_pass;
+    Sp.stop = in_opt ? c->d_stop.p : nullptr;
+    Sp.pt_data = c->d_pt_data.p;
+    Sp.win_nid = in_opt ? c->d_win_nid.p : nullptr;
+    L.stop = Sp.stop;
+    L.pass = c->opt_pass;
+    Pp.stop = Sp.stop;
+    Pp.pass = c->opt_pass;
     Sp.accumulate = accumulate;
     Sp.pair_base = 0;
     Sp.win_base = 0;
@@ -5186,8 +5266,8 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     }
     if (rc || !c->comm) return rc;
     rc = comm_exchange(c, accumulate != 0);
-    if (!rc && c->opt_hist) {  // the reduced energies into the optimize() history
-        k_energy_to_history<<<1, 256, 0, st>>>(c->d_win_energy.p, c->d_ehist.p, c->d_eslot.p, 2 * c->n_win);
+    if (!rc && in_opt) {  // the reduced energies into the optimize() history
+        k_energy_to_history<<<1, 256, 0, st>>>(c->d_win_energy.p, c->d_ehist.p, c->opt_pass, 2 * c->n_win);
         HIP_TRY(hipGetLastError());
     }
     return rc;
@@ -5196,11 +5276,14 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
 int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, float *new_energy,
                                 float *new_energy_wo, float *center, uint8_t *center_ok, float *jpjdf) {
     if (!c || win < 0 || win >= c->n_win) return fail(-1, "bad arguments");
-    HIP_TRY(hipSetDevice(c->device));
+    if (c->marg) return fail(-1, "not on a marginalisation context");
     const WinDev &D = c->wd[win];
     const WinHost &H = c->wh[win];
+    // every caller slot is written: a sharded window holds only its run of the residuals
+    if (H.R_all != D.R) return fail(-1, "ldso_ba_linearize_residuals: the window is sharded (single-shard only)");
+    HIP_TRY(hipSetDevice(c->device));
     const size_t R = (size_t)D.R;
-    if (R == 0 || D.n_top_items == 0) return 0;
+    if (R == 0 || D.n_top_items == 0) return 0;  // no residuals: nothing to write
     int rc;
     const size_t Rt = (size_t)c->R_tot, slots = c->d_pt_rec.n;
     if ((rc = c->d_sx_state.ensure(Rt)) || (rc = c->d_sx_newstate.ensure(Rt)) || (rc = c->d_sx_flags.ensure(Rt)) ||
@@ -5218,7 +5301,7 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
             c->d_sx_center.p + b, c->d_sx_flags.p + b, c->d_rs_flags.p + b);
         HIP_TRY(hipGetLastError());
     }
-    LinParams L;
+    LinParams L{};
     L.items = c->d_top_items.p;
     L.wins = c->d_wins.p;
     L.img = c->img_ext ? c->img_ext : c->d_img.p;
@@ -5613,7 +5696,7 @@ int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
     int dmax = 0;
     for (const WinDev &D : c->wd) dmax = std::max(dmax, D.D);
     if (dmax > kSolveMaxDim) return fail(-1, "device solve supports windows of up to 11 keyframes");
-    SolveParams S;
+    SolveParams S{};
     S.wins = c->d_wins.p;
     S.sys = c->d_sys.p;
     S.prior = c->d_prior.p;
@@ -5626,6 +5709,10 @@ int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
     S.prep_g = c->d_ns_g.p;
     S.iteration = iteration;
     S.n_null = iteration >= 2 ? n_null : 0;
+    if (c->opt_pass >= 0) {  // inside ldso_ba_optimize: the per-window loop exits
+        S.stop = c->d_stop.p;
+        S.status = c->d_status.p;
+    }
     static std::once_flag once;
     std::call_once(once, [] {
         (void)hipFuncSetAttribute((const void *)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -5776,7 +5863,12 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
     if (!c->comm && !c->timing && getenv_flag("LDSO_BA_ITERATE_GRAPH") && !getenv_flag("LDSO_BA_NO_GRAPH")) {
         unsigned long long lb;
         std::memcpy(&lb, &lambda, sizeof(lb));
-        rc = launch_cached_graph(c, c->it_graph[project ? 1 : 0], lb ^ ((unsigned long long)n_null << 56), body);
+        // keyed by everything fixed at capture: lambda, n_null, the solve kernel, the stitch split
+        const char *hs = std::getenv("LDSO_BA_HS_SPLIT");
+        const unsigned long long mode = (c->solve_exact ? 1ull : 0ull) | (getenv_flag("LDSO_BA_SOLVE_LDS") ? 2ull : 0ull) |
+                                        (hs ? (hs[0] == '1' ? 4ull : 8ull) : 0ull);
+        rc = launch_cached_graph(c, c->it_graph[project ? 1 : 0],
+                                 lb ^ ((unsigned long long)n_null << 56) ^ (mode << 60), body);
     } else {
         rc = body();
     }
@@ -5823,20 +5915,58 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
     return 0;
 }
 
-int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *frames, const double *calib_value,
-                     const double *calib_value_zero, const double *ns, double *energy_out,
-                     ldso_ba_frame_state *frames_out, double *calib_out, float *idepth_out) {
+int ldso_ba_check_settings(const ldso_ba_opt_settings *s) {
+    if (!s) return 0;
+    static const struct {
+        int bit;
+        const char *name, *where;
+    } kUnsupported[] = {
+        {LDSO_BA_SOLVER_SVD, "SOLVER_SVD", "EnergyFunctional.cc:383-411"},
+        {LDSO_BA_SOLVER_ORTHOGONALIZE_SYSTEM, "SOLVER_ORTHOGONALIZE_SYSTEM", "EnergyFunctional.cc:325"},
+        {LDSO_BA_SOLVER_ORTHOGONALIZE_POINTMARG, "SOLVER_ORTHOGONALIZE_POINTMARG", "EnergyFunctional.cc:245"},
+        {LDSO_BA_SOLVER_ORTHOGONALIZE_FULL, "SOLVER_ORTHOGONALIZE_FULL", "EnergyFunctional.cc:257"},
+        {LDSO_BA_SOLVER_SVD_CUT7, "SOLVER_SVD_CUT7", "EnergyFunctional.cc:404"},
+        {LDSO_BA_SOLVER_REMOVE_POSEPRIOR, "SOLVER_REMOVE_POSEPRIOR", "FrameHessian.h:147"},
+        {LDSO_BA_SOLVER_USE_GN, "SOLVER_USE_GN", "EnergyFunctional.cc:282"},
+        {LDSO_BA_SOLVER_ORTHOGONALIZE_X, "SOLVER_ORTHOGONALIZE_X", "EnergyFunctional.cc:428"},
+        {LDSO_BA_SOLVER_MOMENTUM, "SOLVER_MOMENTUM", "FullSystem.cc:1840-1867"},
+        {LDSO_BA_SOLVER_STEPMOMENTUM, "SOLVER_STEPMOMENTUM", "FullSystem.cc:913-920"},
+    };
+    for (const auto &u : kUnsupported)
+        if (s->solver_mode & u.bit)
+            return fail(-1, std::string("setting_solverMode: ") + u.name + " (" + u.where + ") is not implemented");
+    if (s->solver_mode & ~(LDSO_BA_SOLVER_DEFAULT | 0xFFF))
+        return fail(-1, "setting_solverMode: unknown bits");
+    if (!(s->solver_mode & LDSO_BA_SOLVER_FIX_LAMBDA))
+        return fail(-1, "setting_solverMode without SOLVER_FIX_LAMBDA (the LM lambda, EnergyFunctional.cc:283) is not "
+                        "implemented");
+    if (!s->force_accept_step)
+        return fail(-1, "setting_forceAceptStep = false (the accept / reject branch with loadStateBackup, "
+                        "FullSystem.cc:935-966) is not implemented");
+    if (s->min_opt_iterations < 0) return fail(-1, "setting_minOptIterations < 0");
+    return 0;
+}
+
+int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *settings,
+                     const ldso_ba_frame_state *frames, const double *calib_value, const double *calib_value_zero,
+                     const double *ns, double *energy_out, ldso_ba_frame_state *frames_out, double *calib_out,
+                     float *idepth_out, int32_t *iterations_out, int32_t *status_out) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
     if (n_its < 0 || !frames || !calib_value || !calib_value_zero) return fail(-1, "bad arguments");
     if (c->marg) return fail(-1, "not on a marginalisation context");
+    int rc;
+    if ((rc = ldso_ba_check_settings(settings))) return rc;
+    const ldso_ba_opt_settings st = settings ? *settings
+                                             : ldso_ba_opt_settings{LDSO_BA_SOLVER_DEFAULT, 1, 1, 1.2f};
+    // without SOLVER_ORTHOGONALIZE_X_LATER the solve never projects (EnergyFunctional.cc:428-432)
+    if (!(st.solver_mode & LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER)) ns = nullptr;
     HIP_TRY(hipSetDevice(c->device));
     const int nw = c->n_win;
-    int rc;
     // ensure(): the buffers keep their addresses across calls, so cached graphs stay valid
     if ((rc = c->d_fstate.ensure(c->n_frames)) || (rc = c->d_calib_val.ensure((size_t)4 * nw)) ||
         (rc = c->d_calib_zero.ensure((size_t)4 * nw)) || (rc = c->d_cprior.ensure((size_t)4 * nw)) ||
         (rc = c->d_add_priors.ensure(nw)) || (rc = c->d_ehist.ensure((size_t)2 * nw * (n_its + 1))) ||
-        (rc = c->d_eslot.ensure(1)))
+        (rc = c->d_stop.ensure(nw)) || (rc = c->d_status.ensure(nw)) || (rc = c->d_win_nid.ensure((size_t)2 * nw)))
         return rc;
     std::vector<double> cp((size_t)4 * nw);
     std::vector<int> ap(nw);
@@ -5855,7 +5985,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     }
     if (ns && (rc = upload_nullspaces(c, ns, 7)))  // evalPT is fixed during optimize(): valid for every iteration
         return rc;
-    FrameStepParams F;
+    FrameStepParams F{};
     F.wins = c->d_wins.p;
     F.fstate = c->d_fstate.p;
     F.calib_val = c->d_calib_val.p;
@@ -5865,20 +5995,29 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     F.x = c->d_x.p;
     F.precalc = c->d_precalc.p;
     F.prior = c->d_prior.p;
-    F.eslot = c->d_eslot.p;
-    HIP_TRY(hipMemsetAsync(c->d_eslot.p, 0, sizeof(int), c->stream));
-    // one GN iteration: solveSystemF, resubstituteF_MT, doStepFromBackup + setPrecalcValues,
-    // linearizeAll + applyRes (+ the accumulation the next solve uses)
+    F.stop = c->d_stop.p;
+    F.status = c->d_status.p;
+    F.win_nid = c->d_win_nid.p;
+    F.min_its = st.min_opt_iterations;
+    F.th = st.th_opt_iterations;
+    // one GN iteration: solveSystemF (a NaN x: the window is lost), resubstituteF_MT,
+    // doStepFromBackup + setPrecalcValues (canbreak), linearizeAll + applyRes (+ the accumulation
+    // the next solve uses); windows that left the loop skip every launch
     auto gn_iteration = [&](int it) -> int {
         int r;
         if ((r = solve_device_launch(c, it, ns ? 7 : 0))) return r;
         // the frame / calibration step + FrameFramePrecalc and the resubstitution with the point
         // step applied in place, in one launch (the solve wrote x and xAd)
-        const ResubParams R = resub_params(c, 0, c->P_tot, 1e-5, true);
+        FrameStepParams Fi = F;
+        Fi.it = it;
+        ResubParams R = resub_params(c, 0, c->P_tot, 1e-5, true);
+        R.stop = c->d_stop.p;
+        R.it = it;
         if ((r = timed_launch(c, 3, c->stream, [&] {
-                 k_step_resub<<<nw + (c->P_tot + 255) / 256, 256, 0, c->stream>>>(F, R, nw);
+                 k_step_resub<<<nw + (c->P_tot + 255) / 256, 256, 0, c->stream>>>(Fi, R, nw);
              })))
             return r;
+        c->opt_pass = it + 1;
         return ldso_ba_linearize(c, 0, it + 1 < n_its ? 1 : 0);
     };
     // FullSystem::optimize (FullSystem.cc:853-976) with setting_forceAceptStep: resetOOB, then
@@ -5886,10 +6025,14 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     // sequence is fixed by (n_its, nullspaces or not), so without a communicator or kernel timing
     // the calls after the first replay ONE captured HIP graph of it (graph launches are
     // separated by ~9 us on the GPU; one per call instead of one per iteration), cached in the
-    // context and re-captured only after a device (re)allocation or for another n_its.
-    c->opt_hist = true;  // every pass of this call writes its energies into the history too
+    // context and re-captured after a device (re)allocation or when anything fixed at capture
+    // changes: n_its, the settings, the solve kernel (exact or not), the stitch split.
     auto body = [&]() -> int {
         int r;
+        // every window in the loop: stop = INT_MAX-ish (0x7f7f7f7f), status LDSO_BA_OPT_RAN_ALL
+        HIP_TRY(hipMemsetAsync(c->d_stop.p, 0x7f, (size_t)nw * sizeof(int), c->stream));
+        HIP_TRY(hipMemsetAsync(c->d_status.p, 0, (size_t)nw * sizeof(int), c->stream));
+        c->opt_pass = 0;  // every pass of this call writes its energies into the history too
         if ((r = ldso_ba_reset_oob(c, -1)) || (r = ldso_ba_linearize(c, 0, n_its > 0 ? 1 : 0))) return r;
         for (int it = 0; it < n_its; it++)
             if ((r = gn_iteration(it))) return r;
@@ -5897,21 +6040,31 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
     };
     const bool use_graph = !c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH");
     if (use_graph && c->opt_warm) {
-        rc = launch_cached_graph(c, c->opt_graph[ns ? 1 : 0], (unsigned long long)n_its, body);
+        unsigned th_bits;
+        std::memcpy(&th_bits, &st.th_opt_iterations, sizeof(th_bits));
+        const char *hs = std::getenv("LDSO_BA_HS_SPLIT");
+        const unsigned long long key = (unsigned long long)(n_its & 0xFFFF) |
+                                       ((unsigned long long)(std::min(st.min_opt_iterations, 255)) << 16) |
+                                       ((unsigned long long)(c->solve_exact ? 1 : 0) << 24) |
+                                       ((unsigned long long)(getenv_flag("LDSO_BA_SOLVE_LDS") ? 1 : 0) << 25) |
+                                       ((unsigned long long)(hs ? (hs[0] == '1' ? 1 : 2) : 0) << 26) |
+                                       ((unsigned long long)th_bits << 32);
+        rc = launch_cached_graph(c, c->opt_graph[ns ? 1 : 0], key, body);
     } else {
         rc = body();  // the first call runs directly (one-time setup stays out of any capture)
         c->opt_warm = rc == 0;
     }
-    c->opt_hist = false;
+    c->opt_pass = -1;
     if (rc) return rc;
     // every result into one pinned buffer (energy history, frame states, calibration, the window
     // descriptors, the idepth column), one synchronisation
     const size_t hb = (size_t)2 * nw * (n_its + 1) * sizeof(double),
                  fb = (size_t)c->n_frames * sizeof(ldso_ba_frame_state), cb = (size_t)4 * nw * sizeof(double),
                  wb = (size_t)nw * sizeof(WinDev), ib = (size_t)c->P_tot * sizeof(float),
-                 tb = (size_t)c->n_frames * sizeof(float);
+                 tb = (size_t)c->n_frames * sizeof(float), sb = (size_t)nw * sizeof(int);
     auto up16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
-    const size_t o_f = up16(hb), o_c = o_f + up16(fb), o_w = o_c + up16(cb), o_t = o_w + up16(wb), o_i = o_t + up16(tb);
+    const size_t o_f = up16(hb), o_c = o_f + up16(fb), o_w = o_c + up16(cb), o_t = o_w + up16(wb), o_s = o_t + up16(tb),
+                 o_u = o_s + up16(sb), o_i = o_u + up16(sb);
     if ((rc = pin_map_ensure(c, o_i + ib))) return rc;
     char *po = c->pin_map, *pd = c->pin_map_dev;
     {  // one launch writes every result into the mapped buffer (the idepth column only)
@@ -5926,6 +6079,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         if (calib_out) seg(c->d_calib_val.p, o_c, cb);
         seg(c->d_wins.p, o_w, wb);  // the host mirror of WinDev (calibration, cDeltaF) follows the device
         seg(c->d_frame_th.p, o_t, tb);  // setNewFrameEnergyTH of the last pass (ldso_ba_get_frame_energy_th)
+        seg(c->d_stop.p, o_s, sb);      // the loop exits
+        seg(c->d_status.p, o_u, sb);
         if (idepth_out && c->P_tot) {
             K.pt_data = c->d_pt_data.p;
             K.idepth_dst = reinterpret_cast<float *>(pd + o_i);
@@ -5935,6 +6090,15 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_frame_state *f
         HIP_TRY(hipGetLastError());
     }
     if ((rc = ldso_ba_sync(c))) return rc;
+    {
+        const int *stop = reinterpret_cast<const int *>(po + o_s), *status = reinterpret_cast<const int *>(po + o_u);
+        for (int w = 0; w < nw; w++) {
+            // lost at iteration k: stop = k and k + 1 solves ran; converged at k: stop = k + 1
+            const int its = status[w] == LDSO_BA_OPT_LOST ? stop[w] + 1 : std::min(stop[w], n_its);
+            if (iterations_out) iterations_out[w] = its;
+            if (status_out) status_out[w] = status[w];
+        }
+    }
     if (energy_out) {
         const double *e = reinterpret_cast<const double *>(po);
         for (int s = 0; s <= n_its; s++)

@@ -1,5 +1,5 @@
 // se3.h -- the double-precision SE(3) and FrameFramePrecalc arithmetic of the path, shared by the
-// host helpers (host_math.cpp) and the device GN loop (ldso_ba.hip k_frame_step), statement for
+// host helpers (host_math.cpp) and the device GN loop (ldso_ba.hip k_step_resub), statement for
 // statement, FP contraction off: Sophus SE3 exp / log / product / inverse / Adj
 // (thirdparty/Sophus/sophus/se3.hpp, so3.hpp), FrameHessian::setState's PRE_worldToCam
 // (FrameHessian.h:95-114), AffLight::fromToVecExposure (AffLight.h:27-35), the per-pair body of
@@ -269,6 +269,34 @@ LDSO_HD inline void calib_step(double value[4], const double *x4, const double v
         scaledf[i] = (float)(sc[i] * value[i]);
         c_delta[i] = (float)(value[i] - value_zero[i]);
     }
+}
+
+// doStepFromBackup's return value canbreak (FullSystem.cc:1836-1838, 1894-1897, 1914-1931) at
+// stepfac 1 on the visual-only path (sumI = sumIH = 0): float accumulators fed double products
+// (float += double rounds the double sum), averaged over the frames, against 5e-4 / 5e-5 x
+// setting_thOptIterations in double.  sum_nid / num_id: the window's sum of |idepth_backup| and its
+// point count (window_nid).  xw: the window's x [8N+4] (step = -x).
+LDSO_HD inline bool step_canbreak(int N, const double *xw, float sum_nid, float num_id, float th_opt) {
+#pragma clang fp contract(off)
+    float sumA = 0, sumB = 0, sumT = 0, sumR = 0;
+    for (int f = 0; f < N; f++) {
+        double st[8];
+        for (int i = 0; i < 8; i++) st[i] = -xw[4 + 8 * f + i];
+        sumA = (float)((double)sumA + st[6] * st[6]);
+        sumB = (float)((double)sumB + st[7] * st[7]);
+        sumT = (float)((double)sumT + ((st[0] * st[0] + st[1] * st[1]) + st[2] * st[2]));
+        sumR = (float)((double)sumR + ((st[3] * st[3] + st[4] * st[4]) + st[5] * st[5]));
+    }
+    const float n = (float)N;
+    sumA /= n;
+    sumB /= n;
+    sumR /= n;
+    sumT /= n;
+    const float sumNID = sum_nid / num_id;
+    const double th = (double)th_opt, sumI = 0.0, sumIH = 0.0;
+    return (double)sqrtf(sumA) < 0.0005 * th && (double)sqrtf(sumB) < 0.00005 * th &&
+           (double)sqrtf(sumR) < 0.00005 * th && (double)(sqrtf(sumT) * sumNID) < 0.00005 * th &&
+           sqrt(sumI) < 0.00005 * th && sqrt(sumIH) < 0.00005 * th;
 }
 
 }  // namespace ldso_ba

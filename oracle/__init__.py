@@ -59,6 +59,8 @@ def lib():
             "oracle_set_adjoints": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p]),
             "oracle_frame_take_data": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p]),
             "oracle_nullspaces": (C.c_int, [C.c_int, C.c_void_p, f64p]),
+            "oracle_do_step_from_backup": (C.c_int, [C.c_int, C.c_void_p, f64p, f64p, f64p, C.c_int, i32p, f32p, f32p,
+                                                     C.c_float, C.c_void_p, f32p, f32p, f32p]),
             "oracle_time_iterations": (C.c_double, [C.c_void_p, C.c_int]),
             "oracle_ad_ht_delta": (C.c_int, [C.c_int, f64p, f64p, f64p, f32p]),
             "oracle_calc_m_energy": (C.c_double, [C.c_int, f64p, f64p, f32p, f64p]),
@@ -231,6 +233,28 @@ def frame_terms(window):
     lib().oracle_nullspaces(N, fr.ctypes.data, _p(ns, f64p))
     return dict(precalc=pre, ad_host=adH, ad_target=adT, c_prior=cp, frame_prior=prior, frame_delta=delta,
                 frame_delta_prior=dprior, nullspaces=ns)
+
+
+def do_step_from_backup(frames, x, calib_value, calib_value_zero, point_host, idepth_backup, point_step,
+                        th_opt_iterations=1.2):
+    """FullSystem::doStepFromBackup for one window -> (frames, calib_value, value_scaledf, cDeltaF,
+    idepth, canbreak); calib_value is stepped in place as well."""
+    fr = np.ascontiguousarray(frames)
+    out = np.zeros_like(fr)
+    P = int(np.asarray(point_host).size)
+    ph = np.ascontiguousarray(point_host, np.int32)
+    ib = np.ascontiguousarray(idepth_backup, np.float32)
+    ps = np.ascontiguousarray(point_step, np.float32)
+    idepth = np.zeros(P, np.float32)
+    sf = np.zeros(4, np.float32)
+    cd = np.zeros(4, np.float32)
+    cz = np.ascontiguousarray(calib_value_zero, np.float64)
+    rc = lib().oracle_do_step_from_backup(len(fr), fr.ctypes.data, _p(np.ascontiguousarray(x, np.float64), f64p),
+                                          _p(calib_value, f64p), _p(cz, f64p), P, _p(ph, i32p), _p(ib, f32p),
+                                          _p(ps, f32p), float(th_opt_iterations), out.ctypes.data, _p(idepth, f32p),
+                                          _p(sf, f32p), _p(cd, f32p))
+    assert rc >= 0
+    return out, calib_value, sf, cd, idepth, bool(rc)
 
 
 # ---- coarse tracker (ldso_oracle_tracker.cpp): the checker of include/ldso_ct.h -------------

@@ -1840,6 +1840,76 @@ int oracle_nullspaces(int N, const ldso_ba_frame_state *frames, double *out) {
     return 0;
 }
 
+// FullSystem::doStepFromBackup (FullSystem.cc:1826-1931), the branch without SOLVER_MOMENTUM
+// (:1868-1912) with every step factor 1 (optimize() passes stepsize = 1 unless
+// SOLVER_STEPMOMENTUM), on the visual-only path (the inertial x_step / x_backup stay zero, so
+// sumI = sumIH = 0).  The steps are those resubstituteF_MT leaves (EnergyFunctional.cc:611-622):
+// HCalib->step = -x.head<4>(), fh->step.head<8>() = -x.segment<8>(4 + 8 idx), tail 0; the point
+// steps come from the caller (oracle_resubstitute).  Float sums exactly as written: sumA etc. are
+// float accumulators fed double products (float += double), sumNID a float sum of fabsf over the
+// window's active points in frames -> features order (here: host frames in window order, each
+// host's points in the window's point order).  Returns canbreak (0 / 1).
+int oracle_do_step_from_backup(int N, const ldso_ba_frame_state *backup, const double *x, double *calib_value,
+                               const double *calib_value_zero, int n_points, const int *point_host,
+                               const float *idepth_backup, const float *point_step, float th_opt_iterations,
+                               ldso_ba_frame_state *out, float *idepth_out, float *calib_scaled_out,
+                               float *c_delta_out) {
+    if (N < 1 || !backup || !x || !calib_value || !out || n_points < 0 ||
+        (n_points > 0 && (!point_host || !idepth_backup || !point_step || !idepth_out)))
+        return -1;
+    const float stepfacC = 1, stepfacT = 1, stepfacR = 1, stepfacA = 1, stepfacD = 1;
+    double pstepfac[10];
+    for (int i = 0; i < 3; i++) pstepfac[i] = stepfacT;
+    for (int i = 3; i < 6; i++) pstepfac[i] = stepfacR;
+    for (int i = 6; i < 10; i++) pstepfac[i] = stepfacA;
+    float sumA = 0, sumB = 0, sumT = 0, sumR = 0, sumID = 0, numID = 0;
+    float sumNID = 0;
+    double sumI = 0, sumIH = 0;
+    // Hcalib->mpCH->setValue(value_backup + stepfacC * step)  (CalibHessian.h:71-85)
+    for (int k = 0; k < CPARS; k++) calib_value[k] = calib_value[k] + stepfacC * (-x[k]);
+    if (calib_scaled_out)
+        for (int k = 0; k < CPARS; k++) calib_scaled_out[k] = (float)((k < 2 ? SCALE_F : SCALE_C) * calib_value[k]);
+    if (c_delta_out && calib_value_zero)
+        for (int k = 0; k < CPARS; k++) c_delta_out[k] = (float)(calib_value[k] - calib_value_zero[k]);
+    for (int f = 0; f < N; f++) {
+        const ldso_ba_frame_state &B = backup[f];
+        double step[10];
+        for (int i = 0; i < 10; i++) step[i] = i < 8 ? -x[CPARS + 8 * f + i] : 0.0;
+        ldso_ba_frame_state &O = out[f];
+        O = B;
+        // Vec10 step = state_backup + pstepfac .* step; head<6> = log(exp(pstepfac .* step) exp(state_backup))
+        double a[6], bk[6], lg[6];
+        for (int i = 0; i < 6; i++) {
+            a[i] = pstepfac[i] * step[i];
+            bk[i] = B.state[i];
+        }
+        se3_log(se3_mul(se3_exp(a), se3_exp(bk)), lg);
+        for (int i = 0; i < 10; i++) O.state[i] = i < 6 ? lg[i] : B.state[i] + pstepfac[i] * step[i];
+        sumA += step[6] * step[6];
+        sumB += step[7] * step[7];
+        sumT += (step[0] * step[0] + step[1] * step[1]) + step[2] * step[2];
+        sumR += (step[3] * step[3] + step[4] * step[4]) + step[5] * step[5];
+        for (int p = 0; p < n_points; p++) {
+            if (point_host[p] != f) continue;
+            const float ib = idepth_backup[p], st = point_step[p];
+            idepth_out[p] = ib + stepfacD * st;  // setIdepth / setIdepthZero (the same value)
+            sumID += st * st;
+            sumNID += fabsf(ib);
+            numID++;
+        }
+    }
+    sumA /= N;
+    sumB /= N;
+    sumR /= N;
+    sumT /= N;
+    sumID /= numID;
+    sumNID /= numID;
+    sumI /= N;
+    const double th = th_opt_iterations;
+    return sqrtf(sumA) < 0.0005 * th && sqrtf(sumB) < 0.00005 * th && sqrtf(sumR) < 0.00005 * th &&
+           sqrtf(sumT) * sumNID < 0.00005 * th && std::sqrt(sumI) < 0.00005 * th && std::sqrt(sumIH) < 0.00005 * th;
+}
+
 // ---- point marginalisation --------------------------------------
 // FullSystem::flagPointsForRemoval's per-residual part for the MARGINALIZED points
 // (FullSystem.cc:1390-1398) with PointFrameResidual::fixLinearizationF (Residuals.cc:219-245;

@@ -74,6 +74,14 @@ int oracle_frame_take_data(int n_frames, const ldso_ba_frame_state *frames, doub
 /* FrameHessian::setStateZero nullspaces + FullSystem::getNullspaces (pose x6, scale x1):
  * out [7][8N+4] in the order orthogonalize() stacks them. */
 int oracle_nullspaces(int n_frames, const ldso_ba_frame_state *frames, double *out);
+/* FullSystem::doStepFromBackup (FullSystem.cc:1826-1931; non-momentum, step factors 1, no inertial
+ * terms) for one window: frames / calibration / point idepths stepped from their backups by the
+ * solve's x and the resubstituted point steps; returns canbreak (0 / 1) or -1. */
+int oracle_do_step_from_backup(int n_frames, const ldso_ba_frame_state *backup, const double *x, double *calib_value,
+                               const double *calib_value_zero, int n_points, const int *point_host,
+                               const float *idepth_backup, const float *point_step, float th_opt_iterations,
+                               ldso_ba_frame_state *out, float *idepth_out, float *calib_scaled_out,
+                               float *c_delta_out);
 
 /* Point marginalisation of the points pts[n] (flagPointsForRemoval's relinearisation +
  * fixLinearizationF, then marginalizePointsF's addPoint<2> / SC addPoint(p, false) / stitch):

@@ -581,15 +581,20 @@ static int gpu_optimize_tests() {
     for (int k = 0; k < 4; k++) cv[k] = cz[k] = G.calib->value[k];
     std::vector<ldso_ba_frame_state> fo(N);
     std::vector<float> id(S.P);
-    CHECK(ldso_ba_optimize(raw, 3, S.fs.data(), cv.data(), cz.data(), ns.data(), e_raw.data(), fo.data(), co.data(),
-                           id.data()) == 0,
+    int32_t its_raw = -1, status_raw = -1;
+    CHECK(ldso_ba_optimize(raw, 3, nullptr, S.fs.data(), cv.data(), cz.data(), ns.data(), e_raw.data(), fo.data(),
+                           co.data(), id.data(), &its_raw, &status_raw) == 0,
           "ldso_ba_optimize: %s", ldso_ba_last_error());
 
     std::vector<Vec3> e_face;
     const long passes0 = ef->devicePasses();
-    const Vec3 last = ef->optimize(3, G.calib, &e_face);
+    bool lost = true;
+    int its_face = -1;
+    const Vec3 last = ef->optimize(3, G.calib, &e_face, &lost, &its_face);
     CHECK(ef->ok(), "EnergyFunctional::optimize: %s", ef->lastError().c_str());
-    CHECK(ef->devicePasses() == passes0 + 4, "optimize(3) ran %ld passes", ef->devicePasses() - passes0);
+    CHECK(!lost && status_raw != LDSO_BA_OPT_LOST, "optimize reported lost");
+    CHECK(its_face == its_raw && its_raw >= 1 && its_raw <= 3, "iterations: face %d, C ABI %d", its_face, its_raw);
+    CHECK(ef->devicePasses() == passes0 + 1 + its_raw, "optimize(3) ran %ld passes", ef->devicePasses() - passes0);
     CHECK(e_face.size() == 4, "energy history size %zu", e_face.size());
     for (size_t s2 = 0; s2 < e_face.size() && s2 < 4; s2++)
         CHECK(e_face[s2][0] == e_raw[3 * s2] && e_face[s2][2] == e_raw[3 * s2 + 2], "optimize energy %zu: %.17g vs %.17g",

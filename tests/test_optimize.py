@@ -1,25 +1,33 @@
-"""FullSystem::optimize on the device (FullSystem.cc:844-976, 1843-1922):
-ldso_ba_optimize runs resetOOB + linearizeAll and n GN iterations (solveSystemF, resubstituteF_MT,
-doStepFromBackup + setPrecalcValues, linearizeAll) with no host round trip.
+"""FullSystem::optimize on the device (FullSystem.cc:844-970, 1826-1931):
+ldso_ba_optimize runs resetOOB + linearizeAll and up to n GN iterations (solveSystemF,
+resubstituteF_MT, doStepFromBackup + setPrecalcValues, linearizeAll) with no host round trip, and
+leaves the loop per window on the reference's exits: canbreak once iteration >=
+setting_minOptIterations (:968-969) and isLost on a NaN solution (:907-911).
 
-The check is the same loop driven from the host: the oracle's linearize / accumulate / solve /
-resubstitute, the step with the library's host doStepFromBackup (ldso_ba_frame_step, the se3.h
-statements the device runs), the window's frame terms refreshed on the host
-(Window.refresh_frame_terms) and the points' idepth updated as setIdepth / setIdepthZero.  Host
-and device share every statement of the step; what differs is the stitched system (the GPU's
-float partial sums are reassociated, ~1e-6 relative per block, test_gpu_parity) and hence x,
+The check is the same loop driven from the host entirely by the oracle: its linearize /
+accumulate / solve / resubstitute, its restatement of doStepFromBackup and canbreak
+(oracle_do_step_from_backup), its FrameFramePrecalc / setAdjointsF / takeData (oracle.frame_terms),
+and the reference's break / lost tests.  What differs between the two is the stitched system (the
+GPU's float partial sums are reassociated, ~1e-6 relative per block, test_gpu_parity) and hence x,
 plus libm's last ulp (glibc vs the device library) in sin / cos / atan / exp.  Bars: the initial
 pass bit-exact in #IN and 1e-12 in energy; after steps, energies within the north star's 1e-4
-relative (measured 2e-6 .. 2e-5 over 3 iterations) and #IN within 0.2 %; the accumulated frame and point steps within 5 % (norm) of the
+relative and #IN within 0.2 %; the accumulated frame and point steps within 5 % (norm) of the
 host loop's (x is sensitive to 1e-6 changes of H along the near-gauge directions, which are only
-projected out from iteration 2 on: test_gpu_parity's sensitivity envelope).
+projected out from iteration 2 on: test_gpu_parity's sensitivity envelope); iteration counts and
+exit statuses EQUAL.  The windows are chosen with the canbreak criterion at least 20 % away from
+its threshold at every iteration (the ratios are printed), so the reassociation cannot flip it.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
 import oracle
 from ldso_amd import _lib as L
 from ldso_amd import synth
+
+CONVERGES = dict(synth.S7, seed=62)           # canbreak at iteration 3 (criterion ratios 1.32 -> 0.79)
+RUNS_ALL = dict(n_frames=5, n_points=500, seed=61)  # no canbreak within 6 iterations
 
 
 def frame_step(frames, x, cval, czero):
@@ -60,8 +68,54 @@ def test_frame_step_known_answers(built):
     np.testing.assert_array_equal(cd, (cval - cz).astype(np.float32))
 
 
-def host_optimize(w, n_its, ns):
-    """The same loop from the host: oracle pass/solve/resubstitute + host doStepFromBackup."""
+def canbreak_numpy(N, x, idepth_backup, th=1.2):
+    """FullSystem.cc:1894-1931 in float64 numpy (no float accumulators): the criterion's ratios to
+    its thresholds; canbreak iff all are < 1."""
+    st = -np.asarray(x)[4:].reshape(N, 8)
+    sA = np.mean(st[:, 6] ** 2)
+    sB = np.mean(st[:, 7] ** 2)
+    sT = np.mean((st[:, :3] ** 2).sum(1))
+    sR = np.mean((st[:, 3:6] ** 2).sum(1))
+    nid = np.mean(np.abs(np.asarray(idepth_backup, np.float64)))
+    return np.array([np.sqrt(sA) / (5e-4 * th), np.sqrt(sB) / (5e-5 * th), np.sqrt(sR) / (5e-5 * th),
+                     np.sqrt(sT) * nid / (5e-5 * th)])
+
+
+def test_oracle_step_matches_frame_step_and_criterion(built):
+    """The oracle's doStepFromBackup restatement against the product's host frame step (the same
+    Sophus statements written twice: states within 1 ulp-level 1e-15, calibration bit-exact), the
+    point step (setIdepth(idepth_backup + step)), and its canbreak against the float64 formula on
+    steps scaled to either side of the thresholds."""
+    w = synth.make_window(n_frames=4, n_points=120, width=160, height=120, seed=5)
+    rng = np.random.default_rng(5)
+    N = w.n_frames
+    fr = np.ascontiguousarray(w.frames).copy()
+    ib = w.point_data[:, 2].copy()
+    ps = (rng.standard_normal(w.n_points) * 1e-3).astype(np.float32)
+    for scale in (1e-6, 1e-5, 1e-4, 1e-2):
+        x = rng.standard_normal(8 * N + 4) * scale
+        cval = w.calib.astype(np.float64) / 50
+        cz = cval.copy()
+        o_fr, o_cv, o_sf, o_cd, o_id, cb = oracle.do_step_from_backup(fr, x, cval.copy(), cz, w.point_host, ib, ps)
+        p_fr, p_sf, p_cd = frame_step(fr, x, cval.copy(), cz)
+        np.testing.assert_allclose(o_fr["state"], p_fr["state"], rtol=1e-13, atol=1e-16)
+        np.testing.assert_array_equal(o_sf, p_sf)
+        np.testing.assert_array_equal(o_cd, p_cd)
+        np.testing.assert_array_equal(o_id, (ib + ps).astype(np.float32))
+        r = canbreak_numpy(N, x, ib)
+        if np.all(r < 0.99) or np.any(r > 1.01):  # away from the float-rounding edge
+            assert cb == bool(np.all(r < 1)), (scale, r, cb)
+    # th_opt_iterations scales the thresholds; 0 never breaks
+    x = rng.standard_normal(8 * N + 4) * 1e-7
+    assert oracle.do_step_from_backup(fr, x, w.calib / 50.0, w.calib / 50.0, w.point_host, ib, ps, 1.2)[5]
+    assert not oracle.do_step_from_backup(fr, x, w.calib / 50.0, w.calib / 50.0, w.point_host, ib, ps, 0.0)[5]
+
+
+def host_optimize(w, n_its, ns, th=1.2, min_its=1):
+    """FullSystem::optimize's loop from the host, every statement the oracle's: pass, solveSystemF,
+    the lost test (FullSystem.cc:907-911), resubstituteF_MT, doStepFromBackup (canbreak),
+    setPrecalcValues, linearizeAll + applyRes, the break test (:968-969).
+    -> (energies per pass, frames, calib value, idepth, iterations entered, status, ratios)."""
     ow = oracle.OracleWindow(w, threads=0)
     ow.reset_oob()
     e, sysm = ow.iteration()
@@ -69,93 +123,231 @@ def host_optimize(w, n_its, ns):
     cval = w.calib.astype(np.float64) * (1.0 / 50.0)
     czero = cval.copy()
     frames = np.ascontiguousarray(w.frames).copy()
+    ratios = []
+    status, its = L.OPT_RAN_ALL, n_its
     for it in range(n_its):
         x = oracle.solve_system(w.n_frames, it, 1e-5, sysm, nullspaces=ns)
+        if np.isnan(np.linalg.norm(x)):
+            status, its = L.OPT_LOST, it + 1
+            break
         step = ow.resubstitute(x, 1e-5)
-        frames, sf, cd = frame_step(frames, x, cval, czero)
+        ratios.append(canbreak_numpy(w.n_frames, x, w.point_data[:, 2]))
+        frames, cval, sf, cd, idepth, canbreak = oracle.do_step_from_backup(
+            frames, x, cval, czero, w.point_host, w.point_data[:, 2], step, th)
         w.frames = frames
         w.calib = sf.copy()
         w.c_delta = cd.copy()
         w.point_data = w.point_data.copy()
-        idepth = (w.point_data[:, 2] + np.float32(1.0) * step).astype(np.float32)
         w.point_data[:, 2] = idepth
         w.point_data[:, 3] = idepth
         w.point_data[:, 5] = idepth - idepth
-        w.refresh_frame_terms()
+        t = oracle.frame_terms(w)
+        for k in ("precalc", "ad_host", "ad_target", "c_prior", "frame_prior", "frame_delta", "frame_delta_prior"):
+            setattr(w, k, t[k])
         ow.update(w)
         e, sysm = ow.iteration()
         energies.append(e)
-    return np.array(energies), frames, cval, w.point_data[:, 2].copy()
+        if canbreak and it >= min_its:
+            status, its = L.OPT_CONVERGED, it + 1
+            break
+    return np.array(energies), frames, cval, w.point_data[:, 2].copy(), its, status, np.array(ratios)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [dict(n_frames=5, n_points=500, seed=61), dict(synth.S7, seed=62)], ids=["N5", "S7"])
-def test_device_optimize_matches_host_loop(built, cfg):
-    from ldso_amd import BAContext
-
-    n_its = 3
+def check_against_host(cfg, e_dev, fr_dev, c_dev, idep_dev, its_dev, st_dev, n_its, ns, frames=None):
     w = synth.make_window(**cfg)
-    ns = w.nullspaces()
-    ctx = BAContext(0).load([w])
-    e_dev, fr_dev, c_dev, idep_dev = ctx.optimize(n_its, nullspaces=[ns])
-    e_host, fr_host, c_host, idep_host = host_optimize(synth.make_window(**cfg), n_its, ns)
-    assert e_dev[0, 0, 2] == e_host[0][2] and abs(e_dev[0, 0, 0] - e_host[0][0]) <= 1e-12 * abs(e_host[0][0])
-    for s in range(1, n_its + 1):
-        print(f"it {s}: device {e_dev[s, 0]}, host {e_host[s]}")
-        assert abs(e_dev[s, 0, 0] - e_host[s][0]) <= 1e-4 * abs(e_host[s][0]), (s, e_dev[s, 0], e_host[s])
-        assert abs(e_dev[s, 0, 2] - e_host[s][2]) <= 2e-3 * e_host[s][2], (s, e_dev[s, 0], e_host[s])
+    if frames is not None:
+        w.frames = frames
+    e_host, fr_host, c_host, idep_host, its_host, st_host, ratios = host_optimize(w, n_its, ns)
+    print(f"{cfg}: host {its_host} its status {st_host}, device {its_dev} status {st_dev}; ratios\n{ratios}")
+    assert (its_dev, st_dev) == (its_host, st_host)
+    passes = len(e_host)
+    assert e_dev[0, 2] == e_host[0][2] and abs(e_dev[0, 0] - e_host[0][0]) <= 1e-12 * abs(e_host[0][0])
+    for s in range(1, passes):
+        assert abs(e_dev[s, 0] - e_host[s][0]) <= 1e-4 * abs(e_host[s][0]), (s, e_dev[s], e_host[s])
+        assert abs(e_dev[s, 2] - e_host[s][2]) <= 2e-3 * e_host[s][2], (s, e_dev[s], e_host[s])
+    for s in range(passes, n_its + 1):  # rows after the exit repeat the last pass
+        np.testing.assert_array_equal(e_dev[s], e_dev[passes - 1])
+    if st_host == L.OPT_LOST:
+        return
     w0 = synth.make_window(**cfg)
     ds_h = fr_host["state"] - w0.frames["state"]
     assert np.linalg.norm(fr_dev["state"] - fr_host["state"]) <= 0.05 * np.linalg.norm(ds_h)
     dc_h = c_host - w0.calib.astype(np.float64) / 50.0
-    assert np.linalg.norm(c_dev[0] - c_host) <= 0.05 * np.linalg.norm(dc_h) + 1e-12
+    assert np.linalg.norm(c_dev - c_host) <= 0.05 * np.linalg.norm(dc_h) + 1e-12
     di_h = idep_host - w0.point_data[:, 2]
-    assert np.linalg.norm(idep_dev[0] - idep_host) <= 0.05 * np.linalg.norm(di_h)
+    assert np.linalg.norm(idep_dev - idep_host) <= 0.05 * np.linalg.norm(di_h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [RUNS_ALL, CONVERGES], ids=["N5_runs_all", "S7_converges"])
+def test_device_optimize_matches_host_loop(built, cfg):
+    from ldso_amd import BAContext
+
+    n_its = 6
+    w = synth.make_window(**cfg)
+    ns = w.nullspaces()
+    ctx = BAContext(0).load([w])
+    e, fr, c, idep, its, st = ctx.optimize(n_its, nullspaces=[ns])
+    check_against_host(cfg, e[:, 0], fr, c[0], idep[0], int(its[0]), int(st[0]), n_its, ns)
     # the context keeps the stepped state: a further pass starts from it
     ctx.linearize()
-    assert abs(ctx.energy(0)[0] - e_dev[-1, 0, 0]) <= 1e-9 * abs(e_dev[-1, 0, 0])
+    assert abs(ctx.energy(0)[0] - e[-1, 0, 0]) <= 1e-9 * abs(e[-1, 0, 0])
     ctx.close()
 
 
 @pytest.mark.gpu
-def test_device_optimize_batched_windows(built):
-    """Every resident window runs its own loop; each equals the same window optimised alone."""
+def test_device_optimize_batched_windows_exit_independently(built):
+    """One captured sequence serves windows that leave the loop at different iterations: the
+    converging S7 window stops after its canbreak while the N5 window runs on, and each equals
+    the same window optimised alone (and the host loop's iteration count)."""
     from ldso_amd import BAContext
 
-    cfgs = [dict(n_frames=4, n_points=300, seed=71), dict(n_frames=6, n_points=400, seed=72)]
+    cfgs = [CONVERGES, RUNS_ALL, dict(n_frames=4, n_points=300, seed=71)]
     ws = [synth.make_window(**c) for c in cfgs]
     both = BAContext(0).load(ws)
-    e2, fr2, _, id2 = both.optimize(2, nullspaces=[w.nullspaces() for w in ws])
-    off = 0
-    for i, c in enumerate(cfgs):
-        w = synth.make_window(**c)
-        one = BAContext(0).load([w])
-        e1, fr1, _, id1 = one.optimize(2, nullspaces=[w.nullspaces()])
-        np.testing.assert_allclose(e2[:, i, 0], e1[:, 0, 0], rtol=1e-9)
-        np.testing.assert_array_equal(e2[:, i, 2], e1[:, 0, 2])
-        np.testing.assert_allclose(fr2["state"][off:off + w.n_frames], fr1["state"], rtol=1e-9, atol=1e-15)
-        np.testing.assert_allclose(id2[i], id1[0], rtol=1e-6)
-        off += w.n_frames
-        one.close()
+    for call in range(2):  # the second call replays the captured graph
+        e2, fr2, _, id2, its2, st2 = both.optimize(6, nullspaces=[w.nullspaces() for w in ws])
+        off = 0
+        for i, c in enumerate(cfgs):
+            w = synth.make_window(**c)
+            one = BAContext(0).load([w])
+            e1, fr1, _, id1, its1, st1 = one.optimize(6, nullspaces=[w.nullspaces()])
+            assert (its2[i], st2[i]) == (its1[0], st1[0]), (call, i)
+            np.testing.assert_allclose(e2[:, i, 0], e1[:, 0, 0], rtol=1e-9)
+            np.testing.assert_array_equal(e2[:, i, 2], e1[:, 0, 2])
+            np.testing.assert_allclose(fr2["state"][off:off + w.n_frames], fr1["state"], rtol=1e-9, atol=1e-15)
+            np.testing.assert_allclose(id2[i], id1[0], rtol=1e-6)
+            off += w.n_frames
+            one.close()
+        assert st2[0] == L.OPT_CONVERGED and its2[0] < 6 and st2[1] == L.OPT_RAN_ALL and its2[1] == 6
+        both.close()
+        ws = [synth.make_window(**c) for c in cfgs]
+        both = BAContext(0).load(ws)
     both.close()
 
 
 @pytest.mark.gpu
-def test_graph_replay_equals_direct_launches(built, monkeypatch):
-    """ldso_ba_optimize replays captured HIP graphs of one GN iteration after the first (cached in
-    the context across calls); the result must equal direct launches bit for bit
-    (LDSO_BA_NO_GRAPH=1), over enough iterations to use every graph variant (before / after the
-    projection starts, the last pass) and over a second call that reuses them."""
+def test_device_optimize_reports_lost(built):
+    """A NaN exposure in frame 2's state (the uploaded precalc is clean, so the initial pass and
+    the first solve are finite): the first setPrecalcValues makes the pairs of frame 2 NaN, the
+    second solve's x is NaN, and the window is lost at iteration 1 (FullSystem.cc:907-911) --
+    exactly when the host loop is; its states are those after the first step; a clean window
+    batched with it runs on unaffected."""
     from ldso_amd import BAContext
 
-    cfg = dict(synth.S7, seed=63)
+    cfg = dict(n_frames=5, n_points=400, seed=81)
+    w = synth.make_window(**cfg)
+    w.refresh_frame_terms()
+    bad = np.ascontiguousarray(w.frames).copy()
+    bad["ab_exposure"][2] = np.nan
+    ns = w.nullspaces()
+    w.frames = bad
+    clean = synth.make_window(**RUNS_ALL)
+    ctx = BAContext(0).load([w, clean])
+    e, fr, c, idep, its, st = ctx.optimize(4, nullspaces=[ns, clean.nullspaces()])
+    assert (int(its[0]), int(st[0])) == (2, L.OPT_LOST)
+    w2 = synth.make_window(**cfg)
+    w2.refresh_frame_terms()
+    _, fr_h, *_ = host_optimize(w2, 1, ns)  # the state after the one step that was applied
+    w3 = synth.make_window(**cfg)
+    w3.refresh_frame_terms()
+    w3.frames = bad.copy()
+    e_h, _, _, _, its_h, st_h, _ = host_optimize(w3, 4, ns)
+    assert (its_h, st_h) == (2, L.OPT_LOST)
+    np.testing.assert_array_equal(e[2:, 0], np.repeat(e[1:2, 0], 3, axis=0))  # rows after: the last pass
+    d = fr["state"][:5] - fr_h["state"]
+    assert np.linalg.norm(d[np.isfinite(d)]) <= 0.05 * np.linalg.norm((fr_h["state"] - bad["state"]))
+    one = BAContext(0).load([synth.make_window(**RUNS_ALL)])
+    e1, fr1, _, id1, its1, st1 = one.optimize(4, nullspaces=[clean.nullspaces()])
+    assert (its[1], st[1]) == (its1[0], st1[0])
+    np.testing.assert_allclose(e[:, 1, 0], e1[:, 0, 0], rtol=1e-9)
+    np.testing.assert_allclose(id1[0], idep[1], rtol=1e-6)
+    one.close()
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_optimize_settings(built):
+    """Unsupported settings are rejected (not run as the default); min_opt_iterations and
+    th_opt_iterations move the exit as in the reference (th = 0 never breaks)."""
+    from ldso_amd import BAContext
+
+    w = synth.make_window(**CONVERGES)
+    ns = w.nullspaces()
+    ctx = BAContext(0).load([w])
+    for bad in (L.OptSettings.default(solver_mode=L.SOLVER_DEFAULT | L.SOLVER_SVD),
+                L.OptSettings.default(solver_mode=L.SOLVER_DEFAULT | L.SOLVER_MOMENTUM),
+                L.OptSettings.default(solver_mode=L.SOLVER_ORTHOGONALIZE_X_LATER),
+                L.OptSettings.default(force_accept_step=0)):
+        with pytest.raises(RuntimeError, match="not implemented"):
+            ctx.optimize(3, nullspaces=[ns], settings=bad)
+    ctx.close()
+    runs = {}
+    for name, s in (("default", None), ("th0", L.OptSettings.default(th_opt_iterations=0.0)),
+                    ("min5", L.OptSettings.default(min_opt_iterations=5))):
+        c = BAContext(0).load([synth.make_window(**CONVERGES)])
+        runs[name] = c.optimize(6, nullspaces=[ns], settings=s)
+        c.close()
+    assert runs["default"][5][0] == L.OPT_CONVERGED and runs["default"][4][0] == 4
+    assert runs["th0"][5][0] == L.OPT_RAN_ALL and runs["th0"][4][0] == 6
+    assert runs["min5"][4][0] == 6  # canbreak from iteration 3 on, but only taken at iteration >= 5
+    # the first four passes are the same computation in all three
+    np.testing.assert_array_equal(runs["default"][0][:5], runs["th0"][0][:5])
+
+
+def test_check_settings_without_gpu(built):
+    """ldso_ba_check_settings is host-only: the defaults pass, every unsupported mode names itself."""
+    lib = L.lib()
+    assert lib.ldso_ba_check_settings(None) == 0
+    assert lib.ldso_ba_check_settings(C.byref(L.OptSettings.default())) == 0
+    for bit, name in ((L.SOLVER_SVD, "SOLVER_SVD"), (L.SOLVER_ORTHOGONALIZE_SYSTEM, "ORTHOGONALIZE_SYSTEM"),
+                      (L.SOLVER_USE_GN, "USE_GN"), (L.SOLVER_MOMENTUM, "SOLVER_MOMENTUM"),
+                      (L.SOLVER_STEPMOMENTUM, "STEPMOMENTUM"), (L.SOLVER_SVD_CUT7, "SVD_CUT7")):
+        assert lib.ldso_ba_check_settings(C.byref(L.OptSettings.default(solver_mode=L.SOLVER_DEFAULT | bit))) == -1
+        assert name in lib.ldso_ba_last_error().decode()
+    assert lib.ldso_ba_check_settings(C.byref(L.OptSettings.default(force_accept_step=0))) == -1
+    assert "forceAceptStep" in lib.ldso_ba_last_error().decode()
+
+
+@pytest.mark.gpu
+def test_graph_replay_equals_direct_launches(built, monkeypatch):
+    """ldso_ba_optimize replays a captured HIP graph of the whole call after the first (cached in
+    the context across calls); the result must equal direct launches bit for bit
+    (LDSO_BA_NO_GRAPH=1), over enough iterations to use every variant (before / after the
+    projection starts, the last pass), a window that exits early, and a second call that reuses
+    them."""
+    from ldso_amd import BAContext
+
     outs = []
     for env in ("0", "1"):
         monkeypatch.setenv("LDSO_BA_NO_GRAPH", env)
-        w = synth.make_window(**cfg)
+        ws = [synth.make_window(**dict(synth.S7, seed=63)), synth.make_window(**CONVERGES)]
+        ctx = BAContext(0).load(ws)
+        nss = [w.nullspaces() for w in ws]
+        # twice on one context: the second call replays the graph cached by the first
+        outs.append(ctx.optimize(6, nullspaces=nss) + ctx.optimize(4, nullspaces=nss))
+        ctx.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
+@pytest.mark.gpu
+def test_graph_recaptured_when_solve_mode_changes(built, monkeypatch):
+    """The cached graph is keyed by what is fixed at capture: switching the solve
+    kernel with LDSO_BA_TUNE_SOLVE_EXACT after two optimize calls must run the exact solve,
+    i.e. equal the same sequence run with direct launches."""
+    from ldso_amd import BAContext
+
+    outs = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("LDSO_BA_NO_GRAPH", env)
+        w = synth.make_window(**dict(synth.S7, seed=65))
         ctx = BAContext(0).load([w])
-        # twice on one context: the second call replays the graphs cached by the first
-        outs.append(ctx.optimize(6, nullspaces=[w.nullspaces()]) + ctx.optimize(4, nullspaces=[w.nullspaces()]))
+        ns = [w.nullspaces()]
+        r = ctx.optimize(3, nullspaces=ns) + ctx.optimize(3, nullspaces=ns)
+        ctx.set_tuning(12, 1)  # LDSO_BA_TUNE_SOLVE_EXACT
+        r = r + ctx.optimize(3, nullspaces=ns)
+        outs.append(r)
         ctx.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
