@@ -1148,18 +1148,64 @@ struct PointParams {
     int shift_prior;  // AccumulatedSCHessianSSE::addPoint's shiftPriorToZero (false when marginalising)
     const int *stop;  // ldso_ba_optimize (LinParams::stop)
     int pass;
+    // ldso_ba_optimize: blocks [0, n_nid) compute doStepFromBackup's sumNID / numID of window
+    // blockIdx.x (point_nid); the point-chunk blocks follow
+    float *win_nid;
+    int n_nid, nid_chunk;
 };
+
+// doStepFromBackup's sumNID and numID (FullSystem.cc:1899-1909) for the step that follows this
+// pass: the float sum of fabsf(idepth_backup) over the window's points in frames -> features order
+// (host frames in window order, each host's points in the caller's order: the device point order),
+// i.e. over the idepths this pass linearised at.  The chain of float adds is sequential by
+// definition, so one lane walks it from LDS (the block stages chunks of the idepths), in a block of
+// its own at the front of k_point_sc's grid: it runs beside the point-chunk blocks, off the
+// pass's critical path.  With sharded points each rank sums its own run; the exchange adds the
+// ranks' partials.
+__device__ void point_nid(const PointParams &P, int w, float *lds) {
+    if (P.stop && P.pass > P.stop[w]) return;
+    const WinDev &W = P.wins[w];
+    const int n = W.P, tid = threadIdx.x, chunk = P.nid_chunk;
+    const float *pd = P.pt_data + (size_t)W.point_base * LDSO_BA_POINT_STRIDE + 2;
+    float s = 0.0f;
+    for (int q0 = 0; q0 < n; q0 += chunk) {
+        const int m = min(chunk, n - q0);
+        for (int i = tid; i < m; i += blockDim.x) lds[i] = fabsf(pd[(size_t)(q0 + i) * LDSO_BA_POINT_STRIDE]);
+        for (int i = m + tid; i < ((m + 3) & ~3); i += blockDim.x) lds[i] = 0.0f;  // +0 leaves s unchanged
+        __syncthreads();
+        if (tid == 0) {
+            const float4 *l4 = reinterpret_cast<const float4 *>(lds);
+#pragma unroll 8
+            for (int i = 0; i < (m + 3) / 4; i++) {
+                const float4 v = l4[i];
+                s += v.x;
+                s += v.y;
+                s += v.z;
+                s += v.w;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        P.win_nid[2 * w] = s;
+        P.win_nid[2 * w + 1] = (float)n;  // numID++ per point: exact below 2^24
+    }
+}
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
 constexpr int kScBatch = 2;  // residual records per round trip (4 and 8 measured equal, r2)
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
-    const int item = P.item_base + blockIdx.x;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    if ((int)blockIdx.x < P.n_nid) {
+        point_nid(P, blockIdx.x, smem);
+        return;
+    }
+    const int item = P.item_base + blockIdx.x - P.n_nid;
     const int4 it = P.items[item];
     if (P.stop && P.pass > P.stop[it.w]) return;  // window left the GN loop
     const WinDev &W = P.wins[it.w];
     const int host = it.z, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
     const int Kj = 8 * (W.N - 1);
-    extern __shared__ __attribute__((aligned(16))) float smem[];
     float *U = smem;               // [64][KP]
     float *Wt = smem + 64 * KP;    // [64]
     const int tid = threadIdx.x;
@@ -1280,8 +1326,6 @@ struct StitchParams {
     double *ehist;         // non-null (ldso_ba_optimize): also win_energy into row `pass` of the history
     const int *stop;       // ldso_ba_optimize (LinParams::stop): host / pair blocks of stopped windows skip
     int pass;
-    const float *pt_data;  // with win_nid: doStepFromBackup's sumNID / numID of every window
-    float *win_nid;
     int accumulate;
     int th_cap;  // newest-frame energies staged in LDS by setNewFrameEnergyTH
     int pair_base;  // first global pair of this launch
@@ -1450,31 +1494,6 @@ __device__ void frame_threshold_and_energy(const StitchParams &P, const WinDev &
     }
 }
 
-// doStepFromBackup's sumNID and numID (FullSystem.cc:1899-1909) for the step that follows this pass:
-// the float sum of fabsf(idepth_backup) over the window's points in frames -> features order (host
-// frames in window order, each host's points in the caller's order: the device point order), i.e.
-// over the idepths this pass linearised at.  One wavefront; 64 idepths per load, added lane by
-// lane (readlane) so the sum rounds exactly as the reference's sequential loop.  With sharded
-// points each rank sums its own run; the exchange adds the ranks' partials.
-__device__ void window_nid(const StitchParams &P, const WinDev &W, int w) {
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x, n = W.P;
-    const float *pd = P.pt_data + (size_t)W.point_base * LDSO_BA_POINT_STRIDE + 2;
-    auto load = [&](int q0) { return q0 + lane < n ? fabsf(pd[(size_t)(q0 + lane) * LDSO_BA_POINT_STRIDE]) : 0.0f; };
-    float s = 0.0f, v = load(0);
-    for (int q0 = 0; q0 < n; q0 += 64) {
-        const float nv = load(q0 + 64);  // the next round's loads in flight during this round's adds
-#pragma unroll
-        for (int l = 0; l < 64; l++)  // padding lanes add +0: s is unchanged
-            s += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-        v = nv;
-    }
-    if (lane == 0) {
-        P.win_nid[2 * w] = s;
-        P.win_nid[2 * w + 1] = (float)n;  // numID++ per point: exact below 2^24
-    }
-}
-
 // slot (r, c) of the 13x13 finish() matrix -> index into the 96-slot partial layout
 __device__ __forceinline__ int top_slot(int r, int c) {
     if (r > c) {
@@ -1516,7 +1535,6 @@ __global__ __launch_bounds__(kStThreads) void k_stitch(StitchParams P) {
     if ((int)blockIdx.x < P.n_win) {  // the longest single-block chain goes first in the grid
         const int w = P.win_base + blockIdx.x;
         frame_threshold_and_energy<kStThreads>(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
-        if (P.win_nid) window_nid(P, P.wins[w], w);
         return;
     }
     const int pair = P.pair_base + blockIdx.x - P.n_win;
@@ -1929,7 +1947,6 @@ __global__ __launch_bounds__(kHsThreads) void k_stitch_host(StitchParams P) {
     if ((int)blockIdx.x < P.n_win) {  // setNewFrameEnergyTH + the energy sum, as k_stitch
         const int w = P.win_base + blockIdx.x;
         frame_threshold_and_energy<kHsThreads>(P, P.wins[w], w, reinterpret_cast<unsigned *>(sm));
-        if (P.win_nid) window_nid(P, P.wins[w], w);
         return;
     }
     if (!P.accumulate) return;
@@ -5106,7 +5123,7 @@ int comm_exchange(ldso_ba_ctx *c, bool accumulate) {
     if (accumulate) NCCL_TRY(ncclAllReduce(c->d_sys.p, c->d_sys.p, c->d_sys.n, ncclFloat64, ncclSum, c->comm, st));
     NCCL_TRY(ncclAllReduce(c->d_win_energy.p, c->d_win_energy.p, (size_t)2 * c->n_win, ncclFloat64, ncclSum, c->comm,
                            st));
-    if (c->opt_pass >= 0)  // optimize(): doStepFromBackup's sumNID / numID over every rank's points
+    if (c->opt_pass >= 0 && accumulate)  // optimize(): the next step's sumNID / numID over every rank's points
         NCCL_TRY(ncclAllReduce(c->d_win_nid.p, c->d_win_nid.p, (size_t)2 * c->n_win, ncclFloat32, ncclSum, c->comm, st));
     const long long stride = c->x_stride;
     const dim3 grid((unsigned)std::min<long long>((stride + 255) / 256, 64), (unsigned)c->n_win);
@@ -5209,12 +5226,16 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.ehist = in_opt && !c->comm ? c->d_ehist.p : nullptr;  // with RCCL: after the exchange
     Sp.pass = c->opt_pass;
     Sp.stop = in_opt ? c->d_stop.p : nullptr;
-    Sp.pt_data = c->d_pt_data.p;
-    Sp.win_nid = in_opt ? c->d_win_nid.p : nullptr;
     L.stop = Sp.stop;
     L.pass = c->opt_pass;
     Pp.stop = Sp.stop;
     Pp.pass = c->opt_pass;
+    const size_t sc_smem = std::max<size_t>(c->sc_smem_max, 4096);  // point_nid stages >= 1024 idepths
+    if (in_opt && accumulate) {  // the next step's sumNID / numID (its backup idepths are this pass's)
+        Pp.win_nid = c->d_win_nid.p;
+        Pp.n_nid = c->n_win;
+        Pp.nid_chunk = (int)std::min<size_t>(1024, (sc_smem / sizeof(float)) & ~(size_t)3);
+    }
     Sp.accumulate = accumulate;
     Sp.pair_base = 0;
     Sp.win_base = 0;
@@ -5239,8 +5260,9 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
         });
         if (rc) return rc;
     }
-    if (accumulate && Pp.n_items > 0) {
-        rc = timed_launch(c, 1, st, [&] { k_point_sc<<<Pp.n_items, kScThreads, c->sc_smem_max, st>>>(Pp); });
+    if (accumulate && Pp.n_nid + Pp.n_items > 0) {
+        rc = timed_launch(c, 1, st,
+                          [&] { k_point_sc<<<Pp.n_nid + Pp.n_items, kScThreads, sc_smem, st>>>(Pp); });
         if (rc) return rc;
     }
     if (c->host_stitch) {

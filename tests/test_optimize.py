@@ -27,7 +27,10 @@ from ldso_amd import _lib as L
 from ldso_amd import synth
 
 CONVERGES = dict(synth.S7, seed=62)           # canbreak at iteration 3 (criterion ratios 1.32 -> 0.79)
-RUNS_ALL = dict(n_frames=5, n_points=500, seed=61)  # no canbreak within 6 iterations
+RUNS_ALL = dict(synth.S7, seed=63)            # no canbreak within 6 iterations (ratios >= 1.31)
+# (A 5-frame / 500-point window that never converges -- steps 7-50x the thresholds at every
+# iteration -- drifts 3.5e-4 in energy from the host loop by its 4th pass: its x follows the 1e-6
+# reassociation differences of H chaotically.  The S7 windows stay within 2e-6 over 6 passes.)
 
 
 def frame_step(frames, x, cval, czero):
@@ -161,6 +164,8 @@ def check_against_host(cfg, e_dev, fr_dev, c_dev, idep_dev, its_dev, st_dev, n_i
     print(f"{cfg}: host {its_host} its status {st_host}, device {its_dev} status {st_dev}; ratios\n{ratios}")
     assert (its_dev, st_dev) == (its_host, st_host)
     passes = len(e_host)
+    for s in range(passes):
+        print(f"pass {s}: device {e_dev[s]}, host {e_host[s]}, rel {abs(e_dev[s, 0] / e_host[s][0] - 1):.3g}")
     assert e_dev[0, 2] == e_host[0][2] and abs(e_dev[0, 0] - e_host[0][0]) <= 1e-12 * abs(e_host[0][0])
     for s in range(1, passes):
         assert abs(e_dev[s, 0] - e_host[s][0]) <= 1e-4 * abs(e_host[s][0]), (s, e_dev[s], e_host[s])

@@ -1,0 +1,26 @@
+# round-4 GPU session: the optimize tests first, then the whole GPU suite, smoke, a bench line.
+# usage: tools/gpu_r4.sh TAG [bench|prof|pmc]...
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+TAG=${1:-x}; shift
+PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+timeout -k 10 300 $PYT tests/test_optimize.py -m gpu > gpurun_out/pytest_opt_$TAG.log 2>&1 || { echo "optimize tests failed"; tail -60 gpurun_out/pytest_opt_$TAG.log; exit 1; }
+tail -3 gpurun_out/pytest_opt_$TAG.log
+timeout -k 10 900 $PYT tests -m gpu > gpurun_out/pytest_$TAG.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_$TAG.log; exit 1; }
+tail -3 gpurun_out/pytest_$TAG.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
+for step in "$@"; do
+  case $step in
+    bench)
+      timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+      cat gpurun_out/bench_$TAG.json ;;
+    prof)
+      export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-secondary > gpurun_out/prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.log; exit 1; } ;;
+    pmc)
+      timeout -k 10 900 python tools/pmc_traffic.py > gpurun_out/pmc_$TAG.log 2>&1 || { echo "pmc failed"; tail -30 gpurun_out/pmc_$TAG.log; exit 1; }
+      tail -30 gpurun_out/pmc_$TAG.log ;;
+  esac
+done
+echo done
