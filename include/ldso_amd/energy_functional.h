@@ -115,6 +115,7 @@ struct CalibHessian {
 
 struct FrameHessian {
     int idx = 0;                       // position in the window (makeIDX)
+    void *user = nullptr;              // the caller's back-pointer (e.g. the reference object), untouched
     int frameID = 0;                   // keyframe id: 0 carries getPrior()'s strong pose prior
     bool flaggedForMarginalization = false;
     double worldToCam_evalPT[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};  // [R | t], row-major
@@ -144,6 +145,7 @@ struct PointHessian {
     PointStatus status = PointStatus::ACTIVE;
     bool alreadyRemoved = false;
     int idxInPoints = -1;
+    void *user = nullptr;  // the caller's back-pointer (e.g. the reference object), untouched
     // PointHessian::setIdepth / setIdepthZero (PointHessian.h)
     void setIdepth(float x) {
         idepth = x;
@@ -198,6 +200,7 @@ struct PointFrameResidual {
     bool isLinearized = false;
     bool isActiveAndIsGoodNEW = false;
     EnergyFunctional *ef = nullptr;   // set by EnergyFunctional::insertResidual, cleared on removal
+    void *user = nullptr;             // the caller's back-pointer (e.g. the reference object), untouched
     int mirrorIdx = -1;               // position in the EnergyFunctional's device mirror
 };
 

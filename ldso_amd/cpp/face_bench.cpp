@@ -11,7 +11,8 @@
 //   shim            INTEGRATION.md §3's reference-side forwarding around one FullSystem::optimize
 //                   (copy-in, optimize, copy-back, linearizeAll(true), residual / point copy-out)
 //                   on stand-ins for the reference's heap objects: the copy loops alone, through
-//                   std::unordered_map (as §3 writes it) and through index vectors
+//                   std::unordered_map (as §3 wrote it in round 3) and by walking the face's own
+//                   containers with the objects' `user` back-pointers (§3 now)
 //   optimize_full   the same + setAdjointsF + setDeltaF + linearizeAll(true) with the complete
 //                   residual / point write-back: everything FullSystem::optimize asks of the
 //                   backend after the frontend's setEvalPT
@@ -164,42 +165,66 @@ int main(int argc, char **argv) {
     std::unordered_map<RefFrame *, FrameHessian *> mf;
     std::unordered_map<RefPoint *, PointHessian *> mp;
     std::unordered_map<RefResidual *, PointFrameResidual *> mr;
-    std::vector<std::pair<RefFrame *, FrameHessian *>> vf;
-    std::vector<std::pair<RefPoint *, PointHessian *>> vp;
-    std::vector<std::pair<RefResidual *, PointFrameResidual *>> vr;
     for (auto &F : ef->frames) {
         rframes.emplace_back(new RefFrame());
         mf[rframes.back().get()] = F.get();
-        vf.emplace_back(rframes.back().get(), F.get());
+        F->user = rframes.back().get();
     }
     for (auto &Pt : ef->allPoints) {
         rpoints.emplace_back(new RefPoint());
         mp[rpoints.back().get()] = Pt.get();
-        vp.emplace_back(rpoints.back().get(), Pt.get());
+        Pt->user = rpoints.back().get();
         for (auto &r : Pt->residuals) {
             rres.emplace_back(new RefResidual());
             mr[rres.back().get()] = r.get();
-            vr.emplace_back(rres.back().get(), r.get());
+            r->user = rres.back().get();
         }
     }
+    // the replacement: walk the face's own containers (frames, allPoints, each point's residuals:
+    // contiguous, in the device's order) and reach the reference object through `user`
+    struct FaceFrames {
+        EnergyFunctional &e;
+        struct It {
+            std::vector<shared_ptr<FrameHessian>>::iterator i;
+            std::pair<RefFrame *, FrameHessian *> operator*() const { return {(RefFrame *)(*i)->user, i->get()}; }
+            It &operator++() { ++i; return *this; }
+            bool operator!=(const It &o) const { return i != o.i; }
+        };
+        It begin() { return {e.frames.begin()}; }
+        It end() { return {e.frames.end()}; }
+    } vf{*ef};
+    struct FacePoints {
+        EnergyFunctional &e;
+        struct It {
+            std::vector<shared_ptr<PointHessian>>::iterator i;
+            std::pair<RefPoint *, PointHessian *> operator*() const { return {(RefPoint *)(*i)->user, i->get()}; }
+            It &operator++() { ++i; return *this; }
+            bool operator!=(const It &o) const { return i != o.i; }
+        };
+        It begin() { return {e.allPoints.begin()}; }
+        It end() { return {e.allPoints.end()}; }
+    } vp{*ef};
+    std::vector<std::pair<RefResidual *, PointFrameResidual *>> vr;  // rebuilt at makeIDX in a real shim
+    for (auto &Pt : ef->allPoints)
+        for (auto &r : Pt->residuals) vr.emplace_back((RefResidual *)r->user, r.get());
     // the copy loops of one FullSystem::optimize through the shim (§3: "replaces
     // FullSystem.cc:853-970" and FullSystem::linearizeAll), without the face calls themselves
     auto shim_loops = [&](auto &F, auto &Pm, auto &Rm) {
-        for (auto &kv : F) std::memcpy(kv.second->state, kv.first->state, sizeof(kv.first->state));  // copyIn
-        for (auto &kv : Pm) {
+        for (auto kv : F) std::memcpy(kv.second->state, kv.first->state, sizeof(kv.first->state));  // copyIn
+        for (auto kv : Pm) {
             kv.second->setIdepth(kv.first->idepth);
             kv.second->setIdepthZero(kv.first->idepth_zero);
         }
         // ... gpu->optimize(...) ...
-        for (auto &kv : F) std::memcpy(kv.first->state, kv.second->state, sizeof(kv.first->state));
-        for (auto &kv : Pm) {
+        for (auto kv : F) std::memcpy(kv.first->state, kv.second->state, sizeof(kv.first->state));
+        for (auto kv : Pm) {
             kv.first->idepth = kv.second->idepth;
             kv.first->idepth_zero = kv.second->idepth_zero;
         }
         // FullSystem::linearizeAll(true): copy-in, gpu->linearizeAll, copy-out
-        for (auto &kv : F) std::memcpy(kv.second->state, kv.first->state, sizeof(kv.first->state));
-        for (auto &kv : Pm) kv.second->setIdepth(kv.first->idepth);
-        for (auto &kv : Rm) {
+        for (auto kv : F) std::memcpy(kv.second->state, kv.first->state, sizeof(kv.first->state));
+        for (auto kv : Pm) kv.second->setIdepth(kv.first->idepth);
+        for (auto kv : Rm) {
             RefResidual &r = *kv.first;
             const PointFrameResidual &g = *kv.second;
             r.state_state = (int)g.state_state;
@@ -211,7 +236,7 @@ int main(int argc, char **argv) {
             r.isActiveAndIsGoodNEW = g.isActiveAndIsGoodNEW;
             std::memcpy(r.JpJdF, g.JpJdF, sizeof(r.JpJdF));
         }
-        for (auto &kv : Pm) {
+        for (auto kv : Pm) {
             kv.first->HdiF = kv.second->HdiF;
             kv.first->bdSumF = kv.second->bdSumF;
             kv.first->idepth_hessian = kv.second->idepth_hessian;
@@ -289,14 +314,14 @@ int main(int argc, char **argv) {
         "\"optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f, \"iterations\": %d, "
         "\"iterations_default\": %d}, "
         "\"shim\": {\"what\": \"INTEGRATION.md 3 copy loops of one FullSystem::optimize, %d residuals, %d points, "
-        "caches evicted between calls\", \"unordered_map_ms\": %.6f, \"index_vector_ms\": %.6f, "
+        "caches evicted between calls\", \"unordered_map_ms\": %.6f, \"back_pointer_ms\": %.6f, "
         "\"shim_ms_per_gn_iteration\": %.6f, \"unordered_map_ms_per_gn_iteration\": %.6f, "
         "\"frac_of_face_gn_iteration\": %.4f, \"unordered_map_frac_of_face_gn_iteration\": %.4f}, "
         "\"optimize_full\": {\"ms\": %.6f, \"what\": \"optimize(6) + setAdjointsF + setDeltaF + linearizeAll(true) "
         "with the residual / point write-back\"}, "
         "\"c_abi_optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f}, "
         "\"flag_loop\": {\"residuals\": %d, \"ms\": %.6f, \"device_passes\": %ld}}\n",
-        n_its, reps, ok ? "true" : "false", ms_opt, ms_opt / n_its, n_its, its_default, (int)vr.size(), (int)vp.size(),
+        n_its, reps, ok ? "true" : "false", ms_opt, ms_opt / n_its, n_its, its_default, (int)vr.size(), (int)ef->allPoints.size(),
         ms_shim_map, ms_shim_vec, ms_shim_vec / n_its, ms_shim_map / n_its, ms_shim_vec / ms_opt, ms_shim_map / ms_opt,
         ms_full, ms_raw, ms_raw / n_its, nres, ms_flag, flag_passes);
     return ok ? 0 : 1;
