@@ -1,30 +1,34 @@
 // ldso_ba.hip -- MI355X (gfx950) kernels and C ABI of LDSO's photometric-BA hot path.
 //
-// One Gauss-Newton pass over every loaded window (ldso_ba_linearize) is three stream-ordered
-// launches plus a memset of the packed systems:
+// One Gauss-Newton pass over every loaded window (ldso_ba_linearize) is four stream-ordered
+// launches:
 //
-//   k_linearize   one wavefront per <= 64-residual chunk of one (host,target) bucket: linearize
-//                 (Residuals.cc:15-217) with 8 lanes per residual (one per pattern pixel),
-//                 applyRes (Residuals.h:70-88) with a lane per residual, and the chunk's
-//                 AccumulatorApprox block (AccumulatedTopHessian.cc:66-99,
-//                 MatrixAccumulators.h:893-1045) as 32 fp32 MFMAs into a 96-float partial.  The
-//                 pair precalc, frame thresholds and image base are wave-uniform (scalar loads);
-//                 the vector traffic is the point record and 12 intensity taps per pattern pixel
-//                 from band-interleaved frames (band_offset) via buffer loads.
-//   k_point_sc    per point: Hdd/bd/Hcd sums (AccumulatedTopHessian.cc:94-116), HdiF
-//                 (AccumulatedSCHessian.cc:24-33); then the Schur terms of a 64-point chunk of one
-//                 host as one symmetric rank-64 update G += U^T diag(HdiF) U staged in LDS (the
-//                 accD/accE/accEB/accHcc/accbc sums of AccumulatedSCHessian.cc:35-50).
-//   k_stitch      block per (host,target) pair: the Top adjoint sandwiches
-//                 (AccumulatedTopHessian.cc:213-239) and the SC sandwiches for (i=h, j=t)
-//                 (AccumulatedSCHessian.cc:80-114) in double, one contribution record per
-//                 (pair, block); one block per window runs setNewFrameEnergyTH
-//                 (FullSystem.cc:2078-2109) as a radix select and sums the linearizeAll energy.
-//   k_stitch_sum  thread per packed output element: its contribution records summed in one fixed
-//                 pair order (no atomics: the stitched system is bitwise repeatable).
+//   k_linearize        one wavefront per <= 64-residual chunk of one (host,target) bucket:
+//                      linearize (Residuals.cc:15-217) with 8 lanes per residual (one per pattern
+//                      pixel; the residual's tap footprint loaded as 16-B band columns into an LDS
+//                      box, phase_a_pieces), applyRes (Residuals.h:70-88) with a lane per residual,
+//                      and the chunk's AccumulatorApprox block (AccumulatedTopHessian.cc:66-99,
+//                      MatrixAccumulators.h:893-1045) as 32 fp32 MFMAs into a 96-float partial.
+//                      The pair precalc, frame thresholds and image base are wave-uniform.
+//   k_point_sc         per point: Hdd/bd/Hcd sums (AccumulatedTopHessian.cc:94-116), HdiF
+//                      (AccumulatedSCHessian.cc:24-33); then the Schur terms of a 64-point chunk of
+//                      one host as one symmetric rank-64 update G += U^T diag(HdiF) U staged in LDS
+//                      (the accD/accE/accEB/accHcc/accbc sums of AccumulatedSCHessian.cc:35-50).
+//                      Inside ldso_ba_optimize its leading blocks also sum doStepFromBackup's sumNID.
+//   k_stitch_host      block per host frame (windows of up to 12 keyframes): the host's dense
+//                      partial {HA, bA, Hsc, bsc} from its Top blocks and chunk SYRK partials
+//                      (AccumulatedTopHessian.cc:213-239, AccumulatedSCHessian.cc:80-114) in double;
+//                      one block per window runs setNewFrameEnergyTH (FullSystem.cc:2078-2109) as a
+//                      radix select and sums the linearizeAll energy.
+//   k_stitch_host_sum  thread per packed output element: the window's host partials summed in host
+//                      order (no atomics: the stitched system is bitwise repeatable).
+// Windows of 13-16 keyframes use k_stitch + k_stitch_sum instead (one contribution record per
+// (pair, block), summed in a fixed pair order).
 //
-// Outside the pass: k_resubstitute (resubstituteFPt, EnergyFunctional.cc:638-667), k_tile_image
-// (image staging at load/update), k_export_newest + k_frame_th (sharded threshold exchange).
+// Outside the pass: the device solve (k_solve_fast; exact mode k_solve_reg / k_solve), k_step_resub
+// (doStepFromBackup + setPrecalcValues + resubstituteFPt inside ldso_ba_optimize), k_resubstitute,
+// k_activate (optimizeImmaturePoint), k_tile_image / k_intensity_image (image staging at load),
+// k_export_newest + k_frame_th (sharded threshold exchange), k_pack_out (results to mapped memory).
 //
 // The per-residual arithmetic of k_linearize is compiled with contraction off and follows the
 // reference's statement order, so states, energies, JpJdF and the per-point sums are
@@ -446,14 +450,18 @@ constexpr int kTermQ = 9;                      // quantities per transposition r
 #endif
 constexpr int kBoxCols = 9, kBoxBands = 3, kBoxFloats = LDSO_LIN_BOX_STRIDE;
 static_assert(kBoxFloats >= (kBoxCols * kBoxBands + 1) * 4, "box");
+#ifndef LDSO_LIN_ONE_ROUND
+#define LDSO_LIN_ONE_ROUND 0  // phase A's pattern-order sums: all 17 quantities in one LDS transposition round
+#endif
 #ifndef LDSO_LIN_T_STRIDE
-#define LDSO_LIN_T_STRIDE 72
+#define LDSO_LIN_T_STRIDE (LDSO_LIN_ONE_ROUND ? 136 : 72)
 #endif
 // floats between the 8 residuals' term tables of a step (72 = dense; 76 halves the bank conflicts of
 // the pattern-order sums' 16-B reads)
 constexpr int kTermStride = LDSO_LIN_T_STRIDE;
-static_assert(kTermStride >= kTermQ * 8 && 8 * kTermStride <= 8 * kBoxFloats, "term tables");
-constexpr int kTermsOnly = 8 * kTermQ * 8;       // per-pixel addends of one round [8 residuals][9][8]
+constexpr int kRoundQ = LDSO_LIN_ONE_ROUND ? kSums : kTermQ;  // quantities per transposition round
+static_assert(kTermStride >= kRoundQ * 8, "term tables");
+constexpr int kTermsOnly = 8 * kTermStride;      // per-pixel addends of one round [8 residuals][kRoundQ][8]
 // the terms region also holds the 8 residuals' footprint boxes of a step (used before the terms)
 constexpr int kTermsPerWave = LDSO_LIN_PIECES ? (8 * kBoxFloats > kTermsOnly ? 8 * kBoxFloats : kTermsOnly) : kTermsOnly;
 constexpr int kSumsPerWave = 64 * kSumStride;   // per-residual sums [64][17]
@@ -658,14 +666,16 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
         const int ix = pok ? (int)q.Ku : 1, iy = pok ? (int)q.Kv : 1;
         // the box: columns from min(ix) - 1, bands from that of min(iy) - 1
         const int cx0 = grp8_min(ix) - 1, b0 = (grp8_min(iy) - 1) >> 2;
-        const int rx = ix - cx0;
-        const int bA = ((iy - 1) >> 2) - b0, bB = (iy >> 2) - b0, bC = ((iy + 1) >> 2) - b0,
-                  bD = ((iy + 2) >> 2) - b0;
+        const int rx = ix - cx0;  // >= 1
+        // rows iy-1 / iy+2 use columns ix, ix+1 (pattern 0110 from column ix-1), rows iy, iy+1
+        // columns ix-1 .. ix+2 (1111).  The four rows lie in band bA = band(iy-1) and, from row
+        // 4 - ph on (ph = (iy-1) & 3), in band bA + 1: the columns needed in band bA are 1111 unless
+        // only row iy-1 is there (ph 3: 0110); in band bA + 1 none (ph 0), row iy+2 only (ph 1:
+        // 0110) or 1111 (ph 2, 3)
+        const int ph = (iy - 1) & 3, bA = ((iy - 1) >> 2) - b0, bD = bA + (ph != 0 ? 1 : 0);
+        const int colA = ph == 3 ? 6 : 15, colB = ph == 0 ? 0 : ph == 1 ? 6 : 15;
         const bool wide_l = rx + 2 >= kBoxCols || bD >= kBoxBands;
-        // rows iy-1 / iy+2 use columns ix, ix+1, rows iy, iy+1 columns ix-1 .. ix+2
-        int m = wide_l ? 0
-                       : (3 << (bA * kBoxCols + rx)) | (15 << (bB * kBoxCols + rx - 1)) |
-                             (15 << (bC * kBoxCols + rx - 1)) | (3 << (bD * kBoxCols + rx));
+        int m = wide_l ? 0 : (colA | (colB << kBoxCols)) << (bA * kBoxCols + rx - 1);
         m = grp8_or(m);
         const unsigned long long mw = __ballot(wide_l);
         q.wide = ((mw >> (8 * g)) & 0xFFull) != 0;
@@ -701,13 +711,12 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     // the 12 taps of the lane's pixel from the residual's box
     auto box_taps = [&](const Geo8 &q, float *iv) {
         const int ix = (int)q.Ku, iy = (int)q.Kv;
-        // row y of column ix - 1: box float (((y >> 2) - b0) * 9 + ix - 1 - cx0) * 4 + (y & 3); the next
-        // columns are 4 floats apart
-        const int c = ix - 1 - q.cx0;
-        const float *r0 = box + ((((iy - 1) >> 2) - q.b0) * kBoxCols + c) * 4 + ((iy - 1) & 3);
-        const float *r1 = box + (((iy >> 2) - q.b0) * kBoxCols + c) * 4 + (iy & 3);
-        const float *r2 = box + ((((iy + 1) >> 2) - q.b0) * kBoxCols + c) * 4 + ((iy + 1) & 3);
-        const float *r3 = box + ((((iy + 2) >> 2) - q.b0) * kBoxCols + c) * 4 + ((iy + 2) & 3);
+        // row y of column ix - 1: box float (((y >> 2) - b0) * 9 + ix - 1 - cx0) * 4 + (y & 3)
+        // = y + 32 (y >> 2) + 4 (ix - 1 - cx0) - 36 b0; the next columns are 4 floats apart
+        static_assert(kBoxCols == 9, "row offsets below assume 9 columns of 4 floats per band");
+        const int base = 4 * (ix - 1 - q.cx0) - 36 * q.b0;
+        auto row = [&](int y) { return box + (y + ((y >> 2) << 5) + base); };
+        const float *r0 = row(iy - 1), *r1 = row(iy), *r2 = row(iy + 1), *r3 = row(iy + 2);
         iv[0] = r0[4];
         iv[1] = r0[8];
         iv[2] = r1[0];
@@ -753,6 +762,21 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
             S[j * kSumStride + qq] = sum;
         };
         wave_lds_sync();  // every box read is done before the terms overwrite the boxes
+#if LDSO_LIN_ONE_ROUND
+        if (part) {
+#pragma unroll
+            for (int e = 0; e < kSums; e++) T[e * 8 + sl] = tt[e];
+        }
+        wave_lds_sync();
+        if (rok) {
+            sum8(sl, sl);
+            sum8(8 + sl, 8 + sl);
+            if (sl == 0) sum8(16, 16);
+        } else if (owner && sl == 0 && j < jlimit) {
+            S[j * kSumStride] = -1.0f;  // energy slot: pattern not ok
+        }
+        wave_lds_sync();
+#else
         if (part) {
 #pragma unroll
             for (int e = 0; e < kTermQ; e++) T[e * 8 + sl] = tt[e];
@@ -772,6 +796,7 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
         wave_lds_sync();
         if (rok) sum8(kTermQ + sl, sl);
         wave_lds_sync();
+#endif
     };
     Geo8 cur, nxt;
     pc[3] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1194,6 +1219,10 @@ __device__ void point_nid(const PointParams &P, int w, float *lds) {
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
 constexpr int kScBatch = 2;  // residual records per round trip (4 and 8 measured equal, r2)
+#ifndef LDSO_SC_SPLIT_GATHER
+#define LDSO_SC_SPLIT_GATHER 0  // both waves gather: point terms (wave 0) and JpJdF (wave 1) at once
+#endif
+constexpr int kScGather = 6;  // records per wave per round trip in the split gather (S7: all six)
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     if ((int)blockIdx.x < P.n_nid) {
@@ -1211,6 +1240,99 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int tid = threadIdx.x;
     for (int i = tid; i < 64 * KP; i += blockDim.x) U[i] = 0;
     __syncthreads();
+#if LDSO_SC_SPLIT_GATHER
+    // the two waves gather the block's records at once: wave 0 the point terms of every residual
+    // (Hcd_r, Hdd_r, bd_r, active: record float4s 2-3), summed in residual order, wave 1 the JpJdF of
+    // the active ones (float4s 0-1, with 3 for the active flag) into the point's U row
+    const int pl = tid & 63;
+    if (pl < it.y) {
+#pragma clang fp contract(off)
+        const int p = it.x + pl;
+        const int nres = P.pt_nres[p];
+        const unsigned long long tgs = P.pt_tgt[p];
+        const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * 4;
+        const size_t sstride = (size_t)W.P * 4;
+        auto rec_of = [&](int k) {
+            const int tg = (int)((tgs >> (4 * k)) & 15ull);
+            return rp + (tg < host ? tg : tg - 1) * sstride;
+        };
+        float *row = U + pl * KP;
+        if (tid < 64) {
+            float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
+            int ngood = 0;
+            for (int k0 = 0; k0 < nres; k0 += kScGather) {
+                float4 hc[kScGather], hb[kScGather];
+#pragma unroll
+                for (int u = 0; u < kScGather; u++) {
+                    const float4 *q = rec_of(min(k0 + u, nres - 1));
+                    hc[u] = q[2];
+                    hb[u] = q[3];
+                }
+#pragma unroll
+                for (int u = 0; u < kScGather; u++) {
+                    if (k0 + u >= nres || hb[u].z == 0.0f) continue;
+                    ngood++;
+                    bd += hb[u].y;
+                    hdd += hb[u].x;
+                    hcd[0] += hc[u].x;
+                    hcd[1] += hc[u].y;
+                    hcd[2] += hc[u].z;
+                    hcd[3] += hc[u].w;
+                }
+            }
+            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+            const float priorF = pd[4], deltaF = pd[5];
+            float HdiF = 0, bdSum = 0, ih = 0;
+            if (ngood > 0) {
+                // AccumulatedSCHessian.cc:24-33 (Hdd_accLF = bd_accLF = Hcd_accLF = 0 in the hot path)
+                float H = hdd + 0.0f + priorF;
+                if (H < 1e-10f) H = 1e-10f;
+                ih = H;
+                HdiF = (float)(1.0 / (double)H);
+                bdSum = bd + 0.0f;
+                if (P.shift_prior) bdSum += priorF * deltaF;
+                row[Kj + 0] = hcd[0] + 0.0f;
+                row[Kj + 1] = hcd[1] + 0.0f;
+                row[Kj + 2] = hcd[2] + 0.0f;
+                row[Kj + 3] = hcd[3] + 0.0f;
+                row[Kj + 4] = bdSum;
+            }
+            Wt[pl] = HdiF;
+            float *o = P.pt_out + (size_t)p * 12;
+            o[0] = HdiF;
+            o[1] = bdSum;
+            o[2] = ih;
+            o[3] = hdd;
+            o[4] = bd;
+            o[5] = hcd[0];
+            o[6] = hcd[1];
+            o[7] = hcd[2];
+            o[8] = hcd[3];
+            o[9] = (float)ngood;
+        } else {
+            for (int k0 = 0; k0 < nres; k0 += kScGather) {
+                float4 j0[kScGather], j1[kScGather];
+                float act[kScGather];
+#pragma unroll
+                for (int u = 0; u < kScGather; u++) {
+                    const float4 *q = rec_of(min(k0 + u, nres - 1));
+                    j0[u] = q[0];
+                    j1[u] = q[1];
+                    act[u] = q[3].z;
+                }
+#pragma unroll
+                for (int u = 0; u < kScGather; u++) {
+                    const int k = k0 + u;
+                    if (k >= nres || act[u] == 0.0f) continue;
+                    const int tg = (int)((tgs >> (4 * k)) & 15ull);
+                    const int slot = tg < host ? tg : tg - 1;
+                    *(float4 *)(row + 8 * slot) = j0[u];
+                    *(float4 *)(row + 8 * slot + 4) = j1[u];
+                }
+            }
+        }
+    }
+#else
     if (tid < it.y) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
@@ -1283,6 +1405,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         o[8] = hcd[3];
         o[9] = (float)ngood;
     }
+#endif
     __syncthreads();
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
     syrk_tiles(U, Wt, KP, nt, ntiles, it.y,

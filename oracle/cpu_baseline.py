@@ -148,7 +148,9 @@ def main():
     common = {"unit": "point-residuals/s", "kind": "port", "cpu_model": info.get("Model name"),
               "sockets": info.get("Socket(s)"), "cores_per_socket": info.get("Core(s) per socket"),
               "threads_per_core": info.get("Thread(s) per core"),
-              "flags": "g++ " + " ".join(oracle.NATIVE_FLAGS) + " (FP contraction: compiler default)"}
+              "flags": "g++ " + " ".join(oracle.NATIVE_FLAGS) + " (FP contraction: compiler default); scalar "
+                       "restatement auto-vectorised by g++, as the reference's own timed path (no SSE intrinsics "
+                       "on it: BASELINE.md §2)"}
     out = {}
     r6 = run(lib_path, 6, a.seconds)
     out["six_threads"] = dict(common, cores=6, **{k: v for k, v in r6.items()},
