@@ -24,6 +24,7 @@
 #include <cstring>
 #include <memory>
 #include <random>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -224,9 +225,7 @@ int main(int argc, char **argv) {
         // FullSystem::linearizeAll(true): copy-in, gpu->linearizeAll, copy-out
         for (auto kv : F) std::memcpy(kv.second->state, kv.first->state, sizeof(kv.first->state));
         for (auto kv : Pm) kv.second->setIdepth(kv.first->idepth);
-        for (auto kv : Rm) {
-            RefResidual &r = *kv.first;
-            const PointFrameResidual &g = *kv.second;
+        auto copy_out = [](RefResidual &r, const PointFrameResidual &g) {
             r.state_state = (int)g.state_state;
             r.state_NewState = (int)g.state_NewState;
             r.state_energy = g.state_energy;
@@ -235,6 +234,19 @@ int main(int argc, char **argv) {
             std::memcpy(r.centerProjectedTo, g.centerProjectedTo, sizeof(r.centerProjectedTo));
             r.isActiveAndIsGoodNEW = g.isActiveAndIsGoodNEW;
             std::memcpy(r.JpJdF, g.JpJdF, sizeof(r.JpJdF));
+        };
+        if constexpr (std::is_same_v<std::decay_t<decltype(Rm)>, std::vector<std::pair<RefResidual *, PointFrameResidual *>>>) {
+            // the objects are scattered on the heap: prefetch a few residuals ahead
+            const size_t n = Rm.size();
+            for (size_t k = 0; k < n; k++) {
+                if (k + 8 < n) {
+                    __builtin_prefetch(Rm[k + 8].first, 1);
+                    __builtin_prefetch(Rm[k + 8].second, 0);
+                }
+                copy_out(*Rm[k].first, *Rm[k].second);
+            }
+        } else {
+            for (auto kv : Rm) copy_out(*kv.first, *kv.second);
         }
         for (auto kv : Pm) {
             kv.first->HdiF = kv.second->HdiF;

@@ -392,10 +392,10 @@ __device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int 
         const float *pa = U + 4 * a, *pb = U + 4 * bb;
 #pragma unroll 4
         for (int p = 0; p < cnt; p++, pa += KP, pb += KP) {
-            const float w = Wt[p];
             const float4 ua = *(const float4 *)pa;
             const float4 ub = *(const float4 *)pb;
-            const f2 a01 = f2{ua.x, ua.y} * w, a23 = f2{ua.z, ua.w} * w;
+            (void)Wt;  // the rows carry sqrt(HdiF): U'^T U' = U^T diag(HdiF) U
+            const f2 a01 = f2{ua.x, ua.y}, a23 = f2{ua.z, ua.w};
             const f2 b01 = {ub.x, ub.y}, b10 = {ub.y, ub.x}, b23 = {ub.z, ub.w}, b32 = {ub.w, ub.z};
             c[0] += a01 * b01;  // (0,0) (1,1)
             c[1] += a01 * b10;  // (0,1) (1,0)
@@ -437,33 +437,18 @@ __device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kTopRow = 36;
 constexpr int kTermQ = 9;                      // quantities per transposition round (17 = 9 + 8)
-#ifndef LDSO_LIN_PIECE8_SKIP
-#define LDSO_LIN_PIECE8_SKIP 1  // skip the 9th-column load when no residual of the step needs it
-#endif
-#ifndef LDSO_LIN_PIECES
-#define LDSO_LIN_PIECES 1  // layout 3: tap footprints loaded as 16-B band columns through LDS (0: 12 gathers per lane)
-#endif
-// k_linearize footprint box of one residual (layout 3, LDSO_LIN_PIECES): 3 bands x 9 columns of
+// k_linearize footprint box of one residual (layout 3): 3 bands x 9 columns of
 // 16-B band-column pieces (4 rows each) + one dummy slot, in floats
-#ifndef LDSO_LIN_BOX_STRIDE
-#define LDSO_LIN_BOX_STRIDE 112
-#endif
-constexpr int kBoxCols = 9, kBoxBands = 3, kBoxFloats = LDSO_LIN_BOX_STRIDE;
+constexpr int kBoxCols = 9, kBoxBands = 3, kBoxFloats = 112;
 static_assert(kBoxFloats >= (kBoxCols * kBoxBands + 1) * 4, "box");
-#ifndef LDSO_LIN_ONE_ROUND
-#define LDSO_LIN_ONE_ROUND 0  // phase A's pattern-order sums: all 17 quantities in one LDS transposition round
-#endif
-#ifndef LDSO_LIN_T_STRIDE
-#define LDSO_LIN_T_STRIDE (LDSO_LIN_ONE_ROUND ? 136 : 72)
-#endif
 // floats between the 8 residuals' term tables of a step (72 = dense; 76 halves the bank conflicts of
 // the pattern-order sums' 16-B reads)
-constexpr int kTermStride = LDSO_LIN_T_STRIDE;
-constexpr int kRoundQ = LDSO_LIN_ONE_ROUND ? kSums : kTermQ;  // quantities per transposition round
+constexpr int kTermStride = 72;
+constexpr int kRoundQ = kTermQ;
 static_assert(kTermStride >= kRoundQ * 8, "term tables");
 constexpr int kTermsOnly = 8 * kTermStride;      // per-pixel addends of one round [8 residuals][kRoundQ][8]
 // the terms region also holds the 8 residuals' footprint boxes of a step (used before the terms)
-constexpr int kTermsPerWave = LDSO_LIN_PIECES ? (8 * kBoxFloats > kTermsOnly ? 8 * kBoxFloats : kTermsOnly) : kTermsOnly;
+constexpr int kTermsPerWave = 8 * kBoxFloats > kTermsOnly ? 8 * kBoxFloats : kTermsOnly;
 constexpr int kSumsPerWave = 64 * kSumStride;   // per-residual sums [64][17]
 
 __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, const Geo &g, const PhotoSums &s,
@@ -487,17 +472,8 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
     const bool geo = i < 10, ind = i >= 13;
     const float a0c = i == 13 ? 1.f : 0.f, a1c = i == 14 ? 1.f : 0.f;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#if LDSO_LIN_TOP_FULL
-    {  // every residual's row at once; K rows (residual 32 half + 8 kk + m, c), half by half as below
-        float4 *row = reinterpret_cast<float4 *>(tab + lane * kTopRow);
-#pragma unroll
-        for (int k = 0; k < 9; k++) row[k] = v[k];
-    }
-    wave_lds_sync();
-#endif
 #pragma unroll
     for (int half = 0; half < 2; half++) {
-#if !LDSO_LIN_TOP_FULL
         if ((lane >> 5) == half) {
             float4 *row = reinterpret_cast<float4 *>(tab + (lane & 31) * kTopRow);
 #pragma unroll
@@ -505,9 +481,6 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
         }
         wave_lds_sync();
         const float *base = tab + kk * 8 * kTopRow;  // K rows (residual kk*8 + m, c)
-#else
-        const float *base = tab + (32 * half + kk * 8) * kTopRow;
-#endif
 #pragma unroll 4
         for (int m = 0; m < 8; m++) {
             const float *rr = base + m * kTopRow;
@@ -519,9 +492,7 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A0, B0, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A1, B1, acc, 0, 0, 0);
         }
-#if !LDSO_LIN_TOP_FULL
         wave_lds_sync();
-#endif
     }
     // lane holds D[4 kk + v][i]; scatter into the 96-slot partial layout read by k_stitch
 #pragma unroll
@@ -549,45 +520,27 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
 //   Top      the chunk's AccumulatorApprox block on the matrix cores (top_mfma).
 // kMarg: the marginalisation pass (addPoint<2> sums with fixLinearizationF's res_toZeroF).
 // ============================================================================================
-#ifndef LDSO_LIN_PT_TABLE
-#define LDSO_LIN_PT_TABLE 1  // phase A reads each residual's (u, v, idepth, state) from a per-wave LDS table
-#endif
-constexpr int kPtTable = LDSO_LIN_PT_TABLE ? 64 * 4 : 0;  // floats: [64 residuals][u, v, idepth, state]
-#ifndef LDSO_LIN_TOP_FULL
-#define LDSO_LIN_TOP_FULL 1  // the Top operand table holds all 64 residuals (one staging round, not two)
-#endif
-constexpr int kTopRows = LDSO_LIN_TOP_FULL ? 64 : 32;
+constexpr int kPtTable = 64 * 4;  // floats: [64 residuals][u, v, idepth, state]
+constexpr int kTopRows = 32;  // the Top operand table holds one half (32 residuals) at a time
+constexpr int kTopTab = kTopRows * kTopRow;
 constexpr int kWaveLdsA = kTermsPerWave + kSumsPerWave + kPtTable;
 // floats of LDS per wavefront (the Top operand table reuses the wave's region after phase B)
-constexpr int kWaveLds = kWaveLdsA > kTopRows * kTopRow ? kWaveLdsA : kTopRows * kTopRow;
+constexpr int kWaveLds = kWaveLdsA > kTopTab ? kWaveLdsA : kTopTab;
 // LDS requested per 4-wave workgroup: sets the resident workgroups per CU (= waves per SIMD).
 // 160 KB / 32 KB = 5: measured fastest (64 x S7: 121.6 us; 4 blocks 125.7, 3 blocks 143.5; 6
 // waves/SIMD need <= 80 VGPRs and spill, 145 us).
-#ifndef LDSO_LIN_CW_LDS
-#define LDSO_LIN_CW_LDS 1  // color / weights staged in the sums table (0: gathered per step)
-#endif
-#ifndef LDSO_LIN_BLOCKS_PER_CU
-#define LDSO_LIN_BLOCKS_PER_CU 4
-#endif
-#ifndef LDSO_LIN_MIN_BLOCKS
-#define LDSO_LIN_MIN_BLOCKS 4  // register budget: 4 waves / SIMD (106 VGPRs; 5 waves spill 44 B: 127.5 vs 117.4 us)
-#endif
-constexpr size_t kLinLdsBytes = (160 * 1024 / LDSO_LIN_BLOCKS_PER_CU) & ~(size_t)511;
+// 4 workgroups (16 waves) per CU: LDS (kLinLdsBytes) and the register budget of __launch_bounds__
+// (<= 128 VGPRs; 101 used).  5 per CU measured slower (r3: 127.5 vs 117.4 us with 44 B spilled; r4:
+// 123.7 vs 106.1 us, 32 B spilled, the pt table dropped for LDS)
+constexpr int kLinBlocksPerCu = 4;
+constexpr size_t kLinLdsBytes = (160 * 1024 / kLinBlocksPerCu) & ~(size_t)511;
 static_assert(kLinLdsBytes >= 4 * kWaveLds * sizeof(float), "k_linearize LDS");
-static_assert(!LDSO_LIN_PIECES || LDSO_LIN_CW_LDS, "the footprint path reads color / weights from the sums table");
 
 // 8-lane group reductions (lanes 8g .. 8g+7) on DPP: quad swaps, then the half-row mirror
 // (lane i <-> 7 - i) joins the two quads.
-#ifndef LDSO_LIN_DPP_MOV
-#define LDSO_LIN_DPP_MOV 1
-#endif
-#if LDSO_LIN_DPP_MOV
 // every lane active, full row / bank masks: no "old" value, so the DPP move can fold into the
 // min / or (one DPP-modified VALU op per stage instead of a copy, a DPP move and the op)
 #define LDSO_DPP(v, ctrl) __builtin_amdgcn_mov_dpp(v, ctrl, 0xF, 0xF, true)
-#else
-#define LDSO_DPP(v, ctrl) __builtin_amdgcn_update_dpp(v, v, ctrl, 0xF, 0xF, false)
-#endif
 __device__ __forceinline__ int grp8_min(int v) {
     v = min(v, LDSO_DPP(v, 0xB1));    // quad_perm [1,0,3,2]
     v = min(v, LDSO_DPP(v, 0x4E));    // quad_perm [2,3,0,1]
@@ -604,7 +557,7 @@ __device__ __forceinline__ float4 ldb4(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
 }
 
-// Phase A of k_linearize on image layout 3 with footprint pieces (LDSO_LIN_PIECES).  The 8 pattern
+// Phase A of k_linearize on image layout 3 with footprint pieces.  The 8 pattern
 // pixels of a residual read their 96 taps (12 each, load12's stencil) from the residual's tap
 // footprint: the 16-B band columns (4 rows of one column) that hold at least one of the taps,
 // i.e. exactly the 128-B lines the per-lane gathers touch.  The residual's 8 lanes load them with
@@ -640,15 +593,9 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     // projection of the lane's pattern pixel of residual 8k + g (Residuals.cc:128-135) and the box
     auto geo = [&](int k, Geo8 &q) {
         const int j = 8 * k + g;
-#if LDSO_LIN_PT_TABLE
         const float4 pt = *reinterpret_cast<const float4 *>(S + kSumsPerWave + 4 * (j & 63));
         const float pu = pt.x, pv = pt.y, pz = pt.z;
         const int st = __float_as_int(pt.w);
-#else
-        const int st = __shfl(my_state, j, kWave);
-        const float pu = __shfl(my_pd0.x, j, kWave), pv = __shfl(my_pd0.y, j, kWave),
-                    pz = __shfl(my_pd0.z, j, kWave);
-#endif
         const bool go = j < jlimit && st != LDSO_BA_RES_OOB;
         if constexpr (kMarg) {
             q.jx = __shfl(jp_dx, j, kWave);
@@ -693,19 +640,15 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
         for (int b = 0; b < kBoxBands; b++)
             pc[b] = ldb4(rsrc, (m >> (b * kBoxCols + sl)) & 1 ? base + b * band + col : kOOB);
         const bool n8 = sl < kBoxBands && ((m >> (sl * kBoxCols + 8)) & 1);
-#if LDSO_LIN_PIECE8_SKIP
         any8 = __ballot(n8) != 0;
         if (any8)
-#endif
             pc[3] = ldb4(rsrc, n8 ? base + sl * band + ((unsigned)(q.cx0 + 8) << 4) : kOOB);
     };
     auto store = [&]() {
         float4 *bx = reinterpret_cast<float4 *>(box);
 #pragma unroll
         for (int b = 0; b < kBoxBands; b++) bx[b * kBoxCols + sl] = pc[b];
-#if LDSO_LIN_PIECE8_SKIP
         if (any8)
-#endif
             bx[sl < kBoxBands ? sl * kBoxCols + 8 : kBoxBands * kBoxCols] = pc[3];
     };
     // the 12 taps of the lane's pixel from the residual's box
@@ -762,21 +705,6 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
             S[j * kSumStride + qq] = sum;
         };
         wave_lds_sync();  // every box read is done before the terms overwrite the boxes
-#if LDSO_LIN_ONE_ROUND
-        if (part) {
-#pragma unroll
-            for (int e = 0; e < kSums; e++) T[e * 8 + sl] = tt[e];
-        }
-        wave_lds_sync();
-        if (rok) {
-            sum8(sl, sl);
-            sum8(8 + sl, 8 + sl);
-            if (sl == 0) sum8(16, 16);
-        } else if (owner && sl == 0 && j < jlimit) {
-            S[j * kSumStride] = -1.0f;  // energy slot: pattern not ok
-        }
-        wave_lds_sync();
-#else
         if (part) {
 #pragma unroll
             for (int e = 0; e < kTermQ; e++) T[e * 8 + sl] = tt[e];
@@ -796,7 +724,6 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
         wave_lds_sync();
         if (rok) sum8(kTermQ + sl, sl);
         wave_lds_sync();
-#endif
     };
     Geo8 cur, nxt;
     pc[3] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -826,7 +753,7 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
 }
 
 template <int kImg, bool kMarg>
-__global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParams P) {
+__global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P) {
     static_assert(kImg == 1 || kImg == 3, "image layouts 1 and 3");
     extern __shared__ __attribute__((aligned(16))) float lds_dyn[];
     const int lane = threadIdx.x & 63;
@@ -866,7 +793,6 @@ __global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParam
     float new_energy = P.rs_newenergy[rq];
     float4 centre = P.rs_center[rq];
     const float4 my_pd0 = *(const float4 *)(P.pt_data + (size_t)my_point * LDSO_BA_POINT_STRIDE);
-#if LDSO_LIN_CW_LDS
     // the point's color[8] and weights[8] (record floats 8..23: one 64-B piece per residual)
     // into this residual's row of the sums table: phase A's pattern lanes read them from LDS at
     // the step that later overwrites the row with the residual's sums (no per-step gathers)
@@ -884,7 +810,6 @@ __global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParam
             row[4 * u + 3] = v[u].w;
         }
     }
-#endif
     if (!valid) my_state = LDSO_BA_RES_OOB;
     // marginalisation pass: Jp * delta of fixLinearizationF (Residuals.cc:221-232) from the centre
     // geometry, per residual, before the pattern pixels need it (dot products left to right)
@@ -915,15 +840,11 @@ __global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParam
     }
 
     // ---------------- phase A: pattern pixels, 8 residuals per step -------------------------
-#if LDSO_LIN_CW_LDS
     wave_lds_sync();  // every row's color / weights are in before any lane reads another's
-#endif
-    if constexpr (kImg == 3 && LDSO_LIN_PIECES) {
-#if LDSO_LIN_PT_TABLE
+    if constexpr (kImg == 3) {
         *reinterpret_cast<float4 *>(lds_sums_w + kSumsPerWave + 4 * lane) =
             make_float4(my_pd0.x, my_pd0.y, my_pd0.z, __int_as_float(my_state));
         wave_lds_sync();
-#endif
         phase_a_pieces<kMarg>(lane, lds_terms_w, lds_sums_w, pre, jlimit, my_state, my_pd0, jp_dx, jp_dy, da, db,
                               rsrc, band, wM3, hM3);
     } else {
@@ -956,15 +877,9 @@ __global__ __launch_bounds__(256, LDSO_LIN_MIN_BLOCKS) void k_linearize(LinParam
                 q.jx = __shfl(jp_dx, j, kWave);
                 q.jy = __shfl(jp_dy, j, kWave);
             }
-#if LDSO_LIN_CW_LDS
             (void)p;
             q.color = S[j * kSumStride + sl];
             q.weight = S[j * kSumStride + 8 + sl];
-#else
-            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-            q.color = pd[8 + sl];
-            q.weight = pd[16 + sl];
-#endif
             const float up = pu + px, vp = pv + py;
             float ptp[3];
 #pragma unroll
@@ -1218,17 +1133,14 @@ __device__ void point_nid(const PointParams &P, int w, float *lds) {
 }
 
 constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
-constexpr int kScBatch = 2;  // residual records per round trip (4 and 8 measured equal, r2)
-#ifndef LDSO_SC_SPLIT_GATHER
-#define LDSO_SC_SPLIT_GATHER 0  // both waves gather: point terms (wave 0) and JpJdF (wave 1) at once
-#endif
-constexpr int kScGather = 6;  // records per wave per round trip in the split gather (S7: all six)
+constexpr int kScBatch = 3;  // residual records per round trip (r4: 3 -> two round trips at N = 7, 27.6 vs 28.3 us)
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     if ((int)blockIdx.x < P.n_nid) {
         point_nid(P, blockIdx.x, smem);
         return;
     }
+#define SC_STAMP(k)
     const int item = P.item_base + blockIdx.x - P.n_nid;
     const int4 it = P.items[item];
     if (P.stop && P.pass > P.stop[it.w]) return;  // window left the GN loop
@@ -1238,101 +1150,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     float *U = smem;               // [64][KP]
     float *Wt = smem + 64 * KP;    // [64]
     const int tid = threadIdx.x;
-    for (int i = tid; i < 64 * KP; i += blockDim.x) U[i] = 0;
-    __syncthreads();
-#if LDSO_SC_SPLIT_GATHER
-    // the two waves gather the block's records at once: wave 0 the point terms of every residual
-    // (Hcd_r, Hdd_r, bd_r, active: record float4s 2-3), summed in residual order, wave 1 the JpJdF of
-    // the active ones (float4s 0-1, with 3 for the active flag) into the point's U row
-    const int pl = tid & 63;
-    if (pl < it.y) {
-#pragma clang fp contract(off)
-        const int p = it.x + pl;
-        const int nres = P.pt_nres[p];
-        const unsigned long long tgs = P.pt_tgt[p];
-        const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * 4;
-        const size_t sstride = (size_t)W.P * 4;
-        auto rec_of = [&](int k) {
-            const int tg = (int)((tgs >> (4 * k)) & 15ull);
-            return rp + (tg < host ? tg : tg - 1) * sstride;
-        };
-        float *row = U + pl * KP;
-        if (tid < 64) {
-            float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
-            int ngood = 0;
-            for (int k0 = 0; k0 < nres; k0 += kScGather) {
-                float4 hc[kScGather], hb[kScGather];
-#pragma unroll
-                for (int u = 0; u < kScGather; u++) {
-                    const float4 *q = rec_of(min(k0 + u, nres - 1));
-                    hc[u] = q[2];
-                    hb[u] = q[3];
-                }
-#pragma unroll
-                for (int u = 0; u < kScGather; u++) {
-                    if (k0 + u >= nres || hb[u].z == 0.0f) continue;
-                    ngood++;
-                    bd += hb[u].y;
-                    hdd += hb[u].x;
-                    hcd[0] += hc[u].x;
-                    hcd[1] += hc[u].y;
-                    hcd[2] += hc[u].z;
-                    hcd[3] += hc[u].w;
-                }
-            }
-            const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-            const float priorF = pd[4], deltaF = pd[5];
-            float HdiF = 0, bdSum = 0, ih = 0;
-            if (ngood > 0) {
-                // AccumulatedSCHessian.cc:24-33 (Hdd_accLF = bd_accLF = Hcd_accLF = 0 in the hot path)
-                float H = hdd + 0.0f + priorF;
-                if (H < 1e-10f) H = 1e-10f;
-                ih = H;
-                HdiF = (float)(1.0 / (double)H);
-                bdSum = bd + 0.0f;
-                if (P.shift_prior) bdSum += priorF * deltaF;
-                row[Kj + 0] = hcd[0] + 0.0f;
-                row[Kj + 1] = hcd[1] + 0.0f;
-                row[Kj + 2] = hcd[2] + 0.0f;
-                row[Kj + 3] = hcd[3] + 0.0f;
-                row[Kj + 4] = bdSum;
-            }
-            Wt[pl] = HdiF;
-            float *o = P.pt_out + (size_t)p * 12;
-            o[0] = HdiF;
-            o[1] = bdSum;
-            o[2] = ih;
-            o[3] = hdd;
-            o[4] = bd;
-            o[5] = hcd[0];
-            o[6] = hcd[1];
-            o[7] = hcd[2];
-            o[8] = hcd[3];
-            o[9] = (float)ngood;
-        } else {
-            for (int k0 = 0; k0 < nres; k0 += kScGather) {
-                float4 j0[kScGather], j1[kScGather];
-                float act[kScGather];
-#pragma unroll
-                for (int u = 0; u < kScGather; u++) {
-                    const float4 *q = rec_of(min(k0 + u, nres - 1));
-                    j0[u] = q[0];
-                    j1[u] = q[1];
-                    act[u] = q[3].z;
-                }
-#pragma unroll
-                for (int u = 0; u < kScGather; u++) {
-                    const int k = k0 + u;
-                    if (k >= nres || act[u] == 0.0f) continue;
-                    const int tg = (int)((tgs >> (4 * k)) & 15ull);
-                    const int slot = tg < host ? tg : tg - 1;
-                    *(float4 *)(row + 8 * slot) = j0[u];
-                    *(float4 *)(row + 8 * slot + 4) = j1[u];
-                }
-            }
-        }
-    }
-#else
+    SC_STAMP(1);
     if (tid < it.y) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
@@ -1345,6 +1163,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
         float *row = U + tid * KP;
+        unsigned filled = 0;  // target slots whose JpJdF is in the row
         for (int k0 = 0; k0 < nres; k0 += kScBatch) {
             float4 rec[kScBatch][4];
 #pragma unroll
@@ -1373,7 +1192,17 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
                 const int slot = tg < host ? tg : tg - 1;
                 *(float4 *)(row + 8 * slot) = j0;
                 *(float4 *)(row + 8 * slot + 4) = j1;
+                filled |= 1u << slot;
             }
+        }
+        {  // the rest of the row: zeros (the SYRK reads every column of the point's row)
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int sl = 0; sl < W.N - 1; sl++)
+                if (!((filled >> sl) & 1u)) {
+                    *(float4 *)(row + 8 * sl) = z;
+                    *(float4 *)(row + 8 * sl + 4) = z;
+                }
+            for (int c = Kj; c < KP; c++) row[c] = 0.f;
         }
         const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
         const float priorF = pd[4], deltaF = pd[5];
@@ -1393,6 +1222,18 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
             row[Kj + 4] = bdSum;
         }
         Wt[tid] = HdiF;
+        {
+            const float sw = sqrtf(HdiF);
+            float4 *r4 = reinterpret_cast<float4 *>(row);
+            for (int q = 0; q < (Kj + 5 + 3) / 4; q++) {
+                float4 v = r4[q];
+                v.x *= sw;
+                v.y *= sw;
+                v.z *= sw;
+                v.w *= sw;
+                r4[q] = v;
+            }
+        }
         float *o = P.pt_out + (size_t)p * 12;
         o[0] = HdiF;
         o[1] = bdSum;
@@ -1405,11 +1246,13 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         o[8] = hcd[3];
         o[9] = (float)ngood;
     }
-#endif
+    SC_STAMP(2);
     __syncthreads();
+    SC_STAMP(3);
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
     syrk_tiles(U, Wt, KP, nt, ntiles, it.y,
                P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16, tid, blockDim.x);
+#undef SC_STAMP
 }
 
 // ============================================================================================

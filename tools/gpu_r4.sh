@@ -18,6 +18,9 @@ for step in "$@"; do
     prof)
       export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu --no-secondary > gpurun_out/prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.log; exit 1; } ;;
+    mgpu)  # the N > 1 launch rehearsed on one GPU: bench.py starts its 2 ranks itself
+      LDSO_BENCH_SHARE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu --no-tracker --no-secondary > gpurun_out/bench2_$TAG.json 2> gpurun_out/bench2_$TAG.err || { echo "bench --gpus 2 failed"; tail -20 gpurun_out/bench2_$TAG.err; exit 1; }
+      python -c "import json; d = json.load(open('gpurun_out/bench2_$TAG.json')); print('n_gpus', d['n_gpus'], 'value', d['value'], 'sharded_window', json.dumps(d.get('sharded_window'))[:300])" ;;
     pmc)
       timeout -k 10 900 python tools/pmc_traffic.py > gpurun_out/pmc_$TAG.log 2>&1 || { echo "pmc failed"; tail -30 gpurun_out/pmc_$TAG.log; exit 1; }
       tail -30 gpurun_out/pmc_$TAG.log ;;
