@@ -511,6 +511,10 @@ def main():
     world, launched = world_from_env(args.gpus)
     if not launched and args.gpus > 1:  # no launcher: start the ranks here, before any GPU call
         sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    # stdout carries exactly one line, the JSON: everything else written to fd 1 (RCCL's init
+    # banner, library prints) goes to stderr
+    json_out = os.fdopen(os.dup(1), "w", buffering=1)
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N > 1 path on a one-GPU box: LDSO_BENCH_SHARE_GPU=1 puts every rank on
@@ -758,7 +762,7 @@ def main():
             out["speedup_single_window_vs_cpu"] = single["point_residuals_per_s"] / cpu1["value"]
         if cpu6 is not None:
             out["speedup_vs_cpu_six_threads"] = value / cpu6["value"]
-        print(json.dumps(out))
+        print(json.dumps(out), file=json_out, flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
