@@ -453,32 +453,32 @@ constexpr int kSumsPerWave = 64 * kSumStride;   // per-residual sums [64][17]
 
 __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, const Geo &g, const PhotoSums &s,
                                          float *slab_item) {
-    float4 v[9];
-    if (active) {
-        v[0] = make_float4(g.d_C_x[0], g.d_C_y[0], g.d_C_x[1], g.d_C_y[1]);
-        v[1] = make_float4(g.d_C_x[2], g.d_C_y[2], g.d_C_x[3], g.d_C_y[3]);
-        v[2] = make_float4(g.d_xi_x[0], g.d_xi_y[0], g.d_xi_x[1], g.d_xi_y[1]);
-        v[3] = make_float4(g.d_xi_x[2], g.d_xi_y[2], g.d_xi_x[3], g.d_xi_y[3]);
-        v[4] = make_float4(g.d_xi_x[4], g.d_xi_y[4], g.d_xi_x[5], g.d_xi_y[5]);
-        v[5] = make_float4(s.JabJIdx_00, s.JabJIdx_01, s.JabJIdx_10, s.JabJIdx_11);
-        v[6] = make_float4(s.JI_r0, s.JI_r1, s.Jab2_00, s.Jab2_11);
-        v[7] = make_float4(s.Jab2_01, s.Jab_r1, s.Jab_r0, s.rr);
-        v[8] = make_float4(s.JIdx2_00, s.JIdx2_10, s.JIdx2_11, 0.f);
-    } else {
+    // the residual's operand row; an inactive residual's row is zero (written by a separate
+    // exec-masked path, so the active values need no zero-select merge in registers)
+    auto stage = [&](float4 *row) {
+        if (active) {
+            row[0] = make_float4(g.d_C_x[0], g.d_C_y[0], g.d_C_x[1], g.d_C_y[1]);
+            row[1] = make_float4(g.d_C_x[2], g.d_C_y[2], g.d_C_x[3], g.d_C_y[3]);
+            row[2] = make_float4(g.d_xi_x[0], g.d_xi_y[0], g.d_xi_x[1], g.d_xi_y[1]);
+            row[3] = make_float4(g.d_xi_x[2], g.d_xi_y[2], g.d_xi_x[3], g.d_xi_y[3]);
+            row[4] = make_float4(g.d_xi_x[4], g.d_xi_y[4], g.d_xi_x[5], g.d_xi_y[5]);
+            row[5] = make_float4(s.JabJIdx_00, s.JabJIdx_01, s.JabJIdx_10, s.JabJIdx_11);
+            row[6] = make_float4(s.JI_r0, s.JI_r1, s.Jab2_00, s.Jab2_11);
+            row[7] = make_float4(s.Jab2_01, s.Jab_r1, s.Jab_r0, s.rr);
+            row[8] = make_float4(s.JIdx2_00, s.JIdx2_10, s.JIdx2_11, 0.f);
+        } else {
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int k = 0; k < 9; k++) v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+            for (int k = 0; k < 9; k++) row[k] = z;
+        }
+    };
     const int i = lane & 15, kk = lane >> 4;
     const bool geo = i < 10, ind = i >= 13;
     const float a0c = i == 13 ? 1.f : 0.f, a1c = i == 14 ? 1.f : 0.f;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int half = 0; half < 2; half++) {
-        if ((lane >> 5) == half) {
-            float4 *row = reinterpret_cast<float4 *>(tab + (lane & 31) * kTopRow);
-#pragma unroll
-            for (int k = 0; k < 9; k++) row[k] = v[k];
-        }
+        if ((lane >> 5) == half) stage(reinterpret_cast<float4 *>(tab + (lane & 31) * kTopRow));
         wave_lds_sync();
         const float *base = tab + kk * 8 * kTopRow;  // K rows (residual kk*8 + m, c)
 #pragma unroll 4
@@ -557,6 +557,25 @@ __device__ __forceinline__ float4 ldb4(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
 }
 
+// a / b rounded to nearest for finite a, b whose quotient needs no exponent scaling (|b| and
+// |a / b| well inside the normal range): the compiler's IEEE sequence without v_div_scale /
+// v_div_fmas / v_div_fixup, which only act outside that range -- the same rcp, Newton step and
+// two fma corrections, so the same bits (8 instead of 11 VALU).  Used for the pattern-pixel
+// projections, whose in-bounds results (1.1 < Ku < w - 3 with 0 < drescale) are of that kind; a
+// denominator of 0, a tiny one or a non-finite operand can give a different non-finite or
+// out-of-range value than IEEE division would, and every such value fails the bounds test either way.
+__device__ __forceinline__ float div_rn_normal(float a, float b) {
+#pragma clang fp contract(off)
+    float r = __builtin_amdgcn_rcpf(b);
+    const float e = fmaf(-b, r, 1.0f);
+    r = fmaf(e, r, r);
+    float q = a * r;
+    float rem = fmaf(-b, q, a);
+    q = fmaf(rem, r, q);
+    rem = fmaf(-b, q, a);
+    return fmaf(rem, r, q);
+}
+
 // Phase A of k_linearize on image layout 3 with footprint pieces.  The 8 pattern
 // pixels of a residual read their 96 taps (12 each, load12's stencil) from the residual's tap
 // footprint: the 16-B band columns (4 rows of one column) that hold at least one of the taps,
@@ -605,8 +624,8 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
         float ptp[3];
 #pragma unroll
         for (int i = 0; i < 3; i++) ptp[i] = (pre[3 * i] * up + pre[3 * i + 1] * vp + pre[3 * i + 2] * 1.0f) + pre[9 + i] * pz;
-        q.Ku = ptp[0] / ptp[2];
-        q.Kv = ptp[1] / ptp[2];
+        q.Ku = div_rn_normal(ptp[0], ptp[2]);
+        q.Kv = div_rn_normal(ptp[1], ptp[2]);
         const bool pok = go && q.Ku > 1.1f && q.Kv > 1.1f && q.Ku < wM3 && q.Kv < hM3;
         const unsigned long long m1 = __ballot(pok);
         q.gok = ((m1 >> (8 * g)) & 0xFFull) == 0xFFull;
@@ -728,17 +747,21 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     Geo8 cur, nxt;
     pc[3] = make_float4(0.f, 0.f, 0.f, 0.f);
     unsigned wide_steps = 0;
-    issue(0, cur);
-    for (int k = 0; k < nsteps; k++) {
-        store();            // waits for step k's pieces
-        issue(k + 1, nxt);  // step k+1's pieces in flight during step k's arithmetic
+    auto step = [&](int k, Geo8 &now, Geo8 &next) {
+        store();             // waits for step k's pieces
+        issue(k + 1, next);  // step k+1's pieces in flight during step k's arithmetic
         wave_lds_sync();
-        const bool wide = cur.gok && cur.wide;
+        const bool wide = now.gok && now.wide;
         if (__ballot(wide)) wide_steps |= 1u << k;
         float iv[12];
-        if (cur.gok && !wide) box_taps(cur, iv);
-        terms(k, cur, !wide, iv);
-        cur = nxt;
+        if (now.gok && !wide) box_taps(now, iv);
+        terms(k, now, !wide, iv);
+    };
+    issue(0, cur);
+    for (int k = 0; k < nsteps; k += 2) {  // ping-pong: no copies of the in-flight step's geometry
+        step(k, cur, nxt);
+        if (k + 1 >= nsteps) break;
+        step(k + 1, nxt, cur);
     }
     // residuals whose footprint exceeds the box: per-lane gathers, step by step
     while (wide_steps) {
