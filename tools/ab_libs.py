@@ -73,6 +73,8 @@ def main():
                 for k, v in kt.items():
                     best[(mode, k)] = min(best.get((mode, k), 1e9), v)
         print(l, " ".join(f"{m}:{k}={v:.1f}us" for (m, k), v in sorted(best.items())))
+        print("   rounds acc:k_linearize", " ".join(f"{r['acc']['k_linearize']:.1f}" for r in rs),
+              "noacc:k_linearize", " ".join(f"{r['noacc']['k_linearize']:.1f}" for r in rs))
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@
 set -e
 cd "$(dirname "$0")/../ldso_amd/csrc"
 make -s ../lib/ldso_ct.o ../lib/host_math.o
-HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-result -Wno-unused-const-variable"
+HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-slp-vectorize -Wall -Wno-unused-function -Wno-unused-result -Wno-unused-const-variable"
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   out=../../abl/$name; mkdir -p $out
