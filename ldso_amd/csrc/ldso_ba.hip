@@ -325,6 +325,35 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a / b rounded to nearest for finite a, b whose quotient needs no exponent scaling (|b| and
+// |a / b| well inside the normal range): the compiler's IEEE sequence without v_div_scale /
+// v_div_fmas / v_div_fixup, which only act outside that range -- the same rcp, Newton step and
+// two fma corrections, so the same bits (8 instead of 11 VALU).  Used for the pattern-pixel
+// projections, whose in-bounds results (1.1 < Ku < w - 3 with 0 < drescale) are of that kind; a
+// denominator of 0, a tiny one or a non-finite operand can give a different non-finite or
+// out-of-range value than IEEE division would, and every such value fails the bounds test either way.
+__device__ __forceinline__ float div_rn_normal(float a, float b) {
+#pragma clang fp contract(off)
+    float r = __builtin_amdgcn_rcpf(b);
+    const float e = fmaf(-b, r, 1.0f);
+    r = fmaf(e, r, r);
+    float q = a * r;
+    float rem = fmaf(-b, q, a);
+    q = fmaf(rem, r, q);
+    rem = fmaf(-b, q, a);
+    return fmaf(rem, r, q);
+}
+
+// sqrt rounded to nearest for a normal, finite a >= 2^-96: the compiler's correctly rounded
+// sequence (v_sqrt_f32, then the neighbours one ulp down / up tested by an fma residual) without its
+// denormal scaling and its 0 / inf class fixup, which only act outside that range.
+__device__ __forceinline__ float sqrt_rn_normal(float a) {
+    const float s = __builtin_amdgcn_sqrtf(a);
+    const float sd = __int_as_float(__float_as_int(s) - 1), su = __int_as_float(__float_as_int(s) + 1);
+    float r = fmaf(-sd, s, a) <= 0.0f ? sd : s;
+    return fmaf(-su, s, a) > 0.0f ? su : r;
+}
+
 // one pattern pixel of Residuals.cc:128-190: the 17 addends, in the reference's expression order.
 // kMarg: the JI_r / Jab_r / rr addends use res_toZeroF of fixLinearizationF (Residuals.cc:219-245,
 // resF - JIdx Jp_delta - JabF delta_ab) as AccumulatedTopHessianSSE::addPoint<2> does
@@ -336,11 +365,13 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
 #pragma clang fp contract(off)
     const float residual = I - (float)(aff0 * color + aff1);
     const float drdA = (color - b0);
-    float wg = sqrtf(kOutlierTHSumComponent / (kOutlierTHSumComponent + (gx * gx + gy * gy)));
+    // the quotients lie in (0.01, 1] and the square roots' arguments in (1e-5, 1] for every pixel
+    // whose sums are kept (finite sample, |residual| < 1e6): the in-range IEEE sequences, same bits
+    float wg = sqrt_rn_normal(div_rn_normal(kOutlierTHSumComponent, kOutlierTHSumComponent + (gx * gx + gy * gy)));
     wg = 0.5f * (wg + weight);
-    float hw = fabsf(residual) < kHuberTH ? 1 : kHuberTH / fabsf(residual);
+    float hw = fabsf(residual) < kHuberTH ? 1 : div_rn_normal(kHuberTH, fabsf(residual));
     t[0] = wg * wg * hw * residual * residual * (2 - hw);
-    if (hw < 1) hw = sqrtf(hw);
+    if (hw < 1) hw = sqrt_rn_normal(hw);
     hw = hw * wg;
     gx *= hw;
     gy *= hw;
@@ -441,12 +472,19 @@ constexpr int kTermQ = 9;                      // quantities per transposition r
 // 16-B band-column pieces (4 rows each) + one dummy slot, in floats
 constexpr int kBoxCols = 9, kBoxBands = 3, kBoxFloats = 112;
 static_assert(kBoxFloats >= (kBoxCols * kBoxBands + 1) * 4, "box");
-// floats between the 8 residuals' term tables of a step (72 = dense; 76 halves the bank conflicts of
-// the pattern-order sums' 16-B reads)
-constexpr int kTermStride = 72;
+// the 8 residuals' term tables of a step ([kRoundQ][8] floats each).  Lane (g, e) of the pattern-order
+// sums reads quantity e of residual g as two 16-B reads; a ds_read_b128 is served in 16-lane groups
+// ({g, g+3} x e 0..3 with {g+1, g+2} x e 4..7, and the mirror image) on 64 banks.  With dense tables
+// (72 floats apart) every 16-B read of a group starts on an even bank quad -- 2-way conflicts on every
+// read (tools/lds_banks.py).  Residual bases of {0, 32, 51, 83} quads (+112 for g >= 4) put the
+// residual pairs {g, g+1} on even and {g+2, g+3} on odd quads: conflict-free, 852 of the region's
+// floats (the terms alias the footprint boxes, 8 x 112 floats)
+__device__ __forceinline__ int term_base(int g) {
+    const int q = g & 3;
+    return 4 * ((q == 0 ? 0 : q == 1 ? 32 : q == 2 ? 51 : 83) + 112 * (g >> 2));
+}
 constexpr int kRoundQ = kTermQ;
-static_assert(kTermStride >= kRoundQ * 8, "term tables");
-constexpr int kTermsOnly = 8 * kTermStride;      // per-pixel addends of one round [8 residuals][kRoundQ][8]
+constexpr int kTermsOnly = 4 * (112 + 83) + kRoundQ * 8;  // [8 residuals][kRoundQ][8] at term_base
 // the terms region also holds the 8 residuals' footprint boxes of a step (used before the terms)
 constexpr int kTermsPerWave = 8 * kBoxFloats > kTermsOnly ? 8 * kBoxFloats : kTermsOnly;
 constexpr int kSumsPerWave = 64 * kSumStride;   // per-residual sums [64][17]
@@ -557,25 +595,6 @@ __device__ __forceinline__ float4 ldb4(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
 }
 
-// a / b rounded to nearest for finite a, b whose quotient needs no exponent scaling (|b| and
-// |a / b| well inside the normal range): the compiler's IEEE sequence without v_div_scale /
-// v_div_fmas / v_div_fixup, which only act outside that range -- the same rcp, Newton step and
-// two fma corrections, so the same bits (8 instead of 11 VALU).  Used for the pattern-pixel
-// projections, whose in-bounds results (1.1 < Ku < w - 3 with 0 < drescale) are of that kind; a
-// denominator of 0, a tiny one or a non-finite operand can give a different non-finite or
-// out-of-range value than IEEE division would, and every such value fails the bounds test either way.
-__device__ __forceinline__ float div_rn_normal(float a, float b) {
-#pragma clang fp contract(off)
-    float r = __builtin_amdgcn_rcpf(b);
-    const float e = fmaf(-b, r, 1.0f);
-    r = fmaf(e, r, r);
-    float q = a * r;
-    float rem = fmaf(-b, q, a);
-    q = fmaf(rem, r, q);
-    rem = fmaf(-b, q, a);
-    return fmaf(rem, r, q);
-}
-
 // Phase A of k_linearize on image layout 3 with footprint pieces.  The 8 pattern
 // pixels of a residual read their 96 taps (12 each, load12's stencil) from the residual's tap
 // footprint: the 16-B band columns (4 rows of one column) that hold at least one of the taps,
@@ -599,7 +618,7 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
     const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
     const float aff0 = pre[24], aff1 = pre[25], b0a = pre[26];
-    float *T = lds_terms_w + g * kTermStride;
+    float *T = lds_terms_w + term_base(g);
     float *box = lds_terms_w + g * kBoxFloats;
     const int nsteps = (jlimit + 7) >> 3;
     constexpr unsigned kOOB = 0x7FFFFFF0u;  // beyond the frame's buffer range: the load returns 0, no access
@@ -814,7 +833,6 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
     uint8_t flags = P.rs_flags[rq];
     float state_energy = P.rs_energy[rq];
     float new_energy = P.rs_newenergy[rq];
-    float4 centre = P.rs_center[rq];
     const float4 my_pd0 = *(const float4 *)(P.pt_data + (size_t)my_point * LDSO_BA_POINT_STRIDE);
     // the point's color[8] and weights[8] (record floats 8..23: one 64-B piece per residual)
     // into this residual's row of the sums table: phase A's pattern lanes read them from LDS at
@@ -1032,11 +1050,9 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
             const bool pat_ok = !(s.energy < 0.0f);
             bool ok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
                                         wM3, hM3, g);
-            if (ok) {
-                centre.x = g.Ku;
-                centre.y = g.Kv;
-                centre.z = g.new_idepth;
-            }
+            // centerProjectedTo: written where projected, kept (not re-read) where not
+            float *centre = reinterpret_cast<float *>(P.rs_center + r);
+            if (ok) *reinterpret_cast<float3 *>(centre) = make_float3(g.Ku, g.Kv, g.new_idepth);
             ok = ok && pat_ok;
             if (!ok) {
                 energy = state_energy;  // OOB: return state_energy, NewEnergy untouched
@@ -1067,13 +1083,12 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
                     pr[i] = pi[i] + pre[9 + i] * pd0.z;
                 }
                 const float dx = pi[0] / pi[2] - pr[0] / pr[2], dy = pi[1] / pi[2] - pr[1] / pr[2];
-                centre.w = 0.01f * sqrtf(dx * dx + dy * dy);
+                centre[3] = 0.01f * sqrtf(dx * dx + dy * dy);
             }
             P.rs_state[r] = new_state;
             P.rs_flags[r] = flags;
             P.rs_energy[r] = state_energy;
             P.rs_newenergy[r] = new_energy;
-            P.rs_center[r] = centre;
         }
         isIN = (new_state == LDSO_BA_RES_IN);
         P.rs_newstate[r] = new_state;
@@ -1273,8 +1288,8 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     __syncthreads();
     SC_STAMP(3);
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
-    syrk_tiles(U, Wt, KP, nt, ntiles, it.y,
-               P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16, tid, blockDim.x);
+    float *slab = P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16;
+    syrk_tiles(U, Wt, KP, nt, ntiles, it.y, slab, tid, blockDim.x);
 #undef SC_STAMP
 }
 
