@@ -472,19 +472,13 @@ constexpr int kTermQ = 9;                      // quantities per transposition r
 // 16-B band-column pieces (4 rows each) + one dummy slot, in floats
 constexpr int kBoxCols = 9, kBoxBands = 3, kBoxFloats = 112;
 static_assert(kBoxFloats >= (kBoxCols * kBoxBands + 1) * 4, "box");
-// the 8 residuals' term tables of a step ([kRoundQ][8] floats each).  Lane (g, e) of the pattern-order
-// sums reads quantity e of residual g as two 16-B reads; a ds_read_b128 is served in 16-lane groups
-// ({g, g+3} x e 0..3 with {g+1, g+2} x e 4..7, and the mirror image) on 64 banks.  With dense tables
-// (72 floats apart) every 16-B read of a group starts on an even bank quad -- 2-way conflicts on every
-// read (tools/lds_banks.py).  Residual bases of {0, 32, 51, 83} quads (+112 for g >= 4) put the
-// residual pairs {g, g+1} on even and {g+2, g+3} on odd quads: conflict-free, 852 of the region's
-// floats (the terms alias the footprint boxes, 8 x 112 floats)
-__device__ __forceinline__ int term_base(int g) {
-    const int q = g & 3;
-    return 4 * ((q == 0 ? 0 : q == 1 ? 32 : q == 2 ? 51 : 83) + 112 * (g >> 2));
-}
+// floats between the 8 residuals' term tables of a step (dense).  Bank-swizzled bases that make the
+// pattern-order sums' 16-B reads conflict-free turn the terms' paired 4-B stores into 2-way
+// conflicts instead (r4, PMC ablations: 8.66 vs 8.36 M conflict cycles per launch, time unchanged)
+constexpr int kTermStride = 72;
 constexpr int kRoundQ = kTermQ;
-constexpr int kTermsOnly = 4 * (112 + 83) + kRoundQ * 8;  // [8 residuals][kRoundQ][8] at term_base
+static_assert(kTermStride >= kRoundQ * 8, "term tables");
+constexpr int kTermsOnly = 8 * kTermStride;      // per-pixel addends of one round [8 residuals][kRoundQ][8]
 // the terms region also holds the 8 residuals' footprint boxes of a step (used before the terms)
 constexpr int kTermsPerWave = 8 * kBoxFloats > kTermsOnly ? 8 * kBoxFloats : kTermsOnly;
 constexpr int kSumsPerWave = 64 * kSumStride;   // per-residual sums [64][17]
@@ -618,7 +612,7 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
     const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
     const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
     const float aff0 = pre[24], aff1 = pre[25], b0a = pre[26];
-    float *T = lds_terms_w + term_base(g);
+    float *T = lds_terms_w + g * kTermStride;
     float *box = lds_terms_w + g * kBoxFloats;
     const int nsteps = (jlimit + 7) >> 3;
     constexpr unsigned kOOB = 0x7FFFFFF0u;  // beyond the frame's buffer range: the load returns 0, no access
