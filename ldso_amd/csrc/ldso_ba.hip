@@ -1164,7 +1164,11 @@ __device__ void point_nid(const PointParams &P, int w, float *lds) {
     }
 }
 
-constexpr int kScThreads = 128;  // 2 waves: wave 0 gathers the 64 points, both run the SYRK tiles
+// points per k_point_sc block (one SYRK chunk partial).  128 (both waves gather, half the slab
+// partials) measured 28.5 vs 26.5 us with the stitch 0.8 us faster: the SYRK chains double (r4)
+constexpr int kScPoints = 64;
+constexpr int kScThreads = 128;  // 2 waves: a lane per point gathers, both run the SYRK tiles
+static_assert(kScPoints <= kScThreads, "one gathering lane per point");
 constexpr int kScBatch = 3;  // residual records per round trip (r4: 3 -> two round trips at N = 7, 27.6 vs 28.3 us)
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1179,15 +1183,15 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const WinDev &W = P.wins[it.w];
     const int host = it.z, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
     const int Kj = 8 * (W.N - 1);
-    float *U = smem;               // [64][KP]
-    float *Wt = smem + 64 * KP;    // [64]
+    float *U = smem;               // [kScPoints][KP]
+    float *Wt = smem + kScPoints * KP;    // [kScPoints]
     const int tid = threadIdx.x;
     SC_STAMP(1);
     if (tid < it.y) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
         const int nres = P.pt_nres[p];
-        // one round of record loads (slot s of the block's 64 points is contiguous), then the
+        // one round of record loads (slot s of the block's points is contiguous), then the
         // sums in residual order exactly as AccumulatedTopHessian.cc:94-116 adds them
         const unsigned long long tgs = P.pt_tgt[p];
         const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * 4;
@@ -4211,7 +4215,7 @@ int check_window(const ldso_ba_window &w, bool need_images = true) {
     return 0;
 }
 
-size_t sc_smem_bytes(int KP) { return (size_t)(64 * KP + 64) * sizeof(float); }
+size_t sc_smem_bytes(int KP) { return (size_t)(kScPoints * KP + kScPoints) * sizeof(float); }
 
 // frame geometry of the image layout (all strides in float4 units)
 void image_geometry(ldso_ba_ctx *c) {
@@ -4771,7 +4775,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         }
         for (int b = 0; b < N * N; b++) pair_win.push_back(w);
         D.n_top_items = (int)top_items.size() - D.top_item_base;
-        // sc items: chunks of 64 points of one host
+        // sc items: chunks of kScPoints points of one host
         D.sc_item_base = (int)sc_items.size();
         {
             int q = 0;
@@ -4779,8 +4783,8 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
                 const int first = (int)sc_items.size();
                 int q0 = q;
                 while (q < P && H.pt_host[q] == f) q++;
-                for (int s = q0; s < q; s += kWave)
-                    sc_items.push_back(make_int4(point_base + s, std::min(kWave, q - s), f, w));
+                for (int s = q0; s < q; s += kScPoints)
+                    sc_items.push_back(make_int4(point_base + s, std::min(kScPoints, q - s), f, w));
                 host_items.push_back(make_int2(first, (int)sc_items.size() - first));
                 frame_win.push_back(w);
             }
