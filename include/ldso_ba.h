@@ -459,7 +459,7 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              gradients recomputed with makeImages' rule (falls back to 1 when the
  *                              caller's dI gradients are not makeImages'); 1 [I, dx, dy, 0]
  *                              texels in 2x4 tiles; set before ldso_ba_load
- *   LDSO_BA_TUNE_TOP_CHUNK     residuals per k_linearize wavefront: 16, 32, 64, or 0 = automatic
+ *   LDSO_BA_TUNE_TOP_CHUNK     residuals per k_linearize wavefront: a multiple of 8 up to 64, or 0 = automatic
  *                              (64 for large batches, shorter for a single window); set before
  *                              ldso_ba_load
  *   LDSO_BA_TUNE_TIMING_MASK   bit i: bracket kernel slot i with events when timing is enabled

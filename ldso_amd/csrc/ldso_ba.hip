@@ -6253,7 +6253,7 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
         return 0;
     }
     if (key == LDSO_BA_TUNE_TOP_CHUNK) {
-        if (value != 0 && value != 16 && value != 32 && value != 64) return fail(-1, "chunk must be 0, 16, 32 or 64");
+        if (value < 0 || value > 64 || value % 8) return fail(-1, "chunk must be 0 or a multiple of 8 up to 64");
         if (c->n_win) return fail(-1, "chunk size must be chosen before ldso_ba_load");
         c->top_chunk = value;
         return 0;

@@ -1,6 +1,6 @@
 """A/B whole library builds on the bench workload: each build runs in its own process
 (LDSO_BA_LIB=<path>), k_linearize / per-kernel HIP-event times, rounds interleaved.
-  python tools/ab_libs.py lib1.so lib2.so ... [--windows 64] [--rounds 3]"""
+  python tools/ab_libs.py lib1.so lib2.so[:key=value,...] ... [--windows 64] [--rounds 3]"""
 import argparse
 import json
 import os
@@ -18,8 +18,9 @@ from ldso_amd import BAContext, synth
 B = WINDOWS
 ws = [synth.make_window(**synth.S7, seed=1000 + i) for i in range(B)]
 c = BAContext(0)
-if os.environ.get("LDSO_AB_TAPS"):
-    c.set_tuning(12, int(os.environ["LDSO_AB_TAPS"]))
+for kv in filter(None, os.environ.get("LDSO_AB_TUNE", "").split(",")):
+    k, v = kv.split("=")
+    c.set_tuning(int(k), int(v))
 c.load(ws)
 for _ in range(3):
     c.linearize()
@@ -56,10 +57,8 @@ def main():
     res = {l: [] for l in a.libs}
     for _ in range(a.rounds):
         for l in a.libs:
-            path, _, taps = l.partition(":")
-            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(path))
-            if taps:
-                env["LDSO_AB_TAPS"] = taps
+            path, _, tune = l.partition(":")  # lib.so:key=value,key=value -> set_tuning before load
+            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(path), LDSO_AB_TUNE=tune)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
             if p.returncode != 0 or not line:
