@@ -337,7 +337,9 @@ int ldso_ba_packed_system(ldso_ba_ctx *ctx, void **dev_ptr, int64_t *n_doubles, 
 int ldso_ba_unpack_system(ldso_ba_ctx *ctx);
 /* Device-to-device copy of the packed partial systems to (direction 0) or from (direction 1)
  * a caller-owned device buffer of n_doubles (e.g. a torch tensor handed to RCCL); synchronises
- * the context stream.  Direction 1 also invalidates cached host copies. */
+ * the context stream.  Direction 1 also invalidates cached host copies.  The copy runs on the
+ * context stream: work the caller queued on another stream that writes dev_buf (direction 1) or
+ * reads it must be ordered by the caller (e.g. synchronise that stream before the call). */
 int ldso_ba_copy_packed(ldso_ba_ctx *ctx, void *dev_buf, int64_t n_doubles, int32_t direction);
 
 /* Sharded setNewFrameEnergyTH (FullSystem.cc:2078-2109 over activeResiduals that target the
@@ -348,7 +350,8 @@ int ldso_ba_copy_packed(ldso_ba_ctx *ctx, void *dev_buf, int64_t n_doubles, int3
  *   export_newest       writes [n_windows][stride] floats into a caller device buffer (-1 pads)
  *   frame_threshold_gathered  takes the all-gathered [n_ranks][n_windows][stride] buffer and
  *                       re-selects every window's newest-frame threshold on the device.
- * All three synchronise the context stream.  Unsharded contexts never need them. */
+ * All three synchronise the context stream (buffers the caller fills on another stream must be
+ * complete before the call).  Unsharded contexts never need them. */
 int ldso_ba_newest_stride(ldso_ba_ctx *ctx, int64_t *stride);
 int ldso_ba_export_newest(ldso_ba_ctx *ctx, float *dev_buf, int64_t stride);
 int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *ctx, const float *dev_buf, int32_t n_ranks, int64_t stride);

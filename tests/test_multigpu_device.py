@@ -55,6 +55,7 @@ def _worker(rank, world, port, q):
         host = dev.cpu()
         dist.all_reduce(host)
         dev.copy_(host.cuda())
+        torch.cuda.synchronize()  # torch's stream wrote dev; the library reads it on its own stream
         L.check(c._lib.ldso_ba_copy_packed(c._h, dev.data_ptr(), n, 1))
         e = torch.tensor(c.energy(0), dtype=torch.float64)
         dist.all_reduce(e)
@@ -68,6 +69,7 @@ def _worker(rank, world, port, q):
         parts = [torch.empty(stride, dtype=torch.float32) for _ in range(world)]
         dist.all_gather(parts, slot.cpu())
         gathered = torch.cat(parts).cuda()
+        torch.cuda.synchronize()
         L.check(c._lib.ldso_ba_frame_threshold_gathered(c._h, gathered.data_ptr(), world, stride))
         x0 = c.solve_device(0, 1e-5, ns)[0]
         x2 = c.solve_device(2, 1e-5, ns)[0]
