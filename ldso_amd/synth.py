@@ -64,6 +64,22 @@ def make_window(n_frames=7, n_points=2000, width=640, height=480, seed=0, outlie
     return w
 
 
+def in_image_order(w: Window) -> Window:
+    """The same window with each host frame's points in image row order (v, then u): the order in
+    which LDSO's pixel selection emits them.  make_window's points are in random order."""
+    import copy
+    order = np.lexsort((w.point_data[:, 0], np.floor(w.point_data[:, 1]), w.point_host))
+    ridx = np.concatenate([np.arange(w.point_res_begin[p], w.point_res_begin[p + 1]) for p in order])
+    o = copy.copy(w)
+    o.point_host = np.ascontiguousarray(w.point_host[order])
+    o.point_data = np.ascontiguousarray(w.point_data[order])
+    o.point_res_begin = np.concatenate([[0], np.cumsum(np.diff(w.point_res_begin)[order])]).astype(np.int32)
+    for k in ("res_target", "res_state", "res_energy", "res_flags"):
+        setattr(o, k, np.ascontiguousarray(getattr(w, k)[ridx]))
+    o._keep = []
+    return o
+
+
 def make_tracker_scene(width=640, height=480, n_points=(8000, 4000, 2000, 1000, 500, 250), seed=0, blobs=64):
     """A coarse-tracking scene: a smooth textured reference image (sum of
     Gaussian blobs, [0, 255] float, the same family as §8d's frames) and per-level reference point

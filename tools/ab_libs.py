@@ -17,6 +17,8 @@ torch.cuda.init()
 from ldso_amd import BAContext, synth
 B = WINDOWS
 ws = [synth.make_window(**synth.S7, seed=1000 + i) for i in range(B)]
+if IMAGE_ORDER:
+    ws = [synth.in_image_order(w) for w in ws]
 c = BAContext(0)
 for kv in filter(None, os.environ.get("LDSO_AB_TUNE", "").split(",")):
     k, v = kv.split("=")
@@ -52,8 +54,10 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--windows", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--image-order", action="store_true", help="points in image row order (LDSO's)")
     a = ap.parse_args()
-    code = CHILD.replace("ROOT", repr(ROOT)).replace("WINDOWS", str(a.windows))
+    code = CHILD.replace("ROOT", repr(ROOT)).replace("WINDOWS", str(a.windows)).replace(
+        "IMAGE_ORDER", str(a.image_order))
     res = {l: [] for l in a.libs}
     for _ in range(a.rounds):
         for l in a.libs:
