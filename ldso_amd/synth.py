@@ -77,6 +77,7 @@ def in_image_order(w: Window) -> Window:
     for k in ("res_target", "res_state", "res_energy", "res_flags"):
         setattr(o, k, np.ascontiguousarray(getattr(w, k)[ridx]))
     o._keep = []
+    o.point_order, o.res_order = order, ridx  # new index -> index in w
     return o
 
 

@@ -168,6 +168,35 @@ def test_stitch_paths_agree(built, monkeypatch, stitch):
         c2.close()
 
 
+def test_caller_point_order_does_not_matter(built):
+    """The same window with each host's points in image row order (as LDSO's pixel selection emits
+    them) instead of random order: every per-residual and per-point result is the same value for
+    the same residual / point (bit for bit), the system within the block tolerance (the chunks hold
+    other residuals, so the Top partial sums reassociate), #IN equal."""
+    cfg = dict(n_frames=6, n_points=700, seed=91)
+    w = synth.make_window(**cfg)
+    o = synth.in_image_order(synth.make_window(**cfg))
+    c1, c2 = BAContext(0).load([w]), BAContext(0).load([o])
+    for c in (c1, c2):
+        c.linearize()
+    r1, r2 = c1.residuals(0), c2.residuals(0)
+    for k in r1:
+        np.testing.assert_array_equal(r2[k], np.asarray(r1[k])[o.res_order], err_msg=k)
+    p1, p2 = c1.points(0), c2.points(0)
+    for k in p1:
+        np.testing.assert_array_equal(p2[k], np.asarray(p1[k])[o.point_order], err_msg=k)
+    e1, e2 = c1.energy(0), c2.energy(0)
+    assert e1[2] == e2[2] and abs(e1[0] - e2[0]) <= 1e-12 * abs(e1[0])
+    s1, s2 = c1.system(0), c2.system(0)
+    N = cfg["n_frames"]
+    for k in ("HA", "Hsc"):
+        assert block_errors(s2[k], s1[k], N) < BLOCK_TOL, k
+    for k in ("bA", "bsc"):
+        assert vec_block_errors(s2[k], s1[k], N) < BLOCK_TOL, k
+    c1.close()
+    c2.close()
+
+
 def test_repeated_passes_and_oob_stickiness(ctx):
     """OOB is sticky inside optimize(): later passes return the stored state_energy."""
     cfg = dict(n_frames=6, n_points=800, seed=5, baseline=0.12)
