@@ -4653,6 +4653,10 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     for (int w = 0; w < n_windows; w++) r_est += ws[w].n_residuals;
     r_est /= shard_count;
     const int chunk = c->top_chunk ? c->top_chunk : r_est >= 64LL * 4096 ? 64 : r_est >= 32LL * 2048 ? 32 : 16;
+    // k_point_sc points per block: 64 for large loads; a small load (one window: 32 blocks of 64
+    // points on 256 CUs) takes 16-point blocks, whose SYRK chains are a quarter as long (one S7
+    // window's pass 30 -> 28 us; optimize unchanged: its sumNID block is the longest there)
+    const int sc_chunk = r_est < 64LL * 4096 ? 16 : kScPoints;
     int frame_base = 0, pair_base = 0, point_base = 0, res_base = 0;
     size_t smem_max = 0;
 
@@ -4783,8 +4787,8 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
                 const int first = (int)sc_items.size();
                 int q0 = q;
                 while (q < P && H.pt_host[q] == f) q++;
-                for (int s = q0; s < q; s += kScPoints)
-                    sc_items.push_back(make_int4(point_base + s, std::min(kScPoints, q - s), f, w));
+                for (int s = q0; s < q; s += sc_chunk)
+                    sc_items.push_back(make_int4(point_base + s, std::min(sc_chunk, q - s), f, w));
                 host_items.push_back(make_int2(first, (int)sc_items.size() - first));
                 frame_win.push_back(w);
             }

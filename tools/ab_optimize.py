@@ -30,6 +30,15 @@ for B in (1, 64):
         c.optimize(6, nullspaces=ns, settings=st)
     c.sync()
     out[f"optimize_{B}"] = 1e3 * (time.perf_counter() - t0) / REPS
+    if B == 1:  # one linearize + accumulate pass
+        for _ in range(5):
+            c.linearize()
+        c.sync()
+        t0 = time.perf_counter()
+        for _ in range(20 * REPS):
+            c.linearize()
+        c.sync()
+        out["pass_1"] = 1e3 * (time.perf_counter() - t0) / (20 * REPS)
     c.close()
 print("RESULT " + json.dumps(out))
 '''
