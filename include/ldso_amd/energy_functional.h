@@ -126,8 +126,10 @@ struct FrameHessian {
     const float *dI = nullptr;         // level-0 [I, dx, dy] per pixel (FrameHessian::dI)
     float frameEnergyTH = 8 * 8 * 8;   // written back for the newest frame by linearizeAll
     double prior[8] = {0}, delta[8] = {0}, delta_prior[8] = {0};  // takeData / setDeltaF
-    // FrameHessian::takeData (FrameHessian.cc:131-135): prior, delta, delta_prior
-    void takeData();
+    // FrameHessian::takeData (FrameHessian.cc:131-135): prior, delta, delta_prior; the prior
+    // (getPrior, FrameHessian.h:142-170) follows settings' affine modes (NULL: the defaults).  The
+    // EnergyFunctional calls it with its own settings (setSettings).
+    void takeData(const ldso_ba_opt_settings *settings = nullptr);
 };
 
 class EnergyFunctional;
@@ -214,6 +216,16 @@ public:
     bool ok() const { return err_.empty(); }
     const std::string &lastError() const { return err_; }
 
+    // The reference's settings globals this window runs with (src/Setting.cc: setting_solverMode,
+    // setting_forceAceptStep, setting_min/thOptIterations, setting_affineOptModeA / B,
+    // setting_vi_enable), copied in by the caller before the first pass and whenever a driver
+    // changes them.  Checked by the library (ldso_ba_set_settings): an
+    // unsupported value returns false with lastError() set and keeps the previous settings.
+    // Every later entry point runs with them: linearizeAll / optimize (JabF zeroing, priors, solver
+    // mode), solveSystemF (checked again on every call), takeData's affine priors.
+    bool setSettings(const ldso_ba_opt_settings &s);
+    const ldso_ba_opt_settings &settings() const { return settings_; }
+
     // ---- EnergyFunctional.h:55-186 -------------------------------------------------------
     void insertResidual(shared_ptr<PointFrameResidual> r);
     void insertFrame(shared_ptr<FrameHessian> fh, shared_ptr<CalibHessian> Hcalib);
@@ -226,6 +238,8 @@ public:
     // HM += margWeightFac H, bM += margWeightFac b, removePoint, makeIDX
     void marginalizePointsF();
     void dropPointsF();  // removes the points with status OUTLIER or OUT
+    // the non-VI branch (setting_vi_enable = false is the only setting setSettings accepts): the
+    // reference's fourth argument, the InertialHessian, has no counterpart here and must be null
     void solveSystemF(int iteration, double lambda, shared_ptr<CalibHessian> HCalib);
     void solveSystemF(int iteration, double lambda, shared_ptr<CalibHessian> HCalib, std::nullptr_t /*HInertial*/) {
         solveSystemF(iteration, lambda, HCalib);
@@ -260,8 +274,8 @@ public:
     // by the linearizeAll(true) FullSystem::optimize runs next, by syncResiduals(), or before any
     // PointFrameResidual method call.  energies (optional): (E, 0, #IN) of the first pass and of
     // every iteration's (after an exit: repeats of the last); iterations: the iterations entered;
-    // settings: NULL = the reference's defaults (ldso_ba_check_settings rejects the rest).
-    // Returns the last pass's energies.
+    // settings: NULL = this window's settings (setSettings); otherwise they are installed first as
+    // by setSettings (a rejected set fails the call).  Returns the last pass's energies.
     Vec3 optimize(int n_its, shared_ptr<CalibHessian> HCalib, std::vector<Vec3> *energies = nullptr,
                   bool *isLost = nullptr, int *iterations = nullptr, const ldso_ba_opt_settings *settings = nullptr);
     // the residual and point fields of the device's last pass, if the host copies are stale
@@ -315,6 +329,7 @@ private:
     std::vector<shared_ptr<PointHessian>> registry_;  // every inserted point not yet removed
     int device_ = 0;
     double currentLambda_ = 0;  // EnergyFunctional::currentLambda (set by solveSystemF)
+    ldso_ba_opt_settings settings_ = LDSO_BA_OPT_SETTINGS_INIT;
     CalibHessian calib_;
     bool dirty_ = true;
     std::string err_;

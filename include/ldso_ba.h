@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define LDSO_BA_ABI_VERSION 4
+#define LDSO_BA_ABI_VERSION 5
 
 #define LDSO_BA_PATTERN_NUM 8      /* patternNum, Settings.h:225 (staticPattern[8])     */
 #define LDSO_BA_CPARS 4            /* CPARS, NumTypes.h:25                              */
@@ -107,6 +107,7 @@ typedef struct ldso_ba_frame_state {
 } ldso_ba_frame_state;
 
 typedef struct ldso_ba_ctx ldso_ba_ctx;
+struct ldso_ba_opt_settings; /* defined with ldso_ba_check_settings below */
 
 /* ---- host-side helpers (no GPU needed) ---------------------------------------------- */
 
@@ -123,17 +124,21 @@ int ldso_ba_frame_precalc(int32_t n_frames, const ldso_ba_frame_state *frames, c
 int ldso_ba_set_adjoints(int32_t n_frames, const ldso_ba_frame_state *frames, double *ad_host,
                          double *ad_target, double *c_prior);
 
-/* FrameHessian::takeData (FrameHessian.cc:131-135): prior, delta, delta_prior [N][8]. */
-int ldso_ba_frame_take_data(int32_t n_frames, const ldso_ba_frame_state *frames, double *prior,
-                            double *delta, double *delta_prior);
+/* FrameHessian::takeData (FrameHessian.cc:131-135): prior, delta, delta_prior [N][8].  The prior
+ * (getPrior, FrameHessian.h:142-170) follows settings->affine_opt_mode_a / _b (NULL: the defaults);
+ * settings are checked (ldso_ba_check_settings). */
+int ldso_ba_frame_take_data(int32_t n_frames, const ldso_ba_frame_state *frames, const struct ldso_ba_opt_settings *settings,
+                            double *prior, double *delta, double *delta_prior);
 
 /* Solve assembly + Jacobi-scaled LDLT + optional nullspace projection, the non-VI branch of
- * EnergyFunctional::solveSystemF (EnergyFunctional.cc:280-471).  Inputs are the stitched
- * blocks; HM/bM may be NULL (no marginalisation prior).  nullspaces: [n_null][8N+4] column
- * vectors (getNullspaces order) used when (iteration >= 2), may be NULL.  x_out: [8N+4]. */
-int ldso_ba_solve_system(int32_t n_frames, int32_t iteration, double lambda, const double *HA,
-                         const double *bA, const double *HL, const double *bL, const double *HM,
-                         const double *bM, const double *Hsc, const double *bsc,
+ * EnergyFunctional::solveSystemF (EnergyFunctional.cc:280-471) in the default solver mode
+ * (FIX_LAMBDA | ORTHOGONALIZE_X_LATER).  settings (NULL: the defaults) are checked first: another
+ * solver mode or vi_enable returns < 0.  Inputs are the stitched blocks; HM/bM may be NULL (no
+ * marginalisation prior).  nullspaces: [n_null][8N+4] column vectors (getNullspaces order) used when
+ * (iteration >= 2), may be NULL.  x_out: [8N+4]. */
+int ldso_ba_solve_system(const struct ldso_ba_opt_settings *settings, int32_t n_frames, int32_t iteration,
+                         double lambda, const double *HA, const double *bA, const double *HL, const double *bL,
+                         const double *HM, const double *bM, const double *Hsc, const double *bsc,
                          const double *nullspaces, int32_t n_null, double *x_out);
 
 /* FrameHessian::setStateZero nullspaces + FullSystem::getNullspaces (FullSystem.cc:2027-2076):
@@ -392,19 +397,56 @@ int ldso_ba_iterate(ldso_ba_ctx *ctx, int32_t iteration, double lambda, const do
 #define LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER 2048
 #define LDSO_BA_SOLVER_DEFAULT (LDSO_BA_SOLVER_FIX_LAMBDA | LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER)
 
-/* The FullSystem::optimize settings the device loop reads (Setting.cc:23, 36-38, 73). */
+/* The reference's global settings (src/Setting.cc) that change this path's arithmetic or control
+ * flow.  A caller copies its globals into this struct and hands it to
+ * ldso_ba_set_settings (per context), ldso_ba_optimize, ldso_ba_frame_take_data and
+ * ldso_ba_solve_system; every one of them runs ldso_ba_check_settings first, so a setting this
+ * library does not implement is refused (< 0 and a message) instead of silently run as the default.
+ * Start from LDSO_BA_OPT_SETTINGS_INIT (or ldso_ba_default_settings) so that fields added later
+ * keep their defaults. */
 typedef struct ldso_ba_opt_settings {
-    int32_t solver_mode;         /* setting_solverMode (LDSO_BA_SOLVER_DEFAULT)                  */
-    int32_t force_accept_step;   /* setting_forceAceptStep (1); 0 is rejected                      */
-    int32_t min_opt_iterations;  /* setting_minOptIterations (1)                                   */
-    float th_opt_iterations;     /* setting_thOptIterations (1.2f)                                 */
+    int32_t solver_mode;         /* setting_solverMode (LDSO_BA_SOLVER_DEFAULT, Setting.cc:23)     */
+    int32_t force_accept_step;   /* setting_forceAceptStep (1, :73); 0 is rejected                  */
+    int32_t min_opt_iterations;  /* setting_minOptIterations (1, :37)                               */
+    float th_opt_iterations;     /* setting_thOptIterations (1.2f, :38)                             */
+    /* setting_affineOptModeA / B (1e12 / 1e8, Setting.cc:65-66; the KITTI / EuRoC drivers set 0 / 0,
+     * run_dso_kitti.cc:299-300, run_dso_euroc.cc:291-292; TUM-Mono mode 2 sets -1 / -1):
+     *   >= 0  the affine parameter is optimised with this value as its prior (FrameHessian::getPrior,
+     *         FrameHessian.h:154-165; 0 = no prior);
+     *   <  0  it is fixed: prior setting_initialAffA/BPrior (1e14) and JabF[0] / JabF[1] zeroed after
+     *         the pattern sums (Residuals.cc:186-187), which removes it from Jab_r (the Top block's
+     *         b rows of a / b) and from fixLinearizationF's res_toZeroF (Residuals.cc:239-240).
+     * Must be finite. */
+    float affine_opt_mode_a;
+    float affine_opt_mode_b;
+    /* setting_vi_enable (Setting.cc:152: true in the reference; its drivers do not turn it off).
+     * The inertial terms (combineInertialHessians, H_I / b_I in solveSystemF, linearizeInertial,
+     * the inertial step of doStepFromBackup: EnergyFunctional.cc:307-376, FullSystem.cc:879-926,
+     * 1871-1931) are not implemented: 1 is refused.  Visual-only LDSO runs with 0. */
+    int32_t vi_enable;
+    int32_t reserved_;           /* 0 */
 } ldso_ba_opt_settings;
+
+#define LDSO_BA_OPT_SETTINGS_INIT {LDSO_BA_SOLVER_DEFAULT, 1, 1, 1.2f, 1e12f, 1e8f, 0, 0}
+
+/* Writes the defaults above (the reference's Setting.cc values, vi_enable = 0) into *s. */
+void ldso_ba_default_settings(ldso_ba_opt_settings *s);
 
 /* 0 when the settings are what this library runs, else -1 with a message naming the first
  * unsupported setting (SVD / SVD_CUT7 / ORTHOGONALIZE_SYSTEM / USE_GN / MOMENTUM / STEPMOMENTUM /
- * ... or force_accept_step == 0, whose accept / reject branch FullSystem.cc:935-966 is absent).
- * NULL means the defaults (accepted). */
+ * ... , force_accept_step == 0, whose accept / reject branch FullSystem.cc:935-966 is absent,
+ * vi_enable != 0, a non-finite affine mode).  NULL means the defaults (accepted). */
 int ldso_ba_check_settings(const ldso_ba_opt_settings *s);
+
+/* Install settings into a context (NULL: the defaults; a new context starts with the defaults).
+ * Checked first: a rejected set returns < 0 and leaves the context's settings unchanged, so a
+ * context never holds settings the library does not implement.  Every entry point that runs the
+ * path on the context reads them: ldso_ba_linearize (JabF zeroing), ldso_ba_marginalize_points
+ * (res_toZeroF; a marginalisation context takes its parent's settings at
+ * ldso_ba_load_marginalization), ldso_ba_solve / _solve_device / _iterate (solver mode) and
+ * ldso_ba_optimize (all of them; its frame step forms the affine priors from them). */
+int ldso_ba_set_settings(ldso_ba_ctx *ctx, const ldso_ba_opt_settings *s);
+int ldso_ba_get_settings(ldso_ba_ctx *ctx, ldso_ba_opt_settings *out);
 
 /* Per-window outcome of ldso_ba_optimize (status_out). */
 #define LDSO_BA_OPT_RAN_ALL 0      /* n_its iterations, no early exit                            */
@@ -428,7 +470,9 @@ int ldso_ba_check_settings(const ldso_ba_opt_settings *s);
  *     window order) below 5e-4 / 5e-5 x th_opt_iterations (FullSystem.cc:1914-1931) -- once
  *     iteration >= min_opt_iterations: the pass after that step still runs, then the window stops.
  * A stopped window's later launches are no-ops inside the same (captured) sequence.
- *   settings: NULL = the defaults; anything ldso_ba_check_settings rejects returns -1.
+ *   settings: NULL = the context's settings (ldso_ba_set_settings); otherwise they are checked and
+ *   installed into the context first, exactly as ldso_ba_set_settings does (anything
+ *   ldso_ba_check_settings rejects returns -1 and runs nothing).
  *   frames [sum N]: the windows' frame states back to back; calib_value / calib_value_zero
  *   [n_windows][4]: CalibHessian::value / value_zero (unscaled: value_scaled = 50 value);
  *   ns: [7][sum (8N+4)] nullspaces (ldso_ba_nullspaces per window, back to back) or NULL.

@@ -45,7 +45,7 @@ FRAME_STATE_DTYPE = np.dtype(
 assert FRAME_STATE_DTYPE.itemsize == 272
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # setting_solverMode bits (Settings.h:14-25) and ldso_ba_optimize's per-window outcome
 SOLVER_SVD, SOLVER_ORTHOGONALIZE_SYSTEM, SOLVER_ORTHOGONALIZE_POINTMARG, SOLVER_ORTHOGONALIZE_FULL = 1, 2, 4, 8
@@ -57,16 +57,26 @@ OPT_RAN_ALL, OPT_CONVERGED, OPT_LOST = 0, 1, 2
 
 class OptSettings(C.Structure):
     """ldso_ba_opt_settings: setting_solverMode, setting_forceAceptStep, setting_minOptIterations,
-    setting_thOptIterations (Setting.cc:23, 36-38, 73)."""
+    setting_thOptIterations, setting_affineOptModeA / B, setting_vi_enable (Setting.cc:23, 36-38, 65-66,
+    73, 152)."""
     _fields_ = [("solver_mode", C.c_int32), ("force_accept_step", C.c_int32), ("min_opt_iterations", C.c_int32),
-                ("th_opt_iterations", C.c_float)]
+                ("th_opt_iterations", C.c_float), ("affine_opt_mode_a", C.c_float), ("affine_opt_mode_b", C.c_float),
+                ("vi_enable", C.c_int32), ("reserved_", C.c_int32)]
 
     @classmethod
     def default(cls, **kw):
-        s = cls(SOLVER_DEFAULT, 1, 1, 1.2)
+        s = cls(SOLVER_DEFAULT, 1, 1, 1.2, 1e12, 1e8, 0, 0)
         for k, v in kw.items():
             setattr(s, k, v)
         return s
+
+
+# setting_affineOptModeA / B of the reference's drivers (the library default is Setting.cc:65-66)
+AFFINE_MODES = {
+    "default": (1e12, 1e8),     # Setting.cc:65-66
+    "kitti_euroc": (0.0, 0.0),  # run_dso_kitti.cc:299-300, run_dso_euroc.cc:291-292, TUM-Mono mode 1
+    "fixed": (-1.0, -1.0),      # run_dso_tum_mono.cc:291-292 (mode 2: a and b fixed)
+}
 
 
 class LdsoBaWindow(C.Structure):
@@ -109,9 +119,10 @@ ABI = [
     ("ldso_ba_last_error", C.c_char_p, []),
     ("ldso_ba_frame_precalc", C.c_int, [C.c_int32, C.c_void_p, f32p, f32p]),
     ("ldso_ba_set_adjoints", C.c_int, [C.c_int32, C.c_void_p, f64p, f64p, f64p]),
-    ("ldso_ba_frame_take_data", C.c_int, [C.c_int32, C.c_void_p, f64p, f64p, f64p]),
+    ("ldso_ba_frame_take_data", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, f64p, f64p, f64p]),
     ("ldso_ba_solve_system", C.c_int,
-     [C.c_int32, C.c_int32, C.c_double, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, C.c_int32, f64p]),
+     [C.c_void_p, C.c_int32, C.c_int32, C.c_double, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, f64p, C.c_int32,
+      f64p]),
     ("ldso_ba_nullspaces", C.c_int, [C.c_int32, C.c_void_p, f64p]),
     ("ldso_ba_validate_window", C.c_int, [C.POINTER(LdsoBaWindow)]),
     ("ldso_ba_create", C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
@@ -148,6 +159,9 @@ ABI = [
     ("ldso_ba_comm_unique_id", C.c_int, [C.c_void_p]),
     ("ldso_ba_comm_init", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_check_settings", C.c_int, [C.c_void_p]),
+    ("ldso_ba_default_settings", None, [C.c_void_p]),
+    ("ldso_ba_set_settings", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("ldso_ba_get_settings", C.c_int, [C.c_void_p, C.c_void_p]),
     ("ldso_ba_optimize", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, f64p, f64p, f64p, f64p, C.c_void_p,
                                    f64p, f32p, i32p, i32p]),
     ("ldso_ba_frame_step", C.c_int, [C.c_int32, C.c_void_p, f64p, C.c_void_p, f64p, f64p, f32p, f32p]),

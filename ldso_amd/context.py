@@ -37,6 +37,18 @@ class BAContext:
         except Exception:
             pass
 
+    # ---- settings ----------------------------------------------------------------------
+    def set_settings(self, settings=None):
+        """ldso_ba_set_settings: the reference settings this context runs with (an L.OptSettings;
+        None = the defaults).  Unsupported ones raise (the context keeps its previous settings)."""
+        L.check(self._lib.ldso_ba_set_settings(self._h, C.byref(settings) if settings is not None else None))
+        return self
+
+    def settings(self) -> L.OptSettings:
+        out = L.OptSettings()
+        L.check(self._lib.ldso_ba_get_settings(self._h, C.byref(out)))
+        return out
+
     # ---- structure ---------------------------------------------------------------------
     def load(self, windows, shard_rank: int = 0, shard_count: int = 1):
         if isinstance(windows, Window):
@@ -56,7 +68,8 @@ class BAContext:
         calib_value / calib_value_zero: [n_windows][4] CalibHessian::value / value_zero (default:
         each window's calib / 50, i.e. no calibration delta); settings: an L.OptSettings (None =
         the reference's defaults).  Returns (energies [n_its + 1][n_windows][3], frames,
-        calib_value, idepths, iterations [n_windows], status [n_windows] (L.OPT_*))."""
+        calib_value, idepths, iterations [n_windows], status [n_windows] (L.OPT_*)).  Non-None settings
+        are installed into the context first (ldso_ba_set_settings)."""
         nw = len(self.windows)
         frames = np.ascontiguousarray(np.concatenate([np.ascontiguousarray(w.frames) for w in self.windows]))
         if calib_value is None:

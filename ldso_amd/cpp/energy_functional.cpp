@@ -109,10 +109,10 @@ bool read_residuals(ldso_ba_ctx *ctx, const std::vector<PointFrameResidual *> &r
 
 }  // namespace
 
-void FrameHessian::takeData() {
+void FrameHessian::takeData(const ldso_ba_opt_settings *settings) {
     ldso_ba_frame_state S;
     frame_state(*this, S);
-    ldso_ba_frame_take_data(1, &S, prior, delta, delta_prior);
+    ldso_ba_frame_take_data(1, &S, settings, prior, delta, delta_prior);
 }
 
 // Residuals.cc:15-217 (see the header): the OOB early return here, the rest from the window's
@@ -187,6 +187,23 @@ EnergyFunctional::~EnergyFunctional() {
 
 void EnergyFunctional::fail(const char *what) { err_ = std::string(what) + ": " + ldso_ba_last_error(); }
 
+bool EnergyFunctional::setSettings(const ldso_ba_opt_settings &s) {
+    if (!ctx_) return false;
+    if (ldso_ba_set_settings(ctx_, &s) || (margCtx_ && ldso_ba_set_settings(margCtx_, &s))) {
+        fail("ldso_ba_set_settings");
+        return false;
+    }
+    const bool priors_change = s.affine_opt_mode_a != settings_.affine_opt_mode_a ||
+                               s.affine_opt_mode_b != settings_.affine_opt_mode_b;
+    settings_ = s;
+    if (priors_change) {  // takeData's priors follow the affine modes: recompute and re-upload them
+        for (const shared_ptr<FrameHessian> &f : frames) f->takeData(&settings_);
+        fsUp_.clear();
+        epoch_++;
+    }
+    return true;
+}
+
 void EnergyFunctional::packFrames(std::vector<ldso_ba_frame_state> &fs) const {
     fs.resize(frames.size());
     for (size_t f = 0; f < frames.size(); f++) frame_state(*frames[f], fs[f]);
@@ -206,7 +223,7 @@ void EnergyFunctional::insertResidual(shared_ptr<PointFrameResidual> r) {
 // EnergyFunctional.cc:51-98 (the non-VI part): HM, bM grow by the frame's 8 zero rows/columns
 void EnergyFunctional::insertFrame(shared_ptr<FrameHessian> fh, shared_ptr<CalibHessian> Hcalib) {
     residualTouched();
-    fh->takeData();
+    fh->takeData(&settings_);
     frames.push_back(fh);
     fh->idx = (int)frames.size();
     nFrames++;
@@ -418,7 +435,7 @@ void EnergyFunctional::setDeltaF(shared_ptr<CalibHessian> HCalib) {
     for (int k = 0; k < 4; k++) cDeltaF[k] = (float)HCalib->value_minus_value_zero[k];
     std::vector<double> delta((size_t)8 * nFrames);
     for (int f = 0; f < nFrames; f++) {
-        frames[f]->takeData();
+        frames[f]->takeData(&settings_);
         std::memcpy(&delta[(size_t)8 * f], frames[f]->delta, 8 * sizeof(double));
     }
     adHTdeltaF.assign((size_t)nFrames * nFrames * 8, 0.f);
@@ -477,7 +494,7 @@ bool EnergyFunctional::uploadFrameTerms() {
     fDeltaPrior_.assign((size_t)N * 8, 0.0);
     if (ldso_ba_frame_precalc(N, fs_.data(), calib_.value_scaledf, precalc_.data()) ||
         ldso_ba_set_adjoints(N, fs_.data(), adH_.data(), adT_.data(), cPrior_.data()) ||
-        ldso_ba_frame_take_data(N, fs_.data(), fPrior_.data(), fDelta_.data(), fDeltaPrior_.data())) {
+        ldso_ba_frame_take_data(N, fs_.data(), &settings_, fPrior_.data(), fDelta_.data(), fDeltaPrior_.data())) {
         fail("frame terms");
         return false;
     }
@@ -771,6 +788,7 @@ Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std:
     if (nFrames < 2) return out;   // FullSystem.cc:846-851
     if (nFrames < 3) n_its = 20;
     if (nFrames < 4) n_its = 15;
+    if (settings && !setSettings(*settings)) return out;
     epoch_++;
     calib_ = *HCalib;
     if (!upload()) return out;
@@ -784,7 +802,7 @@ Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std:
     std::vector<float> idepth(P);
     double calib_out[4];
     int32_t its = 0, status = 0;
-    if (ldso_ba_optimize(ctx_, n_its, settings, fs_.data(), HCalib->value, HCalib->value_zero, ns.data(), e.data(),
+    if (ldso_ba_optimize(ctx_, n_its, &settings_, fs_.data(), HCalib->value, HCalib->value_zero, ns.data(), e.data(),
                          fo.data(), calib_out, idepth.data(), &its, &status)) {
         fail("ldso_ba_optimize");
         return out;
@@ -832,6 +850,10 @@ Vec3 EnergyFunctional::optimize(int n_its, shared_ptr<CalibHessian> HCalib, std:
 // HM / bM, the pose and scale nullspaces (FullSystem::getNullspaces) and the host LDL^T
 void EnergyFunctional::solveSystemF(int iteration, double lambda, shared_ptr<CalibHessian> HCalib) {
     (void)HCalib;
+    if (ldso_ba_check_settings(&settings_)) {  // the solver mode / vi_enable this branch implements
+        fail("solveSystemF");
+        return;
+    }
     currentLambda_ = lambda;
     const int n = 8 * nFrames + CPARS;
     HA_top = MatXX(n, n);
@@ -860,8 +882,8 @@ void EnergyFunctional::solveSystemF(int iteration, double lambda, shared_ptr<Cal
     lastNullspaces_forLogging = lastNullspaces_pose;
     lastNullspaces_forLogging.push_back(lastNullspaces_scale[0]);
     lastX = VecX(n);
-    if (ldso_ba_solve_system(nFrames, iteration, lambda, HA_top.data(), bA_top.data(), HL_top.data(), bL_top.data(),
-                             HM.data(), bM.data(), H_sc.data(), b_sc.data(), ns.data(), 7, lastX.data()))
+    if (ldso_ba_solve_system(&settings_, nFrames, iteration, lambda, HA_top.data(), bA_top.data(), HL_top.data(),
+                             bL_top.data(), HM.data(), bM.data(), H_sc.data(), b_sc.data(), ns.data(), 7, lastX.data()))
         fail("ldso_ba_solve_system");
 }
 

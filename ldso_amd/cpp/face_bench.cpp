@@ -109,7 +109,8 @@ int main(int argc, char **argv) {
         ef->optimize(n_its, HCalib, nullptr, &lost, &its_default);
     }
     // EnergyFunctional::optimize(6), all iterations
-    ldso_ba_opt_settings all_its = {LDSO_BA_SOLVER_DEFAULT, 1, 1, 0.0f};
+    ldso_ba_opt_settings all_its = LDSO_BA_OPT_SETTINGS_INIT;
+    all_its.th_opt_iterations = 0.0f;
     for (int i = 0; i < 2; i++) ef->optimize(n_its, HCalib, nullptr, nullptr, nullptr, &all_its);
     auto t0 = Clock::now();
     for (int i = 0; i < reps; i++) ef->optimize(n_its, HCalib, nullptr, nullptr, nullptr, &all_its);
@@ -276,7 +277,7 @@ int main(int argc, char **argv) {
     std::vector<double> adH((size_t)N * N * 64), adT((size_t)N * N * 64), cp(4), fp(8 * N), fd(8 * N), fdp(8 * N);
     ldso_ba_frame_precalc(N, fs.data(), calib, precalc.data());
     ldso_ba_set_adjoints(N, fs.data(), adH.data(), adT.data(), cp.data());
-    ldso_ba_frame_take_data(N, fs.data(), fp.data(), fd.data(), fdp.data());
+    ldso_ba_frame_take_data(N, fs.data(), nullptr, fp.data(), fd.data(), fdp.data());
     const float cdelta[4] = {0, 0, 0, 0};
     ldso_ba_window w;
     std::memset(&w, 0, sizeof(w));

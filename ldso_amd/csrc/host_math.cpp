@@ -65,9 +65,10 @@ int set_adjoints(int N, const ldso_ba_frame_state *fr, double *adH, double *adT,
 }
 
 // FrameHessian::takeData / getPrior / get_state_minus_stateZero (FrameHessian.h:59-70,142-174)
-int frame_take_data(int N, const ldso_ba_frame_state *fr, double *prior, double *delta, double *delta_prior) {
+int frame_take_data(int N, const ldso_ba_frame_state *fr, float mode_a, float mode_b, double *prior, double *delta,
+                    double *delta_prior) {
     for (int f = 0; f < N; f++)
-        frame_take_data_one(fr[f], prior ? prior + 8 * f : nullptr, delta ? delta + 8 * f : nullptr,
+        frame_take_data_one(fr[f], mode_a, mode_b, prior ? prior + 8 * f : nullptr, delta ? delta + 8 * f : nullptr,
                             delta_prior ? delta_prior + 8 * f : nullptr);
     return 0;
 }

@@ -154,6 +154,7 @@ struct LinParams {
     const float *ad_ht_delta;  // [pair_global][8] EnergyFunctional::adHTdeltaF (marginalisation pass)
     const int *stop;           // ldso_ba_optimize: [win] first pass index a window skips - 1 (see opt_pass)
     int pass;                  // ldso_ba_optimize: this pass's index (0 = the initial linearizeAll)
+    int aff_fix;               // bit 0: setting_affineOptModeA < 0, bit 1: ...B < 0 (JabF zeroed, Residuals.cc:186-187)
 };
 
 struct Geo {
@@ -358,10 +359,13 @@ __device__ __forceinline__ float sqrt_rn_normal(float a) {
 // kMarg: the JI_r / Jab_r / rr addends use res_toZeroF of fixLinearizationF (Residuals.cc:219-245,
 // resF - JIdx Jp_delta - JabF delta_ab) as AccumulatedTopHessianSSE::addPoint<2> does
 // (AccumulatedTopHessian.cc:44-45, 66-76); jx, jy = Jp_delta_x/y, da, db = adHTdeltaF[6], [7].
+// fixA / fixB (setting_affineOptModeA / B < 0, wave-uniform): JabF[0] / JabF[1] are zeroed after the
+// pattern sums (Residuals.cc:186-187), i.e. they leave JabJIdx and Jab2 alone and remove the affine
+// parameter from Jab_r (AccumulatedTopHessian.cc:71-72) and from res_toZeroF (Residuals.cc:239-240).
 template <bool kMarg>
 __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float color, float weight, float aff0,
                                             float aff1, float b0, float t[kSums], float jx, float jy, float da,
-                                            float db) {
+                                            float db, bool fixA, bool fixB) {
 #pragma clang fp contract(off)
     const float residual = I - (float)(aff0 * color + aff1);
     const float drdA = (color - b0);
@@ -376,7 +380,8 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
     gx *= hw;
     gy *= hw;
     const float resF = residual * hw;
-    const float jab0 = drdA * hw;
+    const float jab0 = fixA ? 0.0f : drdA * hw;  // JabF[0], JabF[1] as Jab_r and res_toZeroF see them
+    const float jab1 = fixB ? 0.0f : hw;
     t[2] = gx * gx;
     t[4] = gy * gy;
     t[3] = gx * gy;
@@ -393,12 +398,12 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
         ra = ra - gx * jx;
         ra = ra - gy * jy;
         ra = ra - jab0 * da;
-        ra = ra - hw * db;
+        ra = ra - jab1 * db;
     }
     t[12] = ra * gx;
     t[13] = ra * gy;
     t[14] = ra * jab0;
-    t[15] = ra * hw;
+    t[15] = ra * jab1;
     t[16] = ra * ra;
 }
 
@@ -605,9 +610,10 @@ template <bool kMarg>
 __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, float *S, const float *pre, int jlimit,
                                                int my_state, float4 my_pd0, float jp_dx, float jp_dy, float da,
                                                float db, __amdgpu_buffer_rsrc_t rsrc, unsigned band, float wM3,
-                                               float hM3) {
+                                               float hM3, int aff_fix) {
 #pragma clang fp contract(off)
     const int g = lane >> 3, sl = lane & 7;
+    const bool fixA = (aff_fix & 1) != 0, fixB = (aff_fix & 2) != 0;
     // staticPattern[8] (Setting.cc:275) offset of this lane's pixel
     const int px = sl == 1 || sl == 6 ? -1 : sl == 2 ? 1 : sl == 3 ? -2 : sl == 5 ? 2 : 0;
     const int py = sl == 0 ? -2 : sl <= 2 ? -1 : sl <= 5 ? 0 : sl == 6 ? 1 : 2;
@@ -719,7 +725,7 @@ __device__ __forceinline__ void phase_a_pieces(int lane, float *lds_terms_w, flo
             const float3 s3 = bilin12(iv, q.Ku - ix, q.Kv - iy);
             fin = isfinite(s3.x);
             pixel_terms<kMarg>(s3.x, s3.y, s3.z, color, weight, aff0, aff1, b0a, tt, kMarg ? q.jx : 0.f,
-                               kMarg ? q.jy : 0.f, da, db);
+                               kMarg ? q.jy : 0.f, da, db, fixA, fixB);
         }
         const unsigned long long m2 = __ballot(fin);
         const bool rok = part && ((m2 >> (8 * g)) & 0xFFull) == 0xFFull;
@@ -881,7 +887,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
             make_float4(my_pd0.x, my_pd0.y, my_pd0.z, __int_as_float(my_state));
         wave_lds_sync();
         phase_a_pieces<kMarg>(lane, lds_terms_w, lds_sums_w, pre, jlimit, my_state, my_pd0, jp_dx, jp_dy, da, db,
-                              rsrc, band, wM3, hM3);
+                              rsrc, band, wM3, hM3, __builtin_amdgcn_readfirstlane(P.aff_fix));
     } else {
 #pragma clang fp contract(off)
         const int g = lane >> 3, sl = lane & 7;
@@ -958,7 +964,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
                 }
                 fin = isfinite(I);
                 pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt, kMarg ? q.jx : 0.f,
-                                   kMarg ? q.jy : 0.f, da, db);
+                                   kMarg ? q.jy : 0.f, da, db, (P.aff_fix & 1) != 0, (P.aff_fix & 2) != 0);
             }
             const unsigned long long m2 = __ballot(fin);
             const bool rok = q.gok && ((m2 >> (8 * g)) & 0xFFull) == 0xFFull;
@@ -3724,6 +3730,7 @@ struct FrameStepParams {
     const float *win_nid;  // [win][2]: sumNID, numID of the idepths the step starts from (window_nid)
     int it, min_its;
     float th;  // setting_thOptIterations
+    float aff_a, aff_b;  // setting_affineOptModeA / B: the affine priors of takeData (getPrior)
 };
 // one window's step: a whole 256-thread block (blk = the window)
 __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int blk) {
@@ -3777,7 +3784,7 @@ __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int b
     }
     if (tid < N) {
         double pr[8], dp[8];
-        frame_take_data_one(fs[tid], pr, nullptr, dp);
+        frame_take_data_one(fs[tid], P.aff_a, P.aff_b, pr, nullptr, dp);
         const bool add = P.add_priors[blk] != 0;
         for (int i = 0; i < 8; i++) {
             const int q = W.vec_base + 4 + 8 * tid + i;
@@ -3953,13 +3960,18 @@ struct ldso_ba_ctx {
     int opt_it = 0;
     // captured launch sequences: ldso_ba_optimize's GN iterations [projection][last pass][ns given]
     // and ldso_ba_iterate's pass + solve + resubstitution [projection]
+    // a cached graph and everything fixed at its capture, compared field by field (no packing into
+    // one word: a collision would replay a graph whose launch parameters differ)
     struct Graph {
         hipGraphExec_t exec = nullptr;
-        unsigned long long gen = 0, key = 0;
+        unsigned long long gen = 0;
+        std::vector<unsigned long long> key;
     };
     Graph opt_graph[2], it_graph[2];  // ldso_ba_optimize's whole call (without / with nullspaces)
     bool opt_warm = false;            // an optimize call ran directly on this context
     int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major
+    // the reference's settings this context runs with (ldso_ba_set_settings; always checked)
+    ldso_ba_opt_settings settings = LDSO_BA_OPT_SETTINGS_INIT;
     int n_win = 0, width = 0, height = 0, npix = 0;
     std::vector<WinHost> wh;
     std::vector<WinDev> wd;
@@ -4054,6 +4066,11 @@ struct ldso_ba_ctx {
 };
 
 namespace {
+
+// LinParams::aff_fix of the context's settings: which of JabF[0] / JabF[1] linearize zeroes
+inline int aff_fix_bits(const ldso_ba_ctx *c) {
+    return (c->settings.affine_opt_mode_a < 0 ? 1 : 0) | (c->settings.affine_opt_mode_b < 0 ? 2 : 0);
+}
 
 // grow-only pinned host staging (the address is kept while it fits)
 int pin_ensure(char *&p, size_t &cap, size_t bytes) {
@@ -4357,19 +4374,27 @@ int ldso_ba_set_adjoints(int32_t n, const ldso_ba_frame_state *f, double *adH, d
     if (n < 1 || n > LDSO_BA_MAX_FRAMES || !f || !adH || !adT) return fail(-1, "bad arguments");
     return set_adjoints(n, f, adH, adT, cp);
 }
-int ldso_ba_frame_take_data(int32_t n, const ldso_ba_frame_state *f, double *prior, double *delta, double *dp) {
+int ldso_ba_frame_take_data(int32_t n, const ldso_ba_frame_state *f, const ldso_ba_opt_settings *st, double *prior,
+                            double *delta, double *dp) {
     if (n < 1 || n > LDSO_BA_MAX_FRAMES || !f) return fail(-1, "bad arguments");
-    return frame_take_data(n, f, prior, delta, dp);
+    int rc;
+    if ((rc = ldso_ba_check_settings(st))) return rc;
+    const ldso_ba_opt_settings s = st ? *st : ldso_ba_opt_settings LDSO_BA_OPT_SETTINGS_INIT;
+    return frame_take_data(n, f, s.affine_opt_mode_a, s.affine_opt_mode_b, prior, delta, dp);
 }
 int ldso_ba_nullspaces(int32_t n, const ldso_ba_frame_state *f, double *out) {
     if (n < 1 || n > LDSO_BA_MAX_FRAMES || !f || !out) return fail(-1, "bad arguments");
     return nullspaces(n, f, out);
 }
-int ldso_ba_solve_system(int32_t n, int32_t it, double lambda, const double *HA, const double *bA, const double *HL,
-                         const double *bL, const double *HM, const double *bM, const double *Hsc, const double *bsc,
-                         const double *ns, int32_t nn, double *x) {
+int ldso_ba_solve_system(const ldso_ba_opt_settings *st, int32_t n, int32_t it, double lambda, const double *HA,
+                         const double *bA, const double *HL, const double *bL, const double *HM, const double *bM,
+                         const double *Hsc, const double *bsc, const double *ns, int32_t nn, double *x) {
     if (n < 1 || n > LDSO_BA_MAX_FRAMES || !HA || !bA || !HL || !bL || !Hsc || !bsc || !x)
         return fail(-1, "bad arguments");
+    int rc;
+    if ((rc = ldso_ba_check_settings(st))) return rc;  // the default solver mode only, no inertial terms
+    // without SOLVER_ORTHOGONALIZE_X_LATER the solve never projects (EnergyFunctional.cc:428-432)
+    if (st && !(st->solver_mode & LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER)) nn = 0;
     return solve_system(n, it, lambda, HA, bA, HL, bL, HM, bM, Hsc, bsc, ns, nn, x);
 }
 
@@ -4982,6 +5007,7 @@ int ldso_ba_load_marginalization(ldso_ba_ctx *marg, const ldso_ba_ctx *parent, i
     const WinDev &pw = parent->wd[parent_win];
     if (points->n_frames != pw.N || points->width != pw.width || points->height != pw.height)
         return fail(-1, "marginalisation window does not match the parent window's frames");
+    marg->settings = parent->settings;  // the parent's affine modes shape res_toZeroF and Jab_r
     return load_impl(marg, 1, points, 0, 1, parent, parent_win);
 }
 
@@ -5169,11 +5195,12 @@ int ldso_ba_comm_init(ldso_ba_ctx *c, const uint8_t *id_in, int32_t rank, int32_
 
 int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
+    int rc;
+    if ((rc = ldso_ba_check_settings(&c->settings))) return rc;
     HIP_TRY(hipSetDevice(c->device));
     c->sys_host_valid = false;
     c->energy_valid = false;
     c->th_host_valid = false;
-    int rc;
     LinParams L{};
     L.items = c->d_top_items.p;
     L.wins = c->d_wins.p;
@@ -5198,6 +5225,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     L.tiles_per_row = c->tiles_per_row;
     L.fix = fix;
     L.accumulate = accumulate;
+    L.aff_fix = aff_fix_bits(c);
     L.item_base = 0;
     L.n_items = c->n_top_items;
     L.n_blocks = (L.n_items + 3) / 4;
@@ -5330,6 +5358,7 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
         HIP_TRY(hipGetLastError());
     }
     LinParams L{};
+    L.aff_fix = aff_fix_bits(c);
     L.items = c->d_top_items.p;
     L.wins = c->d_wins.p;
     L.img = c->img_ext ? c->img_ext : c->d_img.p;
@@ -5551,8 +5580,8 @@ int ldso_ba_solve(ldso_ba_ctx *c, int32_t win, int32_t iteration, double lambda,
     std::vector<double> HA((size_t)n * n), bA(n), HL((size_t)n * n), bL(n), Hsc((size_t)n * n), bsc(n);
     int rc = ldso_ba_get_system(c, win, HA.data(), bA.data(), HL.data(), bL.data(), Hsc.data(), bsc.data());
     if (rc) return rc;
-    return solve_system(c->wh[win].N, iteration, lambda, HA.data(), bA.data(), HL.data(), bL.data(), nullptr, nullptr,
-                        Hsc.data(), bsc.data(), ns, n_null, x_out);
+    return ldso_ba_solve_system(&c->settings, c->wh[win].N, iteration, lambda, HA.data(), bA.data(), HL.data(),
+                                bL.data(), nullptr, nullptr, Hsc.data(), bsc.data(), ns, n_null, x_out);
 }
 
 int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t *state, float *state_energy,
@@ -5718,6 +5747,11 @@ int upload_nullspaces(ldso_ba_ctx *c, const double *ns, int n_null) {
     c->ns_cache_null = n_null;
     return 0;
 }
+// SOLVER_ORTHOGONALIZE_X_LATER in the context's solver mode: the solve projects x from iteration 2
+// (EnergyFunctional.cc:428-432); without it the nullspaces are ignored
+inline bool ortho_x_later(const ldso_ba_ctx *c) {
+    return (c->settings.solver_mode & LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER) != 0;
+}
 // k_solve_fast (or the exact k_solve_reg / k_solve) for every loaded window; n_null > 0 projects
 // with the nullspaces upload_nullspaces prepared (iteration >= 2), n_null == 0 does not project
 int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
@@ -5781,9 +5815,10 @@ int ldso_ba_solve_device(ldso_ba_ctx *c, int32_t iteration, double lambda, const
     (void)lambda;  // SOLVER_FIX_LAMBDA, as the host solver
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
     if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
-    HIP_TRY(hipSetDevice(c->device));
-    const bool project = iteration >= 2 && ns && n_null > 0;
     int rc;
+    if ((rc = ldso_ba_check_settings(&c->settings))) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    const bool project = iteration >= 2 && ns && n_null > 0 && ortho_x_later(c);
     if (project && (rc = upload_nullspaces(c, ns, n_null))) return rc;
     rc = solve_device_launch(c, iteration, project ? n_null : 0);
     if (rc) return rc;
@@ -5830,10 +5865,22 @@ int ldso_ba_resubstitute_device(ldso_ba_ctx *c, double lambda, float *point_step
 
 }  // extern "C"
 namespace {
+// The launch parameters a captured pass / solve sequence depends on besides the call's own
+// arguments: the solve kernel (exact or fast), the stitch split, and every setting the kernels read.
+std::vector<unsigned long long> capture_key(const ldso_ba_ctx *c) {
+    const char *hs = std::getenv("LDSO_BA_HS_SPLIT");
+    unsigned a, b, th;
+    std::memcpy(&a, &c->settings.affine_opt_mode_a, 4);
+    std::memcpy(&b, &c->settings.affine_opt_mode_b, 4);
+    std::memcpy(&th, &c->settings.th_opt_iterations, 4);
+    return {(unsigned long long)c->solve_exact, (unsigned long long)getenv_flag("LDSO_BA_SOLVE_LDS"),
+            (unsigned long long)(hs ? (hs[0] == '1' ? 1 : 2) : 0), (unsigned long long)(unsigned)c->settings.solver_mode,
+            (unsigned long long)(unsigned)c->settings.min_opt_iterations, a, b, th};
+}
 // Launch a captured sequence: replay g if it was captured under the current allocation
 // generation and key, else capture `body`'s launches on the context stream, instantiate, cache.
 template <typename F>
-int launch_cached_graph(ldso_ba_ctx *c, ldso_ba_ctx::Graph &g, unsigned long long key, F &&body) {
+int launch_cached_graph(ldso_ba_ctx *c, ldso_ba_ctx::Graph &g, const std::vector<unsigned long long> &key, F &&body) {
     const unsigned long long gen = g_alloc_gen.load();
     if (g.exec && (g.gen != gen || g.key != key)) {
         (void)hipGraphExecDestroy(g.exec);
@@ -5872,10 +5919,11 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
                     float *point_step_out, double *energy_out) {
     if (!c || c->n_win == 0) return fail(-1, "no windows loaded");
     if (n_null < 0 || n_null > 7) return fail(-1, "n_null must be in [0, 7]");
-    HIP_TRY(hipSetDevice(c->device));
     int rc;
+    if ((rc = ldso_ba_check_settings(&c->settings))) return rc;
+    HIP_TRY(hipSetDevice(c->device));
     // the projection uses the nullspaces of THIS call (as ldso_ba_solve_device)
-    const bool project = iteration >= 2 && n_null > 0 && ns;
+    const bool project = iteration >= 2 && n_null > 0 && ns && ortho_x_later(c);
     if (project && (rc = upload_nullspaces(c, ns, n_null)))  // before (outside) the captured sequence
         return rc;
     // pass + solve + resubstitution (LDSO_BA_ITERATE_GRAPH=1: one captured graph per (projection,
@@ -5891,12 +5939,12 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
     if (!c->comm && !c->timing && getenv_flag("LDSO_BA_ITERATE_GRAPH") && !getenv_flag("LDSO_BA_NO_GRAPH")) {
         unsigned long long lb;
         std::memcpy(&lb, &lambda, sizeof(lb));
-        // keyed by everything fixed at capture: lambda, n_null, the solve kernel, the stitch split
-        const char *hs = std::getenv("LDSO_BA_HS_SPLIT");
-        const unsigned long long mode = (c->solve_exact ? 1ull : 0ull) | (getenv_flag("LDSO_BA_SOLVE_LDS") ? 2ull : 0ull) |
-                                        (hs ? (hs[0] == '1' ? 4ull : 8ull) : 0ull);
-        rc = launch_cached_graph(c, c->it_graph[project ? 1 : 0],
-                                 lb ^ ((unsigned long long)n_null << 56) ^ (mode << 60), body);
+        // keyed by everything fixed at capture: lambda, n_null, the solve kernel, the stitch split,
+        // the settings the pass reads
+        std::vector<unsigned long long> key = capture_key(c);
+        key.push_back(lb);
+        key.push_back((unsigned long long)n_null);
+        rc = launch_cached_graph(c, c->it_graph[project ? 1 : 0], key, body);
     } else {
         rc = body();
     }
@@ -5972,6 +6020,32 @@ int ldso_ba_check_settings(const ldso_ba_opt_settings *s) {
         return fail(-1, "setting_forceAceptStep = false (the accept / reject branch with loadStateBackup, "
                         "FullSystem.cc:935-966) is not implemented");
     if (s->min_opt_iterations < 0) return fail(-1, "setting_minOptIterations < 0");
+    if (s->vi_enable)
+        return fail(-1, "setting_vi_enable = true: the inertial terms (combineInertialHessians and H_I / b_I in "
+                        "solveSystemF, EnergyFunctional.cc:307-376; linearizeInertial, FullSystem.cc:879-926; the "
+                        "inertial step and canbreak terms of doStepFromBackup, FullSystem.cc:1871-1931) are not "
+                        "implemented: run visual-only (setting_vi_enable = false)");
+    if (!std::isfinite(s->affine_opt_mode_a) || !std::isfinite(s->affine_opt_mode_b))
+        return fail(-1, "setting_affineOptModeA / B must be finite");
+    if (s->reserved_ != 0) return fail(-1, "ldso_ba_opt_settings.reserved_ must be 0");
+    return 0;
+}
+
+void ldso_ba_default_settings(ldso_ba_opt_settings *s) {
+    if (s) *s = ldso_ba_opt_settings LDSO_BA_OPT_SETTINGS_INIT;
+}
+
+int ldso_ba_set_settings(ldso_ba_ctx *c, const ldso_ba_opt_settings *s) {
+    if (!c) return fail(-1, "bad arguments");
+    int rc;
+    if ((rc = ldso_ba_check_settings(s))) return rc;
+    c->settings = s ? *s : ldso_ba_opt_settings LDSO_BA_OPT_SETTINGS_INIT;
+    return 0;
+}
+
+int ldso_ba_get_settings(ldso_ba_ctx *c, ldso_ba_opt_settings *out) {
+    if (!c || !out) return fail(-1, "bad arguments");
+    *out = c->settings;
     return 0;
 }
 
@@ -5983,11 +6057,10 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *
     if (n_its < 0 || !frames || !calib_value || !calib_value_zero) return fail(-1, "bad arguments");
     if (c->marg) return fail(-1, "not on a marginalisation context");
     int rc;
-    if ((rc = ldso_ba_check_settings(settings))) return rc;
-    const ldso_ba_opt_settings st = settings ? *settings
-                                             : ldso_ba_opt_settings{LDSO_BA_SOLVER_DEFAULT, 1, 1, 1.2f};
+    if (settings && (rc = ldso_ba_set_settings(c, settings))) return rc;  // checked, then installed
+    const ldso_ba_opt_settings st = c->settings;
     // without SOLVER_ORTHOGONALIZE_X_LATER the solve never projects (EnergyFunctional.cc:428-432)
-    if (!(st.solver_mode & LDSO_BA_SOLVER_ORTHOGONALIZE_X_LATER)) ns = nullptr;
+    if (!ortho_x_later(c)) ns = nullptr;
     HIP_TRY(hipSetDevice(c->device));
     const int nw = c->n_win;
     // ensure(): the buffers keep their addresses across calls, so cached graphs stay valid
@@ -6028,6 +6101,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *
     F.win_nid = c->d_win_nid.p;
     F.min_its = st.min_opt_iterations;
     F.th = st.th_opt_iterations;
+    F.aff_a = st.affine_opt_mode_a;
+    F.aff_b = st.affine_opt_mode_b;
     // one GN iteration: solveSystemF (a NaN x: the window is lost), resubstituteF_MT,
     // doStepFromBackup + setPrecalcValues (canbreak), linearizeAll + applyRes (+ the accumulation
     // the next solve uses); windows that left the loop skip every launch
@@ -6068,15 +6143,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *
     };
     const bool use_graph = !c->comm && !c->timing && !getenv_flag("LDSO_BA_NO_GRAPH");
     if (use_graph && c->opt_warm) {
-        unsigned th_bits;
-        std::memcpy(&th_bits, &st.th_opt_iterations, sizeof(th_bits));
-        const char *hs = std::getenv("LDSO_BA_HS_SPLIT");
-        const unsigned long long key = (unsigned long long)(n_its & 0xFFFF) |
-                                       ((unsigned long long)(std::min(st.min_opt_iterations, 255)) << 16) |
-                                       ((unsigned long long)(c->solve_exact ? 1 : 0) << 24) |
-                                       ((unsigned long long)(getenv_flag("LDSO_BA_SOLVE_LDS") ? 1 : 0) << 25) |
-                                       ((unsigned long long)(hs ? (hs[0] == '1' ? 1 : 2) : 0) << 26) |
-                                       ((unsigned long long)th_bits << 32);
+        std::vector<unsigned long long> key = capture_key(c);  // the settings were installed above
+        key.push_back((unsigned long long)(unsigned)n_its);
         rc = launch_cached_graph(c, c->opt_graph[ns ? 1 : 0], key, body);
     } else {
         rc = body();  // the first call runs directly (one-time setup stays out of any capture)

@@ -20,8 +20,6 @@ constexpr float kScaleC = 50.0f;
 // src/Setting.cc
 constexpr float kOutlierTHSumComponent = 50.0f * 50.0f;  // :41
 constexpr float kHuberTH = 9.0f;                           // :76
-constexpr float kAffineOptModeA = 1e12f;                   // :65
-constexpr float kAffineOptModeB = 1e8f;                    // :66
 constexpr float kFrameEnergyTHN = 0.7f;                    // :79
 constexpr float kFrameEnergyTHConstWeight = 0.5f;          // :77
 constexpr float kFrameEnergyTHFacMedian = 1.5f;            // :81
@@ -98,7 +96,8 @@ int set_error(int code, const std::string &msg);
 
 int frame_precalc(int N, const ldso_ba_frame_state *fr, const float calib[4], float *out);
 int set_adjoints(int N, const ldso_ba_frame_state *fr, double *adH, double *adT, double *cPrior);
-int frame_take_data(int N, const ldso_ba_frame_state *fr, double *prior, double *delta, double *delta_prior);
+int frame_take_data(int N, const ldso_ba_frame_state *fr, float mode_a, float mode_b, double *prior, double *delta,
+                    double *delta_prior);
 int nullspaces(int N, const ldso_ba_frame_state *fr, double *out);
 int solve_system(int N, int iteration, double lambda, const double *HA, const double *bA, const double *HL,
                  const double *bL, const double *HM, const double *bM, const double *Hsc, const double *bsc,

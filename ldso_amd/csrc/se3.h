@@ -211,8 +211,12 @@ LDSO_HD inline void pair_precalc(const Pose &ev_t, const Pose &evInvH, const Pos
     o[26] = (float)(fh.state_zero[7] * kScaleB);  // PRE_b0_mode = aff_g2l_0().b
 }
 
-// FrameHessian::takeData / getPrior / get_state_minus_stateZero / get_state_minus_statePriorZero
-LDSO_HD inline void frame_take_data_one(const ldso_ba_frame_state &F, double *prior, double *delta, double *delta_prior) {
+// FrameHessian::takeData / getPrior / get_state_minus_stateZero / get_state_minus_statePriorZero.
+// mode_a / mode_b: setting_affineOptModeA / B (getPrior, FrameHessian.h:142-170: the prior on a / b
+// is the mode itself when >= 0, setting_initialAffA/BPrior when < 0; the first frame always gets
+// the initial priors).  The float settings widen to the double prior as in the reference.
+LDSO_HD inline void frame_take_data_one(const ldso_ba_frame_state &F, float mode_a, float mode_b, double *prior,
+                                        double *delta, double *delta_prior) {
 #pragma clang fp contract(off)
     double p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (F.is_first_frame) {
@@ -221,8 +225,8 @@ LDSO_HD inline void frame_take_data_one(const ldso_ba_frame_state &F, double *pr
         p[6] = kInitialAffAPrior;
         p[7] = kInitialAffBPrior;
     } else {
-        p[6] = kAffineOptModeA < 0 ? kInitialAffAPrior : kAffineOptModeA;
-        p[7] = kAffineOptModeB < 0 ? kInitialAffBPrior : kAffineOptModeB;
+        p[6] = mode_a < 0 ? kInitialAffAPrior : mode_a;
+        p[7] = mode_b < 0 ? kInitialAffBPrior : mode_b;
     }
     double mz[6], z[6], lg[6];
     for (int i = 0; i < 6; i++) {

@@ -41,6 +41,9 @@ class Window:
     frame_prior: np.ndarray = None    # f64[N, 8]
     frame_delta: np.ndarray = None    # f64[N, 8]
     frame_delta_prior: np.ndarray = None  # f64[N, 8]
+    # the reference settings takeData's priors follow (setting_affineOptModeA / B): an L.OptSettings,
+    # None = the defaults.  The context that runs the window must hold the same (BAContext.set_settings).
+    settings: object = None
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -71,7 +74,8 @@ class Window:
         self.frame_prior = np.zeros((N, 8), np.float64)
         self.frame_delta = np.zeros((N, 8), np.float64)
         self.frame_delta_prior = np.zeros((N, 8), np.float64)
-        L.check(lib.ldso_ba_frame_take_data(N, fr.ctypes.data, L.ptr(self.frame_prior, L.f64p),
+        sp = C.byref(self.settings) if self.settings is not None else None
+        L.check(lib.ldso_ba_frame_take_data(N, fr.ctypes.data, sp, L.ptr(self.frame_prior, L.f64p),
                                             L.ptr(self.frame_delta, L.f64p), L.ptr(self.frame_delta_prior, L.f64p)))
         if self.c_delta is None:
             self.c_delta = np.zeros(4, np.float32)  # CalibHessian::value_minus_value_zero

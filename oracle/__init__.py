@@ -40,6 +40,8 @@ def lib():
         Lb = C.CDLL(LIB_PATH)
         sig = {
             "oracle_set_threads": (None, [C.c_int]),
+            "oracle_set_affine_opt_modes": (None, [C.c_float, C.c_float]),
+            "oracle_get_affine_opt_modes": (None, [f32p, f32p]),
             "oracle_get_threads": (C.c_int, []),
             "oracle_create": (C.c_void_p, [C.c_void_p]),
             "oracle_destroy": (None, [C.c_void_p]),
@@ -202,6 +204,29 @@ class OracleWindow:
 
     def time_iterations(self, iters: int) -> float:
         return float(lib().oracle_time_iterations(self._h, int(iters)))
+
+
+def get_affine_opt_modes():
+    a, b = C.c_float(), C.c_float()
+    lib().oracle_get_affine_opt_modes(C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+class affine_opt_modes:
+    """with oracle.affine_opt_modes(a, b): setting_affineOptModeA / B for the oracle (process-wide
+    globals, as in the reference), restored on exit."""
+
+    def __init__(self, a, b):
+        self.ab = (float(a), float(b))
+
+    def __enter__(self):
+        self.saved = get_affine_opt_modes()
+        lib().oracle_set_affine_opt_modes(*self.ab)
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_affine_opt_modes(*self.saved)
+        return False
 
 
 def solve_system(n_frames, iteration, lam, sysm, HM=None, bM=None, nullspaces=None):

@@ -1498,6 +1498,17 @@ static void orthogonalize_x(int n, const double *ns, int k, std::vector<double> 
 extern "C" {
 
 void oracle_set_threads(int n) { g_threads = std::max(0, std::min(n, NUM_THREADS_MAX)); }
+// setting_affineOptModeA / B as a driver sets them before the system starts (run_dso_kitti.cc:299-300,
+// run_dso_euroc.cc:291-292, run_dso_tum_mono.cc:284-292): read by linearize (Residuals.cc:186-187)
+// and takeData's getPrior (FrameHessian.h:154-165) as the reference reads its globals
+void oracle_set_affine_opt_modes(float a, float b) {
+    setting_affineOptModeA = a;
+    setting_affineOptModeB = b;
+}
+void oracle_get_affine_opt_modes(float *a, float *b) {
+    *a = setting_affineOptModeA;
+    *b = setting_affineOptModeB;
+}
 int oracle_get_threads(void) { return g_threads; }
 
 oracle_window *oracle_create(const ldso_ba_window *w) {

@@ -69,6 +69,8 @@ int oracle_frame_precalc(int n_frames, const ldso_ba_frame_state *frames, const 
                          float *precalc_out);
 int oracle_set_adjoints(int n_frames, const ldso_ba_frame_state *frames, double *ad_host,
                         double *ad_target, double *c_prior);
+void oracle_set_affine_opt_modes(float a, float b);
+void oracle_get_affine_opt_modes(float *a, float *b);
 int oracle_frame_take_data(int n_frames, const ldso_ba_frame_state *frames, double *prior,
                            double *delta, double *delta_prior);
 /* FrameHessian::setStateZero nullspaces + FullSystem::getNullspaces (pose x6, scale x1):

@@ -548,7 +548,7 @@ static int gpu_optimize_tests() {
     std::vector<double> adH((size_t)N * N * 64), adT((size_t)N * N * 64), cp(4), fp(8 * N), fd(8 * N), fdp(8 * N);
     ldso_ba_frame_precalc(N, S.fs.data(), S.calib, precalc.data());
     ldso_ba_set_adjoints(N, S.fs.data(), adH.data(), adT.data(), cp.data());
-    ldso_ba_frame_take_data(N, S.fs.data(), fp.data(), fd.data(), fdp.data());
+    ldso_ba_frame_take_data(N, S.fs.data(), nullptr, fp.data(), fd.data(), fdp.data());
     const float cdelta[4] = {0, 0, 0, 0};
     ldso_ba_window w;
     std::memset(&w, 0, sizeof(w));

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(built):
     bound = {name for name, _, _ in L.ABI}
     assert set(syms) == bound, set(syms) ^ bound
     lib = L.lib()
-    assert lib.ldso_ba_abi_version() == L.ABI_VERSION == 4
+    assert lib.ldso_ba_abi_version() == L.ABI_VERSION == 5
     assert lib.ldso_ba_num_kernels() >= 3
 
 
@@ -90,7 +90,7 @@ def test_solver_matches_oracle_solver(built):
     for it in (0, 3):
         x = np.zeros(n)
         args = [L.ptr(np.ascontiguousarray(sysm[k]), L.f64p) for k in ("HA", "bA", "HL", "bL")]
-        rc = lib.ldso_ba_solve_system(w.n_frames, it, 1e-5, *args, L.ptr(None, L.f64p), L.ptr(None, L.f64p),
+        rc = lib.ldso_ba_solve_system(None, w.n_frames, it, 1e-5, *args, L.ptr(None, L.f64p), L.ptr(None, L.f64p),
                                       L.ptr(np.ascontiguousarray(sysm["Hsc"]), L.f64p),
                                       L.ptr(np.ascontiguousarray(sysm["bsc"]), L.f64p), L.ptr(ns, L.f64p), 7,
                                       L.ptr(x, L.f64p))
@@ -161,7 +161,7 @@ def test_product_solver_known_answer(built):
     z = np.zeros(n)
     x = np.zeros(n)
     lib = L.lib()
-    rc = lib.ldso_ba_solve_system(N, 0, 1e-5, L.ptr(H, L.f64p), L.ptr(b, L.f64p), L.ptr(Z, L.f64p), L.ptr(z, L.f64p),
+    rc = lib.ldso_ba_solve_system(None, N, 0, 1e-5, L.ptr(H, L.f64p), L.ptr(b, L.f64p), L.ptr(Z, L.f64p), L.ptr(z, L.f64p),
                                   L.ptr(None, L.f64p), L.ptr(None, L.f64p), L.ptr(Z, L.f64p), L.ptr(z, L.f64p),
                                   L.ptr(None, L.f64p), 0, L.ptr(x, L.f64p))
     assert rc == 0
@@ -190,7 +190,7 @@ def test_product_solver_projection_known_answer(built, degenerate):
     x0, x2 = np.zeros(n), np.zeros(n)
     lib = L.lib()
     for it, x in ((0, x0), (2, x2)):
-        rc = lib.ldso_ba_solve_system(N, it, 1e-5, L.ptr(H, L.f64p), L.ptr(b, L.f64p), L.ptr(Z, L.f64p),
+        rc = lib.ldso_ba_solve_system(None, N, it, 1e-5, L.ptr(H, L.f64p), L.ptr(b, L.f64p), L.ptr(Z, L.f64p),
                                       L.ptr(z, L.f64p), L.ptr(None, L.f64p), L.ptr(None, L.f64p), L.ptr(Z, L.f64p),
                                       L.ptr(z, L.f64p), L.ptr(ns, L.f64p), 7, L.ptr(x, L.f64p))
         assert rc == 0

@@ -14,7 +14,7 @@ def _frames(w):
     delta = np.zeros((N, 8))
     dprior = np.zeros((N, 8))
     fr = np.ascontiguousarray(w.frames)
-    L.check(L.lib().ldso_ba_frame_take_data(N, fr.ctypes.data, L.ptr(prior, L.f64p), L.ptr(delta, L.f64p),
+    L.check(L.lib().ldso_ba_frame_take_data(N, fr.ctypes.data, None, L.ptr(prior, L.f64p), L.ptr(delta, L.f64p),
                                             L.ptr(dprior, L.f64p)))
     return prior, delta, dprior
 
@@ -94,7 +94,7 @@ def test_frame_delta_is_stable_for_small_rotations(built):
         fr["state"][1, 3:6] += mag * np.array([1.0, -2.0, 0.5])
         fr["state"][1, 0:3] += mag * np.array([0.3, 0.1, -0.2])
         delta, pr, dp = np.zeros((3, 8)), np.zeros((3, 8)), np.zeros((3, 8))
-        L.check(L.lib().ldso_ba_frame_take_data(3, fr.ctypes.data, L.ptr(pr, L.f64p), L.ptr(delta, L.f64p),
+        L.check(L.lib().ldso_ba_frame_take_data(3, fr.ctypes.data, None, L.ptr(pr, L.f64p), L.ptr(delta, L.f64p),
                                                 L.ptr(dp, L.f64p)))
         od = np.zeros((3, 8))
         oracle.lib().oracle_frame_take_data(3, fr.ctypes.data, oracle._p(pr, oracle.f64p), oracle._p(od, oracle.f64p),

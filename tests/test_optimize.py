@@ -156,10 +156,15 @@ def host_optimize(w, n_its, ns, th=1.2, min_its=1):
     return np.array(energies), frames, cval, w.point_data[:, 2].copy(), its, status, np.array(ratios)
 
 
-def check_against_host(cfg, e_dev, fr_dev, c_dev, idep_dev, its_dev, st_dev, n_its, ns, frames=None):
+def check_against_host(cfg, e_dev, fr_dev, c_dev, idep_dev, its_dev, st_dev, n_its, ns, frames=None, settings=None):
+    """settings: the L.OptSettings the device ran with (the caller sets the oracle's globals to the
+    same affine modes); its priors go into the host loop's initial window."""
     w = synth.make_window(**cfg)
     if frames is not None:
         w.frames = frames
+    if settings is not None:
+        w.settings = settings
+        w.refresh_frame_terms()
     e_host, fr_host, c_host, idep_host, its_host, st_host, ratios = host_optimize(w, n_its, ns)
     print(f"{cfg}: host {its_host} its status {st_host}, device {its_dev} status {st_dev}; ratios\n{ratios}")
     assert (its_dev, st_dev) == (its_host, st_host)
