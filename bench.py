@@ -101,17 +101,36 @@ def launch_ranks(n, cmd, env=None, poll_s=0.5):
 
 
 def load_pmc(workload):
-    """HBM traffic per k_linearize launch from a committed rocprofv3 --pmc summary, if one
-    exists for this exact workload (written by tools/pmc_traffic.py); else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_k_linearize.json")
+    """HBM traffic per k_linearize launch from the committed rocprofv3 --pmc summary
+    (profiles/pmc_k_linearize.json, written by tools/pmc_traffic.py in separate counter passes), if
+    it exists for this exact workload -> (bytes, provenance), else (None, reason).  It is NOT measured
+    in this run: the provenance names the file, the session that measured it and whether the
+    library build it measured is this run's (sha256 of libldso_ba.so)."""
+    import hashlib
+
+    rel = os.path.join("profiles", "pmc_k_linearize.json")
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, rel)) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None, {"file": rel, "note": "no committed PMC summary"}
+    if d.get("workload") != workload:
+        return None, {"file": rel, "note": "committed PMC summary is for another workload"}
+    try:
+        with open(L_PATH(), "rb") as f:
+            mine = hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        mine = None
+    prov = {"file": rel, "measured_in_this_run": False, "session": d.get("session"),
+            "lib_sha256": d.get("lib_sha256"), "same_build_as_this_run": bool(mine and mine == d.get("lib_sha256")),
+            "method": "rocprofv3 --pmc, separate passes: 2 x FETCH_SIZE + WRITE_SIZE per launch (tools/pmc_traffic.py)"}
+    return d.get("hbm_bytes_per_launch"), prov
+
+
+def L_PATH():
+    from ldso_amd import _lib
+
+    return _lib.LIB_PATH
 
 
 def cpp_face_leg():
@@ -161,7 +180,13 @@ def time_optimize(ctx, nss, n_its=6, reps=10, settings=None):
            "iterations_run": int(its[0]) if len(its) == 1 else
            {"min": int(its.min()), "max": int(its.max()), "mean": float(its.mean())},
            "converged_windows": int((status == 1).sum()), "lost_windows": int((status == 2).sum())}
-    out["ms_per_iteration"] = ms / max(1, int(its.max()))
+    if settings is not None and settings.th_opt_iterations == 0.0:
+        out["ms_per_iteration"] = ms / n_its  # every window runs all n_its iterations
+    else:
+        # a window that left the loop still has every later kernel of the captured sequence launched
+        # (it returns at once): the call's time is not per iteration run, so none is derived from it
+        out["ms_per_iteration"] = None
+        out["note"] = ("early exits skip work, not launches: per-iteration cost only from optimize_all_its")
     return out
 
 
@@ -633,7 +658,7 @@ def main():
     achieved = bytes_per_launch / klin_avg_s / 1e9 if klin_avg_s > 0 else 0.0
     workload = f"{B} x S7 synthetic windows/GPU ({N} KF, {P} pts, 640x480)" if (N, P) == (7, 2000) else \
         f"{B} x synthetic windows/GPU ({N} KF, {P} pts, 640x480)"
-    traffic = load_pmc(workload)
+    traffic, traffic_source = load_pmc(workload)
 
     # N > 1: one S11 window sharded over every rank, the library's RCCL exchange in each pass
     sharded = None
@@ -736,6 +761,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "kernel": "k_linearize",
                 "avg_launch_us": klin_avg_s * 1e6,
                 "algo_bytes_per_launch": bytes_per_launch,

@@ -326,13 +326,17 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// a / b rounded to nearest for finite a, b whose quotient needs no exponent scaling (|b| and
-// |a / b| well inside the normal range): the compiler's IEEE sequence without v_div_scale /
-// v_div_fmas / v_div_fixup, which only act outside that range -- the same rcp, Newton step and
-// two fma corrections, so the same bits (8 instead of 11 VALU).  Used for the pattern-pixel
-// projections, whose in-bounds results (1.1 < Ku < w - 3 with 0 < drescale) are of that kind; a
-// denominator of 0, a tiny one or a non-finite operand can give a different non-finite or
-// out-of-range value than IEEE division would, and every such value fails the bounds test either way.
+// a / b rounded to nearest, without v_div_scale / v_div_fmas / v_div_fixup: the compiler's IEEE
+// sequence's rcp, Newton step and two fma corrections, so the same bits as a / b (8 instead of 11
+// VALU) PROVIDED a and b are finite, |b| is normal and below 2^126 (so rcp(b) is normal) and the
+// quotient and the intermediate products stay in the normal range.  Outside that precondition the
+// result may differ from IEEE division (e.g. a denormal b makes rcp overflow to inf and the result
+// NaN).  Used for the pattern-pixel projections, where a pixel is kept only when 1.1 < Ku < w - 3:
+// a non-finite or out-of-range quotient fails that test whichever way it was rounded, so the one
+// input that can decide differently is a subnormal (or > 2^126) homogeneous depth ptp[2] with a
+// comparably tiny ptp[0] / ptp[1] -- a point on the target camera's plane at infinity, which LDSO's
+// windows do not produce -- that IEEE division would place inside the image and this sequence
+// marks OOB.  pixel_terms uses it only on image layout 3 (see there).
 __device__ __forceinline__ float div_rn_normal(float a, float b) {
 #pragma clang fp contract(off)
     float r = __builtin_amdgcn_rcpf(b);
@@ -347,7 +351,8 @@ __device__ __forceinline__ float div_rn_normal(float a, float b) {
 
 // sqrt rounded to nearest for a normal, finite a >= 2^-96: the compiler's correctly rounded
 // sequence (v_sqrt_f32, then the neighbours one ulp down / up tested by an fma residual) without its
-// denormal scaling and its 0 / inf class fixup, which only act outside that range.
+// denormal scaling and its 0 / inf class fixup, which only act outside that range (outside it the
+// result may differ from sqrtf; pixel_terms only takes roots of quotients in (1e-5, 1]).
 __device__ __forceinline__ float sqrt_rn_normal(float a) {
     const float s = __builtin_amdgcn_sqrtf(a);
     const float sd = __int_as_float(__float_as_int(s) - 1), su = __int_as_float(__float_as_int(s) + 1);
@@ -362,20 +367,25 @@ __device__ __forceinline__ float sqrt_rn_normal(float a) {
 // fixA / fixB (setting_affineOptModeA / B < 0, wave-uniform): JabF[0] / JabF[1] are zeroed after the
 // pattern sums (Residuals.cc:186-187), i.e. they leave JabJIdx and Jab2 alone and remove the affine
 // parameter from Jab_r (AccumulatedTopHessian.cc:71-72) and from res_toZeroF (Residuals.cc:239-240).
-template <bool kMarg>
+// kIeee: plain IEEE division and sqrtf (image layout 1, whose gradients are the caller's and may be
+// anything, e.g. inf, where 2500 / (2500 + inf) must give 0).  Otherwise (layout 3: the gradients are
+// recomputed with makeImages' clamp, |g| <= 255, and the sample is finite wherever the sums are
+// kept) the quotients lie in (0.01, 1], the square roots' arguments in (1e-5, 1] and the Huber
+// quotient's |residual| below 2^126, i.e. inside div_rn_normal / sqrt_rn_normal's precondition: same bits.
+template <bool kMarg, bool kIeee = false>
 __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float color, float weight, float aff0,
                                             float aff1, float b0, float t[kSums], float jx, float jy, float da,
                                             float db, bool fixA, bool fixB) {
 #pragma clang fp contract(off)
     const float residual = I - (float)(aff0 * color + aff1);
     const float drdA = (color - b0);
-    // the quotients lie in (0.01, 1] and the square roots' arguments in (1e-5, 1] for every pixel
-    // whose sums are kept (finite sample, |residual| < 1e6): the in-range IEEE sequences, same bits
-    float wg = sqrt_rn_normal(div_rn_normal(kOutlierTHSumComponent, kOutlierTHSumComponent + (gx * gx + gy * gy)));
+    auto div = [](float a, float b) { return kIeee ? a / b : div_rn_normal(a, b); };
+    auto sqrt_ = [](float a) { return kIeee ? sqrtf(a) : sqrt_rn_normal(a); };
+    float wg = sqrt_(div(kOutlierTHSumComponent, kOutlierTHSumComponent + (gx * gx + gy * gy)));
     wg = 0.5f * (wg + weight);
-    float hw = fabsf(residual) < kHuberTH ? 1 : div_rn_normal(kHuberTH, fabsf(residual));
+    float hw = fabsf(residual) < kHuberTH ? 1 : div(kHuberTH, fabsf(residual));
     t[0] = wg * wg * hw * residual * residual * (2 - hw);
-    if (hw < 1) hw = sqrt_rn_normal(hw);
+    if (hw < 1) hw = sqrt_(hw);
     hw = hw * wg;
     gx *= hw;
     gy *= hw;
@@ -407,12 +417,13 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
     t[16] = ra * ra;
 }
 
-// G += U^T diag(Wt) U over the upper 4x4 tiles of the (KP x KP) block of one point chunk
+// G += U'^T U' over the upper 4x4 tiles of the (KP x KP) block of one point chunk, whose rows U' carry
+// sqrt(HdiF) (k_point_sc): U'^T U' = U^T diag(HdiF) U
 // (AccumulatedSCHessianSSE::addPoint's accD/accE/accEB/accHcc/accbc updates, summed by point):
 // 16 products per point as 8 packed FMAs on diagonal pairs (after 2 packed weight multiplies),
 // e.g. {acc00, acc11} += {ua.x, ua.y} * {ub.x, ub.y} and {acc01, acc10} += {ua.x, ua.y} *
 // {ub.y, ub.x}: both operands are natural register pairs (or a swapped one), no broadcast moves.
-__device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int KP, int nt, int ntiles, int cnt,
+__device__ __forceinline__ void syrk_tiles(const float *U, int KP, int nt, int ntiles, int cnt,
                                            float *slab, int tid, int nthreads) {
     for (int tile = tid; tile < ntiles; tile += nthreads) {
         int a = 0, rem = tile;
@@ -430,7 +441,6 @@ __device__ __forceinline__ void syrk_tiles(const float *U, const float *Wt, int 
         for (int p = 0; p < cnt; p++, pa += KP, pb += KP) {
             const float4 ua = *(const float4 *)pa;
             const float4 ub = *(const float4 *)pb;
-            (void)Wt;  // the rows carry sqrt(HdiF): U'^T U' = U^T diag(HdiF) U
             const f2 a01 = f2{ua.x, ua.y}, a23 = f2{ua.z, ua.w};
             const f2 b01 = {ub.x, ub.y}, b10 = {ub.y, ub.x}, b23 = {ub.z, ub.w}, b32 = {ub.w, ub.z};
             c[0] += a01 * b01;  // (0,0) (1,1)
@@ -963,7 +973,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
                     gy = w11 * q.t11.z + w01 * q.t01.z + w10 * q.t10.z + w00 * q.t00.z;
                 }
                 fin = isfinite(I);
-                pixel_terms<kMarg>(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt, kMarg ? q.jx : 0.f,
+                pixel_terms<kMarg, kImg == 1>(I, gx, gy, q.color, q.weight, aff0, aff1, b0, tt, kMarg ? q.jx : 0.f,
                                    kMarg ? q.jy : 0.f, da, db, (P.aff_fix & 1) != 0, (P.aff_fix & 2) != 0);
             }
             const unsigned long long m2 = __ballot(fin);
@@ -1182,7 +1192,6 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         point_nid(P, blockIdx.x, smem);
         return;
     }
-#define SC_STAMP(k)
     const int item = P.item_base + blockIdx.x - P.n_nid;
     const int4 it = P.items[item];
     if (P.stop && P.pass > P.stop[it.w]) return;  // window left the GN loop
@@ -1190,9 +1199,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int host = it.z, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
     const int Kj = 8 * (W.N - 1);
     float *U = smem;               // [kScPoints][KP]
-    float *Wt = smem + kScPoints * KP;    // [kScPoints]
     const int tid = threadIdx.x;
-    SC_STAMP(1);
     if (tid < it.y) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
@@ -1263,7 +1270,6 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
             row[Kj + 3] = hcd[3] + 0.0f;
             row[Kj + 4] = bdSum;
         }
-        Wt[tid] = HdiF;
         {
             const float sw = sqrtf(HdiF);
             float4 *r4 = reinterpret_cast<float4 *>(row);
@@ -1288,13 +1294,10 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         o[8] = hcd[3];
         o[9] = (float)ngood;
     }
-    SC_STAMP(2);
     __syncthreads();
-    SC_STAMP(3);
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
     float *slab = P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16;
-    syrk_tiles(U, Wt, KP, nt, ntiles, it.y, slab, tid, blockDim.x);
-#undef SC_STAMP
+    syrk_tiles(U, KP, nt, ntiles, it.y, slab, tid, blockDim.x);
 }
 
 // ============================================================================================
@@ -4232,7 +4235,7 @@ int check_window(const ldso_ba_window &w, bool need_images = true) {
     return 0;
 }
 
-size_t sc_smem_bytes(int KP) { return (size_t)(kScPoints * KP + kScPoints) * sizeof(float); }
+size_t sc_smem_bytes(int KP) { return (size_t)kScPoints * KP * sizeof(float); }
 
 // frame geometry of the image layout (all strides in float4 units)
 void image_geometry(ldso_ba_ctx *c) {

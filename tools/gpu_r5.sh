@@ -1,11 +1,11 @@
-# round-4 GPU session: the optimize tests first, then the whole GPU suite, smoke, a bench line.
-# usage: tools/gpu_r4.sh TAG [bench|prof|pmc]...
+# round-5 GPU session: the settings + optimize tests first, then the whole GPU suite, smoke, a bench line.
+# usage: tools/gpu_r5.sh TAG [bench|prof|pmc]...
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 TAG=${1:-x}; shift
 PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
-timeout -k 10 300 $PYT tests/test_optimize.py -m gpu > gpurun_out/pytest_opt_$TAG.log 2>&1 || { echo "optimize tests failed"; tail -60 gpurun_out/pytest_opt_$TAG.log; exit 1; }
+timeout -k 10 300 $PYT tests/test_settings.py tests/test_optimize.py -m gpu > gpurun_out/pytest_opt_$TAG.log 2>&1 || { echo "optimize tests failed"; tail -60 gpurun_out/pytest_opt_$TAG.log; exit 1; }
 tail -3 gpurun_out/pytest_opt_$TAG.log
 timeout -k 10 900 $PYT tests -m gpu > gpurun_out/pytest_$TAG.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_$TAG.log; exit 1; }
 tail -3 gpurun_out/pytest_$TAG.log

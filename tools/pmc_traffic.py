@@ -19,6 +19,16 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def lib_sha256(path=os.path.join(ROOT, "ldso_amd", "lib", "libldso_ba.so")):
+    import hashlib
+
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def run_pass(counters, outdir, args):
     os.makedirs(outdir, exist_ok=True)
     cmd = ["rocprofv3", "--pmc"] + counters + ["--kernel-include-regex", "k_linearize", "-d", outdir, "-o", "run",
@@ -49,6 +59,8 @@ def main():
     ap.add_argument("--windows", type=int, default=64)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc"))
+    ap.add_argument("--session", default=os.environ.get("LDSO_PMC_SESSION", ""),
+                    help="the measurement session's name, recorded with the result (provenance)")
     args = ap.parse_args()
     res = {}
     n_gather = None
@@ -81,6 +93,10 @@ def main():
         "TCP_TCC_read_requests_per_gather_residual": res["TCP_TCC_READ_REQ_sum"] / n_gather
         if n_gather and res.get("TCP_TCC_READ_REQ_sum") is not None else None,
         "counters": res,
+        # provenance: the session that measured it and the exact library build it measured (bench.py
+        # reports whether its own build is the same one)
+        "session": args.session,
+        "lib_sha256": lib_sha256(),
     }
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "pmc_k_linearize.json"), "w") as f:
