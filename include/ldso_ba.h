@@ -206,10 +206,11 @@ void *ldso_ba_stream(ldso_ba_ctx *ctx);
 
 /* In-library exchange over RCCL (xGMI): rank 0 makes the id, the caller hands it to every rank
  * (any channel), each rank attaches its context.  From then on every ldso_ba_linearize ends,
- * stream-ordered and without a host synchronisation, with the exchange of SURVEY §8e: a sum
- * all-reduce (fp64) of the packed systems (with accumulate), of the energy / #IN pairs, and an
- * all-gather of the newest-frame energies followed by the exact threshold re-selection.  Load
- * each rank with ldso_ba_load(ctx, n, windows, rank, world). */
+ * stream-ordered and without a host synchronisation, with the exchange of SURVEY §8e in TWO
+ * collectives: ONE sum all-reduce (fp64) of a contiguous buffer holding the packed systems (with
+ * accumulate), the energy / #IN pairs and, inside ldso_ba_optimize, the ranks' partial sumNID /
+ * numID of doStepFromBackup; then an all-gather of the newest-frame energies followed by the exact
+ * threshold re-selection.  Load each rank with ldso_ba_load(ctx, n, windows, rank, world). */
 #define LDSO_BA_COMM_ID_BYTES 128
 int ldso_ba_comm_unique_id(uint8_t *id_out);
 int ldso_ba_comm_init(ldso_ba_ctx *ctx, const uint8_t *id, int32_t rank, int32_t world);
@@ -495,6 +496,14 @@ int ldso_ba_optimize(ldso_ba_ctx *ctx, int32_t n_its, const ldso_ba_opt_settings
 int ldso_ba_frame_step(int32_t n_frames, const ldso_ba_frame_state *in, const double *x, ldso_ba_frame_state *out,
                        double *calib_value, const double *calib_value_zero, float *calib_scaled_out,
                        float *c_delta_out);
+
+/* doStepFromBackup's canbreak (FullSystem.cc:1894-1931, visual-only, stepfac 1) on the host, the
+ * statements the device loop evaluates (se3.h step_canbreak): from the window's x [8N+4] (step = -x),
+ * sumNID (the float sum of |idepth_backup| over the window's points in frames -> features order;
+ * with sharded points the ranks' partial sums added), numID and setting_thOptIterations.
+ * *canbreak_out = 1 or 0. */
+int ldso_ba_step_canbreak(int32_t n_frames, const double *x, float sum_nid, float num_id, float th_opt_iterations,
+                          int32_t *canbreak_out);
 
 /* Per-kernel HIP-event timing (bench/profiling).  When enabled every kernel launch of
  * ldso_ba_linearize is bracketed by events; get returns summed ms and launch counts for

@@ -165,6 +165,7 @@ ABI = [
     ("ldso_ba_optimize", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, f64p, f64p, f64p, f64p, C.c_void_p,
                                    f64p, f32p, i32p, i32p]),
     ("ldso_ba_frame_step", C.c_int, [C.c_int32, C.c_void_p, f64p, C.c_void_p, f64p, f64p, f32p, f32p]),
+    ("ldso_ba_step_canbreak", C.c_int, [C.c_int32, f64p, C.c_float, C.c_float, C.c_float, i32p]),
     ("ldso_ba_set_kernel_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("ldso_ba_set_tuning", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("ldso_ba_get_kernel_times", C.c_int, [C.c_void_p, f64p, i64p, C.c_int32]),

@@ -1138,7 +1138,7 @@ struct PointParams {
     int pass;
     // ldso_ba_optimize: blocks [0, n_nid) compute doStepFromBackup's sumNID / numID of window
     // blockIdx.x (point_nid); the point-chunk blocks follow
-    float *win_nid;
+    double *win_nid;  // [win][2] (ldso_ba_ctx::win_nid)
     int n_nid, nid_chunk;
 };
 
@@ -1175,8 +1175,8 @@ __device__ void point_nid(const PointParams &P, int w, float *lds) {
         __syncthreads();
     }
     if (tid == 0) {
-        P.win_nid[2 * w] = s;
-        P.win_nid[2 * w + 1] = (float)n;  // numID++ per point: exact below 2^24
+        P.win_nid[2 * w] = (double)s;  // exact; read back as float (a sharded window: the ranks' sum)
+        P.win_nid[2 * w + 1] = (double)(float)n;  // numID++ per point (float): exact below 2^24
     }
 }
 
@@ -3730,7 +3730,7 @@ struct FrameStepParams {
     // ldso_ba_optimize's loop exits (FullSystem.cc:922, 968-969): windows with it >= stop[w] skip;
     // canbreak at it >= min_its sets stop[w] = it + 1 (the pass after this step still runs)
     int *stop, *status;
-    const float *win_nid;  // [win][2]: sumNID, numID of the idepths the step starts from (window_nid)
+    const double *win_nid;  // [win][2]: sumNID, numID of the idepths the step starts from (point_nid)
     int it, min_its;
     float th;  // setting_thOptIterations
     float aff_a, aff_b;  // setting_affineOptModeA / B: the affine priors of takeData (getPrior)
@@ -3744,7 +3744,7 @@ __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int b
     const int N = W.N, tid = threadIdx.x;
     const double *xw = P.x + W.vec_base;
     if (P.stop && tid == 128 && P.it >= P.min_its &&
-        step_canbreak(N, xw, P.win_nid[2 * blk], P.win_nid[2 * blk + 1], P.th)) {
+        step_canbreak(N, xw, (float)P.win_nid[2 * blk], (float)P.win_nid[2 * blk + 1], P.th)) {
         P.stop[blk] = P.it + 1;
         P.status[blk] = LDSO_BA_OPT_CONVERGED;
     }
@@ -3996,7 +3996,14 @@ struct ldso_ba_ctx {
     DevBuf<int4> d_top_items, d_sc_items;
     DevBuf<int2> d_pair_items, d_host_items;
     DevBuf<float> d_top_slab, d_sc_slab;
-    DevBuf<double> d_item_energy, d_sys, d_win_energy, d_stage;
+    // d_sys = the exchange buffer: every window's packed system [sys_n], then the linearizeAll
+    // energy / #IN pairs [n_win][2] (win_energy()), then doStepFromBackup's sumNID / numID
+    // [n_win][2] (win_nid(), double: the ranks' float partials summed) -- contiguous, so that the
+    // multi-GPU exchange reduces all three in ONE collective
+    DevBuf<double> d_item_energy, d_sys, d_stage;
+    size_t sys_n = 0;
+    double *win_energy() const { return d_sys.p + sys_n; }
+    double *win_nid() const { return d_sys.p + sys_n + 2 * (size_t)n_win; }
     DevBuf<int2> d_sum_blocks;  // k_stitch_sum: {window, first packed element} per 256-thread block
     int n_sum_blocks = 0;
     // in-library multi-GPU exchange (ldso_ba_comm_init): RCCL communicator over this context's
@@ -4011,7 +4018,6 @@ struct ldso_ba_ctx {
     DevBuf<ldso_ba_frame_state> d_fstate;
     DevBuf<double> d_calib_val, d_calib_zero, d_cprior, d_ehist;
     DevBuf<int> d_stop, d_status;  // ldso_ba_optimize: per window, see FrameStepParams
-    DevBuf<float> d_win_nid;       // [win][2] sumNID, numID of the last pass (window_nid)
     DevBuf<int> d_add_priors;
     DevBuf<float> d_xad;            // [win][kXadStride]
     DevBuf<double> d_prior, d_x, d_ns;  // per-window (8N+4)-vectors: priors (HL diag, bL), x, nullspaces
@@ -4574,7 +4580,6 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_sc_slab.release();
     c->d_item_energy.release();
     c->d_sys.release();
-    c->d_win_energy.release();
     c->d_stage.release();
     c->d_sum_blocks.release();
     c->d_x_local.release();
@@ -4586,7 +4591,6 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_ehist.release();
     c->d_stop.release();
     c->d_status.release();
-    c->d_win_nid.release();
     c->d_add_priors.release();
     if (c->comm) (void)ncclCommDestroy(c->comm);
     c->d_xad.release();
@@ -4898,7 +4902,8 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_top_slab, std::max<size_t>(1, top_items.size() * kTopVals));
     ALLOC(c->d_sc_slab, std::max<size_t>(1, (size_t)sc_slab_total));
     ALLOC(c->d_item_energy, std::max<size_t>(1, top_items.size() * 2));
-    ALLOC(c->d_sys, (size_t)sys_total);
+    ALLOC(c->d_sys, (size_t)sys_total + 4 * (size_t)n_windows);  // + win_energy() + win_nid()
+    c->sys_n = (size_t)sys_total;
     ALLOC(c->d_stage, (size_t)std::max<long long>(1, stage_total));
     {
         std::vector<int2> sb;
@@ -4910,7 +4915,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         ALLOC(c->d_sum_blocks, sb.size());
         HIP_TRY(hipMemcpyAsync(c->d_sum_blocks.p, sb.data(), sb.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
     }
-    ALLOC(c->d_win_energy, (size_t)n_windows * 2);
     ALLOC(c->d_xad, (size_t)n_windows * kXadStride);
     ALLOC(c->d_prior, (size_t)2 * vec_total);
     ALLOC(c->d_x, (size_t)vec_total);
@@ -5155,11 +5159,13 @@ int comm_exchange(ldso_ba_ctx *c, bool accumulate) {
         if (int rc = c->d_x_local.alloc((size_t)c->n_win * m)) return rc;
         if (int rc = c->d_x_gathered.alloc((size_t)c->comm_world * c->n_win * m)) return rc;
     }
-    if (accumulate) NCCL_TRY(ncclAllReduce(c->d_sys.p, c->d_sys.p, c->d_sys.n, ncclFloat64, ncclSum, c->comm, st));
-    NCCL_TRY(ncclAllReduce(c->d_win_energy.p, c->d_win_energy.p, (size_t)2 * c->n_win, ncclFloat64, ncclSum, c->comm,
-                           st));
-    if (c->opt_pass >= 0 && accumulate)  // optimize(): the next step's sumNID / numID over every rank's points
-        NCCL_TRY(ncclAllReduce(c->d_win_nid.p, c->d_win_nid.p, (size_t)2 * c->n_win, ncclFloat32, ncclSum, c->comm, st));
+    // ONE fp64 sum all-reduce of the contiguous exchange buffer: the packed systems (with
+    // accumulate), the energy / #IN pairs, and inside optimize() the next step's sumNID / numID
+    // partials (each rank's float chain over its own run of points, widened exactly to double)
+    const size_t nw2 = (size_t)2 * c->n_win;
+    double *xb = accumulate ? c->d_sys.p : c->win_energy();
+    const size_t xn = (accumulate ? c->sys_n : 0) + nw2 + (c->opt_pass >= 0 && accumulate ? nw2 : 0);
+    NCCL_TRY(ncclAllReduce(xb, xb, xn, ncclFloat64, ncclSum, c->comm, st));
     const long long stride = c->x_stride;
     const dim3 grid((unsigned)std::min<long long>((stride + 255) / 256, 64), (unsigned)c->n_win);
     k_export_newest<<<grid, 256, 0, st>>>(c->d_wins.p, c->d_rs_energy_wo.p, c->d_x_local.p, stride);
@@ -5258,7 +5264,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Sp.adT = c->d_adT.p;
     Sp.sys = c->d_sys.p;
     Sp.stage = c->d_stage.p;
-    Sp.win_energy = c->d_win_energy.p;
+    Sp.win_energy = c->win_energy();
     const bool in_opt = c->opt_pass >= 0;
     Sp.ehist = in_opt && !c->comm ? c->d_ehist.p : nullptr;  // with RCCL: after the exchange
     Sp.pass = c->opt_pass;
@@ -5269,7 +5275,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.pass = c->opt_pass;
     const size_t sc_smem = std::max<size_t>(c->sc_smem_max, 4096);  // point_nid stages >= 1024 idepths
     if (in_opt && accumulate) {  // the next step's sumNID / numID (its backup idepths are this pass's)
-        Pp.win_nid = c->d_win_nid.p;
+        Pp.win_nid = c->win_nid();
         Pp.n_nid = c->n_win;
         Pp.nid_chunk = (int)std::min<size_t>(1024, (sc_smem / sizeof(float)) & ~(size_t)3);
     }
@@ -5326,7 +5332,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     if (rc || !c->comm) return rc;
     rc = comm_exchange(c, accumulate != 0);
     if (!rc && in_opt) {  // the reduced energies into the optimize() history
-        k_energy_to_history<<<1, 256, 0, st>>>(c->d_win_energy.p, c->d_ehist.p, c->opt_pass, 2 * c->n_win);
+        k_energy_to_history<<<1, 256, 0, st>>>(c->win_energy(), c->d_ehist.p, c->opt_pass, 2 * c->n_win);
         HIP_TRY(hipGetLastError());
     }
     return rc;
@@ -5500,7 +5506,7 @@ int ldso_ba_get_energy(ldso_ba_ctx *c, int32_t win, double *out) {
     int rc = ldso_ba_sync(c);
     if (rc) return rc;
     double e[2];
-    HIP_TRY(hipMemcpy(e, c->d_win_energy.p + 2 * win, sizeof(e), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(e, c->win_energy() + 2 * win, sizeof(e), hipMemcpyDeviceToHost));
     out[0] = e[0];
     out[1] = 0;
     out[2] = e[1];
@@ -5511,7 +5517,7 @@ int ldso_ba_get_energy(ldso_ba_ctx *c, int32_t win, double *out) {
 static int fetch_sys(ldso_ba_ctx *c, int win) {
     if (!c->sys_host_valid) {
         c->sys_valid.assign(c->n_win, 0);
-        c->sys_host.resize(c->d_sys.n);
+        c->sys_host.resize(c->sys_n);
         c->sys_host_valid = true;
     }
     if (c->sys_valid[win]) return 0;
@@ -5967,7 +5973,7 @@ int ldso_ba_iterate(ldso_ba_ctx *c, int32_t iteration, double lambda, const doub
             K.words[K.n_seg++] = (int)(bytes / 4);
         };
         if (x_out) seg(c->d_x.p, 0, xb);
-        if (energy_out) seg(c->d_win_energy.p, xb, eb);
+        if (energy_out) seg(c->win_energy(), xb, eb);
         if (point_step_out && sb) seg(c->d_pt_step.p, xb + eb, sb);
         if (K.n_seg) {
             k_pack_out<<<std::min(64, (int)((xb + eb + sb) / 1024) + 1), 256, 0, c->stream>>>(K);
@@ -6070,7 +6076,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *
     if ((rc = c->d_fstate.ensure(c->n_frames)) || (rc = c->d_calib_val.ensure((size_t)4 * nw)) ||
         (rc = c->d_calib_zero.ensure((size_t)4 * nw)) || (rc = c->d_cprior.ensure((size_t)4 * nw)) ||
         (rc = c->d_add_priors.ensure(nw)) || (rc = c->d_ehist.ensure((size_t)2 * nw * (n_its + 1))) ||
-        (rc = c->d_stop.ensure(nw)) || (rc = c->d_status.ensure(nw)) || (rc = c->d_win_nid.ensure((size_t)2 * nw)))
+        (rc = c->d_stop.ensure(nw)) || (rc = c->d_status.ensure(nw)))
         return rc;
     std::vector<double> cp((size_t)4 * nw);
     std::vector<int> ap(nw);
@@ -6101,7 +6107,7 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *
     F.prior = c->d_prior.p;
     F.stop = c->d_stop.p;
     F.status = c->d_status.p;
-    F.win_nid = c->d_win_nid.p;
+    F.win_nid = c->win_nid();
     F.min_its = st.min_opt_iterations;
     F.th = st.th_opt_iterations;
     F.aff_a = st.affine_opt_mode_a;
@@ -6245,10 +6251,16 @@ int ldso_ba_frame_step(int32_t n, const ldso_ba_frame_state *in, const double *x
     return 0;
 }
 
+int ldso_ba_step_canbreak(int32_t n, const double *x, float sum_nid, float num_id, float th, int32_t *out) {
+    if (n < 1 || n > LDSO_BA_MAX_FRAMES || !x || !out) return fail(-1, "bad arguments");
+    *out = step_canbreak(n, x, sum_nid, num_id, th) ? 1 : 0;
+    return 0;
+}
+
 int ldso_ba_packed_system(ldso_ba_ctx *c, void **dev_ptr, int64_t *n_doubles, int64_t *stride) {
     if (!c || !dev_ptr) return fail(-1, "bad arguments");
     *dev_ptr = c->d_sys.p;
-    if (n_doubles) *n_doubles = (int64_t)c->d_sys.n;
+    if (n_doubles) *n_doubles = (int64_t)c->sys_n;
     if (stride) *stride = c->n_win ? (int64_t)sys_len(c->wd[0].D) : 0;
     return 0;
 }
@@ -6260,12 +6272,12 @@ int ldso_ba_unpack_system(ldso_ba_ctx *c) {
 }
 
 int ldso_ba_copy_packed(ldso_ba_ctx *c, void *buf, int64_t n, int32_t direction) {
-    if (!c || !buf || n != (int64_t)c->d_sys.n) return fail(-1, "bad arguments (size must equal the packed system)");
+    if (!c || !buf || n != (int64_t)c->sys_n) return fail(-1, "bad arguments (size must equal the packed system)");
     HIP_TRY(hipSetDevice(c->device));
     if (direction == 0)
-        HIP_TRY(hipMemcpyAsync(buf, c->d_sys.p, c->d_sys.bytes(), hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(buf, c->d_sys.p, c->sys_n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     else
-        HIP_TRY(hipMemcpyAsync(c->d_sys.p, buf, c->d_sys.bytes(), hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->d_sys.p, buf, c->sys_n * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->sys_host_valid = false;
     return 0;
