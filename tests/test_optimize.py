@@ -147,6 +147,9 @@ def host_optimize(w, n_its, ns, th=1.2, min_its=1):
         t = oracle.frame_terms(w)
         for k in ("precalc", "ad_host", "ad_target", "c_prior", "frame_prior", "frame_delta", "frame_delta_prior"):
             setattr(w, k, t[k])
+        # the newest frame's setNewFrameEnergyTH of the last pass carries into the next one
+        # (FullSystem.cc:2078-2109 writes frameHessians.back()->frameEnergyTH), as on the device
+        w.frame_energy_th = ow.frame_energy_th().copy()
         ow.update(w)
         e, sysm = ow.iteration()
         energies.append(e)
