@@ -14,6 +14,9 @@ ap.add_argument("--points", type=int, default=2000)
 a = ap.parse_args()
 ws = [synth.make_window(n_frames=a.frames, n_points=a.points, seed=1000 + i) for i in range(a.windows)]
 ctx = BAContext(0)
+for kv in filter(None, os.environ.get("LDSO_AB_TUNE", "").split(",")):  # set_tuning before load (A/B)
+    k, v = kv.split("=")
+    ctx.set_tuning(int(k), int(v))
 ctx.load(ws)
 for w in ws:
     w.dI = None
