@@ -280,6 +280,26 @@ public:
                   bool *isLost = nullptr, int *iterations = nullptr, const ldso_ba_opt_settings *settings = nullptr);
     // the residual and point fields of the device's last pass, if the host copies are stale
     void syncResiduals();
+
+    // FullSystem::linearizeAll(true)'s per-residual bookkeeping (FullSystem.cc:1771-1822), in compact
+    // form, from the device arrays of the last linearizeAll(true): the residuals applyRes left
+    // inactive (the reductor's toRemove, for ef->dropResidual), and per point (allPoints order) the
+    // largest relBS of its active residuals and their number (p->maxRelBaseline / numGoodResiduals;
+    // LDSO never clears isNew, so every active new residual contributes).  A forwarding shim applies
+    // these instead of copying every field of every residual back into the reference's objects.
+    struct FixPassResult {
+        std::vector<PointFrameResidual *> toRemove;
+        std::vector<float> maxRelBS;
+        std::vector<int> numGood;
+    };
+    const FixPassResult &fixPassResult() const { return fix_; }
+    // the last pass's state_state / centerProjectedTo of residual mirrorIdx (PointFrameResidual::
+    // mirrorIdx), for the consumers that read a few residuals after linearizeAll(true) --
+    // lastResiduals' states (FullSystem.cc:1776-1782), CoarseTracker::makeCoarseDepthL0's
+    // centerProjectedTo (CoarseTracker.cc:369-375) -- without a full write-back; downloaded once per
+    // pass on first use
+    ResState residualState(int mirrorIdx);
+    const float *residualCenter(int mirrorIdx);
     // device linearisation passes run so far (linearizeAll, the per-residual relinearisation,
     // every pass of optimize): one per call site
     long devicePasses() const { return passes_; }
@@ -322,6 +342,7 @@ private:
     bool uploadFrameTerms();
     bool runRelinearization();
     bool readBack(bool points_and_th);
+    bool readPassSummary(bool fix);
     void fail(const char *what);
     void packFrames(std::vector<ldso_ba_frame_state> &fs) const;
     ldso_ba_ctx *ctx_ = nullptr;
@@ -353,6 +374,11 @@ private:
     // the per-residual relinearisation (linearizeResidual): valid while epoch_ is unchanged and
     // the residual's point still has the snapshot's coordinates and inverse depths
     uint64_t epoch_ = 1, cacheEpoch_ = 0;
+    // the last pass's compact outputs (readPassSummary) and their lazily downloaded companions
+    FixPassResult fix_;
+    std::vector<int8_t> outState_;
+    std::vector<float> outCenter_;
+    long outStatePass_ = -1, outCenterPass_ = -1;
     std::vector<int8_t> cNewState_;
     std::vector<uint8_t> cCenterOk_;
     std::vector<float> cNewEnergy_, cEwo_, cCenter_, cJp_, cSnap_;

@@ -688,6 +688,79 @@ bool EnergyFunctional::readBack(bool points_and_th) {
     return true;
 }
 
+// linearizeAll's read-back of what its callers need at once: the frame thresholds, the points'
+// HdiF / bdSumF / idepth_hessian, the residual states and, on the fix pass, FixPassResult from the
+// flags and relBS; every other residual field stays on the device until a consumer asks
+// (syncResiduals, a residual method, residualCenter)
+bool EnergyFunctional::readPassSummary(bool fix) {
+    const size_t R = resPtr_.size(), P = ptPtr_.size();
+    const int N = nFrames;
+    std::vector<uint8_t> fl(R);
+    std::vector<float> rb(fix ? R : 0);
+    outState_.resize(R);
+    if (R && ldso_ba_get_residuals(ctx_, 0, nullptr, outState_.data(), nullptr, nullptr, nullptr, fl.data(), nullptr,
+                                   fix ? rb.data() : nullptr)) {
+        fail("ldso_ba_get_residuals");
+        return false;
+    }
+    outStatePass_ = passes_;
+    std::vector<float> hdi(P), bds(P), ih(P), th(N);
+    if (P && ldso_ba_get_points(ctx_, 0, hdi.data(), bds.data(), ih.data(), nullptr, nullptr, nullptr)) {
+        fail("ldso_ba_get_points");
+        return false;
+    }
+    for (size_t q = 0; q < P; q++) {
+        ptPtr_[q]->HdiF = hdi[q];
+        ptPtr_[q]->bdSumF = bds[q];
+        ptPtr_[q]->idepth_hessian = ih[q];
+    }
+    if (ldso_ba_get_frame_energy_th(ctx_, 0, th.data()) == 0) {
+        for (int f = 0; f < N; f++) frames[f]->frameEnergyTH = th[f];
+        thUp_ = th;  // the device holds these already
+        frameTH_ = th;
+    }
+    if (fix) {
+        fix_.toRemove.clear();
+        fix_.maxRelBS.assign(P, 0.f);
+        fix_.numGood.assign(P, 0);
+        for (size_t q = 0; q < P; q++)
+            for (int k = resBegin_[q]; k < resBegin_[q + 1]; k++) {
+                if (!(fl[k] & LDSO_BA_FLAG_ACTIVE)) {
+                    fix_.toRemove.push_back(resPtr_[k]);
+                } else if (fl[k] & LDSO_BA_FLAG_NEW) {  // FullSystem.cc:1799-1813
+                    fix_.maxRelBS[q] = std::max(fix_.maxRelBS[q], rb[k]);
+                    fix_.numGood[q]++;
+                }
+            }
+    }
+    return true;
+}
+
+ResState EnergyFunctional::residualState(int k) {
+    if (outStatePass_ != passes_ || resSync_ != ResSync::DeviceNewer) {  // not from the last pass
+        if (resSync_ == ResSync::DeviceNewer && ldso_ba_get_residuals(ctx_, 0, nullptr, outState_.data(), nullptr,
+                                                                      nullptr, nullptr, nullptr, nullptr, nullptr) == 0)
+            outStatePass_ = passes_;
+        else
+            return resPtr_[k]->state_state;  // the host copy is current
+    }
+    return (ResState)outState_[k];
+}
+
+const float *EnergyFunctional::residualCenter(int k) {
+    if (resSync_ != ResSync::DeviceNewer) return resPtr_[k]->centerProjectedTo;  // the host copy is current
+    if (outCenterPass_ != passes_) {
+        outCenter_.resize(3 * resPtr_.size());
+        if (ldso_ba_get_residuals(ctx_, 0, nullptr, nullptr, nullptr, nullptr, outCenter_.data(), nullptr, nullptr,
+                                  nullptr)) {
+            fail("ldso_ba_get_residuals");
+            return resPtr_[k]->centerProjectedTo;
+        }
+        outCenterPass_ = passes_;
+    }
+    return &outCenter_[3 * (size_t)k];
+}
+
 void EnergyFunctional::syncResiduals() {
     if (resSync_ != ResSync::DeviceNewer || !ctx_ || dirty_) return;
     resSync_ = ResSync::Synced;  // before the reads: the residual setters called below see it synced
@@ -708,7 +781,8 @@ Vec3 EnergyFunctional::linearizeAll(bool fixLinearization) {
         fail("ldso_ba_get_energy");
         return out;
     }
-    if (!readBack(true)) return out;
+    if (!readPassSummary(fixLinearization)) return out;
+    resSync_ = ResSync::DeviceNewer;  // the residual objects' fields follow on demand (syncResiduals)
     if (!fixLinearization) resInA = (int)e[2];
     out = {e[0], e[1], e[2]};
     return out;

@@ -150,16 +150,21 @@ int main(int argc, char **argv) {
         float frameEnergyTH;
         char other[512];  // the rest of a FrameHessian
     };
+    struct RefResidual;
     struct RefPoint {
         float idepth, idepth_zero, HdiF, bdSumF, idepth_hessian, step;
-        char other[160];
+        float maxRelBaseline;
+        int numGoodResiduals;
+        std::pair<RefResidual *, int> lastResiduals[2];
+        char other[128];
     };
     struct RefResidual {
         int state_state, state_NewState;
         double state_energy, state_NewEnergy, state_NewEnergyWithOutlier;
         float centerProjectedTo[3], JpJdF[8];
         bool isActiveAndIsGoodNEW;
-        char other[96];
+        int mirrorIdx;  // the face's index, copied at makeIDX as hostIDX / targetIDX are
+        char other[92];
     };
     std::vector<std::unique_ptr<RefFrame>> rframes;
     std::vector<std::unique_ptr<RefPoint>> rpoints;
@@ -180,6 +185,15 @@ int main(int argc, char **argv) {
             rres.emplace_back(new RefResidual());
             mr[rres.back().get()] = r.get();
             r->user = rres.back().get();
+            rres.back()->mirrorIdx = r->mirrorIdx;
+        }
+        // lastResiduals: the point's residuals to the two newest keyframes (FullSystem.cc:566-567)
+        RefPoint &rp = *rpoints.back();
+        rp.lastResiduals[0] = rp.lastResiduals[1] = {nullptr, 0};
+        for (auto &r : Pt->residuals) {
+            const int t = r->target.lock()->idx;
+            if (t == N - 1) rp.lastResiduals[0].first = (RefResidual *)r->user;
+            if (t == N - 2) rp.lastResiduals[1].first = (RefResidual *)r->user;
         }
     }
     // the replacement: walk the face's own containers (frames, allPoints, each point's residuals:
@@ -255,21 +269,57 @@ int main(int argc, char **argv) {
             kv.first->idepth_hessian = kv.second->idepth_hessian;
         }
     };
-    ef->syncResiduals();
-    auto time_shim = [&](auto &F, auto &Pm, auto &Rm) {
+    // the round-5 protocol: copy back only what the reference's consumers read.
+    // After optimize: the frames' states and the points' idepths.  After linearizeAll(true): the
+    // points' HdiF / idepth_hessian (CoarseTracker, flagPointsForRemoval), maxRelBaseline /
+    // numGoodResiduals from the face's per-point FixPassResult, lastResiduals' states (by mirror
+    // index), and the toRemove list for dropResidual.  centerProjectedTo stays with the face: its one
+    // consumer per keyframe (CoarseTracker::makeCoarseDepthL0) reads gpu->residualCenter(mirrorIdx).
+    std::vector<RefResidual *> toRemove;
+    auto shim_digest = [&]() {
+        for (auto &F : ef->frames)
+            std::memcpy(((RefFrame *)F->user)->state, F->state, sizeof(F->state));
+        // the face's own containers in order; FixPassResult is indexed like allPoints
+        const auto &fx = ef->fixPassResult();
+        const size_t P = ef->allPoints.size();
+        for (size_t q = 0; q < P; q++) {
+            if (q + 8 < P) __builtin_prefetch(ef->allPoints[q + 8]->user, 1);
+            const PointHessian &g = *ef->allPoints[q];
+            RefPoint &p = *(RefPoint *)g.user;
+            p.idepth = g.idepth;
+            p.idepth_zero = g.idepth_zero;
+            p.HdiF = g.HdiF;
+            p.idepth_hessian = g.idepth_hessian;
+            if (fx.numGood.size() == P) {
+                p.maxRelBaseline = std::max(p.maxRelBaseline, fx.maxRelBS[q]);
+                p.numGoodResiduals += fx.numGood[q];
+            }
+            for (auto &lr : p.lastResiduals)
+                if (lr.first) lr.second = (int)ef->residualState(lr.first->mirrorIdx);
+        }
+        toRemove.clear();
+        for (PointFrameResidual *g : fx.toRemove) toRemove.push_back((RefResidual *)g->user);
+    };
+    auto time_shim = [&](auto &&loops) {
         // between calls the frontend touches other memory (tracking, images): evict the caches
         std::vector<char> evict((size_t)64 << 20, 1);
         double tot = 0;
         for (int i = 0; i < reps; i++) {
             for (size_t k = 0; k < evict.size(); k += 64) evict[k]++;
             auto t1 = Clock::now();
-            shim_loops(F, Pm, Rm);
+            loops();
             tot += ms_since(t1);
         }
         return tot / reps;
     };
-    const double ms_shim_map = time_shim(mf, mp, mr);
-    const double ms_shim_vec = time_shim(vf, vp, vr);
+    // the face state after FullSystem::optimize: optimize, then linearizeAll(true) (its FixPassResult)
+    ef->optimize(n_its, HCalib, nullptr, nullptr, nullptr, &all_its);
+    ef->linearizeAll(true);
+    (void)ef->residualState(0);  // states of the pass downloaded once (as the first consumer would)
+    const double ms_shim_digest = time_shim(shim_digest);
+    ef->syncResiduals();  // the round-4 per-field loops read every residual object
+    const double ms_shim_map = time_shim([&] { shim_loops(mf, mp, mr); });
+    const double ms_shim_vec = time_shim([&] { shim_loops(vf, vp, vr); });
     const bool ok = ef->ok();
 
     // the C ABI alone on a context of the same window
@@ -326,16 +376,20 @@ int main(int argc, char **argv) {
         "{\"window\": \"S7 (7 KF, 2000 pts, 640x480, seed 1)\", \"n_its\": %d, \"reps\": %d, \"ok\": %s, "
         "\"optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f, \"iterations\": %d, "
         "\"iterations_default\": %d}, "
-        "\"shim\": {\"what\": \"INTEGRATION.md 3 copy loops of one FullSystem::optimize, %d residuals, %d points, "
-        "caches evicted between calls\", \"unordered_map_ms\": %.6f, \"back_pointer_ms\": %.6f, "
-        "\"shim_ms_per_gn_iteration\": %.6f, \"unordered_map_ms_per_gn_iteration\": %.6f, "
-        "\"frac_of_face_gn_iteration\": %.4f, \"unordered_map_frac_of_face_gn_iteration\": %.4f}, "
+        "\"shim\": {\"what\": \"INTEGRATION.md 3 reference-side copy loops of one FullSystem::optimize, %d residuals, "
+        "%d points, caches evicted between calls: the consumers' fields only (FixPassResult, lastResiduals by "
+        "mirror index; digest_ms, the protocol of 3) vs every residual field through back-pointers / "
+        "unordered_map (round 4)\", \"digest_ms\": %.6f, \"per_field_back_pointer_ms\": %.6f, "
+        "\"unordered_map_ms\": %.6f, \"shim_ms_per_gn_iteration\": %.6f, "
+        "\"frac_of_face_gn_iteration\": %.4f, \"per_field_frac_of_face_gn_iteration\": %.4f, "
+        "\"to_remove\": %zu}, "
         "\"optimize_full\": {\"ms\": %.6f, \"what\": \"optimize(6) + setAdjointsF + setDeltaF + linearizeAll(true) "
         "with the residual / point write-back\"}, "
         "\"c_abi_optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f}, "
         "\"flag_loop\": {\"residuals\": %d, \"ms\": %.6f, \"device_passes\": %ld}}\n",
         n_its, reps, ok ? "true" : "false", ms_opt, ms_opt / n_its, n_its, its_default, (int)vr.size(), (int)ef->allPoints.size(),
-        ms_shim_map, ms_shim_vec, ms_shim_vec / n_its, ms_shim_map / n_its, ms_shim_vec / ms_opt, ms_shim_map / ms_opt,
+        ms_shim_digest, ms_shim_vec, ms_shim_map, ms_shim_digest / n_its, ms_shim_digest / ms_opt, ms_shim_vec / ms_opt,
+        toRemove.size(),
         ms_full, ms_raw, ms_raw / n_its, nres, ms_flag, flag_passes);
     return ok ? 0 : 1;
 }

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <unordered_map>
 #include <vector>
@@ -306,6 +307,15 @@ struct Cycle {
         std::vector<uint8_t> fl(R);
         oracle_get_residuals(ow, ns.data(), st.data(), se.data(), ewo.data(), ctr.data(), fl.data(), jp.data(),
                              rbs.data());
+        // the compact per-pass outputs before any write-back: states and centres by mirror index
+        int bad_lazy = 0;
+        for (int k = 0; k < R; k++) {
+            const PointFrameResidual &r = *O.order[k];
+            bad_lazy += ef.residualState(r.mirrorIdx) != st[k];
+            bad_lazy += std::memcmp(ef.residualCenter(r.mirrorIdx), &ctr[3 * k], 12) != 0;
+        }
+        CHECK(bad_lazy == 0, "it %d: %d residualState / residualCenter values differ from the oracle", it, bad_lazy);
+        ef.syncResiduals();  // linearizeAll leaves the residual objects' fields on the device until asked
         int bad = 0, why[7] = {0, 0, 0, 0, 0, 0, 0};
         for (int k = 0; k < R; k++) {
             const PointFrameResidual &r = *O.order[k];
@@ -648,6 +658,31 @@ static int gpu_optimize_tests() {
     std::vector<uint8_t> ofl(R);
     oracle_get_residuals(ow, ons.data(), ost.data(), ose.data(), oew.data(), octr.data(), ofl.data(), ojp.data(),
                          orb.data());
+    {   // FixPassResult against the oracle's reductor bookkeeping (FullSystem.cc:1799-1822)
+        const auto &fx = ef->fixPassResult();
+        std::map<const PointFrameResidual *, int> idx;
+        for (int k = 0; k < R; k++) idx[O.order[k]] = k;
+        int n_inactive = 0, bad_rm = 0;
+        for (int k = 0; k < R; k++) n_inactive += !(ofl[k] & 1);
+        for (const PointFrameResidual *r : fx.toRemove) bad_rm += (ofl[idx.at(r)] & 1) != 0;
+        CHECK(bad_rm == 0 && (int)fx.toRemove.size() == n_inactive, "toRemove: %zu listed, %d inactive, %d wrong",
+              fx.toRemove.size(), n_inactive, bad_rm);
+        int bad_pt = 0;
+        for (size_t q = 0; q < ef->allPoints.size(); q++) {
+            float mx = 0;
+            int cnt = 0;
+            for (const auto &r : ef->allPoints[q]->residuals) {
+                const int k = idx.at(r.get());
+                if ((ofl[k] & 1) && r->isNew) {
+                    mx = std::max(mx, orb[k]);
+                    cnt++;
+                }
+            }
+            bad_pt += fx.maxRelBS[q] != mx || fx.numGood[q] != cnt;
+        }
+        CHECK(bad_pt == 0, "maxRelBS / numGood of %d points differ from the oracle", bad_pt);
+    }
+    ef->syncResiduals();
     int bad = 0;
     for (int k = 0; k < R; k++) {
         const PointFrameResidual &r = *O.order[k];
