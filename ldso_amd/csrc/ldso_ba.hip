@@ -141,7 +141,7 @@ struct LinParams {
     float *rs_newenergy;   // state_NewEnergy (persists: applyRes copies it on a later OOB)
     float *rs_energy_wo;   // state_NewEnergyWithOutlier
     float4 *rs_center;     // centerProjectedTo, relBS
-    float4 *pt_rec;        // [slots][4]: JpJdF[8], Hcd_r[4], (Hdd_r, bd_r, active, 0)
+    float4 *pt_rec;        // [slots][kRecQ]: JpJdF[8], (j0, j1, bd_r, active) -- see write_record
     float *top_slab;       // [items][96]
     double *item_energy;   // [items][2]
     int n_items;             // chunks of this launch: [item_base, item_base + n_items)
@@ -303,18 +303,24 @@ __device__ inline void point_terms(const Geo &g, const PhotoSums &s, float jpjdf
 
 // applyRes(true) + takeData record of one residual (Residuals.h:70-88, 120-129) at its slot
 // (target-slot major, point minor: a bucket chunk writes 64 consecutive records and a block of
-// k_point_sc reads them back coalesced): JpJdF and the point-side Top terms if active,
-// otherwise only the "not active" marker.
+// k_point_sc reads them back coalesced), 48 B: JpJdF[8], then (j0, j1, bd_r, 1) with
+// (j0, j1) = JIdx2 Jpdd if active, otherwise only the "not active" marker (0 in .w).  The
+// point-side Top terms Hdd_r = Jpdd^T (j0, j1) and Hcd_r = Jpdc^T (j0, j1) (AccumulatedTopHessian.cc:
+// 94-97) are not stored: k_point_sc forms them from (j0, j1) and the centre geometry, which it
+// recomputes from the point and the pair precalc with the same statements (centre_projection), so
+// the sums come out bit for bit as if they had been stored (64 -> 48 B written and read back).
+constexpr int kRecQ = 3;  // float4 per record
 __device__ __forceinline__ void write_record(float4 *rec, bool active, const Geo &g, const PhotoSums &s) {
     if (active) {
         float jp[8], hc[4], hdd, bd;
-        point_terms(g, s, jp, hc, hdd, bd);
+        point_terms(g, s, jp, hc, hdd, bd);  // hc, hdd: dead here (recomputed by k_point_sc)
+        const float j0 = s.JIdx2_00 * g.d_d_x + s.JIdx2_10 * g.d_d_y;  // point_terms' statements
+        const float j1 = s.JIdx2_10 * g.d_d_x + s.JIdx2_11 * g.d_d_y;
         rec[0] = make_float4(jp[0], jp[1], jp[2], jp[3]);
         rec[1] = make_float4(jp[4], jp[5], jp[6], jp[7]);
-        rec[2] = make_float4(hc[0], hc[1], hc[2], hc[3]);
-        rec[3] = make_float4(hdd, bd, 1.f, 0.f);
+        rec[2] = make_float4(j0, j1, bd, 1.f);
     } else {
-        rec[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+        rec[2] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 constexpr int kSums = 17;      // energy, wJI2, JIdx2 (3), JabJIdx (4), Jab2 (3), JI_r (2), Jab_r (2), rr
@@ -1036,7 +1042,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
         float e_wo = -1;
         if (old_state == LDSO_BA_RES_OOB) {
             energy = state_energy;  // linearize returns state_energy; applyRes returns early
-            P.pt_rec[(size_t)my_slot * 4 + 3] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
+            P.pt_rec[(size_t)my_slot * kRecQ + 2] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
         } else {
             const float4 pd0 = my_pd0;
             const float *Sr = lds_sums_w + lane * kSumStride;
@@ -1082,7 +1088,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
             active = (new_state == LDSO_BA_RES_IN);
             flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
             state_energy = new_energy;
-            write_record(P.pt_rec + (size_t)my_slot * 4, active, g, s);
+            write_record(P.pt_rec + (size_t)my_slot * kRecQ, active, g, s);
             if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
                 // linearizeAll_Reductor relBS (FullSystem.cc:1800-1812)
 #pragma clang fp contract(off)
@@ -1128,7 +1134,8 @@ struct PointParams {
     const float *__restrict__ pt_data;
     const int *__restrict__ pt_nres;
     const unsigned long long *__restrict__ pt_tgt;  // [P]: residual targets, 4 bits each, caller order
-    const float4 *__restrict__ pt_rec;               // [slots][4] (WinDev::rec_base layout)
+    const float4 *__restrict__ pt_rec;               // [slots][kRecQ] (WinDev::rec_base layout)
+    const float *__restrict__ precalc;               // the pass's pair precalc (centre geometry)
     float *pt_out;                     // [P][12]
     float *sc_slab;
     int n_items;
@@ -1183,6 +1190,7 @@ __device__ void point_nid(const PointParams &P, int w, float *lds) {
 // points per k_point_sc block (one SYRK chunk partial).  128 (both waves gather, half the slab
 // partials) measured 28.5 vs 26.5 us with the stitch 0.8 us faster: the SYRK chains double (r4)
 constexpr int kScPoints = 64;
+constexpr int kPrePitch = 12;  // floats of staged precalc (R0, t0) per target in k_point_sc's LDS
 constexpr int kScThreads = 128;  // 2 waves: a lane per point gathers, both run the SYRK tiles
 static_assert(kScPoints <= kScThreads, "one gathering lane per point");
 constexpr int kScBatch = 3;  // residual records per round trip (r4: 3 -> two round trips at N = 7, 27.6 vs 28.3 us)
@@ -1200,6 +1208,14 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int Kj = 8 * (W.N - 1);
     float *U = smem;               // [kScPoints][KP]
     const int tid = threadIdx.x;
+    // the host's pair precalc R0 / t0 (record floats 12..23) for every target, staged once per block:
+    // every residual's centre geometry reads them from LDS (kPrePitch floats per target)
+    float *pre_lds = smem + kScPoints * KP;
+    for (int e = tid; e < W.N * 12; e += blockDim.x) {
+        const int t = e / 12, k = e - 12 * t;
+        pre_lds[t * kPrePitch + k] = P.precalc[(size_t)(W.pair_base + host + W.N * t) * LDSO_BA_PRECALC_STRIDE + 12 + k];
+    }
+    __syncthreads();
     if (tid < it.y) {
 #pragma clang fp contract(off)
         const int p = it.x + tid;
@@ -1207,37 +1223,40 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         // one round of record loads (slot s of the block's points is contiguous), then the
         // sums in residual order exactly as AccumulatedTopHessian.cc:94-116 adds them
         const unsigned long long tgs = P.pt_tgt[p];
-        const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * 4;
-        const size_t sstride = (size_t)W.P * 4;
+        const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * kRecQ;
+        const size_t sstride = (size_t)W.P * kRecQ;
+        const float4 pd0 = *reinterpret_cast<const float4 *>(P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE);
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
         float *row = U + tid * KP;
         unsigned filled = 0;  // target slots whose JpJdF is in the row
         for (int k0 = 0; k0 < nres; k0 += kScBatch) {
-            float4 rec[kScBatch][4];
+            float4 rec[kScBatch][kRecQ];
 #pragma unroll
             for (int u = 0; u < kScBatch; u++) {
                 const int k = min(k0 + u, nres - 1);
                 const int tg = (int)((tgs >> (4 * k)) & 15ull);
                 const float4 *q = rp + (tg < host ? tg : tg - 1) * sstride;
-                rec[u][0] = q[0];
-                rec[u][1] = q[1];
-                rec[u][2] = q[2];
-                rec[u][3] = q[3];
+#pragma unroll
+                for (int v = 0; v < kRecQ; v++) rec[u][v] = q[v];
             }
 #pragma unroll
             for (int u = 0; u < kScBatch; u++) {
                 const int k = k0 + u;
-                if (k >= nres || rec[u][3].z == 0.0f) continue;
+                if (k >= nres || rec[u][2].w == 0.0f) continue;
                 ngood++;
-                const float4 j0 = rec[u][0], j1 = rec[u][1], hc = rec[u][2], hb = rec[u][3];
-                bd += hb.y;
-                hdd += hb.x;
-                hcd[0] += hc.x;
-                hcd[1] += hc.y;
-                hcd[2] += hc.z;
-                hcd[3] += hc.w;
                 const int tg = (int)((tgs >> (4 * k)) & 15ull);
+                // the residual's centre geometry, as k_linearize's phase B formed it (same inputs,
+                // same statements), then point_terms' Hdd_r / Hcd_r from its (j0, j1)
+                Geo g;
+                (void)centre_projection(pre_lds + tg * kPrePitch - 12,  // R0 = [12..20], t0 = [21..23]
+                                        pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3], W.wM3,
+                                        W.hM3, g);
+                const float4 j0 = rec[u][0], j1 = rec[u][1], jb = rec[u][2];
+                bd += jb.z;
+                hdd += jb.x * g.d_d_x + jb.y * g.d_d_y;
+#pragma unroll
+                for (int i = 0; i < 4; i++) hcd[i] += g.d_C_x[i] * jb.x + g.d_C_y[i] * jb.y;
                 const int slot = tg < host ? tg : tg - 1;
                 *(float4 *)(row + 8 * slot) = j0;
                 *(float4 *)(row + 8 * slot + 4) = j1;
@@ -3680,11 +3699,11 @@ __device__ __forceinline__ void resubstitute_one(const ResubParams &P, int k) {
     b -= d;
     const int h = P.pt_host[p];
     const unsigned long long tgs = P.pt_tgt[p];
-    const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * 4;
+    const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * kRecQ;
     for (int q = 0; q < P.pt_nres[p]; q++) {
         const int tg = (int)((tgs >> (4 * q)) & 15ull);
-        const float4 *rq = rp + (size_t)(tg < h ? tg : tg - 1) * W.P * 4;
-        if (rq[3].z == 0.0f) continue;  // not active
+        const float4 *rq = rp + (size_t)(tg < h ? tg : tg - 1) * W.P * kRecQ;
+        if (rq[2].w == 0.0f) continue;  // not active
         const float *xa = xad + (size_t)(h * N + tg) * 8;
         const float4 j0 = rq[0], j1 = rq[1];
         const float dd = xa[0] * j0.x + xa[1] * j0.y + xa[2] * j0.z + xa[3] * j0.w + xa[4] * j1.x + xa[5] * j1.y +
@@ -4241,7 +4260,9 @@ int check_window(const ldso_ba_window &w, bool need_images = true) {
     return 0;
 }
 
-size_t sc_smem_bytes(int KP) { return (size_t)kScPoints * KP * sizeof(float); }
+size_t sc_smem_bytes(int KP) {
+    return ((size_t)kScPoints * KP + (size_t)LDSO_BA_MAX_FRAMES * kPrePitch) * sizeof(float);
+}
 
 // frame geometry of the image layout (all strides in float4 units)
 void image_geometry(ldso_ba_ctx *c) {
@@ -4894,7 +4915,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_rs_newenergy, std::max<size_t>(1, rs_energy.size()));
     ALLOC(c->d_rs_energy_wo, std::max<size_t>(1, rs_energy.size()));
     ALLOC(c->d_rs_center, std::max<size_t>(1, rs_energy.size()));
-    ALLOC(c->d_pt_rec, std::max<size_t>(1, (size_t)rec_base * 4));
+    ALLOC(c->d_pt_rec, std::max<size_t>(1, (size_t)rec_base * kRecQ));
     ALLOC(c->d_top_items, std::max<size_t>(1, top_items.size()));
     ALLOC(c->d_sc_items, std::max<size_t>(1, sc_items.size()));
     ALLOC(c->d_pair_items, pair_items.size());
@@ -5245,6 +5266,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.pt_nres = c->d_pt_nres.p;
     Pp.pt_tgt = c->d_pt_tgt.p;
     Pp.pt_rec = c->d_pt_rec.p;
+    Pp.precalc = c->d_precalc.p;
     Pp.pt_out = c->d_pt_out.p;
     Pp.sc_slab = c->d_sc_slab.p;
     Pp.shift_prior = c->marg ? 0 : 1;
@@ -5408,9 +5430,9 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     HIP_TRY(hipMemcpyAsync(ce.data(), c->d_sx_center.p + b, R * sizeof(float4), hipMemcpyDeviceToHost, st));
     const size_t slot0 = (size_t)D.rec_base;
     if (jpjdf && D.P > 0) {
-        rec.resize((size_t)D.P * (D.N - 1) * 4);
-        HIP_TRY(hipMemcpyAsync(rec.data(), c->d_sx_rec.p + slot0 * 4, rec.size() * sizeof(float4), hipMemcpyDeviceToHost,
-                               st));
+        rec.resize((size_t)D.P * (D.N - 1) * kRecQ);
+        HIP_TRY(hipMemcpyAsync(rec.data(), c->d_sx_rec.p + slot0 * kRecQ, rec.size() * sizeof(float4),
+                               hipMemcpyDeviceToHost, st));
     }
     if ((rc = ldso_ba_sync(c))) return rc;
     for (size_t pos = 0; pos < R; pos++) {
@@ -5429,7 +5451,7 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
             float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             if (ns[pos] == LDSO_BA_RES_IN) {
                 const size_t sl = (size_t)H.rs_slot[pos] - slot0;
-                const float4 a = rec[sl * 4], q = rec[sl * 4 + 1];
+                const float4 a = rec[sl * kRecQ], q = rec[sl * kRecQ + 1];
                 const float t[8] = {a.x, a.y, a.z, a.w, q.x, q.y, q.z, q.w};
                 std::memcpy(v, t, sizeof(v));
             }
@@ -5614,8 +5636,9 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
     HIP_TRY(hipMemcpy(ce.data(), c->d_rs_center.p + D.res_base, R * sizeof(float4), hipMemcpyDeviceToHost));
     const size_t slot0 = (size_t)D.rec_base;
     if (jpjdf && D.P > 0) {
-        rec.resize((size_t)D.P * (D.N - 1) * 4);
-        HIP_TRY(hipMemcpy(rec.data(), c->d_pt_rec.p + slot0 * 4, rec.size() * sizeof(float4), hipMemcpyDeviceToHost));
+        rec.resize((size_t)D.P * (D.N - 1) * kRecQ);
+        HIP_TRY(hipMemcpy(rec.data(), c->d_pt_rec.p + slot0 * kRecQ, rec.size() * sizeof(float4),
+                          hipMemcpyDeviceToHost));
     }
     for (int pos = 0; pos < R; pos++) {
         const int k = H.rs_orig[pos];
@@ -5632,7 +5655,7 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
         if (rel_bs) rel_bs[k] = ce[pos].w;
         if (jpjdf) {
             const size_t sl = (size_t)H.rs_slot[pos] - slot0;
-            const float4 a = rec[sl * 4], b = rec[sl * 4 + 1];
+            const float4 a = rec[sl * kRecQ], b = rec[sl * kRecQ + 1];
             const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
             std::memcpy(jpjdf + 8 * (size_t)k, v, sizeof(v));
         }
