@@ -429,7 +429,7 @@ __device__ __forceinline__ void pixel_terms(float I, float gx, float gy, float c
 // 16 products per point as 8 packed FMAs on diagonal pairs (after 2 packed weight multiplies),
 // e.g. {acc00, acc11} += {ua.x, ua.y} * {ub.x, ub.y} and {acc01, acc10} += {ua.x, ua.y} *
 // {ub.y, ub.x}: both operands are natural register pairs (or a swapped one), no broadcast moves.
-__device__ __forceinline__ void syrk_tiles(const float *U, int KP, int nt, int ntiles, int cnt,
+__device__ __forceinline__ void syrk_tiles(const float *U, int pitch, int nt, int ntiles, int cnt,
                                            float *slab, int tid, int nthreads) {
     for (int tile = tid; tile < ntiles; tile += nthreads) {
         int a = 0, rem = tile;
@@ -444,7 +444,7 @@ __device__ __forceinline__ void syrk_tiles(const float *U, int KP, int nt, int n
         for (int i = 0; i < 8; i++) c[i] = f2{0.f, 0.f};
         const float *pa = U + 4 * a, *pb = U + 4 * bb;
 #pragma unroll 4
-        for (int p = 0; p < cnt; p++, pa += KP, pb += KP) {
+        for (int p = 0; p < cnt; p++, pa += pitch, pb += pitch) {
             const float4 ua = *(const float4 *)pa;
             const float4 ub = *(const float4 *)pb;
             const f2 a01 = f2{ua.x, ua.y}, a23 = f2{ua.z, ua.w};
@@ -1206,11 +1206,16 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const WinDev &W = P.wins[it.w];
     const int host = it.z, KP = W.KP, nt = KP / 4, ntiles = W.ntiles;
     const int Kj = 8 * (W.N - 1);
-    float *U = smem;               // [kScPoints][KP]
+    // rows of KP + 4 floats: KP is a multiple of 8, so a pitch of 4 mod 8 dwords spreads the lanes'
+    // 16-B row accesses (a lane per point) over distinct bank slots (ds_write_b128: 8-lane groups,
+    // banks mod 32; ds_read_b128: 16-lane groups, banks mod 64); a pitch of KP put lanes q and q + 4
+    // (writes) or q and q + 24 (reads) on the same banks
+    const int KPP = KP + 4;
+    float *U = smem;               // [kScPoints][KPP]
     const int tid = threadIdx.x;
     // the host's pair precalc R0 / t0 (record floats 12..23) for every target, staged once per block:
     // every residual's centre geometry reads them from LDS (kPrePitch floats per target)
-    float *pre_lds = smem + kScPoints * KP;
+    float *pre_lds = smem + kScPoints * KPP;
     for (int e = tid; e < W.N * 12; e += blockDim.x) {
         const int t = e / 12, k = e - 12 * t;
         pre_lds[t * kPrePitch + k] = P.precalc[(size_t)(W.pair_base + host + W.N * t) * LDSO_BA_PRECALC_STRIDE + 12 + k];
@@ -1228,7 +1233,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         const float4 pd0 = *reinterpret_cast<const float4 *>(P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE);
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
-        float *row = U + tid * KP;
+        float *row = U + tid * KPP;
         unsigned filled = 0;  // target slots whose JpJdF is in the row
         for (int k0 = 0; k0 < nres; k0 += kScBatch) {
             float4 rec[kScBatch][kRecQ];
@@ -1316,7 +1321,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     __syncthreads();
     // symmetric rank-k update of the upper 4x4 tiles: G += U^T diag(HdiF) U
     float *slab = P.sc_slab + W.sc_slab_base + (size_t)(item - W.sc_item_base) * ntiles * 16;
-    syrk_tiles(U, KP, nt, ntiles, it.y, slab, tid, blockDim.x);
+    syrk_tiles(U, KPP, nt, ntiles, it.y, slab, tid, blockDim.x);
 }
 
 // ============================================================================================
@@ -4261,7 +4266,7 @@ int check_window(const ldso_ba_window &w, bool need_images = true) {
 }
 
 size_t sc_smem_bytes(int KP) {
-    return ((size_t)kScPoints * KP + (size_t)LDSO_BA_MAX_FRAMES * kPrePitch) * sizeof(float);
+    return ((size_t)kScPoints * (KP + 4) + (size_t)LDSO_BA_MAX_FRAMES * kPrePitch) * sizeof(float);
 }
 
 // frame geometry of the image layout (all strides in float4 units)
