@@ -1193,7 +1193,9 @@ constexpr int kScPoints = 64;
 constexpr int kPrePitch = 12;  // floats of staged precalc (R0, t0) per target in k_point_sc's LDS
 constexpr int kScThreads = 128;  // 2 waves: a lane per point gathers, both run the SYRK tiles
 static_assert(kScPoints <= kScThreads, "one gathering lane per point");
-constexpr int kScBatch = 3;  // residual records per round trip (r4: 3 -> two round trips at N = 7, 27.6 vs 28.3 us)
+// residual records per round trip (r4: 3 -> two round trips at N = 7, 27.6 vs 28.3 us; r5: 6 -> one round
+// trip, 30.0 vs 27.6 us)
+constexpr int kScBatch = 3;
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     if ((int)blockIdx.x < P.n_nid) {
