@@ -3998,7 +3998,7 @@ struct ldso_ba_ctx {
     };
     Graph opt_graph[2], it_graph[2];  // ldso_ba_optimize's whole call (without / with nullspaces)
     bool opt_warm = false;            // an optimize call ran directly on this context
-    int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major
+    int item_order = 0;  // k_linearize chunk order: 0 target-major, 1 host-major, 2 target-major banded
     // the reference's settings this context runs with (ldso_ba_set_settings; always checked)
     ldso_ba_opt_settings settings = LDSO_BA_OPT_SETTINGS_INIT;
     int n_win = 0, width = 0, height = 0, npix = 0;
@@ -4769,6 +4769,40 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
                 res_pos_of[k] = pos;
             }
         }
+        // item order 2: inside each bucket the residuals are ranked by their projection into the
+        // target (row, then column) and dealt round robin over the bucket's chunks, so every chunk
+        // of a bucket sweeps the target image top to bottom and the concurrent chunks of one target
+        // are at the same band at the same step (the target's live lines: one band, not the frame)
+        std::vector<int> bucket_nch(N * N, 0);
+        if (c->item_order == 2) {
+            std::vector<std::pair<std::pair<float, float>, int>> key;
+            for (int b = 0; b < N * N; b++) {
+                const int n = bucket_cnt[b];
+                if (n == 0) continue;
+                const float *pre = in.precalc + (size_t)b * LDSO_BA_PRECALC_STRIDE;  // PRE_KRKiTll, PRE_KtTll
+                key.clear();
+                for (int pos = bucket_start[b]; pos < bucket_start[b + 1]; pos++) key.push_back({{0.f, 0.f}, H.rs_orig[pos]});
+                for (auto &e : key) {
+                    const int k = e.second;  // its point: point_res_begin is sorted
+                    const int p = (int)(std::upper_bound(in.point_res_begin, in.point_res_begin + in.n_points + 1, k) -
+                                        in.point_res_begin) - 1;
+                    const float *d = in.point_data + (size_t)p * LDSO_BA_POINT_STRIDE;
+                    float q[3];
+                    for (int i = 0; i < 3; i++) q[i] = pre[3 * i] * d[0] + pre[3 * i + 1] * d[1] + pre[3 * i + 2] + pre[9 + i] * d[2];
+                    const float y = q[1] / q[2], x = q[0] / q[2];
+                    e.first = {std::isfinite(y) ? y : 0.f, std::isfinite(x) ? x : 0.f};
+                }
+                std::sort(key.begin(), key.end());
+                const int nch = (n + chunk - 1) / chunk, qn = n / nch, rem = n % nch;
+                bucket_nch[b] = nch;
+                for (int i = 0; i < n; i++) {
+                    const int cc = i % nch, kk = i / nch;
+                    const int pos = bucket_start[b] + cc * qn + std::min(cc, rem) + kk;
+                    H.rs_orig[pos] = key[i].second;
+                    res_pos_of[key[i].second] = pos;
+                }
+            }
+        }
         // per-residual arrays (global, sorted)
         for (int pos = 0; pos < R; pos++) {
             const int k = H.rs_orig[pos];
@@ -4831,10 +4865,17 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         for (int bb = 0; bb < N * N; bb++) {
             // bucket b = h + N t; chunks in target-major order (the N-1 buckets reading one target
             // image run together) or host-major (the buckets of one host's points run together)
-            const int b = c->item_order ? (bb / N) + N * (bb % N) : bb;
+            const int b = c->item_order == 1 ? (bb / N) + N * (bb % N) : bb;
             const int first = (int)top_items.size();
-            for (int s = bucket_start[b]; s < bucket_start[b + 1]; s += chunk)
-                top_items.push_back(make_int4(res_base + s, std::min(chunk, bucket_start[b + 1] - s), pair_base + b, w));
+            if (bucket_nch[b] > 0) {  // item order 2: balanced chunks
+                const int n = bucket_cnt[b], nch = bucket_nch[b], qn = n / nch, rem = n % nch;
+                for (int cc = 0; cc < nch; cc++)
+                    top_items.push_back(make_int4(res_base + bucket_start[b] + cc * qn + std::min(cc, rem),
+                                                  qn + (cc < rem ? 1 : 0), pair_base + b, w));
+            } else {
+                for (int s = bucket_start[b]; s < bucket_start[b + 1]; s += chunk)
+                    top_items.push_back(make_int4(res_base + s, std::min(chunk, bucket_start[b + 1] - s), pair_base + b, w));
+            }
             pair_items[pi0 + b] = make_int2(first, (int)top_items.size() - first);
         }
         for (int b = 0; b < N * N; b++) pair_win.push_back(w);
@@ -6357,7 +6398,8 @@ int ldso_ba_set_tuning(ldso_ba_ctx *c, int32_t key, int32_t value) {
     }
     if (key == LDSO_BA_TUNE_ITEM_ORDER) {
         if (c->n_win) return fail(-1, "item order must be chosen before ldso_ba_load");
-        c->item_order = value != 0;
+        if (value < 0 || value > 2) return fail(-1, "item order must be 0, 1 or 2");
+        c->item_order = value;
         return 0;
     }
     if (key == LDSO_BA_TUNE_SOLVE_EXACT) {

@@ -450,7 +450,7 @@ def test_image_layouts_agree(built, layout):
     c.close()
 
 
-@pytest.mark.parametrize("key,value", [(1, 3), (2, 0), (2, 2), (8, 2), (11, 1)])
+@pytest.mark.parametrize("key,value", [(1, 3), (2, 0), (2, 2), (8, 2), (11, 1), (10, 3)])
 def test_removed_tuning_variants_are_rejected(built, key, value):
     c = BAContext(0)
     with pytest.raises(RuntimeError):
@@ -487,6 +487,27 @@ def test_chunk_sizes_agree(built, chunk):
     ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
     e_cpu, s_cpu = ow.iteration()
     compare_pass(c, ow, 0, e_cpu, s_cpu)
+    c.close()
+
+
+@pytest.mark.parametrize("order", [1, 2])
+@pytest.mark.parametrize("chunk", [16, 64])
+def test_item_orders_agree(built, order, chunk):
+    """k_linearize's chunk orders (LDSO_BA_TUNE_ITEM_ORDER: 1 host-major; 2 each bucket ranked by
+    the projection into its target and dealt over balanced chunks) hold other residuals per chunk,
+    so against the oracle: per-residual / per-point outputs bit for bit, the system within
+    BLOCK_TOL, over two windows batched (one with one-residual buckets) and two passes."""
+    cfgs = [dict(n_frames=7, n_points=900, seed=41), dict(n_frames=3, n_points=40, seed=42)]
+    c = BAContext(0)
+    c.set_tuning(6, chunk)   # LDSO_BA_TUNE_TOP_CHUNK
+    c.set_tuning(10, order)  # LDSO_BA_TUNE_ITEM_ORDER
+    c.load([synth.make_window(**cf) for cf in cfgs])
+    ows = [oracle.OracleWindow(synth.make_window(**cf), threads=0) for cf in cfgs]
+    for _ in range(2):
+        c.linearize()
+        for i, ow in enumerate(ows):
+            e_cpu, s_cpu = ow.iteration()
+            compare_pass(c, ow, i, e_cpu, s_cpu)
     c.close()
 
 
