@@ -287,10 +287,15 @@ public:
     // largest relBS of its active residuals and their number (p->maxRelBaseline / numGoodResiduals;
     // LDSO never clears isNew, so every active new residual contributes).  A forwarding shim applies
     // these instead of copying every field of every residual back into the reference's objects.
+    // lastState[2q + i]: state_state of point q's residual to the newest (i = 0) / second-newest
+    // (i = 1) keyframe, -1 without one -- p->lastResiduals[i].second (FullSystem.cc:1776-1782;
+    // makeKeyFrame puts the residual to the new keyframe in lastResiduals[0] and shifts the
+    // previous one to [1] for every point, FullSystem.cc:1247-1262)
     struct FixPassResult {
         std::vector<PointFrameResidual *> toRemove;
         std::vector<float> maxRelBS;
         std::vector<int> numGood;
+        std::vector<int8_t> lastState;
     };
     const FixPassResult &fixPassResult() const { return fix_; }
     // the last pass's state_state / centerProjectedTo of residual mirrorIdx (PointFrameResidual::

@@ -723,8 +723,11 @@ bool EnergyFunctional::readPassSummary(bool fix) {
         fix_.toRemove.clear();
         fix_.maxRelBS.assign(P, 0.f);
         fix_.numGood.assign(P, 0);
+        fix_.lastState.assign(2 * P, -1);
         for (size_t q = 0; q < P; q++)
             for (int k = resBegin_[q]; k < resBegin_[q + 1]; k++) {
+                const int t = resTarget_[k];
+                if (t >= N - 2) fix_.lastState[2 * q + (N - 1 - t)] = outState_[k];
                 if (!(fl[k] & LDSO_BA_FLAG_ACTIVE)) {
                     fix_.toRemove.push_back(resPtr_[k]);
                 } else if (fl[k] & LDSO_BA_FLAG_NEW) {  // FullSystem.cc:1799-1813

@@ -272,8 +272,8 @@ int main(int argc, char **argv) {
     // the round-5 protocol: copy back only what the reference's consumers read.
     // After optimize: the frames' states and the points' idepths.  After linearizeAll(true): the
     // points' HdiF / idepth_hessian (CoarseTracker, flagPointsForRemoval), maxRelBaseline /
-    // numGoodResiduals from the face's per-point FixPassResult, lastResiduals' states (by mirror
-    // index), and the toRemove list for dropResidual.  centerProjectedTo stays with the face: its one
+    // numGoodResiduals and lastResiduals' states from the face's per-point FixPassResult (allPoints
+    // order: no residual object is touched), and the toRemove list for dropResidual.  centerProjectedTo stays with the face: its one
     // consumer per keyframe (CoarseTracker::makeCoarseDepthL0) reads gpu->residualCenter(mirrorIdx).
     std::vector<RefResidual *> toRemove;
     auto shim_digest = [&]() {
@@ -294,8 +294,9 @@ int main(int argc, char **argv) {
                 p.maxRelBaseline = std::max(p.maxRelBaseline, fx.maxRelBS[q]);
                 p.numGoodResiduals += fx.numGood[q];
             }
-            for (auto &lr : p.lastResiduals)
-                if (lr.first) lr.second = (int)ef->residualState(lr.first->mirrorIdx);
+            if (fx.lastState.size() == 2 * P)
+                for (int i = 0; i < 2; i++)
+                    if (p.lastResiduals[i].first) p.lastResiduals[i].second = fx.lastState[2 * q + i];
         }
         toRemove.clear();
         for (PointFrameResidual *g : fx.toRemove) toRemove.push_back((RefResidual *)g->user);
@@ -377,8 +378,8 @@ int main(int argc, char **argv) {
         "\"optimize\": {\"ms_per_optimize\": %.6f, \"ms_per_gn_iteration\": %.6f, \"iterations\": %d, "
         "\"iterations_default\": %d}, "
         "\"shim\": {\"what\": \"INTEGRATION.md 3 reference-side copy loops of one FullSystem::optimize, %d residuals, "
-        "%d points, caches evicted between calls: the consumers' fields only (FixPassResult, lastResiduals by "
-        "mirror index; digest_ms, the protocol of 3) vs every residual field through back-pointers / "
+        "%d points, caches evicted between calls: the consumers' fields only (FixPassResult incl. lastResiduals' "
+        "states by point; digest_ms, the protocol of 3) vs every residual field through back-pointers / "
         "unordered_map (round 4)\", \"digest_ms\": %.6f, \"per_field_back_pointer_ms\": %.6f, "
         "\"unordered_map_ms\": %.6f, \"shim_ms_per_gn_iteration\": %.6f, "
         "\"frac_of_face_gn_iteration\": %.4f, \"per_field_frac_of_face_gn_iteration\": %.4f, "

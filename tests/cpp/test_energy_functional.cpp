@@ -667,20 +667,25 @@ static int gpu_optimize_tests() {
         for (const PointFrameResidual *r : fx.toRemove) bad_rm += (ofl[idx.at(r)] & 1) != 0;
         CHECK(bad_rm == 0 && (int)fx.toRemove.size() == n_inactive, "toRemove: %zu listed, %d inactive, %d wrong",
               fx.toRemove.size(), n_inactive, bad_rm);
-        int bad_pt = 0;
+        int bad_pt = 0, bad_last = 0;
         for (size_t q = 0; q < ef->allPoints.size(); q++) {
             float mx = 0;
             int cnt = 0;
+            int last[2] = {-1, -1};  // lastResiduals[0] / [1]: the residuals to frames N-1 / N-2
             for (const auto &r : ef->allPoints[q]->residuals) {
                 const int k = idx.at(r.get());
                 if ((ofl[k] & 1) && r->isNew) {
                     mx = std::max(mx, orb[k]);
                     cnt++;
                 }
+                const int t = r->target.lock()->idx;
+                if (t >= N - 2) last[N - 1 - t] = ost[k];
             }
             bad_pt += fx.maxRelBS[q] != mx || fx.numGood[q] != cnt;
+            bad_last += fx.lastState[2 * q] != last[0] || fx.lastState[2 * q + 1] != last[1];
         }
         CHECK(bad_pt == 0, "maxRelBS / numGood of %d points differ from the oracle", bad_pt);
+        CHECK(bad_last == 0, "lastResiduals' states of %d points differ from the oracle", bad_last);
     }
     ef->syncResiduals();
     int bad = 0;
