@@ -141,7 +141,9 @@ struct LinParams {
     float *rs_newenergy;   // state_NewEnergy (persists: applyRes copies it on a later OOB)
     float *rs_energy_wo;   // state_NewEnergyWithOutlier
     float4 *rs_center;     // centerProjectedTo, relBS
-    float4 *pt_rec;        // [slots][kRecQ]: JpJdF[8], (j0, j1, bd_r, active) -- see write_record
+    float4 *rec_a;         // [slots]: (j0, j1, JpJdF[6], JpJdF[7]) -- see write_record
+    float2 *rec_b;         // [slots]: (bd_r, idepth linearised at; NaN: not active)
+    float *geo_snap;       // [pairs][kGeoSnap]: the pass's R0, t0 and calibration (the first chunk of a pair)
     float *top_slab;       // [items][96]
     double *item_energy;   // [items][2]
     int n_items;             // chunks of this launch: [item_base, item_base + n_items)
@@ -302,26 +304,36 @@ __device__ inline void point_terms(const Geo &g, const PhotoSums &s, float jpjdf
 }
 
 // applyRes(true) + takeData record of one residual (Residuals.h:70-88, 120-129) at its slot
-// (target-slot major, point minor: a bucket chunk writes 64 consecutive records and a block of
-// k_point_sc reads them back coalesced), 48 B: JpJdF[8], then (j0, j1, bd_r, 1) with
-// (j0, j1) = JIdx2 Jpdd if active, otherwise only the "not active" marker (0 in .w).  The
-// point-side Top terms Hdd_r = Jpdd^T (j0, j1) and Hcd_r = Jpdc^T (j0, j1) (AccumulatedTopHessian.cc:
-// 94-97) are not stored: k_point_sc forms them from (j0, j1) and the centre geometry, which it
-// recomputes from the point and the pair precalc with the same statements (centre_projection), so
-// the sums come out bit for bit as if they had been stored (64 -> 48 B written and read back).
-constexpr int kRecQ = 3;  // float4 per record
-__device__ __forceinline__ void write_record(float4 *rec, bool active, const Geo &g, const PhotoSums &s) {
+// (target-slot major, point minor: a bucket chunk writes consecutive records and a block of
+// k_point_sc reads them back coalesced), 24 B in two arrays: A = (j0, j1, JpJdF[6], JpJdF[7]) with
+// (j0, j1) = JIdx2 Jpdd, B = (bd_r, idepth) if active; only B = (0, NaN) otherwise (an active
+// residual's idepth is never NaN: its centre projection would have failed).  Everything else of
+// the residual's takeData is a function of (j0, j1) and its centre geometry -- JpJdF[0..5] =
+// Jpdxi^T (j0, j1), Hdd_r = Jpdd^T (j0, j1), Hcd_r = Jpdc^T (j0, j1) (AccumulatedTopHessian.cc:
+// 94-97) -- and the geometry is recomputed from the point, the pair precalc and the calibration of
+// the pass (centre_projection: the same statements, so the same bits as if they had been stored):
+// k_point_sc from the live precalc of the pass, the resubstitution and the JpJdF read-back from the
+// geometry snapshot the pass's first chunk of each pair writes (the frame step rewrites the live
+// precalc in the same launch as the resubstitution).  64 -> 48 -> 24 B written and read back.
+constexpr int kGeoSnap = 16;  // floats per pair: R0 [0..8], t0 [9..11], calib fxl, fyl, cxl, cyl [12..15]
+__device__ __forceinline__ void write_record(float4 *rec_a, float2 *rec_b, bool active, float idz, const Geo &g,
+                                             const PhotoSums &s) {
     if (active) {
         float jp[8], hc[4], hdd, bd;
-        point_terms(g, s, jp, hc, hdd, bd);  // hc, hdd: dead here (recomputed by k_point_sc)
+        point_terms(g, s, jp, hc, hdd, bd);  // jp[0..5], hc, hdd: dead here (recomputed from the geometry)
         const float j0 = s.JIdx2_00 * g.d_d_x + s.JIdx2_10 * g.d_d_y;  // point_terms' statements
         const float j1 = s.JIdx2_10 * g.d_d_x + s.JIdx2_11 * g.d_d_y;
-        rec[0] = make_float4(jp[0], jp[1], jp[2], jp[3]);
-        rec[1] = make_float4(jp[4], jp[5], jp[6], jp[7]);
-        rec[2] = make_float4(j0, j1, bd, 1.f);
+        *rec_a = make_float4(j0, j1, jp[6], jp[7]);
+        *rec_b = make_float2(bd, idz);
     } else {
-        rec[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        *rec_b = make_float2(0.f, __builtin_nanf(""));
     }
+}
+// JpJdF[0..5] of a record from its centre geometry: point_terms' statements
+__device__ __forceinline__ void record_jp6(const Geo &g, float j0, float j1, float jp[6]) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int i = 0; i < 6; i++) jp[i] = g.d_xi_x[i] * j0 + g.d_xi_y[i] * j1;
 }
 constexpr int kSums = 17;      // energy, wJI2, JIdx2 (3), JabJIdx (4), Jab2 (3), JI_r (2), Jab_r (2), rr
 constexpr int kSumStride = kSums;  // floats per residual in the sums buffer (energy < 0: pattern not ok)
@@ -827,8 +839,9 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
     const int itemL = P.item_base + lblock * 4 + wave;  // global chunk index
     const int4 it = P.items[itemL];                     // {res_begin, count, pair_global, win}
     if (P.stop && P.pass > P.stop[__builtin_amdgcn_readfirstlane(it.w)]) return;  // window left the GN loop
-    const bool valid = lane < it.y;
-    const int pair = __builtin_amdgcn_readfirstlane(it.z), jlimit = __builtin_amdgcn_readfirstlane(it.y);
+    const int cnt = it.y & 0xFFFF;  // bit 16: the pair's first chunk (writes the geometry snapshot)
+    const bool valid = lane < cnt;
+    const int pair = __builtin_amdgcn_readfirstlane(it.z), jlimit = __builtin_amdgcn_readfirstlane(cnt);
     const WinDev &W = P.wins[__builtin_amdgcn_readfirstlane(it.w)];
     const int N = W.N;
     const int h = (pair - W.pair_base) % N, t = (pair - W.pair_base) / N;
@@ -1042,7 +1055,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
         float e_wo = -1;
         if (old_state == LDSO_BA_RES_OOB) {
             energy = state_energy;  // linearize returns state_energy; applyRes returns early
-            P.pt_rec[(size_t)my_slot * kRecQ + 2] = make_float4(0.f, 0.f, 0.f, 0.f);  // not active
+            P.rec_b[my_slot] = make_float2(0.f, __builtin_nanf(""));  // not active
         } else {
             const float4 pd0 = my_pd0;
             const float *Sr = lds_sums_w + lane * kSumStride;
@@ -1088,7 +1101,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
             active = (new_state == LDSO_BA_RES_IN);
             flags = active ? (flags | LDSO_BA_FLAG_ACTIVE) : (flags & ~LDSO_BA_FLAG_ACTIVE);
             state_energy = new_energy;
-            write_record(P.pt_rec + (size_t)my_slot * kRecQ, active, g, s);
+            write_record(P.rec_a + my_slot, P.rec_b + my_slot, active, pd0.w, g, s);
             if (P.fix && active && (flags & LDSO_BA_FLAG_NEW)) {
                 // linearizeAll_Reductor relBS (FullSystem.cc:1800-1812)
 #pragma clang fp contract(off)
@@ -1120,6 +1133,10 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
         P.item_energy[2 * itemL] = esum;
         P.item_energy[2 * itemL + 1] = (double)__popcll(inmask);
     }
+    // the pass's centre geometry inputs of this pair, for the readers of the records after the
+    // live precalc has moved on (write_record); by the pair's first chunk, after its real work
+    if ((it.y >> 16) && P.geo_snap && lane < kGeoSnap)
+        P.geo_snap[(size_t)pair * kGeoSnap + lane] = lane < 12 ? pre[12 + lane] : W.calib[lane - 12];
     if (!P.accumulate) return;
     wave_lds_sync();  // every lane has read its sums: the wave's LDS becomes the operand table
     top_mfma(lds_terms_w, lane, active, g, s, P.top_slab + (size_t)itemL * kTopVals);
@@ -1134,7 +1151,8 @@ struct PointParams {
     const float *__restrict__ pt_data;
     const int *__restrict__ pt_nres;
     const unsigned long long *__restrict__ pt_tgt;  // [P]: residual targets, 4 bits each, caller order
-    const float4 *__restrict__ pt_rec;               // [slots][kRecQ] (WinDev::rec_base layout)
+    const float4 *__restrict__ rec_a;                // [slots] (WinDev::rec_base layout, write_record)
+    const float2 *__restrict__ rec_b;
     const float *__restrict__ precalc;               // the pass's pair precalc (centre geometry)
     float *pt_out;                     // [P][12]
     float *sc_slab;
@@ -1230,27 +1248,27 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         // one round of record loads (slot s of the block's points is contiguous), then the
         // sums in residual order exactly as AccumulatedTopHessian.cc:94-116 adds them
         const unsigned long long tgs = P.pt_tgt[p];
-        const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * kRecQ;
-        const size_t sstride = (size_t)W.P * kRecQ;
+        const size_t rp = (size_t)W.rec_base + (p - W.point_base), sstride = (size_t)W.P;
         const float4 pd0 = *reinterpret_cast<const float4 *>(P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE);
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
         float *row = U + tid * KPP;
         unsigned filled = 0;  // target slots whose JpJdF is in the row
         for (int k0 = 0; k0 < nres; k0 += kScBatch) {
-            float4 rec[kScBatch][kRecQ];
+            float4 ra[kScBatch];
+            float2 rb[kScBatch];
 #pragma unroll
             for (int u = 0; u < kScBatch; u++) {
                 const int k = min(k0 + u, nres - 1);
                 const int tg = (int)((tgs >> (4 * k)) & 15ull);
-                const float4 *q = rp + (tg < host ? tg : tg - 1) * sstride;
-#pragma unroll
-                for (int v = 0; v < kRecQ; v++) rec[u][v] = q[v];
+                const size_t q = rp + (tg < host ? tg : tg - 1) * sstride;
+                ra[u] = P.rec_a[q];
+                rb[u] = P.rec_b[q];
             }
 #pragma unroll
             for (int u = 0; u < kScBatch; u++) {
                 const int k = k0 + u;
-                if (k >= nres || rec[u][2].w == 0.0f) continue;
+                if (k >= nres || rb[u].y != rb[u].y) continue;  // NaN idepth: not active
                 ngood++;
                 const int tg = (int)((tgs >> (4 * k)) & 15ull);
                 // the residual's centre geometry, as k_linearize's phase B formed it (same inputs,
@@ -1259,14 +1277,16 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
                 (void)centre_projection(pre_lds + tg * kPrePitch - 12,  // R0 = [12..20], t0 = [21..23]
                                         pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3], W.wM3,
                                         W.hM3, g);
-                const float4 j0 = rec[u][0], j1 = rec[u][1], jb = rec[u][2];
-                bd += jb.z;
-                hdd += jb.x * g.d_d_x + jb.y * g.d_d_y;
+                const float4 ja = ra[u];
+                float jp[6];
+                record_jp6(g, ja.x, ja.y, jp);
+                bd += rb[u].x;
+                hdd += ja.x * g.d_d_x + ja.y * g.d_d_y;
 #pragma unroll
-                for (int i = 0; i < 4; i++) hcd[i] += g.d_C_x[i] * jb.x + g.d_C_y[i] * jb.y;
+                for (int i = 0; i < 4; i++) hcd[i] += g.d_C_x[i] * ja.x + g.d_C_y[i] * ja.y;
                 const int slot = tg < host ? tg : tg - 1;
-                *(float4 *)(row + 8 * slot) = j0;
-                *(float4 *)(row + 8 * slot + 4) = j1;
+                *(float4 *)(row + 8 * slot) = make_float4(jp[0], jp[1], jp[2], jp[3]);
+                *(float4 *)(row + 8 * slot + 4) = make_float4(jp[4], jp[5], ja.z, ja.w);
                 filled |= 1u << slot;
             }
         }
@@ -3433,7 +3453,10 @@ struct ResubParams {
     const int *__restrict__ pt_win;
     const int *__restrict__ pt_nres;
     const unsigned long long *__restrict__ pt_tgt;
-    const float4 *__restrict__ pt_rec;
+    const float4 *__restrict__ rec_a;     // the pass's records (write_record)
+    const float2 *__restrict__ rec_b;
+    const float *__restrict__ geo_snap;   // [pairs][kGeoSnap]: the pass's centre geometry inputs
+    const float *__restrict__ pt_geo;     // the point records (u, v)
     const float *__restrict__ pt_out;
     const int *__restrict__ pt_host;
     float *pt_step;
@@ -3706,15 +3729,23 @@ __device__ __forceinline__ void resubstitute_one(const ResubParams &P, int k) {
     b -= d;
     const int h = P.pt_host[p];
     const unsigned long long tgs = P.pt_tgt[p];
-    const float4 *rp = P.pt_rec + ((size_t)W.rec_base + (p - W.point_base)) * kRecQ;
+    const size_t rp = (size_t)W.rec_base + (p - W.point_base);
+    const float2 uv = *reinterpret_cast<const float2 *>(P.pt_geo + (size_t)p * LDSO_BA_POINT_STRIDE);
     for (int q = 0; q < P.pt_nres[p]; q++) {
         const int tg = (int)((tgs >> (4 * q)) & 15ull);
-        const float4 *rq = rp + (size_t)(tg < h ? tg : tg - 1) * W.P * kRecQ;
-        if (rq[2].w == 0.0f) continue;  // not active
+        const size_t rq = rp + (size_t)(tg < h ? tg : tg - 1) * W.P;
+        const float2 rb = P.rec_b[rq];
+        if (rb.y != rb.y) continue;  // not active
+        const float4 ja = P.rec_a[rq];
+        // the residual's JpJdF: (j0, j1) through the centre geometry of the pass (write_record)
+        const float *gs = P.geo_snap + (size_t)(W.pair_base + h + N * tg) * kGeoSnap;
+        Geo g;
+        (void)centre_projection(gs - 12, uv.x, uv.y, rb.y, gs[12], gs[13], gs[14], gs[15], W.wM3, W.hM3, g);
+        float jp[6];
+        record_jp6(g, ja.x, ja.y, jp);
         const float *xa = xad + (size_t)(h * N + tg) * 8;
-        const float4 j0 = rq[0], j1 = rq[1];
-        const float dd = xa[0] * j0.x + xa[1] * j0.y + xa[2] * j0.z + xa[3] * j0.w + xa[4] * j1.x + xa[5] * j1.y +
-                         xa[6] * j1.z + xa[7] * j1.w;
+        const float dd = xa[0] * jp[0] + xa[1] * jp[1] + xa[2] * jp[2] + xa[3] * jp[3] + xa[4] * jp[4] + xa[5] * jp[5] +
+                         xa[6] * ja.z + xa[7] * ja.w;
         b -= dd;
     }
     if (!isfinite(b)) {  // reference returns from the chunk; the step is left unchanged
@@ -3727,6 +3758,33 @@ __device__ __forceinline__ void resubstitute_one(const ResubParams &P, int k) {
 }
 __global__ __launch_bounds__(256) void k_resubstitute(ResubParams P) {
     resubstitute_one(P, blockIdx.x * blockDim.x + threadIdx.x);
+}
+// JpJdF[8] of window w's residuals (device order) from their records and the geometry snapshot of
+// the pass that wrote them (ldso_ba_get_residuals / _linearize_residuals); 0 where not active
+__global__ __launch_bounds__(256) void k_record_jpjdf(const WinDev *__restrict__ wins, int w, const int *__restrict__ rs_slot,
+                                                      const int *__restrict__ pt_host, const float *__restrict__ pt_geo,
+                                                      const float4 *__restrict__ rec_a, const float2 *__restrict__ rec_b,
+                                                      const float *__restrict__ geo_snap, float *out) {
+    const WinDev &W = wins[w];
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= W.R) return;
+    const int slot = rs_slot[W.res_base + k], sl = (slot - W.rec_base) / W.P, q = (slot - W.rec_base) - sl * W.P;
+    const int p = W.point_base + q, h = pt_host[p], tg = sl < h ? sl : sl + 1;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const float2 rb = rec_b[slot];
+    if (rb.y == rb.y) {
+        const float4 ja = rec_a[slot];
+        const float *gs = geo_snap + (size_t)(W.pair_base + h + W.N * tg) * kGeoSnap;
+        const float2 uv = *reinterpret_cast<const float2 *>(pt_geo + (size_t)p * LDSO_BA_POINT_STRIDE);
+        Geo g;
+        (void)centre_projection(gs - 12, uv.x, uv.y, rb.y, gs[12], gs[13], gs[14], gs[15], W.wM3, W.hM3, g);
+        record_jp6(g, ja.x, ja.y, v);
+        v[6] = ja.z;
+        v[7] = ja.w;
+    }
+    float4 *o = reinterpret_cast<float4 *>(out + (size_t)k * 8);
+    o[0] = make_float4(v[0], v[1], v[2], v[3]);
+    o[1] = make_float4(v[4], v[5], v[6], v[7]);
 }
 
 // image layout 3 (default): the intensity channel only, band-interleaved (band_offset: an 8x4
@@ -4018,7 +4076,9 @@ struct ldso_ba_ctx {
     DevBuf<uint8_t> d_rs_tgt, d_rs_flags;
     DevBuf<int8_t> d_rs_state, d_rs_newstate;
     DevBuf<float> d_rs_energy, d_rs_newenergy, d_rs_energy_wo;
-    DevBuf<float4> d_rs_center, d_pt_rec;
+    DevBuf<float4> d_rs_center, d_rec_a;
+    DevBuf<float2> d_rec_b;
+    DevBuf<float> d_geo_snap;  // [pairs][kGeoSnap] (LinParams::geo_snap)
     DevBuf<int4> d_top_items, d_sc_items;
     DevBuf<int2> d_pair_items, d_host_items;
     DevBuf<float> d_top_slab, d_sc_slab;
@@ -4096,7 +4156,9 @@ struct ldso_ba_ctx {
     DevBuf<int8_t> d_sx_state, d_sx_newstate;
     DevBuf<uint8_t> d_sx_flags;
     DevBuf<float> d_sx_energy, d_sx_newenergy, d_sx_ewo;
-    DevBuf<float4> d_sx_center, d_sx_rec, d_pt_vals;
+    DevBuf<float4> d_sx_center, d_sx_rec_a, d_pt_vals;
+    DevBuf<float2> d_sx_rec_b;
+    DevBuf<float> d_sx_geo_snap, d_jp_out;
     DevBuf<double> d_sx_item;
 };
 
@@ -4353,7 +4415,10 @@ ResubParams resub_params(ldso_ba_ctx *c, int begin, int count, double lambda, bo
     R.pt_win = c->d_pt_win.p;
     R.pt_nres = c->d_pt_nres.p;
     R.pt_tgt = c->d_pt_tgt.p;
-    R.pt_rec = c->d_pt_rec.p;
+    R.rec_a = c->d_rec_a.p;
+    R.rec_b = c->d_rec_b.p;
+    R.geo_snap = c->d_geo_snap.p;
+    R.pt_geo = c->d_pt_data.p;
     R.pt_out = c->d_pt_out.p;
     R.pt_host = c->d_pt_host.p;
     R.pt_step = c->d_pt_step.p;
@@ -4598,7 +4663,9 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_rs_newenergy.release();
     c->d_rs_energy_wo.release();
     c->d_rs_center.release();
-    c->d_pt_rec.release();
+    c->d_rec_a.release();
+    c->d_rec_b.release();
+    c->d_geo_snap.release();
     c->d_top_items.release();
     c->d_sc_items.release();
     c->d_adhtd.release();
@@ -4629,7 +4696,10 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_sx_newenergy.release();
     c->d_sx_ewo.release();
     c->d_sx_center.release();
-    c->d_sx_rec.release();
+    c->d_sx_rec_a.release();
+    c->d_sx_rec_b.release();
+    c->d_sx_geo_snap.release();
+    c->d_jp_out.release();
     c->d_pt_vals.release();
     c->d_sx_item.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -4770,10 +4840,13 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
             }
         }
         // item order 2: inside each bucket the residuals are ranked by their projection into the
-        // target (row, then column) and dealt round robin over the bucket's chunks, so every chunk
-        // of a bucket sweeps the target image top to bottom and the concurrent chunks of one target
-        // are at the same band at the same step (the target's live lines: one band, not the frame)
+        // target (row, then column) and dealt round robin, in groups of 8 consecutive ranks (one
+        // phase-A step of a wavefront), over the bucket's chunks: every chunk of a bucket sweeps the
+        // target image top to bottom and the concurrent chunks of one target are at the same band
+        // at the same step (the target's live lines: one band, not the frame).  Chunks stay
+        // multiples of 8 but the last, so the phase-A steps are the same as in order 0.
         std::vector<int> bucket_nch(N * N, 0);
+        std::vector<int> chunk_len;  // item order 2: residuals per chunk, bucket by bucket
         if (c->item_order == 2) {
             std::vector<std::pair<std::pair<float, float>, int>> key;
             for (int b = 0; b < N * N; b++) {
@@ -4793,11 +4866,19 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
                     e.first = {std::isfinite(y) ? y : 0.f, std::isfinite(x) ? x : 0.f};
                 }
                 std::sort(key.begin(), key.end());
-                const int nch = (n + chunk - 1) / chunk, qn = n / nch, rem = n % nch;
+                const int G = (n + 7) / 8, nch = (n + chunk - 1) / chunk;
                 bucket_nch[b] = nch;
+                std::vector<int> start(nch + 1, 0);
+                for (int cc = 0; cc < nch; cc++) {
+                    const int groups = (G - cc + nch - 1) / nch;  // groups cc, cc + nch, ...
+                    int len = 8 * groups;
+                    if ((G - 1) % nch == cc) len -= 8 * G - n;  // the last (short) group ends this chunk
+                    start[cc + 1] = start[cc] + len;
+                    chunk_len.push_back(len);
+                }
                 for (int i = 0; i < n; i++) {
-                    const int cc = i % nch, kk = i / nch;
-                    const int pos = bucket_start[b] + cc * qn + std::min(cc, rem) + kk;
+                    const int g = i / 8, cc = g % nch;
+                    const int pos = bucket_start[b] + start[cc] + 8 * (g / nch) + (i & 7);
                     H.rs_orig[pos] = key[i].second;
                     res_pos_of[key[i].second] = pos;
                 }
@@ -4862,19 +4943,24 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         D.top_item_base = (int)top_items.size();
         const size_t pi0 = pair_items.size();
         pair_items.resize(pi0 + (size_t)N * N);
+        std::vector<int> chunk_off(N * N + 1, 0);  // item order 2: first chunk_len entry of each bucket
+        for (int b = 0; b < N * N; b++) chunk_off[b + 1] = chunk_off[b] + bucket_nch[b];
         for (int bb = 0; bb < N * N; bb++) {
             // bucket b = h + N t; chunks in target-major order (the N-1 buckets reading one target
             // image run together) or host-major (the buckets of one host's points run together)
             const int b = c->item_order == 1 ? (bb / N) + N * (bb % N) : bb;
             const int first = (int)top_items.size();
-            if (bucket_nch[b] > 0) {  // item order 2: balanced chunks
-                const int n = bucket_cnt[b], nch = bucket_nch[b], qn = n / nch, rem = n % nch;
-                for (int cc = 0; cc < nch; cc++)
-                    top_items.push_back(make_int4(res_base + bucket_start[b] + cc * qn + std::min(cc, rem),
-                                                  qn + (cc < rem ? 1 : 0), pair_base + b, w));
+            if (bucket_nch[b] > 0) {  // item order 2: the chunks dealt above
+                int s0 = bucket_start[b];
+                for (int cc = 0; cc < bucket_nch[b]; cc++) {
+                    const int len = chunk_len[chunk_off[b] + cc];
+                    top_items.push_back(make_int4(res_base + s0, len | (cc == 0 ? 1 << 16 : 0), pair_base + b, w));
+                    s0 += len;
+                }
             } else {
-                for (int s = bucket_start[b]; s < bucket_start[b + 1]; s += chunk)
-                    top_items.push_back(make_int4(res_base + s, std::min(chunk, bucket_start[b + 1] - s), pair_base + b, w));
+                for (int s = bucket_start[b]; s < bucket_start[b + 1]; s += chunk)  // bit 16: the pair's first chunk
+                    top_items.push_back(make_int4(res_base + s, std::min(chunk, bucket_start[b + 1] - s) | (s == bucket_start[b] ? 1 << 16 : 0),
+                                                  pair_base + b, w));
             }
             pair_items[pi0 + b] = make_int2(first, (int)top_items.size() - first);
         }
@@ -4963,7 +5049,9 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_rs_newenergy, std::max<size_t>(1, rs_energy.size()));
     ALLOC(c->d_rs_energy_wo, std::max<size_t>(1, rs_energy.size()));
     ALLOC(c->d_rs_center, std::max<size_t>(1, rs_energy.size()));
-    ALLOC(c->d_pt_rec, std::max<size_t>(1, (size_t)rec_base * kRecQ));
+    ALLOC(c->d_rec_a, std::max<size_t>(1, (size_t)rec_base));
+    ALLOC(c->d_rec_b, std::max<size_t>(1, (size_t)rec_base));
+    ALLOC(c->d_geo_snap, std::max<size_t>(1, (size_t)pair_base * kGeoSnap));
     ALLOC(c->d_top_items, std::max<size_t>(1, top_items.size()));
     ALLOC(c->d_sc_items, std::max<size_t>(1, sc_items.size()));
     ALLOC(c->d_pair_items, pair_items.size());
@@ -5029,7 +5117,9 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     UP(c->d_host_items, host_items);
 #undef UP
     HIP_TRY(hipMemsetAsync(c->d_rs_center.p, 0, c->d_rs_center.bytes(), c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_pt_rec.p, 0, c->d_pt_rec.bytes(), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_rec_a.p, 0, c->d_rec_a.bytes(), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_rec_b.p, 0xFF, c->d_rec_b.bytes(), c->stream));  // NaN: not active
+    HIP_TRY(hipMemsetAsync(c->d_geo_snap.p, 0, c->d_geo_snap.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_pt_out.p, 0, c->d_pt_out.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_pt_step.p, 0, c->d_pt_step.bytes(), c->stream));
     HIP_TRY(hipMemsetAsync(c->d_sys.p, 0, c->d_sys.bytes(), c->stream));
@@ -5296,7 +5386,9 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     L.rs_newenergy = c->d_rs_newenergy.p;
     L.rs_energy_wo = c->d_rs_energy_wo.p;
     L.rs_center = c->d_rs_center.p;
-    L.pt_rec = c->d_pt_rec.p;
+    L.rec_a = c->d_rec_a.p;
+    L.rec_b = c->d_rec_b.p;
+    L.geo_snap = c->d_geo_snap.p;
     L.top_slab = c->d_top_slab.p;
     L.item_energy = c->d_item_energy.p;
     L.frame_stride = c->frame_stride;
@@ -5313,7 +5405,8 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.pt_data = c->d_pt_data.p;
     Pp.pt_nres = c->d_pt_nres.p;
     Pp.pt_tgt = c->d_pt_tgt.p;
-    Pp.pt_rec = c->d_pt_rec.p;
+    Pp.rec_a = c->d_rec_a.p;
+    Pp.rec_b = c->d_rec_b.p;
     Pp.precalc = c->d_precalc.p;
     Pp.pt_out = c->d_pt_out.p;
     Pp.sc_slab = c->d_sc_slab.p;
@@ -5408,6 +5501,20 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     return rc;
 }
 
+// k_record_jpjdf into d_jp_out and down to the host: [R][8] in device order
+int record_jpjdf(ldso_ba_ctx *c, int win, const float4 *rec_a, const float2 *rec_b, const float *geo_snap,
+                 std::vector<float> &out) {
+    const WinDev &D = c->wd[win];
+    int rc = c->d_jp_out.ensure((size_t)D.R * 8);
+    if (rc) return rc;
+    k_record_jpjdf<<<(D.R + 255) / 256, 256, 0, c->stream>>>(c->d_wins.p, win, c->d_rs_slot.p, c->d_pt_host.p,
+                                                            c->d_pt_data.p, rec_a, rec_b, geo_snap, c->d_jp_out.p);
+    HIP_TRY(hipGetLastError());
+    out.resize((size_t)D.R * 8);
+    HIP_TRY(hipMemcpyAsync(out.data(), c->d_jp_out.p, out.size() * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    return 0;
+}
+
 int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, float *new_energy,
                                 float *new_energy_wo, float *center, uint8_t *center_ok, float *jpjdf) {
     if (!c || win < 0 || win >= c->n_win) return fail(-1, "bad arguments");
@@ -5420,10 +5527,11 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     const size_t R = (size_t)D.R;
     if (R == 0 || D.n_top_items == 0) return 0;  // no residuals: nothing to write
     int rc;
-    const size_t Rt = (size_t)c->R_tot, slots = c->d_pt_rec.n;
+    const size_t Rt = (size_t)c->R_tot, slots = c->d_rec_a.n;
     if ((rc = c->d_sx_state.ensure(Rt)) || (rc = c->d_sx_newstate.ensure(Rt)) || (rc = c->d_sx_flags.ensure(Rt)) ||
         (rc = c->d_sx_energy.ensure(Rt)) || (rc = c->d_sx_newenergy.ensure(Rt)) || (rc = c->d_sx_ewo.ensure(Rt)) ||
-        (rc = c->d_sx_center.ensure(Rt)) || (rc = c->d_sx_rec.ensure(slots)) ||
+        (rc = c->d_sx_center.ensure(Rt)) || (rc = c->d_sx_rec_a.ensure(slots)) || (rc = c->d_sx_rec_b.ensure(slots)) ||
+        (rc = c->d_sx_geo_snap.ensure(c->d_geo_snap.n)) ||
         (rc = c->d_sx_item.ensure((size_t)2 * c->n_top_items)))
         return rc;
     hipStream_t st = c->stream;
@@ -5454,7 +5562,9 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     L.rs_newenergy = c->d_sx_newenergy.p;
     L.rs_energy_wo = c->d_sx_ewo.p;
     L.rs_center = c->d_sx_center.p;
-    L.pt_rec = c->d_sx_rec.p;
+    L.rec_a = c->d_sx_rec_a.p;
+    L.rec_b = c->d_sx_rec_b.p;
+    L.geo_snap = c->d_sx_geo_snap.p;
     L.top_slab = nullptr;
     L.item_energy = c->d_sx_item.p;
     L.frame_stride = c->frame_stride;
@@ -5471,17 +5581,13 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     if (rc) return rc;
     std::vector<int8_t> ns(R);
     std::vector<float> ne(R), ew(R);
-    std::vector<float4> ce(R), rec;
+    std::vector<float4> ce(R);
     HIP_TRY(hipMemcpyAsync(ns.data(), c->d_sx_newstate.p + b, R, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(ne.data(), c->d_sx_newenergy.p + b, R * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(ew.data(), c->d_sx_ewo.p + b, R * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(ce.data(), c->d_sx_center.p + b, R * sizeof(float4), hipMemcpyDeviceToHost, st));
-    const size_t slot0 = (size_t)D.rec_base;
-    if (jpjdf && D.P > 0) {
-        rec.resize((size_t)D.P * (D.N - 1) * kRecQ);
-        HIP_TRY(hipMemcpyAsync(rec.data(), c->d_sx_rec.p + slot0 * kRecQ, rec.size() * sizeof(float4),
-                               hipMemcpyDeviceToHost, st));
-    }
+    std::vector<float> jp;
+    if (jpjdf && (rc = record_jpjdf(c, win, c->d_sx_rec_a.p, c->d_sx_rec_b.p, c->d_sx_geo_snap.p, jp))) return rc;
     if ((rc = ldso_ba_sync(c))) return rc;
     for (size_t pos = 0; pos < R; pos++) {
         const int k = H.rs_orig[pos];
@@ -5497,12 +5603,7 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
         }
         if (jpjdf) {
             float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (ns[pos] == LDSO_BA_RES_IN) {
-                const size_t sl = (size_t)H.rs_slot[pos] - slot0;
-                const float4 a = rec[sl * kRecQ], q = rec[sl * kRecQ + 1];
-                const float t[8] = {a.x, a.y, a.z, a.w, q.x, q.y, q.z, q.w};
-                std::memcpy(v, t, sizeof(v));
-            }
+            if (ns[pos] == LDSO_BA_RES_IN) std::memcpy(v, &jp[8 * pos], sizeof(v));
             std::memcpy(jpjdf + 8 * (size_t)k, v, sizeof(v));
         }
     }
@@ -5675,18 +5776,17 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
     std::vector<int8_t> ns(R), st(R);
     std::vector<uint8_t> fl(R);
     std::vector<float> se(R), ew(R);
-    std::vector<float4> ce(R), rec;
+    std::vector<float4> ce(R);
     HIP_TRY(hipMemcpy(ns.data(), c->d_rs_newstate.p + D.res_base, R, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(st.data(), c->d_rs_state.p + D.res_base, R, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fl.data(), c->d_rs_flags.p + D.res_base, R, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(se.data(), c->d_rs_energy.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(ew.data(), c->d_rs_energy_wo.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(ce.data(), c->d_rs_center.p + D.res_base, R * sizeof(float4), hipMemcpyDeviceToHost));
-    const size_t slot0 = (size_t)D.rec_base;
-    if (jpjdf && D.P > 0) {
-        rec.resize((size_t)D.P * (D.N - 1) * kRecQ);
-        HIP_TRY(hipMemcpy(rec.data(), c->d_pt_rec.p + slot0 * kRecQ, rec.size() * sizeof(float4),
-                          hipMemcpyDeviceToHost));
+    std::vector<float> jp;
+    if (jpjdf) {
+        if ((rc = record_jpjdf(c, win, c->d_rec_a.p, c->d_rec_b.p, c->d_geo_snap.p, jp))) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
     }
     for (int pos = 0; pos < R; pos++) {
         const int k = H.rs_orig[pos];
@@ -5701,12 +5801,7 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
         }
         if (flags) flags[k] = fl[pos];
         if (rel_bs) rel_bs[k] = ce[pos].w;
-        if (jpjdf) {
-            const size_t sl = (size_t)H.rs_slot[pos] - slot0;
-            const float4 a = rec[sl * kRecQ], b = rec[sl * kRecQ + 1];
-            const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-            std::memcpy(jpjdf + 8 * (size_t)k, v, sizeof(v));
-        }
+        if (jpjdf) std::memcpy(jpjdf + 8 * (size_t)k, &jp[8 * (size_t)pos], 8 * sizeof(float));
     }
     return 0;
 }
@@ -6449,7 +6544,7 @@ int32_t ldso_ba_num_kernels(void) { return kNumKernels; }
 int ldso_ba_stats(ldso_ba_ctx *c, int64_t *device_bytes, int64_t *n_points, int64_t *n_residuals) {
     if (!c) return fail(-1, "null ctx");
     if (device_bytes)
-        *device_bytes = (int64_t)(c->d_img.bytes() + c->d_precalc.bytes() + c->d_pt_data.bytes() + c->d_pt_rec.bytes() +
+        *device_bytes = (int64_t)(c->d_img.bytes() + c->d_precalc.bytes() + c->d_pt_data.bytes() + c->d_rec_a.bytes() + c->d_rec_b.bytes() +
                                   c->d_top_slab.bytes() + c->d_sc_slab.bytes() + c->d_sys.bytes());
     if (n_points) *n_points = c->P_tot;
     if (n_residuals) *n_residuals = c->R_tot;
