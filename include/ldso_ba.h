@@ -520,8 +520,10 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              ldso_ba_load
  *   LDSO_BA_TUNE_TIMING_MASK   bit i: bracket kernel slot i with events when timing is enabled
  *                              (default all; each event pair costs the stream a few us)
- *   LDSO_BA_TUNE_ITEM_ORDER    k_linearize chunk order: 0 (default) target-major, 1 host-major;
- *                              set before ldso_ba_load
+ *   LDSO_BA_TUNE_ITEM_ORDER    k_linearize chunk order: 0 (default) target-major, 1 host-major, 2
+ *                              target-major with each bucket's residuals ranked by their projection
+ *                              into the target and dealt over its chunks in groups of 8 (fewer L2
+ *                              re-reads, slower: DESIGN.md 5e); set before ldso_ba_load
  *   LDSO_BA_TUNE_SOLVE_EXACT   device solve (solve_device / iterate / optimize): 0 (default) the
  *                              unpivoted blocked LDL^T (k_solve_fast: the Jacobi-scaled, damped system
  *                              is positive definite; x within rounding of the pivoted solve); 1 the
