@@ -105,9 +105,8 @@ def load_pmc(workload):
     (profiles/pmc_k_linearize.json, written by tools/pmc_traffic.py in separate counter passes), if
     it exists for this exact workload -> (bytes, provenance), else (None, reason).  It is NOT measured
     in this run: the provenance names the file, the session that measured it and whether the
-    library build it measured is this run's (sha256 of libldso_ba.so)."""
-    import hashlib
-
+    library build it measured is this run's (sha256 of the library's sources, _lib.source_sha256:
+    the .so is relinked wherever the tests build it, so its bytes are no build identity)."""
     rel = os.path.join("profiles", "pmc_k_linearize.json")
     try:
         with open(os.path.join(ROOT, rel)) as f:
@@ -116,13 +115,12 @@ def load_pmc(workload):
         return None, {"file": rel, "note": "no committed PMC summary"}
     if d.get("workload") != workload:
         return None, {"file": rel, "note": "committed PMC summary is for another workload"}
-    try:
-        with open(L_PATH(), "rb") as f:
-            mine = hashlib.sha256(f.read()).hexdigest()
-    except OSError:
-        mine = None
+    from ldso_amd import _lib
+
+    mine = _lib.source_sha256()
     prov = {"file": rel, "measured_in_this_run": False, "session": d.get("session"),
-            "lib_sha256": d.get("lib_sha256"), "same_build_as_this_run": bool(mine and mine == d.get("lib_sha256")),
+            "source_sha256": d.get("source_sha256"),
+            "same_build_as_this_run": bool(mine and mine == d.get("source_sha256")),
             "method": "rocprofv3 --pmc, separate passes: 2 x FETCH_SIZE + WRITE_SIZE per launch (tools/pmc_traffic.py)"}
     return d.get("hbm_bytes_per_launch"), prov
 

@@ -106,6 +106,28 @@ class LdsoBaWindow(C.Structure):
     ]
 
 
+def source_sha256() -> str | None:
+    """sha256 over the sources libldso_ba.so is built from (ldso_amd/csrc, include/ldso_ba.h): the
+    identity of a build that survives a rebuild on another machine (the .so bytes do not)."""
+    import glob
+    import hashlib
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(root, "ldso_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(root, "ldso_amd", "csrc", "*.h")) +
+                   glob.glob(os.path.join(root, "ldso_amd", "csrc", "*.cpp")) +
+                   [os.path.join(root, "ldso_amd", "csrc", "Makefile"), os.path.join(root, "include", "ldso_ba.h")])
+    h = hashlib.sha256()
+    try:
+        for f in files:
+            h.update(os.path.relpath(f, root).encode())
+            with open(f, "rb") as fh:
+                h.update(hashlib.sha256(fh.read()).digest())
+    except OSError:
+        return None
+    return h.hexdigest()
+
+
 def ptr(a, t):
     if a is None:
         return C.cast(None, t)

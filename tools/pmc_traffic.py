@@ -19,6 +19,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def source_sha256():
+    sys.path.insert(0, ROOT)
+    from ldso_amd import _lib
+
+    return _lib.source_sha256()
+
+
 def lib_sha256(path=os.path.join(ROOT, "ldso_amd", "lib", "libldso_ba.so")):
     import hashlib
 
@@ -97,6 +104,7 @@ def main():
         # reports whether its own build is the same one)
         "session": args.session,
         "lib_sha256": lib_sha256(),
+        "source_sha256": source_sha256(),
     }
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "pmc_k_linearize.json"), "w") as f:
