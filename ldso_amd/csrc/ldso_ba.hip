@@ -1175,11 +1175,10 @@ struct PointParams {
 // its own at the front of k_point_sc's grid: it runs beside the point-chunk blocks, off the
 // pass's critical path.  With sharded points each rank sums its own run; the exchange adds the
 // ranks' partials.
-__device__ void point_nid(const PointParams &P, int w, float *lds) {
-    if (P.stop && P.pass > P.stop[w]) return;
-    const WinDev &W = P.wins[w];
-    const int n = W.P, tid = threadIdx.x, chunk = P.nid_chunk;
-    const float *pd = P.pt_data + (size_t)W.point_base * LDSO_BA_POINT_STRIDE + 2;
+__device__ void nid_chain(const WinDev &W, const float *__restrict__ pt_data, double *win_nid, int w, float *lds,
+                          int chunk) {
+    const int n = W.P, tid = threadIdx.x;
+    const float *pd = pt_data + (size_t)W.point_base * LDSO_BA_POINT_STRIDE + 2;
     float s = 0.0f;
     for (int q0 = 0; q0 < n; q0 += chunk) {
         const int m = min(chunk, n - q0);
@@ -1200,9 +1199,13 @@ __device__ void point_nid(const PointParams &P, int w, float *lds) {
         __syncthreads();
     }
     if (tid == 0) {
-        P.win_nid[2 * w] = (double)s;  // exact; read back as float (a sharded window: the ranks' sum)
-        P.win_nid[2 * w + 1] = (double)(float)n;  // numID++ per point (float): exact below 2^24
+        win_nid[2 * w] = (double)s;  // exact; read back as float (a sharded window: the ranks' sum)
+        win_nid[2 * w + 1] = (double)(float)n;  // numID++ per point (float): exact below 2^24
     }
+}
+__device__ void point_nid(const PointParams &P, int w, float *lds) {
+    if (P.stop && P.pass > P.stop[w]) return;
+    nid_chain(P.wins[w], P.pt_data, P.win_nid, w, lds, P.nid_chunk);
 }
 
 // points per k_point_sc block (one SYRK chunk partial).  128 (both waves gather, half the slab
@@ -2419,6 +2422,12 @@ struct SolveParams {
     const double *prep_nm, *prep_g;    // k_ortho_prep's results: Nm [vec][n_null], per window G | G^-1 | fast
     int iteration, n_null;
     int *stop, *status;  // ldso_ba_optimize: windows with iteration >= stop skip; a NaN x marks the window lost
+    // ldso_ba_optimize without a communicator (k_solve_fast): blocks [n_win, 2 n_win) compute the
+    // sumNID / numID of the step that follows (nid_chain) over the idepths this solve's system was
+    // linearised at -- a chain of ~P dependent float adds that fits inside the solve's own time
+    double *win_nid;
+    const float *pt_data;
+    int n_win, nid_chunk;
 };
 constexpr int kPrepGStride = 192;  // doubles per window in prep_g: G [49], G^-1 [49], fast flag, V [49], ev [7], keep [7]
 // H's row stride in LDS: odd (in doubles), so a column walk touches 32 distinct bank pairs
@@ -3351,6 +3360,12 @@ __device__ __forceinline__ double fast_update(const double *Wp, const double *rp
 __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P) {
 #pragma clang fp contract(off)
     extern __shared__ double lds[];
+    if (P.win_nid && (int)blockIdx.x >= P.n_win) {  // doStepFromBackup's sumNID (FullSystem.cc:1899-1909)
+        const int w = blockIdx.x - P.n_win;
+        if (P.stop && P.iteration >= P.stop[w]) return;
+        nid_chain(P.wins[w], P.pt_data, P.win_nid, w, reinterpret_cast<float *>(lds), P.nid_chunk);
+        return;
+    }
     if (P.stop && P.iteration >= P.stop[blockIdx.x]) return;  // the window left the GN loop
     const WinDev W = P.wins[blockIdx.x];  // a register copy (see k_solve)
     const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -4407,6 +4422,12 @@ int upload_priors(ldso_ba_ctx *c, int win) {
     return 0;
 }
 
+// where ldso_ba_optimize computes the step's sumNID: in extra blocks of k_solve_fast, beside the
+// factorisation; with a communicator (each rank sums its own points, the exchange adds the
+// partials) or an exact solve mode, in leading blocks of the pass's k_point_sc
+inline bool nid_in_solve(const ldso_ba_ctx *c) {
+    return !c->comm && !c->solve_exact && !getenv_flag("LDSO_BA_SOLVE_LDS");
+}
 ResubParams resub_params(ldso_ba_ctx *c, int begin, int count, double lambda, bool apply_step) {
     ResubParams R{};
     R.pt_data = apply_step ? c->d_pt_data.p : nullptr;
@@ -5437,7 +5458,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.stop = Sp.stop;
     Pp.pass = c->opt_pass;
     const size_t sc_smem = std::max<size_t>(c->sc_smem_max, 4096);  // point_nid stages >= 1024 idepths
-    if (in_opt && accumulate) {  // the next step's sumNID / numID (its backup idepths are this pass's)
+    if (in_opt && accumulate && !nid_in_solve(c)) {  // the next step's sumNID / numID (its backup idepths are this pass's)
         Pp.win_nid = c->win_nid();
         Pp.n_nid = c->n_win;
         Pp.nid_chunk = (int)std::min<size_t>(1024, (sc_smem / sizeof(float)) & ~(size_t)3);
@@ -5961,8 +5982,15 @@ int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
     });
     if (!c->solve_exact && !getenv_flag("LDSO_BA_SOLVE_LDS")) {  // the default: unpivoted, xAd fused
         const size_t smem = solve_fast_smem_bytes(dmax);
-        return timed_launch(c, 5, c->stream,
-                            [&] { k_solve_fast<<<c->n_win, kSolveFastThreads, smem, c->stream>>>(S); });
+        int grid = c->n_win;
+        if (c->opt_pass >= 0 && nid_in_solve(c)) {  // the step's sumNID chains in blocks of their own
+            S.win_nid = c->win_nid();
+            S.pt_data = c->d_pt_data.p;
+            S.n_win = c->n_win;
+            S.nid_chunk = (int)std::min<size_t>(1024, (smem / sizeof(float)) & ~(size_t)3);
+            grid *= 2;
+        }
+        return timed_launch(c, 5, c->stream, [&] { k_solve_fast<<<grid, kSolveFastThreads, smem, c->stream>>>(S); });
     }
     // exact mode: windows of up to 7 keyframes (n <= 64) the register factorisation, larger the LDS one
     const bool reg = dmax <= kSolveRegDim && !getenv_flag("LDSO_BA_SOLVE_LDS");
