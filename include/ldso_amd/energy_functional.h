@@ -147,6 +147,10 @@ struct PointHessian {
     PointStatus status = PointStatus::ACTIVE;
     bool alreadyRemoved = false;
     int idxInPoints = -1;
+    // the point's index in its host Frame's features vector (set by the caller at insert): the
+    // library keeps each host's points in this order, the order doStepFromBackup sums sumNID in
+    // (FullSystem.cc:1899-1909).  -1 on any point: each host's points in insertion order.
+    int featureRank = -1;
     void *user = nullptr;  // the caller's back-pointer (e.g. the reference object), untouched
     // PointHessian::setIdepth / setIdepthZero (PointHessian.h)
     void setIdepth(float x) {
@@ -363,7 +367,8 @@ private:
     std::vector<ldso_ba_frame_state> fs_;
     std::vector<float> dI_, frameTH_, precalc_, pointData_, resEnergy_;
     std::vector<double> adH_, adT_, cPrior_, fPrior_, fDelta_, fDeltaPrior_;
-    std::vector<int32_t> pointHost_, resBegin_, resTarget_;
+    std::vector<int32_t> pointHost_, resBegin_, resTarget_, pointRank_;
+    bool pointRanked_ = false;
     std::vector<int8_t> resState_;
     std::vector<uint8_t> resFlags_;
     std::vector<PointFrameResidual *> resPtr_;

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define LDSO_BA_ABI_VERSION 5
+#define LDSO_BA_ABI_VERSION 6
 
 #define LDSO_BA_PATTERN_NUM 8      /* patternNum, Settings.h:225 (staticPattern[8])     */
 #define LDSO_BA_CPARS 4            /* CPARS, NumTypes.h:25                              */
@@ -94,6 +94,11 @@ typedef struct ldso_ba_window {
     const int8_t *res_state;       /* [R]: state_state                                       */
     const float *res_energy;       /* [R]: state_energy                                      */
     const uint8_t *res_flags;      /* [R]: LDSO_BA_FLAG_*                                    */
+    /* [P] or NULL: the point's rank among its host frame's points in the order of the host
+     * Frame's features vector.  The library keeps each host's points in this order (NULL: the
+     * caller's order), which is the order doStepFromBackup sums sumNID in (frames -> features,
+     * FullSystem.cc:1899-1909) and so decides the canbreak exit bit for bit.                  */
+    const int32_t *point_rank;
 } ldso_ba_window;
 
 /* Per-frame state needed by FrameFramePrecalc::Set / setAdjointsF / takeData. */

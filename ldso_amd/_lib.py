@@ -45,7 +45,7 @@ FRAME_STATE_DTYPE = np.dtype(
 assert FRAME_STATE_DTYPE.itemsize == 272
 
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # setting_solverMode bits (Settings.h:14-25) and ldso_ba_optimize's per-window outcome
 SOLVER_SVD, SOLVER_ORTHOGONALIZE_SYSTEM, SOLVER_ORTHOGONALIZE_POINTMARG, SOLVER_ORTHOGONALIZE_FULL = 1, 2, 4, 8
@@ -103,6 +103,7 @@ class LdsoBaWindow(C.Structure):
         ("res_state", i8p),
         ("res_energy", f32p),
         ("res_flags", u8p),
+        ("point_rank", i32p),
     ]
 
 

@@ -29,13 +29,16 @@ void frame_state(const FrameHessian &F, ldso_ba_frame_state &S) {
 
 // points + residuals of one ldso_ba_window (caller point order = the order given)
 struct PointPack {
-    std::vector<int32_t> host, begin, target;
+    std::vector<int32_t> host, begin, target, rank;
+    bool ranked = true;  // every point carries its featureRank
     std::vector<float> data, energy;
     std::vector<int8_t> state;
     std::vector<uint8_t> flags;
     std::vector<PointFrameResidual *> res;
     void build(const std::vector<PointHessian *> &pts) {
         host.assign(pts.size(), 0);
+        rank.assign(pts.size(), 0);
+        ranked = true;
         data.assign(pts.size() * LDSO_BA_POINT_STRIDE, 0.f);
         begin.assign(pts.size() + 1, 0);
         target.clear();
@@ -46,6 +49,8 @@ struct PointPack {
         for (size_t q = 0; q < pts.size(); q++) {
             const PointHessian &p = *pts[q];
             host[q] = p.host.lock()->idx;
+            rank[q] = p.featureRank;
+            ranked = ranked && p.featureRank >= 0;
             float *d = &data[q * LDSO_BA_POINT_STRIDE];
             d[0] = p.u;
             d[1] = p.v;
@@ -76,6 +81,7 @@ struct PointPack {
         w.res_state = state.data();
         w.res_energy = energy.data();
         w.res_flags = flags.data();
+        w.point_rank = ranked ? rank.data() : nullptr;
     }
 };
 
@@ -584,6 +590,8 @@ bool EnergyFunctional::upload() {
     PointPack pk;
     pk.build(ptPtr_);
     pointHost_ = pk.host;
+    pointRank_ = pk.rank;
+    pointRanked_ = pk.ranked;
     pointData_ = pk.data;
     resBegin_ = pk.begin;
     resTarget_ = pk.target;
@@ -632,6 +640,7 @@ bool EnergyFunctional::upload() {
     w.res_state = resState_.data();
     w.res_energy = resEnergy_.data();
     w.res_flags = resFlags_.data();
+    w.point_rank = pointRanked_ ? pointRank_.data() : nullptr;
     if (ldso_ba_load(ctx_, 1, &w, 0, 1)) {
         fail("ldso_ba_load");
         return false;

@@ -4738,15 +4738,25 @@ namespace {
 // hosts).  Rank r owns the points whose first residual lies in [r T / G, (r + 1) T / G).
 void shard_points(const ldso_ba_window &in, int rank, int count, std::vector<int> &out) {
     out.clear();
+    // the device point order: host frames in window order, each host's points in features order
+    // (point_rank; the caller's order without it)
+    std::vector<int> order;
+    order.reserve(in.n_points);
+    for (int f = 0; f < in.n_frames; f++) {
+        const size_t b = order.size();
+        for (int p = 0; p < in.n_points; p++)
+            if (in.point_host[p] == f) order.push_back(p);
+        if (in.point_rank)
+            std::stable_sort(order.begin() + b, order.end(),
+                             [&](int a, int c) { return in.point_rank[a] < in.point_rank[c]; });
+    }
     const long long T = in.n_residuals;
     long long acc = 0;
-    for (int f = 0; f < in.n_frames; f++)
-        for (int p = 0; p < in.n_points; p++) {
-            if (in.point_host[p] != f) continue;
-            const long long owner = T > 0 ? std::min<long long>(count - 1, acc * count / T) : p % count;
-            if (owner == rank) out.push_back(p);
-            acc += in.point_res_begin[p + 1] - in.point_res_begin[p];
-        }
+    for (int p : order) {
+        const long long owner = T > 0 ? std::min<long long>(count - 1, acc * count / T) : p % count;
+        if (owner == rank) out.push_back(p);
+        acc += in.point_res_begin[p + 1] - in.point_res_begin[p];
+    }
 }
 
 // parent != nullptr: a marginalisation context over `ws[0]` whose frames are the parent's window

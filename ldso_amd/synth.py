@@ -67,8 +67,14 @@ def make_window(n_frames=7, n_points=2000, width=640, height=480, seed=0, outlie
 def in_image_order(w: Window) -> Window:
     """The same window with each host frame's points in image row order (v, then u): the order in
     which LDSO's pixel selection emits them.  make_window's points are in random order."""
+    return permute_points(w, np.lexsort((w.point_data[:, 0], np.floor(w.point_data[:, 1]), w.point_host)))
+
+
+def permute_points(w: Window, order) -> Window:
+    """The same window with its points (and their residual runs) in the order `order` (new index ->
+    index in w); o.point_order / o.res_order map the new points / residuals back to w's."""
     import copy
-    order = np.lexsort((w.point_data[:, 0], np.floor(w.point_data[:, 1]), w.point_host))
+    order = np.asarray(order)
     ridx = np.concatenate([np.arange(w.point_res_begin[p], w.point_res_begin[p + 1]) for p in order])
     o = copy.copy(w)
     o.point_host = np.ascontiguousarray(w.point_host[order])

@@ -44,6 +44,8 @@ class Window:
     # the reference settings takeData's priors follow (setting_affineOptModeA / B): an L.OptSettings,
     # None = the defaults.  The context that runs the window must hold the same (BAContext.set_settings).
     settings: object = None
+    # i32[P] or None: each point's rank in its host frame's features order (ldso_ba_window::point_rank)
+    point_rank: np.ndarray = None
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -108,6 +110,7 @@ class Window:
             res_state=np.ascontiguousarray(self.res_state, np.int8),
             res_energy=np.ascontiguousarray(self.res_energy, np.float32),
             res_flags=np.ascontiguousarray(self.res_flags, np.uint8),
+            point_rank=None if self.point_rank is None else np.ascontiguousarray(self.point_rank, np.int32),
         )
         self._keep = [a for a in arrs.values() if a is not None]
         s = L.LdsoBaWindow()

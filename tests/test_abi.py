@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol(built):
     bound = {name for name, _, _ in L.ABI}
     assert set(syms) == bound, set(syms) ^ bound
     lib = L.lib()
-    assert lib.ldso_ba_abi_version() == L.ABI_VERSION == 5
+    assert lib.ldso_ba_abi_version() == L.ABI_VERSION == 6
     assert lib.ldso_ba_num_kernels() >= 3
 
 

@@ -364,3 +364,39 @@ def test_graph_recaptured_when_solve_mode_changes(built, monkeypatch):
         ctx.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
+@pytest.mark.gpu
+def test_point_rank_sets_the_device_point_order(built):
+    """ldso_ba_window::point_rank: the library keeps each host's points in features order (the order
+    doStepFromBackup sums sumNID in, FullSystem.cc:1899-1909) whatever order the caller lists them
+    in.  The same window with its points shuffled and each point's rank in the original order
+    optimises bit for bit like the original: energies, iterations, status, frames, idepths."""
+    cfg = dict(n_frames=6, n_points=700, seed=61)
+    w = synth.make_window(**cfg)
+    rank = np.zeros(w.n_points, np.int32)  # each point's index among its host's points, w's order
+    for f in range(w.n_frames):
+        idx = np.flatnonzero(w.point_host == f)
+        rank[idx] = np.arange(idx.size)
+    order = np.random.default_rng(5).permutation(w.n_points)
+    o = synth.permute_points(synth.make_window(**cfg), order)
+    o.point_rank = rank[order]
+    ns = [w.nullspaces()]
+    res = []
+    for win in (w, o):
+        c = BAContext(0).load([win])
+        res.append(c.optimize(6, nullspaces=ns))
+        c.close()
+    (e1, f1, c1, d1, i1, s1), (e2, f2, c2, d2, i2, s2) = res
+    np.testing.assert_array_equal(e1, e2)
+    np.testing.assert_array_equal(i1, i2)
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_array_equal(f1.view(np.uint8), f2.view(np.uint8))
+    np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(d2[0], d1[0][order])
+    # without the ranks the shuffled window sums sumNID in another order (its own energies may
+    # differ in the last bits: the Schur chunks hold other points)
+    c = BAContext(0).load([synth.permute_points(synth.make_window(**cfg), order)])
+    e3 = c.optimize(6, nullspaces=ns)[0]
+    c.close()
+    assert np.isfinite(e3).all()
