@@ -372,6 +372,8 @@ def test_point_rank_sets_the_device_point_order(built):
     doStepFromBackup sums sumNID in, FullSystem.cc:1899-1909) whatever order the caller lists them
     in.  The same window with its points shuffled and each point's rank in the original order
     optimises bit for bit like the original: energies, iterations, status, frames, idepths."""
+    from ldso_amd import BAContext
+
     cfg = dict(n_frames=6, n_points=700, seed=61)
     w = synth.make_window(**cfg)
     rank = np.zeros(w.n_points, np.int32)  # each point's index among its host's points, w's order
