@@ -131,7 +131,6 @@ struct LinParams {
     const float4 *__restrict__ img;  // frames: layout 3 (band_offset) or layout 1 (tex())
     const float *__restrict__ precalc;
     const float *__restrict__ frame_th;
-    const int *__restrict__ rs_point;
     const int *__restrict__ rs_slot;   // record slot (WinDev::rec_base layout)
     const float *__restrict__ pt_data;
     int8_t *rs_state;
@@ -857,8 +856,10 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
     // inside a divergent branch is waited for at the branch's end) so it lands during phase A.
     const int rq = valid ? r : 0;
     int my_state = P.rs_state[rq];
-    const int my_point = P.rs_point[rq];
     const int my_slot = P.rs_slot[rq];
+    // the point from the record slot (rec_base + s P + q, s = the target's slot of host h): no
+    // per-residual point index is read
+    const int my_point = valid ? W.point_base + (my_slot - W.rec_base - (t < h ? t : t - 1) * W.P) : W.point_base;
     uint8_t flags = P.rs_flags[rq];
     float state_energy = P.rs_energy[rq];
     float new_energy = P.rs_newenergy[rq];
@@ -1215,7 +1216,7 @@ constexpr int kPrePitch = 12;  // floats of staged precalc (R0, t0) per target i
 constexpr int kScThreads = 128;  // 2 waves: a lane per point gathers, both run the SYRK tiles
 static_assert(kScPoints <= kScThreads, "one gathering lane per point");
 // residual records per round trip (r4: 3 -> two round trips at N = 7, 27.6 vs 28.3 us; r5: 6 -> one round
-// trip, 30.0 vs 27.6 us)
+// trip, 30.0 vs 27.6 us with 48-B records, 30.6 vs 25.9 us with 24-B records)
 constexpr int kScBatch = 3;
 __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -4086,7 +4087,7 @@ struct ldso_ba_ctx {
     long long frame_stride = 0;
     DevBuf<float> d_precalc, d_frame_th, d_pt_data, d_pt_out, d_pt_step;
     DevBuf<double> d_adH, d_adT;
-    DevBuf<int> d_rs_point, d_rs_slot, d_pt_nres, d_pair_win, d_frame_win, d_pt_host;
+    DevBuf<int> d_rs_slot, d_pt_nres, d_pair_win, d_frame_win, d_pt_host;
     DevBuf<unsigned long long> d_pt_tgt;
     DevBuf<uint8_t> d_rs_tgt, d_rs_flags;
     DevBuf<int8_t> d_rs_state, d_rs_newstate;
@@ -4669,7 +4670,6 @@ void ldso_ba_destroy(ldso_ba_ctx *c) {
     c->d_pt_step.release();
     c->d_adH.release();
     c->d_adT.release();
-    c->d_rs_point.release();
     c->d_rs_slot.release();
     c->d_pt_nres.release();
     c->d_pt_tgt.release();
@@ -4798,7 +4798,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     // host-side layout
     std::vector<int4> top_items, sc_items;
     std::vector<int2> pair_items, host_items;
-    std::vector<int> pair_win, frame_win, rs_point, rs_slot, pt_nres, pt_host;
+    std::vector<int> pair_win, frame_win, rs_slot, pt_nres, pt_host;
     std::vector<unsigned long long> pt_tgt;
     int rec_base = 0;
     std::vector<uint8_t> rs_tgt, rs_flags;
@@ -4922,7 +4922,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
             rs_flags.push_back(in.res_flags[k]);
             rs_state.push_back(in.res_state[k]);
             rs_energy.push_back(in.res_energy[k]);
-            rs_point.push_back(0);
             rs_slot.push_back(0);
         }
         H.rs_slot.assign(R, 0);
@@ -4941,7 +4940,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
             unsigned long long tg = 0;
             for (int k = 0; k < e - b; k++) {
                 const int pos = res_pos_of[b + k];
-                rs_point[res_base + pos] = point_base + q;
                 const int tgk = in.res_target[b + k], hk = in.point_host[p];
                 const int slot = rec_base + (tgk < hk ? tgk : tgk - 1) * P + q;
                 rs_slot[res_base + pos] = slot;
@@ -5066,7 +5064,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     ALLOC(c->d_pt_host, std::max<size_t>(1, pt_host.size()));
     ALLOC(c->d_adH, adH.size());
     ALLOC(c->d_adT, adT.size());
-    ALLOC(c->d_rs_point, std::max<size_t>(1, rs_point.size()));
     ALLOC(c->d_pt_nres, std::max<size_t>(1, pt_nres.size()));
     ALLOC(c->d_rs_slot, std::max<size_t>(1, rs_slot.size()));
     ALLOC(c->d_pt_tgt, std::max<size_t>(1, pt_tgt.size()));
@@ -5130,7 +5127,6 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     UP(c->d_pt_host, pt_host);
     UP(c->d_adH, adH);
     UP(c->d_adT, adT);
-    UP(c->d_rs_point, rs_point);
     UP(c->d_pt_nres, pt_nres);
     UP(c->d_rs_slot, rs_slot);
     UP(c->d_pt_tgt, pt_tgt);
@@ -5407,7 +5403,6 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     L.ad_ht_delta = c->marg ? c->d_adhtd.p : nullptr;
     L.precalc = c->d_precalc.p;
     L.frame_th = c->d_frame_th.p;
-    L.rs_point = c->d_rs_point.p;
     L.rs_slot = c->d_rs_slot.p;
     L.pt_data = c->d_pt_data.p;
     L.rs_state = c->d_rs_state.p;
@@ -5583,7 +5578,6 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     L.ad_ht_delta = nullptr;
     L.precalc = c->d_precalc.p;
     L.frame_th = c->d_frame_th.p;
-    L.rs_point = c->d_rs_point.p;
     L.rs_slot = c->d_rs_slot.p;
     L.pt_data = c->d_pt_data.p;
     L.rs_state = c->d_sx_state.p;
