@@ -493,8 +493,8 @@ __device__ __forceinline__ void syrk_tiles(const float *U, int pitch, int nt, in
 //   for j < 10, and B[(r,c)][10 + m] = column m of [JabJIdx | JI_r] row c.
 // Rows 13 / 14 of A are the indicators of c = 0 / c = 1 and columns 13..15 of B carry the six
 // BotRight terms, so D[13][13..15] and D[14][13..15] are their sums.  32 v_mfma_f32_16x16x4f32
-// per wavefront, operands staged through the wave's LDS (36 floats per residual, two halves of 32
-// residuals).  fp32 products accumulated in fp32 like the blocked AccumulatorApprox sums
+// per wavefront, operands staged through the wave's LDS (36 floats per residual, all 64 rows at
+// once).  fp32 products accumulated in fp32 like the blocked AccumulatorApprox sums
 // (tolerance-checked).
 // ---------------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -539,25 +539,30 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
     const int i = lane & 15, kk = lane >> 4;
     const bool geo = i < 10, ind = i >= 13;
     const float a0c = i == 13 ? 1.f : 0.f, a1c = i == 14 ? 1.f : 0.f;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-        if ((lane >> 5) == half) stage(reinterpret_cast<float4 *>(tab + (lane & 31) * kTopRow));
-        wave_lds_sync();
-        const float *base = tab + kk * 8 * kTopRow;  // K rows (residual kk*8 + m, c)
+    // all 64 rows staged at once (one table, one barrier), two independent accumulator chains
+    stage(reinterpret_cast<float4 *>(tab + lane * kTopRow));
+    wave_lds_sync();
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    {
+        const float *base = tab + kk * 16 * kTopRow;  // K rows (residual kk*16 + m, c)
 #pragma unroll 4
-        for (int m = 0; m < 8; m++) {
-            const float *rr = base + m * kTopRow;
-            const float2 p = *reinterpret_cast<const float2 *>(rr + 2 * i);
-            const float4 q = *reinterpret_cast<const float4 *>(rr + 32);
-            const float A0 = ind ? a0c : p.x, A1 = ind ? a1c : p.y;
-            const float B0 = geo ? q.x * p.x + q.y * p.y : p.x;
-            const float B1 = geo ? q.y * p.x + q.z * p.y : p.y;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A0, B0, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A1, B1, acc, 0, 0, 0);
+        for (int m = 0; m < 16; m += 2) {
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const float *rr = base + (m + u) * kTopRow;
+                const float2 p = *reinterpret_cast<const float2 *>(rr + 2 * i);
+                const float4 q = *reinterpret_cast<const float4 *>(rr + 32);
+                const float A0 = ind ? a0c : p.x, A1 = ind ? a1c : p.y;
+                const float B0 = geo ? q.x * p.x + q.y * p.y : p.x;
+                const float B1 = geo ? q.y * p.x + q.z * p.y : p.y;
+                f32x4 &acc = u ? acc1 : acc0;
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A0, B0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A1, B1, acc, 0, 0, 0);
+            }
         }
-        wave_lds_sync();
     }
+    wave_lds_sync();
+    const f32x4 acc = acc0 + acc1;
     // lane holds D[4 kk + v][i]; scatter into the 96-slot partial layout read by k_stitch
 #pragma unroll
     for (int v = 0; v < 4; v++) {
@@ -585,7 +590,9 @@ __device__ __forceinline__ void top_mfma(float *tab, int lane, bool active, cons
 // kMarg: the marginalisation pass (addPoint<2> sums with fixLinearizationF's res_toZeroF).
 // ============================================================================================
 constexpr int kPtTable = 64 * 4;  // floats: [64 residuals][u, v, idepth, state]
-constexpr int kTopRows = 32;  // the Top operand table holds one half (32 residuals) at a time
+// the Top operand table holds all 64 rows: one stage, one barrier, two independent MFMA chains
+// (r5: 94.6 vs 96.5 us against two 32-row halves in one chain; fits the wave's 10 KB of LDS)
+constexpr int kTopRows = 64;
 constexpr int kTopTab = kTopRows * kTopRow;
 constexpr int kWaveLdsA = kTermsPerWave + kSumsPerWave + kPtTable;
 // floats of LDS per wavefront (the Top operand table reuses the wave's region after phase B)
