@@ -1244,6 +1244,28 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
     const int KPP = KP + 4;
     float *U = smem;               // [kScPoints][KPP]
     const int tid = threadIdx.x;
+    // this lane's point and its first records are requested before the block waits for the
+    // precalc staging below, so those round trips overlap (unconditional loads from a clamped index)
+    const bool mine = tid < it.y;
+    const int p = it.x + (mine ? tid : 0);
+    const int nres = P.pt_nres[p];
+    const unsigned long long tgs = P.pt_tgt[p];
+    const float4 pd0 = *reinterpret_cast<const float4 *>(P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE);
+    const float2 pd1 = *reinterpret_cast<const float2 *>(P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE + 4);
+    const size_t rp = (size_t)W.rec_base + (p - W.point_base), sstride = (size_t)W.P;
+    float4 ra[kScBatch];
+    float2 rb[kScBatch];
+    auto load_batch = [&](int k0) {  // records k0 .. k0 + kScBatch - 1 (clamped to the point's last)
+#pragma unroll
+        for (int u = 0; u < kScBatch; u++) {
+            const int k = max(0, min(k0 + u, nres - 1));
+            const int tg = (int)((tgs >> (4 * k)) & 15ull);
+            const size_t q = rp + (nres > 0 ? (tg < host ? tg : tg - 1) : 0) * sstride;
+            ra[u] = P.rec_a[q];
+            rb[u] = P.rec_b[q];
+        }
+    };
+    load_batch(0);
     // the host's pair precalc R0 / t0 (record floats 12..23) for every target, staged once per block:
     // every residual's centre geometry reads them from LDS (kPrePitch floats per target)
     float *pre_lds = smem + kScPoints * KPP;
@@ -1252,30 +1274,15 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
         pre_lds[t * kPrePitch + k] = P.precalc[(size_t)(W.pair_base + host + W.N * t) * LDSO_BA_PRECALC_STRIDE + 12 + k];
     }
     __syncthreads();
-    if (tid < it.y) {
+    if (mine) {
 #pragma clang fp contract(off)
-        const int p = it.x + tid;
-        const int nres = P.pt_nres[p];
-        // one round of record loads (slot s of the block's points is contiguous), then the
-        // sums in residual order exactly as AccumulatedTopHessian.cc:94-116 adds them
-        const unsigned long long tgs = P.pt_tgt[p];
-        const size_t rp = (size_t)W.rec_base + (p - W.point_base), sstride = (size_t)W.P;
-        const float4 pd0 = *reinterpret_cast<const float4 *>(P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE);
+        // the sums in residual order exactly as AccumulatedTopHessian.cc:94-116 adds them
         float hdd = 0, bd = 0, hcd[4] = {0, 0, 0, 0};
         int ngood = 0;
         float *row = U + tid * KPP;
         unsigned filled = 0;  // target slots whose JpJdF is in the row
         for (int k0 = 0; k0 < nres; k0 += kScBatch) {
-            float4 ra[kScBatch];
-            float2 rb[kScBatch];
-#pragma unroll
-            for (int u = 0; u < kScBatch; u++) {
-                const int k = min(k0 + u, nres - 1);
-                const int tg = (int)((tgs >> (4 * k)) & 15ull);
-                const size_t q = rp + (tg < host ? tg : tg - 1) * sstride;
-                ra[u] = P.rec_a[q];
-                rb[u] = P.rec_b[q];
-            }
+            if (k0) load_batch(k0);
 #pragma unroll
             for (int u = 0; u < kScBatch; u++) {
                 const int k = k0 + u;
@@ -1310,8 +1317,7 @@ __global__ __launch_bounds__(kScThreads) void k_point_sc(PointParams P) {
                 }
             for (int c = Kj; c < KP; c++) row[c] = 0.f;
         }
-        const float *pd = P.pt_data + (size_t)p * LDSO_BA_POINT_STRIDE;
-        const float priorF = pd[4], deltaF = pd[5];
+        const float priorF = pd1.x, deltaF = pd1.y;
         float HdiF = 0, bdSum = 0, ih = 0;
         if (ngood > 0) {
             // AccumulatedSCHessian.cc:24-33 (Hdd_accLF = bd_accLF = Hcd_accLF = 0 in the hot path)
