@@ -315,6 +315,15 @@ __device__ inline void point_terms(const Geo &g, const PhotoSums &s, float jpjdf
 // k_point_sc from the live precalc of the pass, the resubstitution and the JpJdF read-back from the
 // geometry snapshot the pass's first chunk of each pair writes (the frame step rewrites the live
 // precalc in the same launch as the resubstitution).  64 -> 48 -> 24 B written and read back.
+// non-temporal stores for k_linearize's per-residual outputs: nothing reads them again while the
+// pass's image lines want the L2 (the next pass, or k_point_sc after the XCD's L2 has turned over
+// many times); k_linearize 93.6 -> 91.2 us, FETCH -1.7 MB (r5, profiles/r5/af)
+typedef float ntf4 __attribute__((ext_vector_type(4)));
+typedef float ntf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_nt(float4 *p, float4 v) { __builtin_nontemporal_store(ntf4{v.x, v.y, v.z, v.w}, reinterpret_cast<ntf4 *>(p)); }
+__device__ __forceinline__ void st_nt(float2 *p, float2 v) { __builtin_nontemporal_store(ntf2{v.x, v.y}, reinterpret_cast<ntf2 *>(p)); }
+template <typename T>
+__device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v, p); }
 constexpr int kGeoSnap = 16;  // floats per pair: R0 [0..8], t0 [9..11], calib fxl, fyl, cxl, cyl [12..15]
 __device__ __forceinline__ void write_record(float4 *rec_a, float2 *rec_b, bool active, float idz, const Geo &g,
                                              const PhotoSums &s) {
@@ -323,10 +332,10 @@ __device__ __forceinline__ void write_record(float4 *rec_a, float2 *rec_b, bool 
         point_terms(g, s, jp, hc, hdd, bd);  // jp[0..5], hc, hdd: dead here (recomputed from the geometry)
         const float j0 = s.JIdx2_00 * g.d_d_x + s.JIdx2_10 * g.d_d_y;  // point_terms' statements
         const float j1 = s.JIdx2_10 * g.d_d_x + s.JIdx2_11 * g.d_d_y;
-        *rec_a = make_float4(j0, j1, jp[6], jp[7]);
-        *rec_b = make_float2(bd, idz);
+        st_nt(rec_a, make_float4(j0, j1, jp[6], jp[7]));
+        st_nt(rec_b, make_float2(bd, idz));
     } else {
-        *rec_b = make_float2(0.f, __builtin_nanf(""));
+        st_nt(rec_b, make_float2(0.f, __builtin_nanf("")));
     }
 }
 // JpJdF[0..5] of a record from its centre geometry: point_terms' statements
@@ -1066,7 +1075,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
         float e_wo = -1;
         if (old_state == LDSO_BA_RES_OOB) {
             energy = state_energy;  // linearize returns state_energy; applyRes returns early
-            P.rec_b[my_slot] = make_float2(0.f, __builtin_nanf(""));  // not active
+            st_nt(P.rec_b + my_slot, make_float2(0.f, __builtin_nanf("")));  // not active
         } else {
             const float4 pd0 = my_pd0;
             const float *Sr = lds_sums_w + lane * kSumStride;
@@ -1092,7 +1101,11 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
                                         wM3, hM3, g);
             // centerProjectedTo: written where projected, kept (not re-read) where not
             float *centre = reinterpret_cast<float *>(P.rs_center + r);
-            if (ok) *reinterpret_cast<float3 *>(centre) = make_float3(g.Ku, g.Kv, g.new_idepth);
+            if (ok) {
+                st_nt(centre, g.Ku);
+                st_nt(centre + 1, g.Kv);
+                st_nt(centre + 2, g.new_idepth);
+            }
             ok = ok && pat_ok;
             if (!ok) {
                 energy = state_energy;  // OOB: return state_energy, NewEnergy untouched
@@ -1125,14 +1138,14 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
                 const float dx = pi[0] / pi[2] - pr[0] / pr[2], dy = pi[1] / pi[2] - pr[1] / pr[2];
                 centre[3] = 0.01f * sqrtf(dx * dx + dy * dy);
             }
-            P.rs_state[r] = new_state;
-            P.rs_flags[r] = flags;
-            P.rs_energy[r] = state_energy;
-            P.rs_newenergy[r] = new_energy;
+            st_nt(P.rs_state + r, new_state);
+            st_nt(P.rs_flags + r, flags);
+            st_nt(P.rs_energy + r, state_energy);
+            st_nt(P.rs_newenergy + r, new_energy);
         }
         isIN = (new_state == LDSO_BA_RES_IN);
-        P.rs_newstate[r] = new_state;
-        P.rs_energy_wo[r] = e_wo;
+        st_nt(P.rs_newstate + r, new_state);
+        st_nt(P.rs_energy_wo + r, e_wo);
     }
 
     // linearizeAll stats: sum of returned energies (double) and #IN, per chunk
