@@ -610,6 +610,14 @@ def main():
     # host-side download leaves the GPU idle between the warmup and the timed steps
     n_gather = sum(int((ctx.residuals(i)["state"] != 1).sum()) for i in range(len(windows)))
     ctx.set_kernel_timing(False)
+    # the same steps without the roofline's event pair (each costs the stream ~5 us of idle GPU on
+    # either side of k_linearize): reported beside the headline, never as it
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    ms_step_no_events = 1e3 * (time.perf_counter() - t0) / args.steps
     ctx.set_tuning(7, -1)
     ctx.set_kernel_timing(True)  # breakdown of every kernel, outside the timed region
     for _ in range(min(args.steps, 20)):
@@ -766,6 +774,7 @@ def main():
                 "algo_bytes_per_residual": algo_bytes_per_residual(N),
             },
             "kernel_ms_per_step": {k: v[0] / max(1, v[1]) for k, v in kall.items() if v[1]},
+            "ms_per_step_without_kernel_events": ms_step_no_events,
             "gn_iteration_batched": gn,
             "single_window": single,
             "s11": s11,
