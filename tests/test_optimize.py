@@ -402,3 +402,52 @@ def test_point_rank_sets_the_device_point_order(built):
     e3 = c.optimize(6, nullspaces=ns)[0]
     c.close()
     assert np.isfinite(e3).all()
+
+
+@pytest.mark.gpu
+def test_canbreak_decision_at_the_threshold(built):
+    """The device loop's exit decided at the exact edge of setting_thOptIterations: the threshold at
+    which the reference's canbreak (se3.h step_canbreak, host) flips for the device's own x and
+    sumNID is found by bisection over float thresholds; ldso_ba_optimize(1) with min_opt_iterations
+    = 0 must stop (CONVERGED) one float above it and run on (RAN_ALL) one float below.  x comes from
+    ldso_ba_iterate's pass + solve on a fresh context (the same kernels as the loop's first
+    iteration), sumNID from the idepths in the device's point order (hosts in turn, float chain)."""
+    from ldso_amd import BAContext
+
+    cfg = dict(n_frames=6, n_points=600, seed=71)
+    w = synth.make_window(**cfg)
+    N = w.n_frames
+    ns = [w.nullspaces()]
+    c = BAContext(0).load([synth.make_window(**cfg)])
+    c.reset_oob()  # as FullSystem::optimize starts
+    _, xs, _ = c.iterate(0, 1e-5, ns)
+    c.close()
+    x = np.ascontiguousarray(xs[0], np.float64)
+    snid = np.float32(0)
+    for f in range(N):  # FullSystem.cc:1899-1909 in the device point order
+        for q in np.flatnonzero(w.point_host == f):
+            snid = np.float32(snid + np.float32(abs(w.point_data[q, 2])))
+    nnid = np.float32(w.n_points)
+    lib = L.lib()
+
+    def host_cb(th):
+        cb = C.c_int32(0)
+        L.check(lib.ldso_ba_step_canbreak(N, L.ptr(x, L.f64p), float(snid), float(nnid), float(th), C.byref(cb)))
+        return bool(cb.value)
+
+    lo, hi = np.float32(1e-8), np.float32(1e8)  # canbreak is monotone in th: false at lo, true at hi
+    assert not host_cb(lo) and host_cb(hi)
+    lo_b, hi_b = int(lo.view(np.int32)), int(hi.view(np.int32))  # positive floats order like their bits
+    while hi_b - lo_b > 1:
+        mid = (lo_b + hi_b) // 2
+        if host_cb(np.int32(mid).view(np.float32)):
+            hi_b = mid
+        else:
+            lo_b = mid
+    t_hi, t_lo = np.int32(hi_b).view(np.float32), np.int32(lo_b).view(np.float32)
+    for th, want in ((t_hi, L.OPT_CONVERGED), (t_lo, L.OPT_RAN_ALL)):
+        c = BAContext(0).load([synth.make_window(**cfg)])
+        st = L.OptSettings.default(min_opt_iterations=0, th_opt_iterations=float(th))
+        _, _, _, _, its, status = c.optimize(1, nullspaces=ns, settings=st)
+        c.close()
+        assert status[0] == want, (float(th), status, its)
