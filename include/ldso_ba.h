@@ -320,7 +320,9 @@ int ldso_ba_get_system(ldso_ba_ctx *ctx, int32_t win, double *HA, double *bA, do
                        double *bL, double *Hsc, double *bsc);
 /* Per residual, in the caller's point-major order. Any pointer may be NULL.
  *   new_state/state [R], state_energy/new_energy_wo [R], center [R][3] (centerProjectedTo),
- *   flags [R], jpjdf [R][8] (JpJdF), rel_bs [R] (linearizeAll_Reductor relBS, fix pass). */
+ *   flags [R], jpjdf [R][8] (JpJdF of the last pass, formed from the pass's record and geometry;
+ *   0 where that pass left the residual inactive -- the reference keeps a stale JpJdF there, which
+ *   nothing reads), rel_bs [R] (linearizeAll_Reductor relBS, fix pass). */
 int ldso_ba_get_residuals(ldso_ba_ctx *ctx, int32_t win, int8_t *new_state, int8_t *state,
                           float *state_energy, float *new_energy_wo, float *center,
                           uint8_t *flags, float *jpjdf, float *rel_bs);
