@@ -771,3 +771,33 @@ def test_degenerate_windows_in_a_batch(built):
     np.testing.assert_allclose(id3[0], id1[0], rtol=1e-6)
     one.close()
     both.close()
+
+
+def test_records_keep_the_pass_geometry(built):
+    """The 24-B records hold (j0, j1) and the pass's idepth; JpJdF[0..5] is re-formed from the
+    centre geometry of the pass (the per-pair snapshot), not from the live state: after the
+    points' idepths and the frames' precalc change (ldso_ba_update_points, ldso_ba_update), the
+    JpJdF read back and the resubstitution's point steps are bit for bit those of the pass, as the
+    reference's stored JpJdF would give (Residuals.h:120-129, EnergyFunctional.cc:638-667)."""
+    cfg = dict(n_frames=5, n_points=400, seed=63)
+    w = synth.make_window(**cfg)
+    c = BAContext(0).load([w])
+    c.linearize()
+    jp1 = c.residuals(0)["jpjdf"]
+    x = np.random.default_rng(3).standard_normal(w.dim) * 1e-4
+    st1 = c.resubstitute(0, x, 1e-5)
+    w2 = synth.make_window(**cfg)
+    fr = np.ascontiguousarray(w2.frames).copy()
+    fr["state"][1, 0] += 1e-3  # another pose: another precalc
+    w2.frames = fr
+    w2.refresh_frame_terms()
+    c.update(0, w2)
+    vals = np.stack([w.point_data[:, 2] * 1.01, w.point_data[:, 3], w.point_data[:, 4], w.point_data[:, 5]], 1)
+    c.update_points(0, vals)
+    jp2 = c.residuals(0)["jpjdf"]
+    st2 = c.resubstitute(0, x, 1e-5)
+    np.testing.assert_array_equal(jp1, jp2)
+    np.testing.assert_array_equal(st1, st2)
+    c.linearize()  # a new pass takes the new state
+    assert not np.array_equal(c.residuals(0)["jpjdf"], jp1)
+    c.close()
