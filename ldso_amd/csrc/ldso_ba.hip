@@ -140,7 +140,8 @@ struct LinParams {
     float *rs_energy;      // state_energy
     float *rs_newenergy;   // state_NewEnergy (persists: applyRes copies it on a later OOB)
     float *rs_energy_wo;   // state_NewEnergyWithOutlier
-    float4 *rs_center;     // centerProjectedTo, relBS
+    float *rs_center;      // four planes of center_stride floats: centerProjectedTo x, y, z and relBS
+    long long center_stride;
     float4 *rec_a;         // [slots]: (j0, j1, JpJdF[6], JpJdF[7]) -- see write_record
     float2 *rec_b;         // [slots]: (bd_r, idepth linearised at; NaN: not active)
     float *geo_snap;       // [pairs][kGeoSnap]: the pass's R0, t0 and calibration (the first chunk of a pair)
@@ -1100,11 +1101,12 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
             bool ok = centre_projection(pre, pd0.x, pd0.y, pd0.w, W.calib[0], W.calib[1], W.calib[2], W.calib[3],
                                         wM3, hM3, g);
             // centerProjectedTo: written where projected, kept (not re-read) where not
-            float *centre = reinterpret_cast<float *>(P.rs_center + r);
+            float *centre = P.rs_center + r;  // planes: coalesced 4-B stores, whole lines
+            const long long cs = P.center_stride;
             if (ok) {
                 st_nt(centre, g.Ku);
-                st_nt(centre + 1, g.Kv);
-                st_nt(centre + 2, g.new_idepth);
+                st_nt(centre + cs, g.Kv);
+                st_nt(centre + 2 * cs, g.new_idepth);
             }
             ok = ok && pat_ok;
             if (!ok) {
@@ -1136,7 +1138,7 @@ __global__ __launch_bounds__(256, kLinBlocksPerCu) void k_linearize(LinParams P)
                     pr[i] = pi[i] + pre[9 + i] * pd0.z;
                 }
                 const float dx = pi[0] / pi[2] - pr[0] / pr[2], dy = pi[1] / pi[2] - pr[1] / pr[2];
-                centre[3] = 0.01f * sqrtf(dx * dx + dy * dy);
+                centre[3 * cs] = 0.01f * sqrtf(dx * dx + dy * dy);
             }
             st_nt(P.rs_state + r, new_state);
             st_nt(P.rs_flags + r, flags);
@@ -3971,8 +3973,8 @@ __global__ __launch_bounds__(256) void k_pack_out(PackOut P) {
 // resetOOB() over a residual range; optionally also the scratch copies of
 // ldso_ba_linearize_residuals: centre "not projected" (all-ones NaN) and the flags copied
 __global__ __launch_bounds__(256) void k_reset_oob(int8_t *state, int8_t *newstate, float *energy, float *newenergy,
-                                                    int n, float4 *center = nullptr, uint8_t *flags = nullptr,
-                                                    const uint8_t *flags_src = nullptr) {
+                                                    int n, float *center = nullptr, long long cstride = 0,
+                                                    uint8_t *flags = nullptr, const uint8_t *flags_src = nullptr) {
     for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
         state[r] = LDSO_BA_RES_IN;
         newstate[r] = LDSO_BA_RES_OUTLIER;
@@ -3980,7 +3982,7 @@ __global__ __launch_bounds__(256) void k_reset_oob(int8_t *state, int8_t *newsta
         newenergy[r] = 0.f;
         if (center) {
             const float q = __uint_as_float(0xFFFFFFFFu);
-            center[r] = make_float4(q, q, q, q);
+            for (int k = 0; k < 4; k++) center[k * cstride + r] = q;
             flags[r] = flags_src[r];
         }
     }
@@ -5466,7 +5468,8 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     L.rs_energy = c->d_rs_energy.p;
     L.rs_newenergy = c->d_rs_newenergy.p;
     L.rs_energy_wo = c->d_rs_energy_wo.p;
-    L.rs_center = c->d_rs_center.p;
+    L.rs_center = reinterpret_cast<float *>(c->d_rs_center.p);
+    L.center_stride = c->R_tot;
     L.rec_a = c->d_rec_a.p;
     L.rec_b = c->d_rec_b.p;
     L.geo_snap = c->d_geo_snap.p;
@@ -5622,7 +5625,7 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     if (R) {  // one launch for the five fills and the flag copy
         k_reset_oob<<<std::min<int>(1024, (int)((R + 255) / 256)), 256, 0, st>>>(
             c->d_sx_state.p + b, c->d_sx_newstate.p + b, c->d_sx_energy.p + b, c->d_sx_newenergy.p + b, (int)R,
-            c->d_sx_center.p + b, c->d_sx_flags.p + b, c->d_rs_flags.p + b);
+            reinterpret_cast<float *>(c->d_sx_center.p) + b, (long long)Rt, c->d_sx_flags.p + b, c->d_rs_flags.p + b);
         HIP_TRY(hipGetLastError());
     }
     LinParams L{};
@@ -5641,7 +5644,8 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     L.rs_energy = c->d_sx_energy.p;
     L.rs_newenergy = c->d_sx_newenergy.p;
     L.rs_energy_wo = c->d_sx_ewo.p;
-    L.rs_center = c->d_sx_center.p;
+    L.rs_center = reinterpret_cast<float *>(c->d_sx_center.p);
+    L.center_stride = (long long)Rt;
     L.rec_a = c->d_sx_rec_a.p;
     L.rec_b = c->d_sx_rec_b.p;
     L.geo_snap = c->d_sx_geo_snap.p;
@@ -5665,7 +5669,10 @@ int ldso_ba_linearize_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, 
     HIP_TRY(hipMemcpyAsync(ns.data(), c->d_sx_newstate.p + b, R, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(ne.data(), c->d_sx_newenergy.p + b, R * sizeof(float), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(ew.data(), c->d_sx_ewo.p + b, R * sizeof(float), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(ce.data(), c->d_sx_center.p + b, R * sizeof(float4), hipMemcpyDeviceToHost, st));
+    for (int k = 0; k < 4; k++)  // the planes back into (x, y, z, relBS) per residual
+        HIP_TRY(hipMemcpy2DAsync(reinterpret_cast<float *>(ce.data()) + k, sizeof(float4),
+                                 reinterpret_cast<const float *>(c->d_sx_center.p) + (size_t)k * Rt + b, sizeof(float),
+                                 sizeof(float), R, hipMemcpyDeviceToHost, st));
     std::vector<float> jp;
     if (jpjdf && (rc = record_jpjdf(c, win, c->d_sx_rec_a.p, c->d_sx_rec_b.p, c->d_sx_geo_snap.p, jp))) return rc;
     if ((rc = ldso_ba_sync(c))) return rc;
@@ -5862,7 +5869,10 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
     HIP_TRY(hipMemcpy(fl.data(), c->d_rs_flags.p + D.res_base, R, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(se.data(), c->d_rs_energy.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(ew.data(), c->d_rs_energy_wo.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(ce.data(), c->d_rs_center.p + D.res_base, R * sizeof(float4), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 4; k++)  // the planes back into (x, y, z, relBS) per residual
+        HIP_TRY(hipMemcpy2D(reinterpret_cast<float *>(ce.data()) + k, sizeof(float4),
+                            reinterpret_cast<const float *>(c->d_rs_center.p) + (size_t)k * c->R_tot + D.res_base,
+                            sizeof(float), sizeof(float), R, hipMemcpyDeviceToHost));
     std::vector<float> jp;
     if (jpjdf) {
         if ((rc = record_jpjdf(c, win, c->d_rec_a.p, c->d_rec_b.p, c->d_geo_snap.p, jp))) return rc;
