@@ -12,7 +12,9 @@ tot_k = tot_g = 0
 for r in tail:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     gap = (s - prev_end) / 1e3 if prev_end else 0.0
-    name = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")[:40]
+    import re
+    m = re.search(r"(k_[a-z_]+)", r["Kernel_Name"])
+    name = m.group(1) if m else r["Kernel_Name"][:40]
     print(f"{name:42s} {((e - s) / 1e3):8.2f} us   gap {gap:8.2f} us")
     tot_k += (e - s) / 1e3
     tot_g += gap
