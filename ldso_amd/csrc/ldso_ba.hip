@@ -3751,8 +3751,13 @@ __device__ __forceinline__ void resubstitute_one(const ResubParams &P, int k) {
 #pragma clang fp contract(off)
     if (k >= P.count) return;
     const int p = P.begin + k;
-    if (P.stop && P.it >= P.stop[P.pt_win[p]]) return;
+    // every per-point load first (one round trip), then the exits
+    const int w = P.pt_win[p], h = P.pt_host[p], nres = P.pt_nres[p];
+    const unsigned long long tgs = P.pt_tgt[p];
     const float *po = P.pt_out + (size_t)p * 12;
+    const float po0 = po[0], po1 = po[1], po5 = po[5], po6 = po[6], po7 = po[7], po8 = po[8], po9 = po[9];
+    const float2 uv = *reinterpret_cast<const float2 *>(P.pt_geo + (size_t)p * LDSO_BA_POINT_STRIDE);
+    if (P.stop && P.it >= P.stop[w]) return;
     // doStepFromBackup's point step (setIdepth / setIdepthZero / setDeltaF)
     auto apply = [&](float step) {
         if (!P.pt_data) return;
@@ -3762,44 +3767,70 @@ __device__ __forceinline__ void resubstitute_one(const ResubParams &P, int k) {
         d[3] = kScaleIdepth * idepth;  // setIdepthZero (LDSO's doStepFromBackup)
         d[5] = idepth - idepth;        // setDeltaF: idepth - idepth_zero
     };
-    if (po[9] == 0) {
+    if (po9 == 0) {
         P.pt_step[p] = 0;
         apply(0.0f);
         return;
     }
-    const int w = P.pt_win[p];
     const WinDev &W = P.wins[w];
     const int N = W.N;
     const float *xad = P.xad + (size_t)w * kXadStride, *xc = xad + (size_t)N * N * 8;
-    float b = po[1];
-    const float d = xc[0] * po[5] + xc[1] * po[6] + xc[2] * po[7] + xc[3] * po[8];
-    b -= d;
-    const int h = P.pt_host[p];
-    const unsigned long long tgs = P.pt_tgt[p];
     const size_t rp = (size_t)W.rec_base + (p - W.point_base);
-    const float2 uv = *reinterpret_cast<const float2 *>(P.pt_geo + (size_t)p * LDSO_BA_POINT_STRIDE);
-    for (int q = 0; q < P.pt_nres[p]; q++) {
+    // residual q's operands -- its record, the pass's geometry of its pair, its xAd row -- loaded
+    // unconditionally (the record's activity is tested after they land) and one residual ahead,
+    // so the chain is one round trip per point instead of two per residual
+    struct Ops {
+        float2 rb;
+        float4 ja;
+        float4 g[4];  // geometry snapshot: R0 (9), t0 (3), calib (4)
+        float4 xa[2];
+    };
+    auto load = [&](int q, Ops &o) {
         const int tg = (int)((tgs >> (4 * q)) & 15ull);
         const size_t rq = rp + (size_t)(tg < h ? tg : tg - 1) * W.P;
-        const float2 rb = P.rec_b[rq];
-        if (rb.y != rb.y) continue;  // not active
-        const float4 ja = P.rec_a[rq];
-        // the residual's JpJdF: (j0, j1) through the centre geometry of the pass (write_record)
-        const float *gs = P.geo_snap + (size_t)(W.pair_base + h + N * tg) * kGeoSnap;
-        Geo g;
-        (void)centre_projection(gs - 12, uv.x, uv.y, rb.y, gs[12], gs[13], gs[14], gs[15], W.wM3, W.hM3, g);
-        float jp[6];
-        record_jp6(g, ja.x, ja.y, jp);
-        const float *xa = xad + (size_t)(h * N + tg) * 8;
-        const float dd = xa[0] * jp[0] + xa[1] * jp[1] + xa[2] * jp[2] + xa[3] * jp[3] + xa[4] * jp[4] + xa[5] * jp[5] +
-                         xa[6] * ja.z + xa[7] * ja.w;
-        b -= dd;
+        o.rb = P.rec_b[rq];
+        o.ja = P.rec_a[rq];
+        const float4 *gs = reinterpret_cast<const float4 *>(P.geo_snap + (size_t)(W.pair_base + h + N * tg) * kGeoSnap);
+#pragma unroll
+        for (int e = 0; e < 4; e++) o.g[e] = gs[e];
+        const float4 *xa = reinterpret_cast<const float4 *>(xad + (size_t)(h * N + tg) * 8);
+        o.xa[0] = xa[0];
+        o.xa[1] = xa[1];
+    };
+    Ops cur, nxt;
+    if (nres > 0) load(0, cur);
+    float b = po1;
+    const float d = xc[0] * po5 + xc[1] * po6 + xc[2] * po7 + xc[3] * po8;
+    b -= d;
+    for (int q = 0; q < nres; q++) {
+        load(min(q + 1, nres - 1), nxt);  // unconditional (a guarded load would be waited for at once)
+        if (cur.rb.y == cur.rb.y) {       // active
+            // the residual's JpJdF: (j0, j1) through the centre geometry of the pass (write_record)
+            float pre[24];
+#pragma unroll
+            for (int e = 0; e < 3; e++) {
+                pre[12 + 4 * e] = cur.g[e].x;
+                pre[13 + 4 * e] = cur.g[e].y;
+                pre[14 + 4 * e] = cur.g[e].z;
+                pre[15 + 4 * e] = cur.g[e].w;
+            }
+            Geo g;
+            (void)centre_projection(pre, uv.x, uv.y, cur.rb.y, cur.g[3].x, cur.g[3].y, cur.g[3].z, cur.g[3].w, W.wM3,
+                                    W.hM3, g);
+            float jp[6];
+            record_jp6(g, cur.ja.x, cur.ja.y, jp);
+            const float4 xa0 = cur.xa[0], xa1 = cur.xa[1];
+            const float dd = xa0.x * jp[0] + xa0.y * jp[1] + xa0.z * jp[2] + xa0.w * jp[3] + xa1.x * jp[4] +
+                             xa1.y * jp[5] + xa1.z * cur.ja.z + xa1.w * cur.ja.w;
+            b -= dd;
+        }
+        cur = nxt;
     }
     if (!isfinite(b)) {  // reference returns from the chunk; the step is left unchanged
         apply(P.pt_step[p]);
         return;
     }
-    const float step = -b * po[0] / (1 + P.lambda);
+    const float step = -b * po0 / (1 + P.lambda);
     P.pt_step[p] = step;
     apply(step);
 }
