@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2740,6 +2741,43 @@ __device__ __forceinline__ void solve_ortho_load(const SolveParams &P, const Win
     if (tid == 0) S.misc[7] = g[98];
 }
 
+// solve_ortho_load split in two for k_solve_fast: the loads into registers at kernel start (their
+// round trip overlaps the assembly's), the LDS stores after the assembly (read only after the
+// factorisation's barriers).  Thread tid holds Nm elements tid + k nthreads (k < 2: n <= 92, 7 n <=
+// 2 x 512) and, below 49 / 14 / 1, its G / G^-1 / V, lr and fast-flag entries.
+struct OrthoPre {
+    double nm[2], g, gi, v, lr, fast;
+    bool on;
+    __device__ void load(const SolveParams &P, const WinDev &W, int tid, int nthreads) {
+        on = P.iteration >= 2 && P.n_null > 0;
+        if (!on) return;
+        const int n = W.D, kk = P.n_null;
+        const double *pnm = P.prep_nm + (size_t)7 * W.vec_base, *pg = P.prep_g + (size_t)kPrepGStride * blockIdx.x;
+#pragma unroll
+        for (int k = 0; k < 2; k++) nm[k] = pnm[min(tid + k * nthreads, kk * n - 1)];
+        const int t49 = min(tid, 48), t14 = min(tid, 13);
+        g = pg[t49];
+        gi = pg[49 + t49];
+        v = pg[99 + t49];
+        lr = pg[148 + t14];
+        fast = pg[98];
+    }
+    __device__ void store(const SolveParams &P, const WinDev &W, const SolveLds &S, int tid, int nthreads) const {
+        if (!on) return;
+        const int n = W.D, kk = P.n_null;
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            if (tid + k * nthreads < kk * n) S.Nm[tid + k * nthreads] = nm[k];
+        if (tid < 49) {
+            S.G[tid] = g;
+            S.Gi[tid] = gi;
+            S.V[tid] = v;
+        }
+        if (tid < 14) S.lr[tid] = lr;
+        if (tid == 0) S.misc[7] = fast;
+    }
+};
+
 __global__ __launch_bounds__(64) void k_ortho_prep(SolveParams P, double *prep_nm, double *prep_g) {
     extern __shared__ double lds[];
     const WinDev W = P.wins[blockIdx.x];
@@ -3398,8 +3436,11 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
         nid_chain(P.wins[w], P.pt_data, P.win_nid, w, reinterpret_cast<float *>(lds), P.nid_chunk);
         return;
     }
-    if (P.stop && P.iteration >= P.stop[blockIdx.x]) return;  // the window left the GN loop
+    static_assert(7 * kSolveMaxDim <= 2 * kSolveFastThreads, "OrthoPre: two Nm elements per thread");
+    // the stop flag and the window's descriptor in one round trip, then the exit
+    const int stop_it = P.stop ? P.stop[blockIdx.x] : INT_MAX;
     const WinDev W = P.wins[blockIdx.x];  // a register copy (see k_solve)
+    if (P.iteration >= stop_it) return;  // the window left the GN loop
     const int n = W.D, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ld = solve_ld(n);
     const SolveLds S(lds, n);
@@ -3408,8 +3449,10 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
     double *rdv = Wc + 2 * kSolveFastPanel * 128;                     // [2][8]: 1/d of each panel step
     XadPre xp;
     if (P.xad) xp.load(W, P.adH, P.adT, tid);
-    solve_ortho_load(P, W, S, tid, kSolveFastThreads);
+    OrthoPre op;
+    op.load(P, W, tid, kSolveFastThreads);
     solve_assemble<kSolveFastThreads>(P, W, S, tid);
+    op.store(P, W, S, tid, kSolveFastThreads);  // published by the factorisation's barriers
     double y[2] = {0.0, 0.0};  // wave 0: the forward substitution's y (rows lane, lane + 64)
     if (wave == 0) {
         y[0] = lane < n ? S.b[lane] : 0.0;
@@ -3901,10 +3944,12 @@ struct FrameStepParams {
 __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int blk) {
     __shared__ double poses[LDSO_BA_MAX_FRAMES][4][12];  // ev, ev^-1, cur, cur^-1: R (9), t (3)
     __shared__ float calib[4];
-    if (P.stop && P.it >= P.stop[blk]) return;  // lost in this iteration's solve, or stopped earlier
+    // the stop flag and the window's descriptor in one round trip, then the exit
+    const int stop_it = P.stop ? P.stop[blk] : INT_MAX;
     WinDev &W = P.wins[blk];
     const int N = W.N, tid = threadIdx.x;
     const double *xw = P.x + W.vec_base;
+    if (P.it >= stop_it) return;  // lost in this iteration's solve, or stopped earlier
     if (P.stop && tid == 128 && P.it >= P.min_its &&
         step_canbreak(N, xw, (float)P.win_nid[2 * blk], (float)P.win_nid[2 * blk + 1], P.th)) {
         P.stop[blk] = P.it + 1;
