@@ -2807,19 +2807,36 @@ __device__ __forceinline__ void solve_ortho_apply_store(const SolveParams &P, co
     const int kk = P.n_null;
     if (P.iteration >= 2 && kk > 0) {
         double *ntx = S.misc, *coef = S.misc + 8;
-        if (lane < kk) {  // a static trip count and unconditional (clamped) loads: only the adds chain
+        if (lane < kk) {  // t += Nm(i, a) y(i) in row order; only the adds chain (no selects on it):
+                          // blocks of 4 rows whose operands are loaded one block ahead, then the tail
             double t = 0.0;
-            const int a = lane;
-#pragma unroll 1
-            for (int i0 = 0; i0 < n; i0 += 4) {
-                double p[4];
+            const int a = lane, nb = n >> 2;
+            double cn[4], cy[4], nn[4], ny[4];
+            auto ld4 = [&](int blk, double (&m)[4], double (&v)[4]) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const int ic = min(i0 + u, n - 1);
-                    p[u] = Nm[(size_t)ic * kk + a] * y[ic];
+                    m[u] = Nm[(size_t)(4 * blk + u) * kk + a];
+                    v[u] = y[4 * blk + u];
+                }
+            };
+            if (nb > 0) ld4(0, cn, cy);
+#pragma unroll 1
+            for (int bk = 0; bk < nb; bk++) {
+                ld4(min(bk + 1, nb - 1), nn, ny);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const double p = cn[u] * cy[u];
+                    t += p;
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) t = i0 + u < n ? t + p[u] : t;
+                for (int u = 0; u < 4; u++) {
+                    cn[u] = nn[u];
+                    cy[u] = ny[u];
+                }
+            }
+            for (int i = 4 * nb; i < n; i++) {
+                const double p = Nm[(size_t)i * kk + a] * y[i];
+                t += p;
             }
             ntx[lane] = t;
             coef[lane] = 0.0;
@@ -3388,12 +3405,17 @@ __device__ __forceinline__ void fast_back_subst(const double *H, const SolveLds 
         if (i < n) y[h] = H[i * ld + i] != 0 ? y[h] / H[i * ld + i] : 0.0;
     }
     constexpr int kSubAhead = 4;
-    for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
-        double f[kSubAhead][kH];
+    // the L columns of a block of kSubAhead steps, loaded one block ahead (H is read-only here)
+    double f[kSubAhead][kH], fn[kSubAhead][kH];
+    auto ldf = [&](int j0, double (&F)[kSubAhead][kH]) {
 #pragma unroll
         for (int u = 0; u < kSubAhead; u++)
 #pragma unroll
-            for (int h = 0; h < kH; h++) f[u][h] = H[max(j0 - u, 0) * ld + ri[h]];
+            for (int h = 0; h < kH; h++) F[u][h] = H[max(j0 - u, 0) * ld + ri[h]];
+    };
+    ldf(n - 1, f);
+    for (int j0 = n - 1; j0 >= 0; j0 -= kSubAhead) {
+        ldf(max(j0 - kSubAhead, 0), fn);
 #pragma unroll
         for (int u = 0; u < kSubAhead; u++) {
             const int j = j0 - u;
@@ -3405,6 +3427,10 @@ __device__ __forceinline__ void fast_back_subst(const double *H, const SolveLds 
                 if (i < j) y[h] = fma(-f[u][h], yj, y[h]);
             }
         }
+#pragma unroll
+        for (int u = 0; u < kSubAhead; u++)
+#pragma unroll
+            for (int h = 0; h < kH; h++) f[u][h] = fn[u][h];
     }
 #pragma unroll
     for (int h = 0; h < kH; h++) {
