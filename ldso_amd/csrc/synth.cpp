@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "synth.h"
@@ -108,6 +109,55 @@ Texture make_texture(Rng &rng) {
     return T;
 }
 
+// The forward-travel scene (motion 1): a street canyon in keyframe 0's camera frame (y down) --
+// road Y = +cam_h, walls X = -wl and X = +wr, a far facade Z = z_far -- so depths range from a few
+// metres (the walls beside the car) to z_far, and the forward travel changes scales by up to ~2x.
+// Its texture is hashed value noise of four octaves (periods 1.6 m .. 0.1 m) evaluated at the hit
+// point's two in-plane coordinates: unbounded, with no texel grid to outgrow.
+struct Street {
+    uint64_t seed;
+    double cam_h, wl, wr, z_far;
+    static double lattice(uint64_t seed, int plane, int oct, long long ix, long long iy) {
+        uint64_t z = seed ^ ((uint64_t)plane * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)oct * 0xC2B2AE3D27D4EB4Full) ^
+                     ((uint64_t)ix * 0x165667B19E3779F9ull) ^ ((uint64_t)iy * 0x27D4EB2F165667C5ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        return (z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+    }
+    double texture(int plane, double a, double b) const {
+        static const double period[4] = {1.6, 0.6, 0.25, 0.1}, amp[4] = {50, 35, 25, 15};
+        double v = 128.0 + 12.0 * (plane - 1.5);
+        for (int o = 0; o < 4; o++) {
+            const double fa = a / period[o], fb = b / period[o];
+            const double ia = std::floor(fa), ib = std::floor(fb), da = fa - ia, db = fb - ib;
+            const long long x = (long long)ia, y = (long long)ib;
+            v += amp[o] * ((1 - da) * (1 - db) * lattice(seed, plane, o, x, y) + da * (1 - db) * lattice(seed, plane, o, x + 1, y) +
+                           (1 - da) * db * lattice(seed, plane, o, x, y + 1) + da * db * lattice(seed, plane, o, x + 1, y + 1));
+        }
+        return v;
+    }
+    // nearest hit of the ray C + s d (s > 0): the depth s and the hit's brightness
+    double hit(const double C[3], const double d[3], double *I) const {
+        double best = 1e300;
+        int plane = -1;
+        auto test = [&](int k, double num, double den) {
+            if (std::fabs(den) < 1e-12) return;
+            const double s = num / den;
+            if (s > 1e-6 && s < best) best = s, plane = k;
+        };
+        test(0, cam_h - C[1], d[1]);   // road
+        test(1, -wl - C[0], d[0]);     // left wall
+        test(2, wr - C[0], d[0]);      // right wall
+        test(3, z_far - C[2], d[2]);   // far facade
+        if (I) {
+            const double X = C[0] + best * d[0], Y = C[1] + best * d[1], Z = C[2] + best * d[2];
+            *I = plane == 0 ? texture(0, X, Z) : plane == 3 ? texture(3, X, Y) : texture(plane, Z, Y);
+        }
+        return best;
+    }
+};
+
 // getInterpolatedElement33BiLin: include/internal/GlobalFuncs.h:185-207
 void interp33bilin(const float *mat, float x, float y, int width, float out[3]) {
     int ix = (int)x;
@@ -138,19 +188,52 @@ int ldso_synth_fill(const ldso_synth_params *prm, ldso_ba_frame_state *frames, f
                     float *res_energy, uint8_t *res_flags) {
     const int N = prm->n_frames, P = prm->n_points, w = prm->width, h = prm->height;
     if (N < 2 || N > LDSO_BA_MAX_FRAMES || P < 0 || w < 32 || h < 32) return -1;
+    if (prm->motion < 0 || prm->motion > 1) return -1;
+    const bool forward = prm->motion == 1;
+    if (forward && !(prm->plane_depth > 0 && prm->fwd_min >= 0 && prm->fwd_max >= prm->fwd_min &&
+                     prm->fwd_max * (N - 1) < 0.5 * prm->plane_depth))
+        return -1;
     Rng rng(prm->seed);
-    // EuRoC output intrinsics (examples/EUROC/EUROC.txt: 0.6 0.9 0.5 0.5 relative)
-    const double fx = 0.6 * w, fy = 0.9 * h, cx = 0.5 * w - 0.5, cy = 0.5 * h - 0.5;
+    // default: EuRoC output intrinsics (examples/EUROC/EUROC.txt: 0.6 0.9 0.5 0.5 relative); or the
+    // caller's pinhole (e.g. KITTI's cropped output model, ldso_amd/synth.py kitti_crop_calib)
+    const bool own_k = prm->fx > 0;
+    const double fx = own_k ? prm->fx : 0.6 * w, fy = own_k ? prm->fy : 0.9 * h;
+    const double cx = own_k ? prm->cx : 0.5 * w - 0.5, cy = own_k ? prm->cy : 0.5 * h - 0.5;
     calib[0] = (float)fx;
     calib[1] = (float)fy;
     calib[2] = (float)cx;
     calib[3] = (float)cy;
     // plane Z = Z0 + gx X + gy Y (world = first keyframe's camera)
-    const double Z0 = rng.uni(1.8, 2.4), gxp = rng.uni(-0.2, 0.2), gyp = rng.uni(-0.2, 0.2);
-    Texture tex = make_texture(rng);
+    const double Z0 = forward ? 0.0 : rng.uni(1.8, 2.4);
+    const double gxp = forward ? 0.0 : rng.uni(-0.2, 0.2), gyp = forward ? 0.0 : rng.uni(-0.2, 0.2);
+    Street street{};
+    Texture tex;
+    if (forward) {
+        street.seed = rng.next();
+        street.cam_h = rng.uni(1.5, 1.8);
+        street.wl = rng.uni(3.0, 6.0);
+        street.wr = rng.uni(3.0, 6.0);
+        street.z_far = prm->plane_depth * rng.uni(0.95, 1.05);
+    } else {
+        tex = make_texture(rng);
+    }
     std::vector<double> Rwc((size_t)N * 9), Cw((size_t)N * 3), affa(N), affb(N);
     const double base = prm->baseline > 0 ? prm->baseline : 0.04;
+    double z_travel = 0;
     for (int f = 0; f < N; f++) {
+        if (forward) {  // a car: mostly +z, slight yaw and lateral drift
+            double om[3] = {0.002 * std::sin((double)f) + rng.uni(-0.001, 0.001), 0.004 * f + rng.uni(-0.002, 0.002),
+                            rng.uni(-0.001, 0.001)};
+            rodrigues(om, &Rwc[f * 9]);
+            if (f > 0) z_travel += rng.uni(prm->fwd_min, prm->fwd_max);
+            Cw[f * 3 + 0] = 0.05 * std::sin(0.5 * f) + rng.uni(-0.01, 0.01);
+            Cw[f * 3 + 1] = rng.uni(-0.01, 0.01);
+            Cw[f * 3 + 2] = z_travel;
+            affa[f] = rng.uni(-0.05, 0.05);
+            affb[f] = rng.uni(-5, 5);
+            if (f == 0) affa[f] = affb[f] = 0;
+            continue;
+        }
         double om[3] = {0.01 * f + rng.uni(-0.002, 0.002), 0.02 * std::sin((double)f) + rng.uni(-0.002, 0.002), 0.005 * f};
         rodrigues(om, &Rwc[f * 9]);
         Cw[f * 3 + 0] = base * f + rng.uni(-0.005, 0.005);
@@ -188,9 +271,15 @@ int ldso_synth_fill(const ldso_synth_params *prm, ldso_ba_frame_state *frames, f
                 double dc[3] = {(x - cx) / fx, (y - cy) / fy, 1.0};
                 double dw[3];
                 for (int i = 0; i < 3; i++) dw[i] = R[i * 3] * dc[0] + R[i * 3 + 1] * dc[1] + R[i * 3 + 2] * dc[2];
-                double s = (Z0 + gxp * C[0] + gyp * C[1] - C[2]) / (dw[2] - gxp * dw[0] - gyp * dw[1]);
-                double X = C[0] + s * dw[0], Y = C[1] + s * dw[1];
-                double I = ea * tex.sample(X, Y) + affb[f];
+                double I;
+                if (forward) {
+                    street.hit(C, dw, &I);
+                    I = ea * I + affb[f];
+                } else {
+                    double s = (Z0 + gxp * C[0] + gyp * C[1] - C[2]) / (dw[2] - gxp * dw[0] - gyp * dw[1]);
+                    double X = C[0] + s * dw[0], Y = C[1] + s * dw[1];
+                    I = ea * tex.sample(X, Y) + affb[f];
+                }
                 if (I < 0) I = 0;
                 if (I > 255) I = 255;
                 img[3 * ((size_t)y * w + x)] = (float)I;
@@ -212,11 +301,19 @@ int ldso_synth_fill(const ldso_synth_params *prm, ldso_ba_frame_state *frames, f
         if (hf >= N) hf = N - 1;
         point_host[p] = hf;
         double u = rng.uni(8, w - 9), v = rng.uni(8, h - 9);
+        if (prm->edge_frac > 0 && rng.uni() < prm->edge_frac) {  // a point in the border band
+            const double side = rng.uni(), off = rng.uni(4, 9);
+            if (side < 0.25) u = off;
+            else if (side < 0.5) u = w - 1 - off;
+            else if (side < 0.75) v = off;
+            else v = h - 1 - off;
+        }
         const double *R = &Rwc[hf * 9], *C = &Cw[hf * 3];
         double dc[3] = {(u - cx) / fx, (v - cy) / fy, 1.0};
         double dw[3];
         for (int i = 0; i < 3; i++) dw[i] = R[i * 3] * dc[0] + R[i * 3 + 1] * dc[1] + R[i * 3 + 2] * dc[2];
-        double s = (Z0 + gxp * C[0] + gyp * C[1] - C[2]) / (dw[2] - gxp * dw[0] - gyp * dw[1]);
+        double s = forward ? street.hit(C, dw, nullptr)
+                           : (Z0 + gxp * C[0] + gyp * C[1] - C[2]) / (dw[2] - gxp * dw[0] - gyp * dw[1]);
         double idepth = 1.0 / s;  // camera-frame depth of the ray point is s (dc.z = 1)
         if (rng.uni() < prm->outlier_frac) idepth *= rng.uni(0.5, 1.6);
         else idepth *= 1.0 + prm->idepth_noise * rng.gauss();

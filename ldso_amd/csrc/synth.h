@@ -21,6 +21,14 @@ typedef struct ldso_synth_params {
     float idepth_noise;     /* relative gaussian noise on inlier idepths             */
     float newest_perturb;   /* pose perturbation of the newest frame's state (rad/m) */
     float baseline;         /* camera travel per keyframe along x (m)                */
+    /* appended in round 6 (all zero = the round-1..5 window) */
+    int32_t motion;         /* 0: sideways (x) travel, EuRoC-style intrinsics fx = 0.6w, fy = 0.9h;
+                             * 1: forward (+z) travel of U(fwd_min, fwd_max) m per keyframe towards a
+                             *    plane plane_depth m ahead, as a KITTI car drives                   */
+    float fx, fy, cx, cy;   /* pinhole intrinsics of the output images (fx <= 0: motion's default)   */
+    float fwd_min, fwd_max; /* forward travel per keyframe (m), motion 1                              */
+    float plane_depth;      /* far facade's distance from the first keyframe (m), motion 1            */
+    float edge_frac;        /* fraction of points drawn in the 4..9-px band along the image border   */
 } ldso_synth_params;
 
 /* Fills a synthetic window.  Output sizes:

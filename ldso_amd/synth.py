@@ -26,17 +26,101 @@ class _Params(C.Structure):
         ("idepth_noise", C.c_float),
         ("newest_perturb", C.c_float),
         ("baseline", C.c_float),
+        ("motion", C.c_int32),
+        ("fx", C.c_float),
+        ("fy", C.c_float),
+        ("cx", C.c_float),
+        ("cy", C.c_float),
+        ("fwd_min", C.c_float),
+        ("fwd_max", C.c_float),
+        ("plane_depth", C.c_float),
+        ("edge_frac", C.c_float),
     ]
+
+
+def kitti_crop_calib(fx, fy, cx, cy, w_org, h_org, w, h):
+    """The output pinhole of LDSO's "crop" undistortion for a distortion-free Pinhole input:
+    Undistort::makeOptimalK_crop (src/frontend/Undistort.cc:558-668) with
+    UndistortPinhole::distortCoordinates (:1103-1125) restated in float32 (the reference computes in
+    float; the crop K is then stored as double and read back as float calibration).  Returns
+    float32 [fx, fy, cx, cy] of the w x h output images."""
+    f32 = np.float32
+    fx, fy, cx, cy = f32(fx), f32(fy), f32(cx), f32(cy)
+    w_lim, h_lim = f32(w_org - 1), f32(h_org - 1)
+
+    def distort(x, y):  # K = identity while the crop is searched: ix = x, iy = y
+        return fx * x + cx, fy * y + cy
+
+    t = (np.arange(100000, dtype=np.int64).astype(f32) - f32(50000.0)) / f32(10000.0)
+    # 1. stretch the centre lines: the first / last sample whose distorted coordinate is inside
+    dx, _ = distort(t, np.zeros_like(t))
+    inside = np.flatnonzero((dx > 0) & (dx < w_lim))
+    min_x, max_x = t[inside[0]], t[inside[-1]]
+    _, dy = distort(np.zeros_like(t), t)
+    inside = np.flatnonzero((dy > 0) & (dy < h_lim))
+    min_y, max_y = t[inside[0]], t[inside[-1]]
+    min_x, max_x, min_y, max_y = (v * f32(1.01) for v in (min_x, max_x, min_y, max_y))
+    # 2. shrink the side(s) with invalid border pixels by 0.995 until none is left
+    ys = np.arange(h).astype(f32)
+    xs = np.arange(w).astype(f32)
+    for _ in range(501):
+        ry = min_y + (max_y - min_y) * ys / (f32(h) - f32(1.0))
+        lx, _ = distort(np.full(h, min_x, f32), ry)
+        rx, _ = distort(np.full(h, max_x, f32), ry)
+        oob_l, oob_r = bool(np.any(~((lx > 0) & (lx < w_lim)))), bool(np.any(~((rx > 0) & (rx < w_lim))))
+        rxs = min_x + (max_x - min_x) * xs / (f32(w) - f32(1.0))
+        _, ty = distort(rxs, np.full(w, min_y, f32))
+        _, by = distort(rxs, np.full(w, max_y, f32))
+        oob_t, oob_b = bool(np.any(~((ty > 0) & (ty < h_lim)))), bool(np.any(~((by > 0) & (by < h_lim))))
+        if not (oob_l or oob_r or oob_t or oob_b):
+            break
+        if (oob_l or oob_r) and (oob_t or oob_b):
+            if (max_x - min_x) > (max_y - min_y):
+                oob_t = oob_b = False
+            else:
+                oob_l = oob_r = False
+        if oob_l:
+            min_x = min_x * f32(0.995)
+        if oob_r:
+            max_x = max_x * f32(0.995)
+        if oob_t:
+            min_y = min_y * f32(0.995)
+        if oob_b:
+            max_y = max_y * f32(0.995)
+    else:
+        raise ValueError("no valid crop")
+    kfx = (f32(w) - f32(1.0)) / (max_x - min_x)
+    kfy = (f32(h) - f32(1.0)) / (max_y - min_y)
+    return np.array([kfx, kfy, -np.float64(min_x) * np.float64(kfx), -np.float64(min_y) * np.float64(kfy)], np.float32)
 
 
 # configs of BASELINE.json used by tests and bench
 S7 = dict(n_frames=7, n_points=2000, width=640, height=480)
 S11 = dict(n_frames=11, n_points=8000, width=640, height=480)
+# BASELINE config 3 (KITTI 00, preset 0: 7 keyframes, 2000 points): the output geometry of
+# examples/Kitti/Kitti00-02.txt (1241 x 376 Pinhole 718.856 718.856 607.1928 185.2157, "crop" to
+# 1232 x 368) and a car's forward travel of 0.5-1 m per keyframe down a street canyon (road, two walls,
+# a facade 25 m ahead: depths from ~3 to 25 m, large
+# scale changes, many pattern pixels leaving the image).  The KITTI driver fixes both affine modes to 0
+# (run_dso_kitti.cc:299-300).
+KITTI00_CALIB = kitti_crop_calib(718.856, 718.856, 607.1928, 185.2157, 1241, 376, 1232, 368)
+KITTI00 = dict(n_frames=7, n_points=2000, width=1232, height=368, calib=KITTI00_CALIB, motion="forward")
+# KITTI 03's raw frame (examples/Kitti/Kitti03.txt: 1242 x 375, Pinhole 721.5377 721.5377 609.5593
+# 172.854) without the crop: a width that is not a multiple of 8 and a height not a multiple of 4.
+KITTI03_RAW = dict(n_frames=7, n_points=2000, width=1242, height=375,
+                   calib=np.array([721.5377, 721.5377, 609.5593, 172.854], np.float32), motion="forward")
 
 
 def make_window(n_frames=7, n_points=2000, width=640, height=480, seed=0, outlier_frac=0.05, idepth_noise=0.01,
-                newest_perturb=1e-3, baseline=0.04, finalize=True) -> Window:
+                newest_perturb=1e-3, baseline=0.04, finalize=True, calib=None, motion="sideways",
+                fwd_step=(0.5, 1.0), plane_depth=25.0, edge_frac=0.0) -> Window:
+    """calib: pinhole [fx, fy, cx, cy] of the output images (None: EuRoC-style 0.6w, 0.9h);
+    motion: "sideways" (x travel of `baseline` per keyframe, the round-1 window) or "forward"
+    (+z travel of U(fwd_step) m per keyframe down a street canyon whose far facade is `plane_depth` m ahead);
+    edge_frac: the fraction of points drawn 4..9 px from the image border instead of in [8, w - 9]."""
     N, P = int(n_frames), int(n_points)
+    k = np.zeros(4, np.float32) if calib is None else np.asarray(calib, np.float32)
+    mot = {"sideways": 0, "forward": 1}[motion]
     R = P * (N - 1)
     frames = np.zeros(N, L.FRAME_STATE_DTYPE)
     dI = np.zeros((N, width * height, 3), np.float32)
@@ -49,7 +133,9 @@ def make_window(n_frames=7, n_points=2000, width=640, height=480, seed=0, outlie
     res_state = np.zeros(R, np.int8)
     res_energy = np.zeros(R, np.float32)
     res_flags = np.zeros(R, np.uint8)
-    prm = _Params(N, P, width, height, int(seed), outlier_frac, idepth_noise, newest_perturb, baseline)
+    prm = _Params(N, P, width, height, int(seed), outlier_frac, idepth_noise, newest_perturb, baseline, mot,
+                  float(k[0]), float(k[1]), float(k[2]), float(k[3]), float(fwd_step[0]), float(fwd_step[1]),
+                  float(plane_depth), float(edge_frac))
     rc = L.synth_lib().ldso_synth_fill(
         C.byref(prm), frames.ctypes.data, L.ptr(dI, L.f32p), L.ptr(calib, L.f32p), L.ptr(fth, L.f32p),
         L.ptr(point_host, L.i32p), L.ptr(point_data, L.f32p), L.ptr(begin, L.i32p), L.ptr(res_target, L.i32p),

@@ -71,7 +71,7 @@ def pc_tuple(pc):
 # ------------------------------------------------------------------------------------------
 # CPU: the oracle against independent known answers
 # ------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("wh", [(640, 480), (752, 480), (320, 240)])
+@pytest.mark.parametrize("wh", [(640, 480), (752, 480), (320, 240), (1232, 368)])
 def test_oracle_make_images_known_answer(built, wh):
     w, h = wh
     color, _ = synth.make_tracker_scene(w, h, seed=3)
@@ -89,6 +89,8 @@ def test_oracle_make_images_known_answer(built, wh):
 def test_levels_and_k_follow_global_calib():
     assert oracle.ct_levels(640, 480) == 4  # pyrLevelsUsed for 640x480 (GlobalCalib.cc:20-30)
     assert oracle.ct_levels(752, 480) == 5
+    assert oracle.ct_levels(1232, 368) == 5  # KITTI's cropped output: 77 x 23 is odd at level 4
+    assert oracle.ct_levels(1242, 375) == 1  # an odd height never halves
     K = oracle.ct_make_k(CALIB_640, 640, 480)
     for l in range(4):
         fx, fy, cx, cy = K[l, :4]
@@ -188,7 +190,7 @@ def _tracker(w, h, color, pcs, calib, B=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wh", [(640, 480), (752, 480)])
+@pytest.mark.parametrize("wh", [(640, 480), (752, 480), (1232, 368)])
 @pytest.mark.parametrize("with_b", [False, True])
 def test_gpu_make_images_bit_exact(built, wh, with_b):
     from ldso_amd.tracker import CoarseTracker
@@ -210,9 +212,9 @@ def test_gpu_make_images_bit_exact(built, wh, with_b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [0, 1])
-def test_gpu_calc_res_and_gs_match_oracle(built, seed):
-    w, h = 640, 480
+@pytest.mark.parametrize("seed,wh", [(0, (640, 480)), (1, (640, 480)), (2, (1232, 368))])
+def test_gpu_calc_res_and_gs_match_oracle(built, seed, wh):
+    w, h = wh
     color, levels, pcs, calib, K = scene(w, h, seed)
     ct = _tracker(w, h, color, pcs, calib)
     for l in range(len(levels)):
