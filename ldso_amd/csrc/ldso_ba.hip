@@ -3968,7 +3968,7 @@ struct FrameStepParams {
 };
 // one window's step: a whole 256-thread block (blk = the window)
 __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int blk) {
-    __shared__ double poses[LDSO_BA_MAX_FRAMES][4][12];  // ev, ev^-1, cur, cur^-1: R (9), t (3)
+    __shared__ double poses[LDSO_BA_MAX_FRAMES][4][7];  // ev, ev^-1, cur, cur^-1: quaternion (4), t (3)
     __shared__ float calib[4];
     // the stop flag and the window's descriptor in one round trip, then the exit
     const int stop_it = P.stop ? P.stop[blk] : INT_MAX;
@@ -3989,8 +3989,8 @@ __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int b
         const Pose e = eval_pose(o), c = current_pose(o);
         const Pose ps[4] = {e, e.inverse(), c, c.inverse()};
         for (int q = 0; q < 4; q++) {
-            for (int k = 0; k < 9; k++) poses[tid][q][k] = ps[q].R.m[k];
-            for (int k = 0; k < 3; k++) poses[tid][q][9 + k] = ps[q].t[k];
+            for (int k = 0; k < 4; k++) poses[tid][q][k] = ps[q].q[k];
+            for (int k = 0; k < 3; k++) poses[tid][q][4 + k] = ps[q].t[k];
         }
     } else if (tid == 64) {
         double *v = P.calib_val + 4 * blk;
@@ -4009,8 +4009,8 @@ __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int b
     __syncthreads();
     auto pose = [&](int f, int q) {
         Pose p;
-        for (int k = 0; k < 9; k++) p.R.m[k] = poses[f][q][k];
-        for (int k = 0; k < 3; k++) p.t[k] = poses[f][q][9 + k];
+        for (int k = 0; k < 4; k++) p.q[k] = poses[f][q][k];
+        for (int k = 0; k < 3; k++) p.t[k] = poses[f][q][4 + k];
         return p;
     };
     for (int e = tid; e < N * N; e += blockDim.x) {

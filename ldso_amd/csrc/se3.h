@@ -1,10 +1,20 @@
 // se3.h -- the double-precision SE(3) and FrameFramePrecalc arithmetic of the path, shared by the
-// host helpers (host_math.cpp) and the device GN loop (ldso_ba.hip k_step_resub), statement for
-// statement, FP contraction off: Sophus SE3 exp / log / product / inverse / Adj
-// (thirdparty/Sophus/sophus/se3.hpp, so3.hpp), FrameHessian::setState's PRE_worldToCam
-// (FrameHessian.h:95-114), AffLight::fromToVecExposure (AffLight.h:27-35), the per-pair body of
-// FrameFramePrecalc::Set (FrameFramePrecalc.cc:6-35) and FrameHessian::takeData
-// (FrameHessian.cc:131-135, FrameHessian.h:59-70, 142-174).
+// host helpers (host_math.cpp) and the device GN loop (ldso_ba.hip k_step_resub), FP contraction
+// off.  Pose restates Sophus's SE3 (thirdparty/Sophus/sophus/se3.hpp, so3.hpp) in its own
+// representation -- a unit quaternion (Eigen coeffs() order x, y, z, w) and a translation -- with
+// Sophus's operations statement for statement: SO3::expAndTheta (half-angle factors,
+// so3.hpp:577-605), SE3::exp (se3.hpp:765-786), the quaternion product followed by SO3's
+// normalising constructor (so3.hpp:320-326, 475-481, 289-295), the quaternion point action
+// (so3.hpp:341-347), inverse (se3.hpp:205-208), SO3::logAndTheta + SE3::log (so3.hpp:239-283,
+// se3.hpp:220-253), rotationMatrix() (Eigen's Quaternion::toRotationMatrix) and Adj (se3.hpp:100-108).
+// Eigen's fixed-size reductions are written in the order its SSE/AVX packet code sums them (the
+// quaternion norm as (x^2 + z^2) + (y^2 + w^2)); where the reference build fuses a multiply-add
+// through Eigen's pmadd the result differs by an ulp.  The ABI hands worldToCam_evalPT over as
+// matrix3x4(); it becomes a quaternion again through Eigen's Quaternion(Matrix3) as SE3(R, t) does.
+// Also here: FrameHessian::setState's PRE_worldToCam (FrameHessian.h:95-114),
+// AffLight::fromToVecExposure (AffLight.h:27-35), the per-pair body of FrameFramePrecalc::Set
+// (FrameFramePrecalc.cc:6-35) and FrameHessian::takeData (FrameHessian.cc:131-135, FrameHessian.h:
+// 59-70, 142-174).
 #pragma once
 #include <math.h>
 
@@ -13,6 +23,7 @@
 namespace ldso_ba {
 
 constexpr double kScaleXiTrans = 0.5, kScaleXiRot = 1.0, kScaleA = 10.0, kScaleB = 1000.0;
+constexpr double kSophusEps = 1e-10;  // Sophus::Constants<double>::epsilon() (common.hpp:144)
 
 struct Mat3 {
     double m[9];
@@ -24,14 +35,15 @@ struct Mat3 {
         return a;
     }
 };
+// Eigen's 3x3 lazy product: each entry summed over k = 0, 1, 2 in order
 LDSO_HD inline Mat3 operator*(const Mat3 &a, const Mat3 &b) {
 #pragma clang fp contract(off)
-    Mat3 c{};
+    Mat3 c;
     for (int r = 0; r < 3; r++)
-        for (int k = 0; k < 3; k++)
-            for (int q = 0; q < 3; q++) c(r, q) += a(r, k) * b(k, q);
+        for (int q = 0; q < 3; q++) c(r, q) = (a(r, 0) * b(0, q) + a(r, 1) * b(1, q)) + a(r, 2) * b(2, q);
     return c;
 }
+// SO3::hat (so3.hpp)
 LDSO_HD inline Mat3 skew(const double v[3]) {
     Mat3 s{};
     s(0, 1) = -v[2];
@@ -42,105 +54,189 @@ LDSO_HD inline Mat3 skew(const double v[3]) {
     s(2, 1) = v[0];
     return s;
 }
+// matrix * vector (Eigen: per row, k = 0, 1, 2 in order)
+LDSO_HD inline void mat_vec(const Mat3 &a, const double v[3], double out[3]) {
+#pragma clang fp contract(off)
+    for (int i = 0; i < 3; i++) out[i] = (a(i, 0) * v[0] + a(i, 1) * v[1]) + a(i, 2) * v[2];
+}
+// Eigen's cross (OrthoMethods.h, the scalar path for double)
+LDSO_HD inline void cross3(const double a[3], const double b[3], double out[3]) {
+#pragma clang fp contract(off)
+    out[0] = a[1] * b[2] - a[2] * b[1];
+    out[1] = a[2] * b[0] - a[0] * b[2];
+    out[2] = a[0] * b[1] - a[1] * b[0];
+}
 
-struct Pose {  // rigid transform x -> R x + t (Sophus SE3 convention)
-    Mat3 R;
+struct Pose {  // Sophus SE3: x -> R(q) x + t
+    double q[4];  // unit quaternion, Eigen coeffs() order: x, y, z, w
     double t[3];
     LDSO_HD static Pose identity() {
         Pose p;
-        p.R = Mat3::eye();
+        p.q[0] = p.q[1] = p.q[2] = 0;
+        p.q[3] = 1;
         p.t[0] = p.t[1] = p.t[2] = 0;
         return p;
     }
+    // SO3Base::normalize (so3.hpp:289-295): coeffs() /= coeffs().norm()
+    LDSO_HD void normalize() {
+#pragma clang fp contract(off)
+        const double len = sqrt((q[0] * q[0] + q[2] * q[2]) + (q[1] * q[1] + q[3] * q[3]));
+        for (int i = 0; i < 4; i++) q[i] = q[i] / len;
+    }
+    // SO3 point action (so3.hpp:341-347): uv = vec x p; uv += uv; p + w uv + vec x uv
+    LDSO_HD void rotate(const double p[3], double out[3]) const {
+#pragma clang fp contract(off)
+        double uv[3], c[3];
+        cross3(q, p, uv);
+        for (int i = 0; i < 3; i++) uv[i] = uv[i] + uv[i];
+        cross3(q, uv, c);
+        for (int i = 0; i < 3; i++) out[i] = (p[i] + q[3] * uv[i]) + c[i];
+    }
+    // SE3 product (se3.hpp:305-309): SO3 product (quaternion product, so3.hpp:320-326, then the
+    // normalising SO3(quaternion) constructor) and translation() + so3() * other.translation()
     LDSO_HD Pose operator*(const Pose &b) const {
 #pragma clang fp contract(off)
+        const double ax = q[0], ay = q[1], az = q[2], aw = q[3];
+        const double bx = b.q[0], by = b.q[1], bz = b.q[2], bw = b.q[3];
         Pose c;
-        c.R = R * b.R;
-        for (int i = 0; i < 3; i++) c.t[i] = R(i, 0) * b.t[0] + R(i, 1) * b.t[1] + R(i, 2) * b.t[2] + t[i];
+        c.q[3] = ((aw * bw - ax * bx) - ay * by) - az * bz;
+        c.q[0] = ((aw * bx + ax * bw) + ay * bz) - az * by;
+        c.q[1] = ((aw * by + ay * bw) + az * bx) - ax * bz;
+        c.q[2] = ((aw * bz + az * bw) + ax * by) - ay * bx;
+        c.normalize();
+        double r[3];
+        rotate(b.t, r);
+        for (int i = 0; i < 3; i++) c.t[i] = t[i] + r[i];
         return c;
     }
+    // SE3::inverse (se3.hpp:205-208): SO3(conjugate) (normalised) and invR * (t * -1)
     LDSO_HD Pose inverse() const {
 #pragma clang fp contract(off)
         Pose c;
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) c.R(i, j) = R(j, i);
-        for (int i = 0; i < 3; i++) c.t[i] = -(c.R(i, 0) * t[0] + c.R(i, 1) * t[1] + c.R(i, 2) * t[2]);
+        c.q[0] = -q[0];
+        c.q[1] = -q[1];
+        c.q[2] = -q[2];
+        c.q[3] = q[3];
+        c.normalize();
+        const double mt[3] = {t[0] * -1.0, t[1] * -1.0, t[2] * -1.0};
+        c.rotate(mt, c.t);
         return c;
     }
-    // exp of the tangent [upsilon(3), omega(3)] (thirdparty/Sophus/sophus/se3.hpp)
-    LDSO_HD static Pose exp(const double xi[6]) {
+    // Eigen's Quaternion::toRotationMatrix (SO3::matrix(), so3.hpp:302-304)
+    LDSO_HD Mat3 rotation_matrix() const {
 #pragma clang fp contract(off)
-        const double *w = xi + 3;
-        double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2], th = sqrt(th2);
-        double a, b, c;
-        if (th < 1e-10) {
-            a = 1 - th2 / 6;
-            b = 0.5 - th2 / 24;
-            c = 1.0 / 6 - th2 / 120;
-        } else {
-            a = sin(th) / th;
-            b = (1 - cos(th)) / th2;
-            c = (th - sin(th)) / (th2 * th);
-        }
-        Mat3 W = skew(w), W2 = W * W, I = Mat3::eye();
-        Pose p;
-        Mat3 V;
-        for (int k = 0; k < 9; k++) {
-            p.R.m[k] = I.m[k] + a * W.m[k] + b * W2.m[k];
-            V.m[k] = I.m[k] + b * W.m[k] + c * W2.m[k];
-        }
-        for (int i = 0; i < 3; i++) p.t[i] = V(i, 0) * xi[0] + V(i, 1) * xi[1] + V(i, 2) * xi[2];
-        return p;
+        const double x = q[0], y = q[1], z = q[2], w = q[3];
+        const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+        const double twx = tx * w, twy = ty * w, twz = tz * w;
+        const double txx = tx * x, txy = ty * x, txz = tz * x;
+        const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+        Mat3 R;
+        R(0, 0) = 1.0 - (tyy + tzz);
+        R(0, 1) = txy - twz;
+        R(0, 2) = txz + twy;
+        R(1, 0) = txy + twz;
+        R(1, 1) = 1.0 - (txx + tzz);
+        R(1, 2) = tyz - twx;
+        R(2, 0) = txz - twy;
+        R(2, 1) = tyz + twx;
+        R(2, 2) = 1.0 - (txx + tyy);
+        return R;
     }
-    // Sophus SE3::log (se3.hpp:220-253) on the rotation matrix: Eigen's matrix -> quaternion
-    // (Quaternion.h, quaternionbase_assign_impl), SO3::logAndTheta's atan form (so3.hpp:239-283),
-    // and V^-1 with the half-angle factor; epsilon 1e-10 (common.hpp:144).  Stable for every
-    // angle (no 1 - cos(theta) cancellation).
-    LDSO_HD void log(double xi[6]) const {
+    // SE3(Matrix3 R, t): SO3(R) = Eigen's Quaternion(Matrix3) (quaternionbase_assign_impl; not
+    // normalised by Sophus, which only asserts orthogonality)
+    LDSO_HD static Pose from_matrix(const double R[9], const double tr[3]) {
 #pragma clang fp contract(off)
-        double q[4];  // x, y, z, w
-        double tr = R(0, 0) + R(1, 1) + R(2, 2);
-        if (tr > 0) {
-            double t = sqrt(tr + 1.0);
-            q[3] = 0.5 * t;
-            t = 0.5 / t;
-            q[0] = (R(2, 1) - R(1, 2)) * t;
-            q[1] = (R(0, 2) - R(2, 0)) * t;
-            q[2] = (R(1, 0) - R(0, 1)) * t;
+        Pose p;
+        double tt = (R[0] + R[4]) + R[8];
+        if (tt > 0) {
+            tt = sqrt(tt + 1.0);
+            p.q[3] = 0.5 * tt;
+            tt = 0.5 / tt;
+            p.q[0] = (R[7] - R[5]) * tt;
+            p.q[1] = (R[2] - R[6]) * tt;
+            p.q[2] = (R[3] - R[1]) * tt;
         } else {
             int i = 0;
-            if (R(1, 1) > R(0, 0)) i = 1;
-            if (R(2, 2) > R(i, i)) i = 2;
+            if (R[4] > R[0]) i = 1;
+            if (R[8] > R[i * 4]) i = 2;
             const int j = (i + 1) % 3, k = (j + 1) % 3;
-            double t = sqrt(R(i, i) - R(j, j) - R(k, k) + 1.0);
-            q[i] = 0.5 * t;
-            t = 0.5 / t;
-            q[3] = (R(k, j) - R(j, k)) * t;
-            q[j] = (R(j, i) + R(i, j)) * t;
-            q[k] = (R(k, i) + R(i, k)) * t;
+            tt = sqrt(((R[i * 4] - R[j * 4]) - R[k * 4]) + 1.0);
+            p.q[i] = 0.5 * tt;
+            tt = 0.5 / tt;
+            p.q[3] = (R[k * 3 + j] - R[j * 3 + k]) * tt;
+            p.q[j] = (R[j * 3 + i] + R[i * 3 + j]) * tt;
+            p.q[k] = (R[k * 3 + i] + R[i * 3 + k]) * tt;
         }
-        const double n2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2], n = sqrt(n2), w = q[3];
-        double f;
-        if (n < 1e-10) f = 2.0 / w - 2.0 * n2 / (w * (w * w));
-        else if (fabs(w) < 1e-10) f = (w > 0 ? M_PI : -M_PI) / n;
-        else f = 2.0 * atan(n / w) / n;
-        const double th = f * n;
-        const double om[3] = {f * q[0], f * q[1], f * q[2]};
-        Mat3 W = skew(om), W2 = W * W;
-        const double d = fabs(th) < 1e-10 ? 1.0 / 12.0
-                                               : (1.0 - th * cos(0.5 * th) / (2.0 * sin(0.5 * th))) / (th * th);
-        for (int i = 0; i < 3; i++) {
-            double s = 0;
-            for (int k = 0; k < 3; k++) s += ((i == k ? 1.0 : 0.0) - 0.5 * W(i, k) + d * W2(i, k)) * t[k];
-            xi[i] = s;
-            xi[3 + i] = om[i];
-        }
+        for (int i = 0; i < 3; i++) p.t[i] = tr[i];
+        return p;
     }
-    // Adj = [R, [t]x R; 0, R]
+    // SE3::exp (se3.hpp:765-786) of the tangent [upsilon(3), omega(3)], with SO3::expAndTheta
+    // (so3.hpp:577-605): the quaternion from the half-angle factors, not normalised
+    LDSO_HD static Pose exp(const double a[6]) {
+#pragma clang fp contract(off)
+        const double *w = a + 3;
+        const double theta_sq = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+        const double theta = sqrt(theta_sq);
+        const double half_theta = 0.5 * theta;
+        double imag, real;
+        if (theta < kSophusEps) {
+            const double theta_po4 = theta_sq * theta_sq;
+            imag = (0.5 - (1.0 / 48.0) * theta_sq) + (1.0 / 3840.0) * theta_po4;
+            real = (1.0 - (1.0 / 8.0) * theta_sq) + (1.0 / 384.0) * theta_po4;
+        } else {
+            imag = sin(half_theta) / theta;
+            real = cos(half_theta);
+        }
+        Pose p;
+        p.q[0] = imag * w[0];
+        p.q[1] = imag * w[1];
+        p.q[2] = imag * w[2];
+        p.q[3] = real;
+        const Mat3 W = skew(w), W2 = W * W;
+        Mat3 V;
+        if (theta < kSophusEps) {
+            V = p.rotation_matrix();
+        } else {
+            const double s1 = (1.0 - cos(theta)) / theta_sq, s2 = (theta - sin(theta)) / (theta_sq * theta);
+            for (int k = 0; k < 9; k++) V.m[k] = ((k % 4 == 0 ? 1.0 : 0.0) + s1 * W.m[k]) + s2 * W2.m[k];
+        }
+        mat_vec(V, a, p.t);
+        return p;
+    }
+    // SE3::log (se3.hpp:220-253) with SO3::logAndTheta's atan form (so3.hpp:239-283)
+    LDSO_HD void log(double xi[6]) const {
+#pragma clang fp contract(off)
+        const double squared_n = (q[0] * q[0] + q[1] * q[1]) + q[2] * q[2];
+        const double n = sqrt(squared_n), w = q[3];
+        double f;  // two_atan_nbyw_by_n
+        if (n < kSophusEps) {
+            const double squared_w = w * w;
+            f = 2.0 / w - (2.0 * squared_n) / (w * squared_w);
+        } else if (fabs(w) < kSophusEps) {
+            f = w > 0 ? M_PI / n : -M_PI / n;
+        } else {
+            f = (2.0 * atan(n / w)) / n;
+        }
+        const double theta = f * n;
+        const double om[3] = {f * q[0], f * q[1], f * q[2]};
+        const Mat3 W = skew(om), W2 = W * W;
+        Mat3 Vi;
+        if (fabs(theta) < kSophusEps) {
+            for (int k = 0; k < 9; k++) Vi.m[k] = ((k % 4 == 0 ? 1.0 : 0.0) - 0.5 * W.m[k]) + (1. / 12.) * W2.m[k];
+        } else {
+            const double half_theta = 0.5 * theta;
+            const double c = (1.0 - (theta * cos(half_theta)) / (2.0 * sin(half_theta))) / (theta * theta);
+            for (int k = 0; k < 9; k++) Vi.m[k] = ((k % 4 == 0 ? 1.0 : 0.0) - 0.5 * W.m[k]) + c * W2.m[k];
+        }
+        mat_vec(Vi, t, xi);
+        for (int i = 0; i < 3; i++) xi[3 + i] = om[i];
+    }
+    // SE3::Adj (se3.hpp:100-108) = [R, hat(t) R; 0, R], R = so3().matrix()
     LDSO_HD void adjoint(double A[36]) const {
 #pragma clang fp contract(off)
         for (int k = 0; k < 36; k++) A[k] = 0;
-        Mat3 tR = skew(t) * R;
+        const Mat3 R = rotation_matrix();
+        const Mat3 tR = skew(t) * R;
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
                 A[i * 6 + j] = R(i, j);
@@ -151,10 +247,7 @@ struct Pose {  // rigid transform x -> R x + t (Sophus SE3 convention)
 };
 
 LDSO_HD inline Pose eval_pose(const ldso_ba_frame_state &f) {
-    Pose p;
-    for (int k = 0; k < 9; k++) p.R.m[k] = f.world_to_cam_evalpt[k];
-    for (int k = 0; k < 3; k++) p.t[k] = f.world_to_cam_evalpt[9 + k];
-    return p;
+    return Pose::from_matrix(f.world_to_cam_evalpt, f.world_to_cam_evalpt + 9);
 }
 // FrameHessian::setState (FrameHessian.h:95-114): PRE_worldToCam = exp(state_scaled[0:6]) * evalPT
 LDSO_HD inline Pose current_pose(const ldso_ba_frame_state &f) {
@@ -188,10 +281,11 @@ LDSO_HD inline void pair_precalc(const Pose &ev_t, const Pose &evInvH, const Pos
     for (int k = 0; k < LDSO_BA_PRECALC_STRIDE; k++) o[k] = 0.f;
     const Pose l0 = ev_t * evInvH;   // leftToLeft_0
     const Pose l = cur_t * curInvH;  // leftToLeft
+    const Mat3 R0d = l0.rotation_matrix(), Rd = l.rotation_matrix();
     float R[9], tt[3];
     for (int k = 0; k < 9; k++) {
-        o[12 + k] = (float)l0.R.m[k];        // PRE_RTll_0
-        o[27 + k] = R[k] = (float)l.R.m[k];  // PRE_RTll
+        o[12 + k] = (float)R0d.m[k];        // PRE_RTll_0
+        o[27 + k] = R[k] = (float)Rd.m[k];  // PRE_RTll
     }
     for (int k = 0; k < 3; k++) {
         o[21 + k] = (float)l0.t[k];          // PRE_tTll_0

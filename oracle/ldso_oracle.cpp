@@ -1233,8 +1233,11 @@ void applyResAll(oracle_window *ow) {
 }
 
 // ---- dense double helpers (host side) -------------------------------------------------
+// Sophus SE3 (thirdparty/Sophus/sophus/se3.hpp, so3.hpp) as Sophus stores it: a unit quaternion
+// (Eigen coeffs() order x, y, z, w) and a translation.  Every operation below restates Sophus's
+// code in its statement order (Eigen's fixed-size sums as its packet code adds them; no FMA).
 struct SE3d {
-    double R[9];
+    double q[4];  // x, y, z, w
     double t[3];
 };
 void hat(const double w[3], double M[9]) {
@@ -1246,40 +1249,134 @@ void mm3(const double *A, const double *B, double *C) {
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) C[i * 3 + j] = A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
 }
-// Sophus::SE3::exp (thirdparty/Sophus/sophus/se3.hpp), tangent = [upsilon, omega]
+void mv3(const double *A, const double *v, double *out) {
+    for (int i = 0; i < 3; i++) out[i] = A[i * 3] * v[0] + A[i * 3 + 1] * v[1] + A[i * 3 + 2] * v[2];
+}
+// SO3Base::normalize (so3.hpp:289-295): Eigen's 4-vector norm sums (x^2 + z^2) + (y^2 + w^2)
+void quat_normalize(double q[4]) {
+    const double len = std::sqrt((q[0] * q[0] + q[2] * q[2]) + (q[1] * q[1] + q[3] * q[3]));
+    for (int i = 0; i < 4; i++) q[i] /= len;
+}
+// Eigen Quaternion::toRotationMatrix (SO3::matrix, so3.hpp:302-304)
+void quat_matrix(const double q[4], double R[9]) {
+    const double tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const double txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const double tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+// the SO3 action on a point (so3.hpp:341-347)
+void quat_rotate(const double q[4], const double p[3], double out[3]) {
+    double uv[3] = {q[1] * p[2] - q[2] * p[1], q[2] * p[0] - q[0] * p[2], q[0] * p[1] - q[1] * p[0]};
+    for (int i = 0; i < 3; i++) uv[i] += uv[i];
+    const double c[3] = {q[1] * uv[2] - q[2] * uv[1], q[2] * uv[0] - q[0] * uv[2], q[0] * uv[1] - q[1] * uv[0]};
+    for (int i = 0; i < 3; i++) out[i] = p[i] + q[3] * uv[i] + c[i];
+}
+// Sophus::SE3::exp (se3.hpp:765-786), tangent = [upsilon, omega], through SO3::expAndTheta
+// (so3.hpp:577-605: imaginary factor sin(theta / 2) / theta, real factor cos(theta / 2))
 SE3d se3_exp(const double a[6]) {
     const double *up = a, *w = a + 3;
-    double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    double th = std::sqrt(th2);
-    double W[9], W2[9];
-    hat(w, W);
-    mm3(W, W, W2);
-    double A, B, C;
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    const double th = std::sqrt(th2);
+    double im, re;
     if (th < 1e-10) {
-        A = 1.0 - th2 / 6.0;
-        B = 0.5 - th2 / 24.0;
-        C = 1.0 / 6.0 - th2 / 120.0;
+        const double th4 = th2 * th2;
+        im = 0.5 - (1.0 / 48.0) * th2 + (1.0 / 3840.0) * th4;
+        re = 1 - (1.0 / 8.0) * th2 + (1.0 / 384.0) * th4;
     } else {
-        A = std::sin(th) / th;
-        B = (1 - std::cos(th)) / th2;
-        C = (th - std::sin(th)) / (th2 * th);
+        im = std::sin(0.5 * th) / th;
+        re = std::cos(0.5 * th);
     }
     SE3d T;
+    T.q[0] = im * w[0];
+    T.q[1] = im * w[1];
+    T.q[2] = im * w[2];
+    T.q[3] = re;
     double V[9];
-    for (int i = 0; i < 9; i++) {
-        double I = (i % 4 == 0) ? 1.0 : 0.0;
-        T.R[i] = I + A * W[i] + B * W2[i];
-        V[i] = I + B * W[i] + C * W2[i];
+    if (th < 1e-10) {
+        quat_matrix(T.q, V);
+    } else {
+        double W[9], W2[9];
+        hat(w, W);
+        mm3(W, W, W2);
+        const double B = (1 - std::cos(th)) / th2, C = (th - std::sin(th)) / (th2 * th);
+        for (int i = 0; i < 9; i++) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + B * W[i] + C * W2[i];
     }
-    for (int i = 0; i < 3; i++) T.t[i] = V[i * 3] * up[0] + V[i * 3 + 1] * up[1] + V[i * 3 + 2] * up[2];
+    mv3(V, up, T.t);
     return T;
 }
-// Sophus::SE3::log (thirdparty/Sophus/sophus/se3.hpp:220-253): the rotation as a unit quaternion
-// (Eigen Quaternion(Matrix3), Quaternion.h quaternionbase_assign_impl), SO3::logAndTheta
-// (so3.hpp:239-283, atan form), V^-1 with theta cos(theta/2) / (2 sin(theta/2)); epsilon 1e-10
+// Sophus::SE3::log (se3.hpp:220-253): SO3::logAndTheta (so3.hpp:239-283, atan form) on the
+// quaternion, V^-1 with theta cos(theta/2) / (2 sin(theta/2)); epsilon 1e-10
 void se3_log(const SE3d &T, double out[6]) {
-    const double *R = T.R;
-    double q[4];  // x, y, z, w
+    const double *q = T.q;
+    const double squared_n = q[0] * q[0] + q[1] * q[1] + q[2] * q[2];
+    const double n = std::sqrt(squared_n), w = q[3];
+    double two_atan_nbyw_by_n;
+    if (n < 1e-10) two_atan_nbyw_by_n = 2.0 / w - 2.0 * squared_n / (w * (w * w));
+    else if (std::fabs(w) < 1e-10) two_atan_nbyw_by_n = (w > 0 ? M_PI : -M_PI) / n;
+    else two_atan_nbyw_by_n = 2.0 * std::atan(n / w) / n;
+    const double theta = two_atan_nbyw_by_n * n;
+    double w3[3] = {two_atan_nbyw_by_n * q[0], two_atan_nbyw_by_n * q[1], two_atan_nbyw_by_n * q[2]};
+    double W[9], W2[9];
+    hat(w3, W);
+    mm3(W, W, W2);
+    double D;
+    if (std::fabs(theta) < 1e-10) D = 1.0 / 12.0;
+    else D = (1.0 - theta * std::cos(0.5 * theta) / (2.0 * std::sin(0.5 * theta))) / (theta * theta);
+    double Vi[9];
+    for (int i = 0; i < 9; i++) Vi[i] = ((i % 4 == 0) ? 1.0 : 0.0) - 0.5 * W[i] + D * W2[i];
+    mv3(Vi, T.t, out);
+    for (int i = 0; i < 3; i++) out[3 + i] = w3[i];
+}
+// SE3 product (se3.hpp:305-309): the quaternion product (so3.hpp:320-326), normalised by the
+// SO3(quaternion) constructor (so3.hpp:475-481), and t_A + R_A t_B through the quaternion action
+SE3d se3_mul(const SE3d &A, const SE3d &B) {
+    const double *a = A.q, *b = B.q;
+    SE3d C;
+    C.q[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    C.q[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    C.q[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    C.q[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+    quat_normalize(C.q);
+    double r[3];
+    quat_rotate(A.q, B.t, r);
+    for (int i = 0; i < 3; i++) C.t[i] = A.t[i] + r[i];
+    return C;
+}
+// SE3::inverse (se3.hpp:205-208): SO3(conjugate) (normalised) applied to -t
+SE3d se3_inv(const SE3d &A) {
+    SE3d C;
+    C.q[0] = -A.q[0];
+    C.q[1] = -A.q[1];
+    C.q[2] = -A.q[2];
+    C.q[3] = A.q[3];
+    quat_normalize(C.q);
+    const double mt[3] = {A.t[0] * -1.0, A.t[1] * -1.0, A.t[2] * -1.0};
+    quat_rotate(C.q, mt, C.t);
+    return C;
+}
+// Sophus SE3::Adj = [R, hat(t) R; 0, R] (se3.hpp:100-108)
+void se3_adj(const SE3d &T, double Adj[36]) {
+    std::memset(Adj, 0, 36 * sizeof(double));
+    double R[9], tx[9], tR[9];
+    quat_matrix(T.q, R);
+    hat(T.t, tx);
+    mm3(tx, R, tR);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            Adj[i * 6 + j] = R[i * 3 + j];
+            Adj[i * 6 + 3 + j] = tR[i * 3 + j];
+            Adj[(3 + i) * 6 + 3 + j] = R[i * 3 + j];
+        }
+}
+// worldToCam_evalPT from the ABI's matrix3x4(): SE3(Matrix3, t) -> SO3(R) = Eigen's
+// Quaternion(Matrix3) (Quaternion.h, quaternionbase_assign_impl)
+SE3d frame_evalpt(const ldso_ba_frame_state &f) {
+    const double *R = f.world_to_cam_evalpt;
+    SE3d T;
+    double *q = T.q;
     const double tr = R[0] + R[4] + R[8];
     if (tr > 0) {
         double t = std::sqrt(tr + 1.0);
@@ -1300,54 +1397,6 @@ void se3_log(const SE3d &T, double out[6]) {
         q[j] = (R[j * 3 + i] + R[i * 3 + j]) * t;
         q[k] = (R[k * 3 + i] + R[i * 3 + k]) * t;
     }
-    const double squared_n = q[0] * q[0] + q[1] * q[1] + q[2] * q[2];
-    const double n = std::sqrt(squared_n), w = q[3];
-    double two_atan_nbyw_by_n;
-    if (n < 1e-10) two_atan_nbyw_by_n = 2.0 / w - 2.0 * squared_n / (w * (w * w));
-    else if (std::fabs(w) < 1e-10) two_atan_nbyw_by_n = (w > 0 ? M_PI : -M_PI) / n;
-    else two_atan_nbyw_by_n = 2.0 * std::atan(n / w) / n;
-    const double theta = two_atan_nbyw_by_n * n;
-    double w3[3] = {two_atan_nbyw_by_n * q[0], two_atan_nbyw_by_n * q[1], two_atan_nbyw_by_n * q[2]};
-    double W[9], W2[9];
-    hat(w3, W);
-    mm3(W, W, W2);
-    double D;
-    if (std::fabs(theta) < 1e-10) D = 1.0 / 12.0;
-    else D = (1.0 - theta * std::cos(0.5 * theta) / (2.0 * std::sin(0.5 * theta))) / (theta * theta);
-    double Vi[9];
-    for (int i = 0; i < 9; i++) Vi[i] = ((i % 4 == 0) ? 1.0 : 0.0) - 0.5 * W[i] + D * W2[i];
-    for (int i = 0; i < 3; i++) out[i] = Vi[i * 3] * T.t[0] + Vi[i * 3 + 1] * T.t[1] + Vi[i * 3 + 2] * T.t[2];
-    for (int i = 0; i < 3; i++) out[3 + i] = w3[i];
-}
-SE3d se3_mul(const SE3d &A, const SE3d &B) {
-    SE3d C;
-    mm3(A.R, B.R, C.R);
-    for (int i = 0; i < 3; i++) C.t[i] = A.R[i * 3] * B.t[0] + A.R[i * 3 + 1] * B.t[1] + A.R[i * 3 + 2] * B.t[2] + A.t[i];
-    return C;
-}
-SE3d se3_inv(const SE3d &A) {
-    SE3d C;
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) C.R[i * 3 + j] = A.R[j * 3 + i];
-    for (int i = 0; i < 3; i++) C.t[i] = -(C.R[i * 3] * A.t[0] + C.R[i * 3 + 1] * A.t[1] + C.R[i * 3 + 2] * A.t[2]);
-    return C;
-}
-// Sophus SE3::Adj = [R, hat(t) R; 0, R]
-void se3_adj(const SE3d &T, double Adj[36]) {
-    std::memset(Adj, 0, 36 * sizeof(double));
-    double tx[9], tR[9];
-    hat(T.t, tx);
-    mm3(tx, T.R, tR);
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            Adj[i * 6 + j] = T.R[i * 3 + j];
-            Adj[i * 6 + 3 + j] = tR[i * 3 + j];
-            Adj[(3 + i) * 6 + 3 + j] = T.R[i * 3 + j];
-        }
-}
-SE3d frame_evalpt(const ldso_ba_frame_state &f) {
-    SE3d T;
-    for (int i = 0; i < 9; i++) T.R[i] = f.world_to_cam_evalpt[i];
     for (int i = 0; i < 3; i++) T.t[i] = f.world_to_cam_evalpt[9 + i];
     return T;
 }
@@ -1704,10 +1753,13 @@ int oracle_frame_precalc(int N, const ldso_ba_frame_state *frames, const float c
             std::memset(o, 0, LDSO_BA_PRECALC_STRIDE * sizeof(float));
             SE3d l2l0 = se3_mul(frame_evalpt(frames[t]), se3_inv(frame_evalpt(frames[h])));
             SE3d l2l = se3_mul(frame_pre_w2c(frames[t]), se3_inv(frame_pre_w2c(frames[h])));
+            double l2l0R[9], l2lR[9];  // rotationMatrix()
+            quat_matrix(l2l0.q, l2l0R);
+            quat_matrix(l2l.q, l2lR);
             float RTll[9], tTll[3];
             for (int i = 0; i < 9; i++) {
-                o[12 + i] = (float)l2l0.R[i];          // PRE_RTll_0
-                o[27 + i] = RTll[i] = (float)l2l.R[i];  // PRE_RTll
+                o[12 + i] = (float)l2l0R[i];          // PRE_RTll_0
+                o[27 + i] = RTll[i] = (float)l2lR[i];  // PRE_RTll
             }
             for (int i = 0; i < 3; i++) {
                 o[21 + i] = (float)l2l0.t[i];          // PRE_tTll_0
