@@ -215,7 +215,13 @@ void *ldso_ba_stream(ldso_ba_ctx *ctx);
  * collectives: ONE sum all-reduce (fp64) of a contiguous buffer holding the packed systems (with
  * accumulate), the energy / #IN pairs and, inside ldso_ba_optimize, the ranks' partial sumNID /
  * numID of doStepFromBackup; then an all-gather of the newest-frame energies followed by the exact
- * threshold re-selection.  Load each rank with ldso_ba_load(ctx, n, windows, rank, world). */
+ * threshold re-selection.  Load each rank with ldso_ba_load(ctx, n, windows, rank, world).
+ * Exactness: the system, energies and threshold of a sharded pass are those of the unsharded pass up
+ * to the reassociation of float sums the block tolerance already allows; sumNID is each rank's float
+ * chain over its run, the partials added in fp64 and read back as float, so the canbreak exit of a
+ * sharded window equals the single-GPU one (FullSystem.cc:1899-1909's one float chain) only up to
+ * that reassociation: a window whose criterion sits within a float rounding of its threshold may
+ * stop one iteration earlier or later than on one GPU. */
 #define LDSO_BA_COMM_ID_BYTES 128
 int ldso_ba_comm_unique_id(uint8_t *id_out);
 int ldso_ba_comm_init(ldso_ba_ctx *ctx, const uint8_t *id, int32_t rank, int32_t world);

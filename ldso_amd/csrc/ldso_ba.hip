@@ -5962,19 +5962,24 @@ int ldso_ba_get_residuals(ldso_ba_ctx *c, int32_t win, int8_t *new_state, int8_t
     const WinHost &H = c->wh[win];
     const int R = D.R;
     if (R == 0) return 0;
-    std::vector<int8_t> ns(R), st(R);
-    std::vector<uint8_t> fl(R);
-    std::vector<float> se(R), ew(R);
-    std::vector<float4> ce(R);
-    HIP_TRY(hipMemcpy(ns.data(), c->d_rs_newstate.p + D.res_base, R, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(st.data(), c->d_rs_state.p + D.res_base, R, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(fl.data(), c->d_rs_flags.p + D.res_base, R, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(se.data(), c->d_rs_energy.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(ew.data(), c->d_rs_energy_wo.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
-    for (int k = 0; k < 4; k++)  // the planes back into (x, y, z, relBS) per residual
+    // only the arrays the caller asked for cross PCIe (a NULL output costs nothing)
+    std::vector<int8_t> ns(new_state ? R : 0), st(state ? R : 0);
+    std::vector<uint8_t> fl(flags ? R : 0);
+    std::vector<float> se(state_energy ? R : 0), ew(new_energy_wo ? R : 0);
+    std::vector<float4> ce(center || rel_bs ? R : 0);
+    if (new_state) HIP_TRY(hipMemcpy(ns.data(), c->d_rs_newstate.p + D.res_base, R, hipMemcpyDeviceToHost));
+    if (state) HIP_TRY(hipMemcpy(st.data(), c->d_rs_state.p + D.res_base, R, hipMemcpyDeviceToHost));
+    if (flags) HIP_TRY(hipMemcpy(fl.data(), c->d_rs_flags.p + D.res_base, R, hipMemcpyDeviceToHost));
+    if (state_energy)
+        HIP_TRY(hipMemcpy(se.data(), c->d_rs_energy.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
+    if (new_energy_wo)
+        HIP_TRY(hipMemcpy(ew.data(), c->d_rs_energy_wo.p + D.res_base, R * sizeof(float), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 4 && (center || rel_bs); k++) {  // the planes back into (x, y, z, relBS) per residual
+        if ((k < 3 && !center) || (k == 3 && !rel_bs)) continue;
         HIP_TRY(hipMemcpy2D(reinterpret_cast<float *>(ce.data()) + k, sizeof(float4),
                             reinterpret_cast<const float *>(c->d_rs_center.p) + (size_t)k * c->R_tot + D.res_base,
                             sizeof(float), sizeof(float), R, hipMemcpyDeviceToHost));
+    }
     std::vector<float> jp;
     if (jpjdf) {
         if ((rc = record_jpjdf(c, win, c->d_rec_a.p, c->d_rec_b.p, c->d_geo_snap.p, jp))) return rc;
@@ -6423,6 +6428,28 @@ int ldso_ba_get_settings(ldso_ba_ctx *c, ldso_ba_opt_settings *out) {
     return 0;
 }
 
+// The loop's first pass and solve use the priors the caller loaded (ldso_ba_window::frame_prior); every
+// later step recomputes them on the device from the settings (k_step_resub, getPrior).  In the
+// reference both come from the same setting_affineOptModeA / B, so a window whose loaded affine priors
+// do not follow the settings the loop runs with is refused rather than run half with each.
+static int check_affine_priors(const ldso_ba_ctx *c, const ldso_ba_frame_state *frames,
+                               const ldso_ba_opt_settings &st) {
+    for (int w = 0; w < c->n_win; w++) {
+        const WinHost &H = c->wh[w];
+        for (int f = 0; f < H.N; f++) {
+            double p[8];
+            frame_take_data_one(frames[c->wd[w].frame_base + f], st.affine_opt_mode_a, st.affine_opt_mode_b, p,
+                                nullptr, nullptr);
+            if (H.frame_prior[8 * f + 6] != p[6] || H.frame_prior[8 * f + 7] != p[7])
+                return fail(-1, "window " + std::to_string(w) + " frame " + std::to_string(f) +
+                                    ": the loaded affine priors (frame_prior[6..7]) do not follow the settings' "
+                                    "setting_affineOptModeA / B; load the window with priors from "
+                                    "ldso_ba_frame_take_data under the same settings");
+        }
+    }
+    return 0;
+}
+
 int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *settings,
                      const ldso_ba_frame_state *frames, const double *calib_value, const double *calib_value_zero,
                      const double *ns, double *energy_out, ldso_ba_frame_state *frames_out, double *calib_out,
@@ -6431,6 +6458,8 @@ int ldso_ba_optimize(ldso_ba_ctx *c, int32_t n_its, const ldso_ba_opt_settings *
     if (n_its < 0 || !frames || !calib_value || !calib_value_zero) return fail(-1, "bad arguments");
     if (c->marg) return fail(-1, "not on a marginalisation context");
     int rc;
+    if (settings && (rc = ldso_ba_check_settings(settings))) return rc;
+    if ((rc = check_affine_priors(c, frames, settings ? *settings : c->settings))) return rc;
     if (settings && (rc = ldso_ba_set_settings(c, settings))) return rc;  // checked, then installed
     const ldso_ba_opt_settings st = c->settings;
     // without SOLVER_ORTHOGONALIZE_X_LATER the solve never projects (EnergyFunctional.cc:428-432)

@@ -96,5 +96,8 @@ def subset_window(window, points):
     w.point_res_begin = np.concatenate([[0], np.cumsum(e - b)]).astype(np.int32)
     for k in ("res_target", "res_state", "res_energy", "res_flags"):
         setattr(w, k, getattr(window, k)[res].copy())
+    # each kept point keeps its features rank (the library orders a host's points by rank, so the
+    # subset's order is the original's restricted to it)
+    w.point_rank = None if window.point_rank is None else np.asarray(window.point_rank)[points].copy()
     w._keep = []
     return w

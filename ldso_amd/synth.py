@@ -165,6 +165,8 @@ def permute_points(w: Window, order) -> Window:
     o = copy.copy(w)
     o.point_host = np.ascontiguousarray(w.point_host[order])
     o.point_data = np.ascontiguousarray(w.point_data[order])
+    # a point's features rank travels with it (ldso_ba_window::point_rank orders by it)
+    o.point_rank = None if w.point_rank is None else np.ascontiguousarray(np.asarray(w.point_rank)[order])
     o.point_res_begin = np.concatenate([[0], np.cumsum(np.diff(w.point_res_begin)[order])]).astype(np.int32)
     for k in ("res_target", "res_state", "res_energy", "res_flags"):
         setattr(o, k, np.ascontiguousarray(getattr(w, k)[ridx]))

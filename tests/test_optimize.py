@@ -24,6 +24,7 @@ import pytest
 
 import oracle
 from ldso_amd import _lib as L
+from ldso_amd import dist as ldist  # (imports torch: before any test loads the HIP library)
 from ldso_amd import synth
 
 CONVERGES = dict(synth.S7, seed=62)           # canbreak at iteration 3 (criterion ratios 1.32 -> 0.79)
@@ -364,6 +365,19 @@ def test_graph_recaptured_when_solve_mode_changes(built, monkeypatch):
         ctx.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
+def test_point_rank_travels_with_its_point(built):
+    """synth.permute_points and dist.subset_window carry each point's features rank with it (the
+    library orders a host's points by rank), and leave a window without ranks without them."""
+    w = synth.make_window(n_frames=4, n_points=50, width=160, height=120, seed=3)
+    assert synth.permute_points(w, np.arange(50)[::-1]).point_rank is None
+    assert ldist.subset_window(w, np.arange(0, 50, 3)).point_rank is None
+    w.point_rank = np.random.default_rng(0).permutation(50).astype(np.int32)
+    order = np.random.default_rng(1).permutation(50)
+    np.testing.assert_array_equal(synth.permute_points(w, order).point_rank, w.point_rank[order])
+    pts = np.array([7, 3, 40, 11])
+    np.testing.assert_array_equal(ldist.subset_window(w, pts).point_rank, w.point_rank[pts])
 
 
 @pytest.mark.gpu

@@ -249,3 +249,24 @@ def test_context_refuses_unsupported_settings(built):
     x = ctx.solve(0, 0)
     assert np.all(np.isfinite(x))
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_optimize_refuses_priors_from_other_affine_modes(built):
+    """ldso_ba_optimize's first pass and solve use the loaded priors, its later steps recompute them
+    from the settings (getPrior): a window whose loaded affine priors follow other modes than the
+    loop's settings is refused (< 0), and a refused call leaves the context's settings as they were."""
+    from ldso_amd import BAContext
+
+    cfg = dict(n_frames=4, n_points=100, width=320, height=240, seed=7)
+    w = window(cfg, settings("kitti_euroc"))  # priors with affineOptMode 0 / 0
+    ctx = BAContext(0).load([w])
+    assert ctx.settings().affine_opt_mode_a == np.float32(1e12)
+    with pytest.raises(RuntimeError, match="affine priors"):
+        ctx.optimize(2)  # the context's defaults (1e12 / 1e8)
+    with pytest.raises(RuntimeError, match="affine priors"):
+        ctx.optimize(2, settings=settings("fixed"))
+    assert ctx.settings().affine_opt_mode_a == np.float32(1e12)  # not installed
+    ctx.optimize(2, settings=settings("kitti_euroc"))
+    assert ctx.settings().affine_opt_mode_a == 0.0
+    ctx.close()
