@@ -8,7 +8,10 @@ are added ("scaling": "weak"; no collective is needed between independent window
 
 roofline: dominant kernel k_linearize, algorithmic bytes per residual
           = 276 B (23 unique 12-B texels) + 8 B state + 88 B/(N-1) point data, times the
-          residuals that do gather (not OOB before the pass), / its mean HIP-event duration.
+          residuals that do gather (not OOB before the pass), / its mean HIP-event duration;
+          frac_step: the same bytes over the sum of the pass's kernel durations (k_linearize,
+          k_point_sc, k_stitch, k_stitch_sum: §8d's step-level definition), frac_step_wall over the
+          step's wall clock.
 value  = residuals that gather in the pass (R_active: not OOB going in, OOB being sticky within
           optimize()) of all ranks per step / max-over-ranks step time.
 cpu_baseline: the oracle restatement (oracle/cpu_baseline.py) compiled -O3 -march=native on the
@@ -736,6 +739,15 @@ def main():
         if cb:
             cpu, cpu1, cpu6 = cb.get("batched"), cb["socket_pinned"], cb["six_threads"]
 
+    # SURVEY §8d's step-level roofline: Achieved = R_active * B_res / (the sum of the pass's kernel
+    # durations), beside the dominant kernel's fraction (`frac`); and the same bytes over the step's
+    # wall clock (every launch gap included)
+    kms = {k: v[0] / max(1, v[1]) for k, v in kall.items() if v[1]}
+    step_kernels = [k for k in ("k_linearize", "k_point_sc", "k_stitch", "k_stitch_sum") if k in kms]
+    step_kernel_ms = sum(kms[k] for k in step_kernels)
+    frac_step = bytes_per_launch / (step_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if step_kernel_ms > 0 else None
+    frac_step_wall = bytes_per_launch / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS if ms_step > 0 else None
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -772,8 +784,12 @@ def main():
                 "avg_launch_us": klin_avg_s * 1e6,
                 "algo_bytes_per_launch": bytes_per_launch,
                 "algo_bytes_per_residual": algo_bytes_per_residual(N),
+                "frac_step": frac_step,
+                "frac_step_kernels": step_kernels,
+                "step_kernel_ms": step_kernel_ms,
+                "frac_step_wall": frac_step_wall,
             },
-            "kernel_ms_per_step": {k: v[0] / max(1, v[1]) for k, v in kall.items() if v[1]},
+            "kernel_ms_per_step": kms,
             "ms_per_step_without_kernel_events": ms_step_no_events,
             "gn_iteration_batched": gn,
             "single_window": single,
