@@ -124,7 +124,10 @@ def load_pmc(workload):
     prov = {"file": rel, "measured_in_this_run": False, "session": d.get("session"),
             "source_sha256": d.get("source_sha256"),
             "same_build_as_this_run": bool(mine and mine == d.get("source_sha256")),
-            "method": "rocprofv3 --pmc, separate passes: 2 x FETCH_SIZE + WRITE_SIZE per launch (tools/pmc_traffic.py)"}
+            "method": "rocprofv3 --pmc, separate passes: 2 x FETCH_SIZE + WRITE_SIZE per launch (tools/pmc_traffic.py)",
+            "fetch_x2_calibration": "profiles/r6/fetch_probe: 16-B pieces of random 128-B lines (1, 2, 4 or 8 per line, "
+                                    "tools/gather_probe_pieces.hip) -- one TCC_EA0_RDREQ per touched line whatever its "
+                                    "used bytes, FETCH_SIZE = exactly half of the whole-line bytes: the x2 applies"}
     return d.get("hbm_bytes_per_launch"), prov
 
 

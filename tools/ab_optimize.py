@@ -1,7 +1,7 @@
 """A/B whole library builds on ldso_ba_optimize (one S7 window, and 64 of them): each build runs in
 its own process (LDSO_BA_LIB=<path>), rounds interleaved, min over rounds of the mean host time
 per optimize(6) call (all six iterations: th_opt_iterations = 0; the graph replayed).
-  python tools/ab_optimize.py lib1.so lib2.so ... [--rounds 3] [--reps 20]"""
+  python tools/ab_optimize.py lib1.so[:key=value,...] lib2.so ... [--rounds 3] [--reps 20]"""
 import argparse
 import json
 import os
@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r'''
-import json, sys, time
+import json, os, sys, time
 sys.path.insert(0, ROOT)
 import torch
 torch.cuda.init()
@@ -21,7 +21,10 @@ st = L.OptSettings.default(th_opt_iterations=0.0)
 for B in (1, 64):
     ws = [synth.make_window(**synth.S7, seed=1000 + i) for i in range(B)]
     ns = [w.nullspaces() for w in ws]
-    c = BAContext(0).load(ws)
+    c = BAContext(0)
+    for kv in filter(None, os.environ.get("LDSO_AB_TUNE", "").split(",")):
+        c.set_tuning(*map(int, kv.split("=")))
+    c.load(ws)
     for _ in range(3):  # the first call sets up and captures the graph
         c.optimize(6, nullspaces=ns, settings=st)
     c.sync()
@@ -54,7 +57,8 @@ def main():
     res = {l: [] for l in a.libs}
     for _ in range(a.rounds):
         for l in a.libs:
-            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(l))
+            path, _, tune = l.partition(":")
+            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(path), LDSO_AB_TUNE=tune)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
             line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
             if p.returncode != 0 or not line:

@@ -6,8 +6,10 @@ profiles/pmc_k_linearize.json.
 
 FETCH_SIZE and WRITE_SIZE are in KiB (TCC_EA0_RDREQ/WRREQ x 64 B).  On gfx950 FETCH_SIZE
 reads 1/2 of the bytes of a wide coalesced 16-B/lane stream; k_linearize's texel reads are
-16-B/lane but scattered, so both the raw and the x2-corrected read figures are recorded and
-the corrected one is used as the traffic estimate (stated as such)."""
+16-B/lane but scattered: tools/gather_probe_pieces.hip (profiles/r6/fetch_probe) calibrates exactly
+that pattern -- 1, 2, 4 or 8 16-B pieces of random 128-B lines of a 1-GiB buffer -- and finds one
+TCC_EA0_RDREQ per touched line and FETCH_SIZE exactly half of the whole-line bytes in every case
+(the HBM delivers whole lines), so the x2-corrected read figure is the traffic; both are recorded."""
 import argparse
 import csv
 import glob

@@ -1,6 +1,6 @@
 """A/B of whole library builds on the device solve alone: one S7 window (and 64), k_solve's
 HIP-event time per launch, for iteration 0 and 2 (projection), each build in its own process.
-  python tools/solve_ab.py lib1.so[:exact] lib2.so ... [--rounds 3]"""
+  python tools/solve_ab.py lib1.so[:exact[:key=value,...]] lib2.so ... [--rounds 3]"""
 import argparse
 import json
 import os
@@ -21,6 +21,8 @@ for B in (1, 64):
     ns = [w.nullspaces() for w in ws]
     c = BAContext(0)
     c.set_tuning(12, int(os.environ.get("LDSO_AB_EXACT", "0")))
+    for kv in filter(None, os.environ.get("LDSO_AB_TUNE", "").split(",")):
+        c.set_tuning(*map(int, kv.split("=")))
     c.load(ws)
     c.linearize()
     for it in (0, 2):
@@ -47,8 +49,9 @@ def main():
     res = {l: [] for l in a.libs}
     for _ in range(a.rounds):
         for l in a.libs:
-            path, _, exact = l.partition(":")
-            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(path), LDSO_AB_EXACT=exact or "0")
+            path, _, rest = l.partition(":")
+            exact, _, tune = rest.partition(":")
+            env = dict(os.environ, LDSO_BA_LIB=os.path.abspath(path), LDSO_AB_EXACT=exact or "0", LDSO_AB_TUNE=tune)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200)
             line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")]
             if p.returncode != 0 or not line:
