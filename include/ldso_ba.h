@@ -213,15 +213,15 @@ void *ldso_ba_stream(ldso_ba_ctx *ctx);
  * (any channel), each rank attaches its context.  From then on every ldso_ba_linearize ends,
  * stream-ordered and without a host synchronisation, with the exchange of SURVEY §8e in TWO
  * collectives: ONE sum all-reduce (fp64) of a contiguous buffer holding the packed systems (with
- * accumulate), the energy / #IN pairs and, inside ldso_ba_optimize, the ranks' partial sumNID /
- * numID of doStepFromBackup; then an all-gather of the newest-frame energies followed by the exact
- * threshold re-selection.  Load each rank with ldso_ba_load(ctx, n, windows, rank, world).
- * Exactness: the system, energies and threshold of a sharded pass are those of the unsharded pass up
- * to the reassociation of float sums the block tolerance already allows; sumNID is each rank's float
- * chain over its run, the partials added in fp64 and read back as float, so the canbreak exit of a
- * sharded window equals the single-GPU one (FullSystem.cc:1899-1909's one float chain) only up to
- * that reassociation: a window whose criterion sits within a float rounding of its threshold may
- * stop one iteration earlier or later than on one GPU. */
+ * accumulate) and the energy / #IN pairs; then an all-gather of per-window slots -- the newest-frame
+ * energies, followed by the exact threshold re-selection, and inside ldso_ba_optimize each rank's
+ * run of |idepth|, from which every rank walks doStepFromBackup's whole sumNID chain.  Load each
+ * rank with ldso_ba_load(ctx, n, windows, rank, world).
+ * Exactness: the system and energies of a sharded pass are those of the unsharded pass up to the
+ * reassociation of float sums the block tolerance already allows; the threshold and sumNID / numID
+ * are the single-GPU ones bit for bit (the runs concatenated in rank order are the unsharded
+ * host-frame order, FullSystem.cc:1899-1909's one float chain), so a sharded window's canbreak
+ * exit is decided on the same sumNID as on one GPU. */
 #define LDSO_BA_COMM_ID_BYTES 128
 int ldso_ba_comm_unique_id(uint8_t *id_out);
 int ldso_ba_comm_init(ldso_ba_ctx *ctx, const uint8_t *id, int32_t rank, int32_t world);
@@ -513,7 +513,7 @@ int ldso_ba_frame_step(int32_t n_frames, const ldso_ba_frame_state *in, const do
 /* doStepFromBackup's canbreak (FullSystem.cc:1894-1931, visual-only, stepfac 1) on the host, the
  * statements the device loop evaluates (se3.h step_canbreak): from the window's x [8N+4] (step = -x),
  * sumNID (the float sum of |idepth_backup| over the window's points in frames -> features order;
- * with sharded points the ranks' partial sums added), numID and setting_thOptIterations.
+ * with sharded points the same chain over the gathered runs), numID and setting_thOptIterations.
  * *canbreak_out = 1 or 0. */
 int ldso_ba_step_canbreak(int32_t n_frames, const double *x, float sum_nid, float num_id, float th_opt_iterations,
                           int32_t *canbreak_out);

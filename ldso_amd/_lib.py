@@ -133,6 +133,7 @@ def ptr(a, t):
     if a is None:
         return C.cast(None, t)
     assert a.flags["C_CONTIGUOUS"], "arrays handed to the C ABI must be C-contiguous"
+    assert a.dtype == np.dtype(t._type_), f"array of {a.dtype} handed as {t.__name__}"
     return a.ctypes.data_as(t)
 
 

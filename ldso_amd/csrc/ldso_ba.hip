@@ -89,7 +89,7 @@ struct WinDev {
     int frame_base, pair_base, point_base, res_base;
     int top_item_base, n_top_items;
     int sc_item_base, n_sc_items;
-    int K, KP, ntiles, pad0;
+    int K, KP, ntiles, p_all;  // p_all: the window's points over every shard (numID)
     long long sc_slab_base;  // floats
     long long sys_base;      // doubles: packed system
     long long stage_base;    // doubles: k_stitch contribution records, N^2 pairs x stage_rec(N)
@@ -1199,17 +1199,30 @@ struct PointParams {
 // (host frames in window order, each host's points in the caller's order: the device point order),
 // i.e. over the idepths this pass linearised at.  The chain of float adds is sequential by
 // definition, so one lane walks it from LDS (the block stages chunks of the idepths), in a block of
-// its own at the front of k_point_sc's grid: it runs beside the point-chunk blocks, off the
-// pass's critical path.  With sharded points each rank sums its own run; the exchange adds the
-// ranks' partials.
-__device__ void nid_chain(const WinDev &W, const float *__restrict__ pt_data, double *win_nid, int w, float *lds,
-                          int chunk) {
-    const int n = W.P, tid = threadIdx.x;
-    const float *pd = pt_data + (size_t)W.point_base * LDSO_BA_POINT_STRIDE + 2;
+// its own beside other work: extra blocks of k_solve_fast (the default), of k_point_sc (exact solve
+// modes), or, with points sharded over ranks, over the exchange's gathered runs (NidSrc).
+// The idepths of one window's chain: its own points (pt_data), or, with points sharded over ranks,
+// every rank's run of |idepth| from the exchange's all-gather, concatenated in rank order -- the
+// runs are contiguous pieces of the host-frame order, so the concatenation is the unsharded order
+// and the chain is bit for bit the single-GPU one (runs zero-padded to prun: + 0 leaves s as is).
+struct NidSrc {
+    const float *pt_data;   // [points][LDSO_BA_POINT_STRIDE], idepth at + 2
+    const float *gathered;  // non-null: [rank][window][slot] exchange slots, the run at + off
+    long long slot, off;
+    int n_ranks, n_win, prun;
+};
+__device__ void nid_chain(const WinDev &W, const NidSrc &src, double *win_nid, int w, float *lds, int chunk) {
+    const int n = src.gathered ? src.n_ranks * src.prun : W.P, tid = threadIdx.x;
+    const float *pd = src.pt_data + (size_t)W.point_base * LDSO_BA_POINT_STRIDE + 2;
+    auto value = [&](int i) {
+        if (!src.gathered) return fabsf(pd[(size_t)i * LDSO_BA_POINT_STRIDE]);
+        const int r = i / src.prun, q = i - r * src.prun;
+        return src.gathered[((size_t)r * src.n_win + w) * src.slot + src.off + q];
+    };
     float s = 0.0f;
     for (int q0 = 0; q0 < n; q0 += chunk) {
         const int m = min(chunk, n - q0);
-        for (int i = tid; i < m; i += blockDim.x) lds[i] = fabsf(pd[(size_t)(q0 + i) * LDSO_BA_POINT_STRIDE]);
+        for (int i = tid; i < m; i += blockDim.x) lds[i] = value(q0 + i);
         for (int i = m + tid; i < ((m + 3) & ~3); i += blockDim.x) lds[i] = 0.0f;  // +0 leaves s unchanged
         __syncthreads();
         if (tid == 0) {
@@ -1226,13 +1239,15 @@ __device__ void nid_chain(const WinDev &W, const float *__restrict__ pt_data, do
         __syncthreads();
     }
     if (tid == 0) {
-        win_nid[2 * w] = (double)s;  // exact; read back as float (a sharded window: the ranks' sum)
-        win_nid[2 * w + 1] = (double)(float)n;  // numID++ per point (float): exact below 2^24
+        win_nid[2 * w] = (double)s;  // exact; read back as float
+        win_nid[2 * w + 1] = (double)(float)W.p_all;  // numID++ per point (float): exact below 2^24
     }
 }
 __device__ void point_nid(const PointParams &P, int w, float *lds) {
     if (P.stop && P.pass > P.stop[w]) return;
-    nid_chain(P.wins[w], P.pt_data, P.win_nid, w, lds, P.nid_chunk);
+    NidSrc src{};
+    src.pt_data = P.pt_data;
+    nid_chain(P.wins[w], src, P.win_nid, w, lds, P.nid_chunk);
 }
 
 // points per k_point_sc block (one SYRK chunk partial).  128 (both waves gather, half the slab
@@ -2459,7 +2474,7 @@ struct SolveParams {
     // sumNID / numID of the step that follows (nid_chain) over the idepths this solve's system was
     // linearised at -- a chain of ~P dependent float adds that fits inside the solve's own time
     double *win_nid;
-    const float *pt_data;
+    NidSrc nid_src;
     int n_win, nid_chunk;
 };
 constexpr int kPrepGStride = 192;  // doubles per window in prep_g: G [49], G^-1 [49], fast flag, V [49], ev [7], keep [7]
@@ -3459,7 +3474,7 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
     if (P.win_nid && (int)blockIdx.x >= P.n_win) {  // doStepFromBackup's sumNID (FullSystem.cc:1899-1909)
         const int w = blockIdx.x - P.n_win;
         if (P.stop && P.iteration >= P.stop[w]) return;
-        nid_chain(P.wins[w], P.pt_data, P.win_nid, w, reinterpret_cast<float *>(lds), P.nid_chunk);
+        nid_chain(P.wins[w], P.nid_src, P.win_nid, w, reinterpret_cast<float *>(lds), P.nid_chunk);
         return;
     }
     static_assert(7 * kSolveMaxDim <= 2 * kSolveFastThreads, "OrthoPre: two Nm elements per thread");
@@ -3540,25 +3555,41 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
 // over the ranks; nth_element needs all of them.  Each rank exports its newest-frame segment
 // of every window into a fixed-stride slot (padding -1, which the selection skips), the host
 // all-gathers the slots, and k_frame_th reruns the exact selection over all ranks' values.
+// slot of window w (pitch `slot` floats): the newest-frame energies [0, stride) (padding -1), then,
+// with prun > 0, the rank's |idepth| run of the window in device point order [stride, stride +
+// prun) (padding 0) -- the sharded sumNID chain's input (NidSrc)
 __global__ __launch_bounds__(256) void k_export_newest(const WinDev *__restrict__ wins, const float *__restrict__ e_wo,
-                                                       float *out, long long stride) {
+                                                       float *out, long long stride, long long slot,
+                                                       const float *__restrict__ pt_data, int prun) {
     const WinDev &W = wins[blockIdx.y];
     const int n = W.newest_end - W.newest_begin;
-    float *dst = out + (size_t)blockIdx.y * stride;
+    float *dst = out + (size_t)blockIdx.y * slot;
     for (long long i = blockIdx.x * 256 + threadIdx.x; i < stride; i += (long long)gridDim.x * 256)
         dst[i] = i < n ? e_wo[W.newest_begin + i] : -1.0f;
+    for (long long i = blockIdx.x * 256 + threadIdx.x; i < prun; i += (long long)gridDim.x * 256)
+        dst[stride + i] = i < W.P ? fabsf(pt_data[(size_t)(W.point_base + i) * LDSO_BA_POINT_STRIDE + 2]) : 0.0f;
 }
 
+// blocks [0, n_win): the exact setNewFrameEnergyTH over every rank's slot; with nid.gathered, blocks
+// [n_win, 2 n_win) the windows' sumNID chains over the gathered runs (ldso_ba_optimize, exact solve modes)
 __global__ __launch_bounds__(kStThreads) void k_frame_th(const WinDev *__restrict__ wins, const float *__restrict__ buf,
-                                                         int n_ranks, int n_win, long long stride, float *frame_th) {
+                                                         int n_ranks, int n_win, long long stride, long long slot,
+                                                         float *frame_th, NidSrc nid, double *win_nid,
+                                                         const int *stop, int pass) {
     __shared__ unsigned keys[kThMaxLds + th_fixed_bytes(kStThreads) / sizeof(unsigned)];
+    if ((int)blockIdx.x >= n_win) {
+        const int w = blockIdx.x - n_win;
+        if (stop && pass > stop[w]) return;
+        nid_chain(wins[w], nid, win_nid, w, reinterpret_cast<float *>(keys), kThMaxLds);
+        return;
+    }
     const int w = blockIdx.x;
     const WinDev &W = wins[w];
     const long long n_cand = (long long)n_ranks * stride;
     select_frame_th<kStThreads>(
         [&](int i) {
             const int r = (int)(i / stride);
-            return buf[((size_t)r * n_win + w) * stride + (i - (long long)r * stride)];
+            return buf[((size_t)r * n_win + w) * slot + (i - (long long)r * stride)];
         },
         (int)n_cand, keys, kThMaxLds, frame_th + W.frame_base + W.N - 1);
 }
@@ -4255,6 +4286,7 @@ struct ldso_ba_ctx {
     ncclComm_t comm = nullptr;
     int comm_rank = 0, comm_world = 1;
     int64_t x_stride = 0;
+    int64_t x_prun = 0;  // |idepth| run length per window slot (max local points over windows and ranks)
     DevBuf<float> d_x_local, d_x_gathered;
     // device GN loop (ldso_ba_optimize): frame states, CalibHessian::value / value_zero and the
     // prior switches per window, the energy history
@@ -4583,10 +4615,24 @@ int upload_priors(ldso_ba_ctx *c, int win) {
 }
 
 // where ldso_ba_optimize computes the step's sumNID: in extra blocks of k_solve_fast, beside the
-// factorisation; with a communicator (each rank sums its own points, the exchange adds the
-// partials) or an exact solve mode, in leading blocks of the pass's k_point_sc
-inline bool nid_in_solve(const ldso_ba_ctx *c) {
-    return !c->comm && !c->solve_exact && !getenv_flag("LDSO_BA_SOLVE_LDS");
+// factorisation; with an exact solve mode in leading blocks of the pass's k_point_sc, or, with a
+// communicator, in extra blocks of the exchange's k_frame_th
+inline bool nid_in_solve(const ldso_ba_ctx *c) { return !c->solve_exact && !getenv_flag("LDSO_BA_SOLVE_LDS"); }
+// the idepths the sumNID chain walks: the context's points, or with a communicator every rank's
+// run of the window from the last exchange's all-gather (the runs concatenated in rank order are
+// the unsharded host-frame order, so the chain is the single-GPU one bit for bit)
+NidSrc nid_source(const ldso_ba_ctx *c) {
+    NidSrc n{};
+    n.pt_data = c->d_pt_data.p;
+    if (c->comm) {
+        n.gathered = c->d_x_gathered.p;
+        n.slot = c->x_stride + c->x_prun;
+        n.off = c->x_stride;
+        n.n_ranks = c->comm_world;
+        n.n_win = c->n_win;
+        n.prun = (int)c->x_prun;
+    }
+    return n;
 }
 ResubParams resub_params(ldso_ba_ctx *c, int begin, int count, double lambda, bool apply_step) {
     ResubParams R{};
@@ -4935,6 +4981,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_win = n_windows;
     c->x_stride = 0;
+    c->x_prun = 0;
     c->width = ws[0].width;
     c->height = ws[0].height;
     c->npix = c->width * c->height;
@@ -5122,6 +5169,7 @@ int load_impl(ldso_ba_ctx *c, int32_t n_windows, const ldso_ba_window *ws, int32
         D.hM3 = (float)(in.height - 3);
         for (int i = 0; i < 4; i++) D.calib[i] = in.calib[i];
         for (int i = 0; i < 4; i++) D.cdelta[i] = in.c_delta[i];
+        D.p_all = in.n_points;  // numID counts every shard's points
         D.K = 8 * (N - 1) + 5;
         D.KP = (D.K + 3) / 4 * 4;
         const int nt = D.KP / 4;
@@ -5485,40 +5533,53 @@ namespace {
 
 // SURVEY.md §8e's exchange, stream-ordered after k_stitch on the context stream (no host
 // synchronisation): one fp64 sum all-reduce of every window's packed {HA, bA, Hsc, bsc} (the priors
-// are not in it: every rank adds its own copy in the solve), one of the linearizeAll energy / #IN pairs, and an all-gather of
-// the newest-frame NewEnergyWithOutlier slots after which k_frame_th re-selects the exact
-// setNewFrameEnergyTH threshold on every rank.
+// are not in it: every rank adds its own copy in the solve) and of the linearizeAll energy / #IN
+// pairs, then an all-gather of per-window slots -- the newest-frame NewEnergyWithOutlier values,
+// after which k_frame_th re-selects the exact setNewFrameEnergyTH threshold on every rank, and,
+// inside ldso_ba_optimize, the rank's run of |idepth|, from which every rank walks the window's
+// whole sumNID chain (doStepFromBackup's float sum in the unsharded order: nid_source).
 int comm_exchange(ldso_ba_ctx *c, bool accumulate) {
     hipStream_t st = c->stream;
-    if (c->x_stride == 0) {  // first exchange since the load: agree on the slot stride
-        int64_t m = 1;
-        for (const WinDev &D : c->wd) m = std::max<int64_t>(m, D.newest_end - D.newest_begin);
+    if (c->x_stride == 0) {  // first exchange since the load: agree on the slot stride and run length
+        int64_t m[2] = {1, 0};
+        for (const WinDev &D : c->wd) {
+            m[0] = std::max<int64_t>(m[0], D.newest_end - D.newest_begin);
+            m[1] = std::max<int64_t>(m[1], D.P);
+        }
+        m[1] = (m[1] + 3) & ~(int64_t)3;  // the chain reads float4s of one rank's run
         DevBuf<int64_t> t;
-        if (int rc = t.alloc(1)) return rc;
-        HIP_TRY(hipMemcpyAsync(t.p, &m, sizeof(m), hipMemcpyHostToDevice, st));
-        NCCL_TRY(ncclAllReduce(t.p, t.p, 1, ncclInt64, ncclMax, c->comm, st));
-        HIP_TRY(hipMemcpyAsync(&m, t.p, sizeof(m), hipMemcpyDeviceToHost, st));
+        if (int rc = t.alloc(2)) return rc;
+        HIP_TRY(hipMemcpyAsync(t.p, m, sizeof(m), hipMemcpyHostToDevice, st));
+        NCCL_TRY(ncclAllReduce(t.p, t.p, 2, ncclInt64, ncclMax, c->comm, st));
+        HIP_TRY(hipMemcpyAsync(m, t.p, sizeof(m), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         t.release();
-        c->x_stride = m;
-        if (int rc = c->d_x_local.alloc((size_t)c->n_win * m)) return rc;
-        if (int rc = c->d_x_gathered.alloc((size_t)c->comm_world * c->n_win * m)) return rc;
+        c->x_stride = m[0];
+        c->x_prun = m[1];
+        const size_t slot_max = (size_t)(m[0] + m[1]);
+        if (int rc = c->d_x_local.alloc((size_t)c->n_win * slot_max)) return rc;
+        if (int rc = c->d_x_gathered.alloc((size_t)c->comm_world * c->n_win * slot_max)) return rc;
     }
-    // ONE fp64 sum all-reduce of the contiguous exchange buffer: the packed systems (with
-    // accumulate), the energy / #IN pairs, and inside optimize() the next step's sumNID / numID
-    // partials (each rank's float chain over its own run of points, widened exactly to double)
     const size_t nw2 = (size_t)2 * c->n_win;
     double *xb = accumulate ? c->d_sys.p : c->win_energy();
-    const size_t xn = (accumulate ? c->sys_n : 0) + nw2 + (c->opt_pass >= 0 && accumulate ? nw2 : 0);
+    const size_t xn = (accumulate ? c->sys_n : 0) + nw2;
     NCCL_TRY(ncclAllReduce(xb, xb, xn, ncclFloat64, ncclSum, c->comm, st));
-    const long long stride = c->x_stride;
-    const dim3 grid((unsigned)std::min<long long>((stride + 255) / 256, 64), (unsigned)c->n_win);
-    k_export_newest<<<grid, 256, 0, st>>>(c->d_wins.p, c->d_rs_energy_wo.p, c->d_x_local.p, stride);
+    // inside optimize() an accumulating pass also ships the idepth runs of the next step's sumNID
+    const bool nid = c->opt_pass >= 0 && accumulate;
+    const long long stride = c->x_stride, prun = nid ? c->x_prun : 0, slot = stride + prun;
+    const dim3 grid((unsigned)std::min<long long>((slot + 255) / 256, 64), (unsigned)c->n_win);
+    k_export_newest<<<grid, 256, 0, st>>>(c->d_wins.p, c->d_rs_energy_wo.p, c->d_x_local.p, stride, slot,
+                                          c->d_pt_data.p, (int)prun);
     HIP_TRY(hipGetLastError());
-    NCCL_TRY(ncclAllGather(c->d_x_local.p, c->d_x_gathered.p, (size_t)c->n_win * stride, ncclFloat32, c->comm, st));
+    NCCL_TRY(ncclAllGather(c->d_x_local.p, c->d_x_gathered.p, (size_t)c->n_win * slot, ncclFloat32, c->comm, st));
+    // the chains run here when the solve does not host them (exact solve modes)
+    const bool chain_here = nid && !nid_in_solve(c);
+    NidSrc src = chain_here ? nid_source(c) : NidSrc{};
+    const int* stop = c->opt_pass >= 0 ? c->d_stop.p : nullptr;
     return timed_launch(c, 4, st, [&] {
-        k_frame_th<<<c->n_win, kStThreads, 0, st>>>(c->d_wins.p, c->d_x_gathered.p, c->comm_world, c->n_win, stride,
-                                                    c->d_frame_th.p);
+        k_frame_th<<<c->n_win * (chain_here ? 2 : 1), kStThreads, 0, st>>>(
+            c->d_wins.p, c->d_x_gathered.p, c->comm_world, c->n_win, stride, slot, c->d_frame_th.p, src,
+            chain_here ? c->win_nid() : nullptr, stop, c->opt_pass);
     });
 }
 }  // namespace
@@ -5544,6 +5605,7 @@ int ldso_ba_comm_init(ldso_ba_ctx *c, const uint8_t *id_in, int32_t rank, int32_
     c->comm_rank = rank;
     c->comm_world = world;
     c->x_stride = 0;
+    c->x_prun = 0;
     return 0;
 }
 
@@ -5623,7 +5685,7 @@ int ldso_ba_linearize(ldso_ba_ctx *c, int32_t fix, int32_t accumulate) {
     Pp.stop = Sp.stop;
     Pp.pass = c->opt_pass;
     const size_t sc_smem = std::max<size_t>(c->sc_smem_max, 4096);  // point_nid stages >= 1024 idepths
-    if (in_opt && accumulate && !nid_in_solve(c)) {  // the next step's sumNID / numID (its backup idepths are this pass's)
+    if (in_opt && accumulate && !nid_in_solve(c) && !c->comm) {  // the next step's sumNID / numID (its backup idepths are this pass's)
         Pp.win_nid = c->win_nid();
         Pp.n_nid = c->n_win;
         Pp.nid_chunk = (int)std::min<size_t>(1024, (sc_smem / sizeof(float)) & ~(size_t)3);
@@ -6161,7 +6223,7 @@ int solve_device_launch(ldso_ba_ctx *c, int iteration, int n_null) {
         int grid = c->n_win;
         if (c->opt_pass >= 0 && nid_in_solve(c)) {  // the step's sumNID chains in blocks of their own
             S.win_nid = c->win_nid();
-            S.pt_data = c->d_pt_data.p;
+            S.nid_src = nid_source(c);
             S.n_win = c->n_win;
             S.nid_chunk = (int)std::min<size_t>(1024, (smem / sizeof(float)) & ~(size_t)3);
             grid *= 2;
@@ -6691,7 +6753,8 @@ int ldso_ba_export_newest(ldso_ba_ctx *c, float *dev_buf, int64_t stride) {
         if (D.newest_end - D.newest_begin > stride) return fail(-1, "stride smaller than a newest-frame segment");
     HIP_TRY(hipSetDevice(c->device));
     const dim3 grid((unsigned)std::min<int64_t>((stride + 255) / 256, 64), (unsigned)c->n_win);
-    k_export_newest<<<grid, 256, 0, c->stream>>>(c->d_wins.p, c->d_rs_energy_wo.p, dev_buf, (long long)stride);
+    k_export_newest<<<grid, 256, 0, c->stream>>>(c->d_wins.p, c->d_rs_energy_wo.p, dev_buf, (long long)stride,
+                                                 (long long)stride, nullptr, 0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
@@ -6704,7 +6767,8 @@ int ldso_ba_frame_threshold_gathered(ldso_ba_ctx *c, const float *dev_buf, int32
     c->th_host_valid = false;
     int rc = timed_launch(c, 4, c->stream, [&] {
         k_frame_th<<<c->n_win, kStThreads, 0, c->stream>>>(c->d_wins.p, dev_buf, n_ranks, c->n_win, (long long)stride,
-                                                           c->d_frame_th.p);
+                                                           (long long)stride, c->d_frame_th.p, NidSrc{}, nullptr,
+                                                           nullptr, 0);
     });
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));

@@ -89,6 +89,9 @@ def lib():
 def _p(a, t):
     if a is None:
         return C.cast(None, t)
+    # the C side reads and writes through this pointer at its own element size: a mismatched or
+    # strided array would be overrun (a float32 calib_value handed as double* once corrupted the heap)
+    assert a.flags["C_CONTIGUOUS"] and a.dtype == np.dtype(t._type_), (a.dtype, t)
     return a.ctypes.data_as(t)
 
 
@@ -274,12 +277,15 @@ def do_step_from_backup(frames, x, calib_value, calib_value_zero, point_host, id
     sf = np.zeros(4, np.float32)
     cd = np.zeros(4, np.float32)
     cz = np.ascontiguousarray(calib_value_zero, np.float64)
+    cv = np.ascontiguousarray(calib_value, np.float64)  # a copy unless already float64 (stepped in place)
     rc = lib().oracle_do_step_from_backup(len(fr), fr.ctypes.data, _p(np.ascontiguousarray(x, np.float64), f64p),
-                                          _p(calib_value, f64p), _p(cz, f64p), P, _p(ph, i32p), _p(ib, f32p),
+                                          _p(cv, f64p), _p(cz, f64p), P, _p(ph, i32p), _p(ib, f32p),
                                           _p(ps, f32p), float(th_opt_iterations), out.ctypes.data, _p(idepth, f32p),
                                           _p(sf, f32p), _p(cd, f32p))
     assert rc >= 0
-    return out, calib_value, sf, cd, idepth, bool(rc)
+    if cv is not calib_value and isinstance(calib_value, np.ndarray) and calib_value.flags.writeable:
+        calib_value[...] = cv
+    return out, cv, sf, cd, idepth, bool(rc)
 
 
 # ---- coarse tracker (ldso_oracle_tracker.cpp): the checker of include/ldso_ct.h -------------

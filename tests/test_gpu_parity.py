@@ -712,19 +712,25 @@ def test_rccl_world1_exchange_keeps_results(built):
     b.close()
 
 
-def test_rccl_world1_optimize_keeps_results(built):
+@pytest.mark.parametrize("exact", [False, True])
+def test_rccl_world1_optimize_keeps_results(built, exact):
     """ldso_ba_optimize on a context with a (world-1) communicator -- direct launches, the
-    exchange after every pass, the energy history written after it -- equals the same call on a
-    context without one (graph replay), bit for bit."""
+    exchange after every pass, the energy history written after it, sumNID walked over the
+    exchange's gathered |idepth| runs (in k_solve_fast's extra blocks, or with the exact solve in
+    k_frame_th's) -- equals the same call on a context without one (graph replay), bit for bit:
+    iteration counts and statuses included, so the canbreak exits saw the same sumNID."""
     from ldso_amd import _lib as L
 
-    cfg = dict(n_frames=6, n_points=700, seed=52)
+    cfg = dict(n_frames=6, n_points=701, seed=52)  # a run length that is not a multiple of 4
     w = synth.make_window(**cfg)
     ns = [w.nullspaces()]
     a = BAContext(0).load([synth.make_window(**cfg)])
     uid = np.zeros(128, np.uint8)
     L.check(L.lib().ldso_ba_comm_unique_id(uid.ctypes.data))
     b = BAContext(0).comm_init(uid.tobytes(), 0, 1).load([synth.make_window(**cfg)], shard_rank=0, shard_count=1)
+    if exact:
+        a.set_tuning(12, 1)  # LDSO_BA_TUNE_SOLVE_EXACT
+        b.set_tuning(12, 1)
     ra = a.optimize(4, nullspaces=ns)
     rb = b.optimize(4, nullspaces=ns)
     for x, y in zip(ra, rb):

@@ -99,13 +99,14 @@ def sharded_optimize(rank, world, cfg, n_its=6, th=1.2, min_its=1, dist_=None):
     """FullSystem::optimize's loop on ONE rank's shard of the window, with the exchange the
     in-library RCCL path does (ldso_ba.hip comm_exchange) and everything else through the library's
     host contract: the rank's run of points (ldso_ba_shard_points) restated by the oracle; per pass
-    ONE fp64 sum all-reduce of [packed {HA, bA, Hsc, bsc} | E, #IN | sumNID, numID] and ONE
-    all-gather of the newest-frame NewEnergyWithOutlier slots -> setNewFrameEnergyTH
-    (ldso_ba_frame_threshold); every rank solves the reduced system redundantly
-    (ldso_ba_solve_system, its own priors), resubstitutes its own points, steps the frames
-    (ldso_ba_frame_step) and evaluates canbreak on the summed sumNID partials
-    (ldso_ba_step_canbreak).  world == 1 (dist_ None) is the unsharded loop of the same code.
-    -> (energies per pass, iterations entered, status, frame states)."""
+    ONE fp64 sum all-reduce of [packed {HA, bA, Hsc, bsc} | E, #IN] and ONE all-gather of per-rank
+    slots [newest-frame NewEnergyWithOutlier values | the rank's |idepth| run, zero-padded] ->
+    setNewFrameEnergyTH (ldso_ba_frame_threshold) and doStepFromBackup's sumNID as one float chain
+    over the runs in rank order (the unsharded order); every rank solves the reduced system
+    redundantly (ldso_ba_solve_system, its own priors), resubstitutes its own points, steps the
+    frames (ldso_ba_frame_step) and evaluates canbreak on that sumNID (ldso_ba_step_canbreak).
+    world == 1 (dist_ None) is the unsharded loop of the same code.
+    -> (energies per pass, iterations entered, status, frame states, sumNID per pass)."""
     import ctypes as C
 
     import oracle
@@ -123,32 +124,39 @@ def sharded_optimize(rank, world, cfg, n_its=6, th=1.2, min_its=1, dist_=None):
     ow = oracle.OracleWindow(sub, threads=0)
     ow.reset_oob()
 
+    def chain(v):  # FullSystem.cc:1899-1909: one float chain, + 0 for padding leaves it as is
+        return np.float32(np.cumsum(v, dtype=np.float32)[-1]) if len(v) else np.float32(0)
+
     def exchange():
         e, sysm = ow.iteration()
         idep = np.abs(sub.point_data[dev_order, 2].astype(np.float32))
-        nid = np.float32(np.cumsum(idep, dtype=np.float32)[-1]) if len(idep) else np.float32(0)  # float chain
-        buf = np.concatenate([ldist.pack_upper(sysm), [e[0], e[2]], [np.float64(nid), np.float64(len(idep))]])
+        buf = np.concatenate([ldist.pack_upper(sysm), [e[0], e[2]]])
         r = ow.residuals()
         seg = r["new_energy_wo"][sub.res_target == N - 1]
         if dist_ is not None:
             t = torch.from_numpy(buf)
             dist_.all_reduce(t)  # the one all-reduce
             buf = t.numpy()
-            stride = torch.tensor([len(seg)], dtype=torch.int64)
-            dist_.all_reduce(stride, op=dist_.ReduceOp.MAX)  # once per load in the library
-            slot = torch.full((int(stride),), -1.0, dtype=torch.float32)
+            m = torch.tensor([len(seg), len(idep)], dtype=torch.int64)
+            dist_.all_reduce(m, op=dist_.ReduceOp.MAX)  # once per load in the library
+            stride, prun = int(m[0]), (int(m[1]) + 3) // 4 * 4
+            slot = torch.full((stride + prun,), -1.0, dtype=torch.float32)
             slot[:len(seg)] = torch.from_numpy(seg)
+            slot[stride:] = 0.0
+            slot[stride:stride + len(idep)] = torch.from_numpy(idep)
             gathered = [torch.empty_like(slot) for _ in range(world)]
             dist_.all_gather(gathered, slot)  # the one all-gather
-            th_new = ldist.frame_threshold(torch.cat(gathered).numpy())
+            th_new = ldist.frame_threshold(torch.cat([g[:stride] for g in gathered]).numpy())
+            nid = chain(torch.cat([g[stride:] for g in gathered]).numpy())
         else:
             th_new = ldist.frame_threshold(seg)
-        red = ldist.unpack_upper(buf[:-4], dim)
+            nid = chain(idep)
+        red = ldist.unpack_upper(buf[:-2], dim)
         red["HL"], red["bL"] = sysm["HL"], sysm["bL"]
-        return red, buf[-4:-2], np.float32(buf[-2]), np.float32(buf[-1]), th_new
+        return red, buf[-2:], nid, np.float32(w.n_points), th_new
 
     red, en, snid, nnid, th_new = exchange()
-    energies = [en]
+    energies, snids = [en], [snid]
     frames = np.ascontiguousarray(sub.frames).copy()
     cval = sub.calib.astype(np.float64) * (1.0 / 50.0)
     czero = cval.copy()
@@ -185,10 +193,11 @@ def sharded_optimize(rank, world, cfg, n_its=6, th=1.2, min_its=1, dist_=None):
         ow.update(sub)
         red, en, snid, nnid, th_new = exchange()
         energies.append(en)
+        snids.append(snid)
         if cb.value and it >= min_its:
             status, its = L.OPT_CONVERGED, it + 1
             break
-    return np.array(energies), its, status, frames
+    return np.array(energies), its, status, frames, np.array(snids)
 
 
 def _opt_worker(rank, world, port, q, cfgs):
@@ -196,7 +205,7 @@ def _opt_worker(rank, world, port, q, cfgs):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = [sharded_optimize(rank, world, c, dist_=dist) for c in cfgs]
-        q.put((rank, [(e, its, st, fr["state"]) for e, its, st, fr in res]))
+        q.put((rank, [(e, its, st, fr["state"], nid) for e, its, st, fr, nid in res]))
     finally:
         dist.destroy_process_group()
 
@@ -204,10 +213,11 @@ def _opt_worker(rank, world, port, q, cfgs):
 @pytest.mark.timeout(600)
 def test_sharded_optimize_loop_matches_unsharded(built):
     """The whole sharded GN loop (shard, pass, one all-reduce + one all-gather, redundant solve,
-    shard-local resubstitution, step, canbreak on the summed sumNID partials) over gloo at world 2:
-    every rank leaves the loop at the same iteration with the same status as the unsharded loop,
-    energies within 1e-5 (the ranks' float partials only reassociate), #IN equal, frame states
-    within 5 % of the unsharded loop's total step."""
+    shard-local resubstitution, step, canbreak on the sumNID chain over the gathered runs) over gloo
+    at world 2: every rank leaves the loop at the same iteration with the same status as the
+    unsharded loop, energies within 1e-5 (the ranks' float partials only reassociate), #IN equal,
+    frame states within 5 % of the unsharded loop's total step; the first pass's sumNID (same
+    idepths on both sides) bit-exact."""
     from ldso_amd import synth
     from test_optimize import CONVERGES, RUNS_ALL
 
@@ -224,10 +234,13 @@ def test_sharded_optimize_loop_matches_unsharded(built):
         p.join(60)
         assert p.exitcode == 0
     for i, c in enumerate(cfgs):
-        e1, its1, st1, fr1 = sharded_optimize(0, 1, c)
+        e1, its1, st1, fr1, nid1 = sharded_optimize(0, 1, c)
         print(f"{c}: unsharded {its1} its status {st1}; sharded {[outs[r][i][1:3] for r in range(world)]}")
         for r in range(world):
-            e2, its2, st2, s2 = outs[r][i]
+            e2, its2, st2, s2, nid2 = outs[r][i]
+            assert nid2[0] == nid1[0]  # the unsharded chain, bit for bit
+            # later passes chain idepths the (reassociated) solves moved apart
+            np.testing.assert_allclose(nid2, nid1, rtol=1e-4)
             assert (its2, st2) == (its1, st1), (r, i)
             np.testing.assert_allclose(e2[:, 0], e1[:, 0], rtol=1e-5)
             np.testing.assert_array_equal(e2[:, 1], e1[:, 1])
