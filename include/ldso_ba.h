@@ -542,7 +542,7 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *ctx, int32_t enable);
  *                              is positive definite; x within rounding of the pivoted solve); 1 the
  *                              pivoted factorisation of the host solver (k_solve_reg / k_solve,
  *                              x bit-identical to ldso_ba_solve)
- * Keys 1, 3, 4, 5, 8, 9 and 11 named experiment variants that measured slower and were removed
+ * Keys 1, 3, 4, 5, 8, 9, 11 and 14 named experiment variants that measured slower and were removed
  * (DESIGN.md §5 keeps their numbers); setting them returns -1. */
 #define LDSO_BA_TUNE_TILED_IMAGES 2
 #define LDSO_BA_TUNE_TOP_CHUNK 6

@@ -450,7 +450,7 @@ def test_image_layouts_agree(built, layout):
     c.close()
 
 
-@pytest.mark.parametrize("key,value", [(1, 3), (2, 0), (2, 2), (8, 2), (11, 1), (10, 3)])
+@pytest.mark.parametrize("key,value", [(1, 3), (2, 0), (2, 2), (8, 2), (11, 1), (10, 3), (14, 1)])
 def test_removed_tuning_variants_are_rejected(built, key, value):
     c = BAContext(0)
     with pytest.raises(RuntimeError):
