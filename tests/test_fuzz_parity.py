@@ -1,0 +1,74 @@
+"""Randomised parity sweep: seeded random windows through one pass (linearizeAll + applyRes +
+accumulate) on the GPU against the oracle, with everything the path branches on drawn at random --
+keyframe count (2..16: the host stitch and, above 11, the per-pair records stitch), point count
+(0..700), frame size (widths not a multiple of 8, heights not a multiple of 4), camera model,
+forward or sideways motion (scale change, OOB pattern pixels), outlier fraction, points near the
+border, the residuals per k_linearize wavefront (8..64 or automatic), both image layouts and the
+affine-optimisation modes.  Bars as tests/test_gpu_parity.py's compare_pass: per residual and per
+point bit-exact, the energy to 1e-12, the stitched blocks within 1e-4, the priors exact.
+Each case prints its draw, so a failure names the configuration to rerun."""
+import numpy as np
+import pytest
+
+import oracle
+from ldso_amd import BAContext, synth
+from ldso_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(160, 120), (317, 203), (640, 480), (1242, 375)]
+AFFINE = [(1e12, 1e8), (0.0, 0.0), (-1.0, -1.0), (-1.0, 5.0)]
+
+
+def draw(case):
+    rng = np.random.default_rng(9000 + case)
+    W, H = SIZES[rng.integers(len(SIZES))]
+    n_win = int(rng.integers(1, 4))
+    wins = []
+    for k in range(n_win):
+        N = int(rng.choice([2, 3, 4, 5, 6, 7, 8, 11, 13, 16], p=[.1, .12, .12, .12, .1, .14, .1, .1, .05, .05]))
+        if case in (10, 11) and k == 0:  # two cases hold a window above 11 keyframes (k_stitch's records)
+            N = 13 if case == 10 else 16
+        P = int(rng.integers(0, 700 if N <= 8 else 300))
+        calib = None
+        if rng.random() < 0.5:
+            f = float(rng.uniform(0.4, 1.2)) * W
+            calib = [f, f * float(rng.uniform(0.95, 1.05)), W / 2 + float(rng.uniform(-0.1, 0.1)) * W,
+                     H / 2 + float(rng.uniform(-0.1, 0.1)) * H]
+        wins.append(dict(n_frames=N, n_points=P, width=W, height=H, seed=int(rng.integers(1 << 30)),
+                         outlier_frac=float(rng.uniform(0.0, 0.3)), motion=str(rng.choice(["sideways", "forward"])),
+                         edge_frac=float(rng.choice([0.0, 0.2])), calib=calib,
+                         plane_depth=max(25.0, 2.5 * (N - 1))))  # the canyon's far facade beyond the travel
+    chunk = int(rng.choice([0, 8, 24, 64]))
+    layout = int(rng.choice([1, 3]))
+    aff = AFFINE[rng.integers(len(AFFINE))]
+    return wins, chunk, layout, aff
+
+
+def window(cfg, s):
+    w = synth.make_window(**cfg)
+    w.settings = s
+    return w.refresh_frame_terms()
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_random_windows_match_oracle(built, case):
+    from test_gpu_parity import compare_pass
+
+    wins, chunk, layout, aff = draw(case)
+    print(f"case {case}: chunk {chunk}, layout {layout}, affine {aff}")
+    for c in wins:
+        print("  ", c)
+    s = L.OptSettings.default(affine_opt_mode_a=aff[0], affine_opt_mode_b=aff[1])
+    ctx = BAContext(0)
+    ctx.set_tuning(6, chunk)   # LDSO_BA_TUNE_TOP_CHUNK
+    ctx.set_tuning(2, layout)  # LDSO_BA_TUNE_TILED_IMAGES
+    ctx.set_settings(s).load([window(c, s) for c in wins])
+    ctx.linearize(fix=False, accumulate=True)
+    with oracle.affine_opt_modes(*aff):
+        for i, c in enumerate(wins):
+            ow = oracle.OracleWindow(window(c, s), threads=0)
+            e_cpu, s_cpu = ow.iteration()
+            compare_pass(ctx, ow, i, e_cpu, s_cpu)
+            ow.close()
+    ctx.close()
