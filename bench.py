@@ -8,7 +8,8 @@ are added ("scaling": "weak"; no collective is needed between independent window
 
 roofline: dominant kernel k_linearize, algorithmic bytes per residual
           = 276 B (23 unique 12-B texels) + 8 B state + 88 B/(N-1) point data, times the
-          residuals that do gather (not OOB before the pass), / its mean HIP-event duration;
+          residuals that do gather (not OOB before the pass), / its mean HIP-event duration
+          over the timed region (the event pair on every EVENT_EVERY-th timed step);
           frac_step: the same bytes over the sum of the pass's kernel durations (k_linearize,
           k_point_sc, k_stitch, k_stitch_sum: §8d's step-level definition), frac_step_wall over the
           step's wall clock.
@@ -38,6 +39,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "point-residuals/sec per GN iter (7-KF window) + ms/solve; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+EVENT_EVERY = 5  # timed steps whose k_linearize the roofline's HIP event pair brackets: every 5th
 
 
 def algo_bytes_per_residual(n_frames):
@@ -594,16 +596,17 @@ def main():
     ctx.sync()
     torch.cuda.synchronize()
 
-    # HIP events bracket only the dominant kernel inside the timed region (each event pair
-    # costs the stream a few us); the per-kernel breakdown is taken afterwards
-    ctx.set_tuning(7, 1)  # LDSO_BA_TUNE_TIMING_MASK: slot 0 = k_linearize
+    # HIP events bracket only the dominant kernel inside the timed region, on every EVENT_EVERY-th
+    # step (each event pair costs the stream ~4-6 us; the sampled launches are the same kernel on
+    # the same inputs); the per-kernel breakdown is taken afterwards
     ctx.set_kernel_timing(True)
     if dist is not None:
         dist.barrier()
     ctx.sync()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for s in range(args.steps):
+        ctx.set_tuning(7, 1 if s % EVENT_EVERY == 0 else 0)  # LDSO_BA_TUNE_TIMING_MASK: slot 0 = k_linearize
         step()
     ctx.sync()
     torch.cuda.synchronize()
@@ -785,6 +788,8 @@ def main():
                 "traffic_source": traffic_source,
                 "kernel": "k_linearize",
                 "avg_launch_us": klin_avg_s * 1e6,
+                "event_launches": int(klin_n),
+                "event_every": EVENT_EVERY,
                 "algo_bytes_per_launch": bytes_per_launch,
                 "algo_bytes_per_residual": algo_bytes_per_residual(N),
                 "frac_step": frac_step,
