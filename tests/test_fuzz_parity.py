@@ -72,3 +72,47 @@ def test_random_windows_match_oracle(built, case):
             compare_pass(ctx, ow, i, e_cpu, s_cpu)
             ow.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_random_point_marginalisation_matches_oracle(built, case):
+    """flagPointsForRemoval -> fixLinearizationF -> marginalizePointsF on random windows (2-11
+    keyframes, the sizes and motions above) with a random subset of points (host 0's and a random
+    fraction of the rest) and random linearisation deltas: residual states, JpJdF and the point
+    terms bit-exact against the oracle, H / b per 8x8 block within 1e-4 (test_marginalization's bars)."""
+    from ldso_amd import dist as ldist
+    from test_marginalization import ad_ht_delta, block_err, vec_err
+
+    rng = np.random.default_rng(7000 + case)
+    W, H = SIZES[rng.integers(len(SIZES))]
+    cfg = dict(n_frames=int(rng.integers(2, 12)), n_points=int(rng.integers(50, 600)), width=W, height=H,
+               seed=int(rng.integers(1 << 30)), motion=str(rng.choice(["sideways", "forward"])),
+               outlier_frac=float(rng.uniform(0.0, 0.2)))
+    frac, scale = float(rng.uniform(0.05, 0.5)), float(rng.choice([0.0, 1.0, 3.0]))
+    print(f"case {case}: {cfg}, fraction {frac:.2f}, delta scale {scale}")
+    w = synth.make_window(**cfg)
+    N = w.n_frames
+    S = np.array(sorted(set(np.flatnonzero(w.point_host == 0)) |
+                        set(np.flatnonzero(rng.random(w.n_points) < frac))), np.int64)
+    adh = ad_ht_delta(w, scale)
+    parent = BAContext(0).load([w])
+    parent.linearize()
+    parent.sync()
+    m = BAContext(0).load_marginalization(parent, 0, ldist.subset_window(w, S))
+    Hm, bm = m.marginalize_points(adh)
+    ow = oracle.OracleWindow(synth.make_window(**cfg), threads=0)
+    Ho, bo = ow.marginalize_points(S.astype(np.int32), adh)
+    assert block_err(Hm, Ho, N) <= 1e-4
+    assert vec_err(bm, bo, N) <= 1e-4
+    rg, ro = m.residuals(0), ow.residuals()
+    rs = np.concatenate([np.arange(w.point_res_begin[p], w.point_res_begin[p + 1]) for p in S])
+    for k in ("new_state", "state", "flags", "state_energy", "center"):
+        np.testing.assert_array_equal(rg[k], ro[k][rs], err_msg=k)
+    act = (ro["flags"][rs] & 1).astype(bool)
+    np.testing.assert_array_equal(rg["jpjdf"][act], ro["jpjdf"][rs][act])
+    pg, po = m.points(0), ow.points()
+    for k in ("HdiF", "bdSumF", "idepth_hessian"):
+        np.testing.assert_array_equal(pg[k], po[k][S], err_msg=k)
+    m.close()
+    parent.close()
+    ow.close()
