@@ -6,7 +6,9 @@ forward or sideways motion (scale change, OOB pattern pixels), outlier fraction,
 border, the residuals per k_linearize wavefront (8..64 or automatic), both image layouts and the
 affine-optimisation modes.  Bars as tests/test_gpu_parity.py's compare_pass: per residual and per
 point bit-exact, the energy to 1e-12, the stitched blocks within 1e-4, the priors exact.
-Each case prints its draw, so a failure names the configuration to rerun."""
+After the accumulating pass each case also runs the fix pass (linearizeAll(true) after resetOOB:
+relBS of the new residuals) against the oracle's.  Each case prints its draw, so a failure names
+the configuration to rerun."""
 import numpy as np
 import pytest
 
@@ -65,11 +67,21 @@ def test_random_windows_match_oracle(built, case):
     ctx.set_tuning(2, layout)  # LDSO_BA_TUNE_TILED_IMAGES
     ctx.set_settings(s).load([window(c, s) for c in wins])
     ctx.linearize(fix=False, accumulate=True)
+    ows = []
     with oracle.affine_opt_modes(*aff):
         for i, c in enumerate(wins):
             ow = oracle.OracleWindow(window(c, s), threads=0)
             e_cpu, s_cpu = ow.iteration()
             compare_pass(ctx, ow, i, e_cpu, s_cpu)
+            ows.append(ow)
+        # then the fix pass (linearizeAll(true): relBS of the new residuals) after resetOOB
+        ctx.reset_oob()
+        ctx.linearize(fix=True, accumulate=False)
+        for i, ow in enumerate(ows):
+            ow.reset_oob()
+            e_cpu = ow.linearize_all(True)
+            compare_pass(ctx, ow, i, e_cpu, None, check_system=False)
+            np.testing.assert_array_equal(ctx.residuals(i)["rel_bs"], ow.residuals()["rel_bs"])
             ow.close()
     ctx.close()
 
