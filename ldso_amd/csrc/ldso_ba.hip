@@ -3360,14 +3360,16 @@ __device__ __forceinline__ double fast_row(const double *v, int k) {
     else
         return k < 64 ? readlane_f64(v[0], k) : readlane_f64(v[1], k - 64);
 }
-// Wave 0: LDL^T of panel columns p .. p+w-1 (rows lane + 64 h) and the forward substitution
-// L y = b over the same columns (y in wave 0's registers across panels).  Lane i updates its
-// rows' panel entries unconditionally -- entries above the diagonal and rows past n turn into
-// finite junk that is never stored nor read -- so a step is one readlane pair, one product
-// cj / d and one fma per later column and row half, with the h = 1 half compiled out for n <= 64.
+// Wave 0: LDL^T of panel columns p .. p+w-1 (rows lane + 64 h).  Lane i updates its rows' panel
+// entries unconditionally -- entries above the diagonal and rows past n turn into finite junk that
+// is never stored nor read -- so a step is one readlane pair, one product cj / d and one fma per
+// later column and row half, with the h = 1 half compiled out for n <= 64.  Only what the pivot
+// chain needs runs here: the step's column c and 1/d go to LDS (Wc, rdv), and the other waves
+// write L(i, k) = c_i / d and d into H (fast_store_l) and run the forward substitution
+// (fast_forward) from them while this wave factorises the next panel: the same statements, so the
+// same bits as when this wave did both (round 6: 40 -> 25 instructions per pivot on the chain).
 template <int kH>
-__device__ __forceinline__ void fast_panel(double *H, double *Wc, double *rdv, double *y, int n, int ld, int p,
-                                           int w, int lane) {
+__device__ __forceinline__ void fast_panel(double *H, double *Wc, double *rdv, int n, int ld, int p, int w, int lane) {
 #pragma clang fp contract(off)
     double r[kSolveFastPanel][kH];
 #pragma unroll
@@ -3393,21 +3395,38 @@ __device__ __forceinline__ void fast_panel(double *H, double *Wc, double *rdv, d
 #pragma unroll
             for (int h = 0; h < kH; h++) r[jj][h] = fma(-r[kk][h], wj, r[jj][h]);
         }
-        const double yk = fast_row<kH>(y, k);  // final: every earlier column already applied
+#pragma unroll
+        for (int h = 0; h < kH; h++) Wc[kk * 128 + lane + 64 * h] = r[kk][h];  // 128 rows a column
+        rdv[kk] = rd;  // every lane the same value: no exec-mask branch
+    }
+}
+// L(i, k) = c_i * (1/d) below the diagonal and d on it, for the w columns of panel p (columns c and
+// 1/d from Wc / rdv), threads t, t + nth, ...; rows above the diagonal are never read
+__device__ __forceinline__ void fast_store_l(double *H, const double *Wp, const double *rp, int n, int ld, int p,
+                                             int w, int t, int nth) {
+#pragma clang fp contract(off)
+    for (int e = t; e < (n - p) * w; e += nth) {
+        const int i = p + e / w, kk = e % w, k = p + kk;
+        if (i >= k) H[i * ld + k] = i > k ? Wp[kk * 128 + i] * rp[kk] : Wp[kk * 128 + i];
+    }
+}
+// the forward substitution L y = b over panel p's w columns (y in the calling wave's registers,
+// rows lane, lane + 64): y_i = fma(-L(i, k), y_k, y_i) for k in order
+template <int kH>
+__device__ __forceinline__ void fast_forward(const double *Wp, const double *rp, double *y, int p, int w, int lane) {
+#pragma clang fp contract(off)
+    for (int kk = 0; kk < w; kk++) {
+        const int k = p + kk;
+        const double yk = fast_row<kH>(y, k), rd = rp[kk];
 #pragma unroll
         for (int h = 0; h < kH; h++) {
             const int i = lane + 64 * h;
-            const double l = i > k ? r[kk][h] * rd : 0.0;  // L(i,k) (rd = 0 for d = 0)
+            const double l = i > k ? Wp[kk * 128 + i] * rd : 0.0;  // L(i,k) (rd = 0 for d = 0)
             y[h] = fma(-l, yk, y[h]);
-            Wc[kk * 128 + i] = r[kk][h];  // 128 rows a column; the trailing updates read rows >= p + w only
-            // L below the diagonal, d on it; rows above it hold junk (nothing reads H's upper
-            // triangle after the assembly)
-            if (i < n) H[i * ld + k] = i > k ? l : d;
         }
-        if (lane == 0) rdv[kk] = rd;
     }
 }
-// Wave 0, after the last panel: D, L^T x = y (y in lanes i, i + 64), x = s y into S.y
+// After the last panel (the wave holding y): D, L^T x = y (y in lanes i, i + 64), x = s y into S.y
 template <int kH>
 __device__ __forceinline__ void fast_back_subst(const double *H, const SolveLds &S, double *y, int n, int ld,
                                                 int lane) {
@@ -3494,24 +3513,31 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
     op.load(P, W, tid, kSolveFastThreads);
     solve_assemble<kSolveFastThreads>(P, W, S, tid);
     op.store(P, W, S, tid, kSolveFastThreads);  // published by the factorisation's barriers
-    double y[2] = {0.0, 0.0};  // wave 0: the forward substitution's y (rows lane, lane + 64)
-    if (wave == 0) {
+    double y[2] = {0.0, 0.0};  // wave 1: the forward substitution's y (rows lane, lane + 64)
+    if (wave == 1) {
         y[0] = lane < n ? S.b[lane] : 0.0;
         y[1] = lane + 64 < n ? S.b[lane + 64] : 0.0;
     }
     auto panel = [&](int p, int w, int buf) {
         double *Wb = Wc + buf * kSolveFastPanel * 128, *rb = rdv + buf * kSolveFastPanel;
         if (n > 64)
-            fast_panel<2>(H, Wb, rb, y, n, ld, p, w, lane);
+            fast_panel<2>(H, Wb, rb, n, ld, p, w, lane);
         else
-            fast_panel<1>(H, Wb, rb, y, n, ld, p, w, lane);
+            fast_panel<1>(H, Wb, rb, n, ld, p, w, lane);
+    };
+    auto forward = [&](const double *Wp, const double *rp, int p, int w) {
+        if (n > 64)
+            fast_forward<2>(Wp, rp, y, p, w, lane);
+        else
+            fast_forward<1>(Wp, rp, y, p, w, lane);
     };
     // Blocked right-looking LDL^T with look-ahead: after panel p is factorised, all waves apply
     // it to the next panel's columns; then wave 0 factorises the next panel while the other
     // waves apply panel p to the rest of the trailing triangle (double-buffered panel columns).
     if (wave == 0) panel(0, min(kSolveFastPanel, n), 0);
     __syncthreads();
-    for (int p = 0, buf = 0; p + kSolveFastPanel < n; p += kSolveFastPanel, buf ^= 1) {
+    int p = 0, buf = 0;
+    for (; p + kSolveFastPanel < n; p += kSolveFastPanel, buf ^= 1) {
         const int w = kSolveFastPanel, m0 = p + w, w1 = min(kSolveFastPanel, n - m0), m1 = m0 + w1;
         const double *Wp = Wc + buf * kSolveFastPanel * 128, *rp = rdv + buf * kSolveFastPanel;
         for (int e = tid; e < (n - m0) * w1; e += kSolveFastThreads) {  // the next panel's columns
@@ -3521,7 +3547,8 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
         __syncthreads();
         if (wave == 0) {
             panel(m0, w1, buf ^ 1);
-        } else {  // the rest of the trailing triangle (m1 <= j <= i < n)
+        } else {  // panel p's forward substitution, the rest of the trailing triangle (m1 <= j <= i < n), L and d of panel p
+            if (wave == 1) forward(Wp, rp, p, w);
             const int nt = n - m1, ne = nt * (nt + 1) / 2;
             for (int e = tid - 64; e < ne; e += kSolveFastThreads - 64) {
                 int ii = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);  // row ii of the nt x nt triangle
@@ -3530,10 +3557,18 @@ __global__ __launch_bounds__(kSolveFastThreads) void k_solve_fast(SolveParams P)
                 const int i = m1 + ii, j = m1 + (e - ii * (ii + 1) / 2);
                 H[i * ld + j] = fast_update(Wp, rp, w, i, j, H[i * ld + j]);
             }
+            fast_store_l(H, Wp, rp, n, ld, p, w, tid - 64, kSolveFastThreads - 64);
         }
         __syncthreads();
     }
-    if (wave == 0) {
+    {  // the last panel (p, buffer buf): its forward substitution and L, then the backward one
+        const double *Wl = Wc + buf * kSolveFastPanel * 128, *rl = rdv + buf * kSolveFastPanel;
+        const int wl = n - p;
+        if (wave == 1) forward(Wl, rl, p, wl);
+        fast_store_l(H, Wl, rl, n, ld, p, wl, tid, kSolveFastThreads);
+    }
+    __syncthreads();
+    if (wave == 1) {
         if (n > 64)
             fast_back_subst<2>(H, S, y, n, ld, lane);
         else
