@@ -20,6 +20,17 @@
 
 #include "ldso_ba_internal.h"
 
+// sin and cos of one argument: on the device one shared range reduction (the device library's
+// sincos gives the bits of its sin and cos); on the host the two libm calls
+LDSO_HD inline void sin_cos(double x, double &s, double &c) {
+#ifdef __HIP_DEVICE_COMPILE__
+    sincos(x, &s, &c);
+#else
+    s = sin(x);
+    c = cos(x);
+#endif
+}
+
 namespace ldso_ba {
 
 constexpr double kScaleXiTrans = 0.5, kScaleXiRot = 1.0, kScaleA = 10.0, kScaleB = 1000.0;
@@ -184,8 +195,10 @@ struct Pose {  // Sophus SE3: x -> R(q) x + t
             imag = (0.5 - (1.0 / 48.0) * theta_sq) + (1.0 / 3840.0) * theta_po4;
             real = (1.0 - (1.0 / 8.0) * theta_sq) + (1.0 / 384.0) * theta_po4;
         } else {
-            imag = sin(half_theta) / theta;
-            real = cos(half_theta);
+            double sh, ch;
+            sin_cos(half_theta, sh, ch);
+            imag = sh / theta;
+            real = ch;
         }
         Pose p;
         p.q[0] = imag * w[0];
@@ -197,7 +210,9 @@ struct Pose {  // Sophus SE3: x -> R(q) x + t
         if (theta < kSophusEps) {
             V = p.rotation_matrix();
         } else {
-            const double s1 = (1.0 - cos(theta)) / theta_sq, s2 = (theta - sin(theta)) / (theta_sq * theta);
+            double st, ct;
+            sin_cos(theta, st, ct);
+            const double s1 = (1.0 - ct) / theta_sq, s2 = (theta - st) / (theta_sq * theta);
             for (int k = 0; k < 9; k++) V.m[k] = ((k % 4 == 0 ? 1.0 : 0.0) + s1 * W.m[k]) + s2 * W2.m[k];
         }
         mat_vec(V, a, p.t);
@@ -225,7 +240,9 @@ struct Pose {  // Sophus SE3: x -> R(q) x + t
             for (int k = 0; k < 9; k++) Vi.m[k] = ((k % 4 == 0 ? 1.0 : 0.0) - 0.5 * W.m[k]) + (1. / 12.) * W2.m[k];
         } else {
             const double half_theta = 0.5 * theta;
-            const double c = (1.0 - (theta * cos(half_theta)) / (2.0 * sin(half_theta))) / (theta * theta);
+            double sh, ch;
+            sin_cos(half_theta, sh, ch);
+            const double c = (1.0 - (theta * ch) / (2.0 * sh)) / (theta * theta);
             for (int k = 0; k < 9; k++) Vi.m[k] = ((k % 4 == 0 ? 1.0 : 0.0) - 0.5 * W.m[k]) + c * W2.m[k];
         }
         mat_vec(Vi, t, xi);
