@@ -6851,6 +6851,13 @@ int ldso_ba_set_kernel_timing(ldso_ba_ctx *c, int32_t enable) {
         c->kms[i] = 0;
         c->kcount[i] = 0;
     }
+    // the events the timed launches will take, created now: hipEventCreate is a host call of tens of
+    // us, which inside a timed loop would stall the launches (kept in the pool across calls)
+    while (c->timing && c->ev_pool.size() < 256) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) break;
+        c->ev_pool.push_back(e);
+    }
     return 0;
 }
 
