@@ -4048,15 +4048,30 @@ __device__ __forceinline__ void frame_step_block(const FrameStepParams &P, int b
         P.status[blk] = LDSO_BA_OPT_CONVERGED;
     }
     ldso_ba_frame_state *fs = P.fstate + W.frame_base;
-    if (tid < N) {
-        ldso_ba_frame_state o;
-        frame_step_one(fs[tid], xw + 4 + 8 * tid, o);
-        fs[tid] = o;
-        const Pose e = eval_pose(o), c = current_pose(o);
-        const Pose ps[4] = {e, e.inverse(), c, c.inverse()};
-        for (int q = 0; q < 4; q++) {
-            for (int k = 0; k < 4; k++) poses[tid][q][k] = ps[q].q[k];
-            for (int k = 0; k < 3; k++) poses[tid][q][4 + k] = ps[q].t[k];
+    if (tid < 64) {
+        // frame_step_one's two exponentials in one SIMT pass of the same code: lane f forms
+        // exp(step_f), lane 32 + f exp(state_f), handed to lane f by a shuffle (N <= 16 < 32)
+        const int f = tid & 31, fc = f < N ? f : 0;
+        const ldso_ba_frame_state in = fs[fc];
+        double v[6];
+        if (tid < 32)
+            frame_step_tangent(xw + 4 + 8 * fc, v);
+        else
+            for (int i = 0; i < 6; i++) v[i] = in.state[i];
+        const Pose ex = Pose::exp(v);
+        Pose eb;
+        for (int k = 0; k < 4; k++) eb.q[k] = __shfl(ex.q[k], fc + 32, 64);
+        for (int k = 0; k < 3; k++) eb.t[k] = __shfl(ex.t[k], fc + 32, 64);
+        if (tid < N) {
+            ldso_ba_frame_state o;
+            frame_step_finish(in, xw + 4 + 8 * tid, ex, eb, o);
+            fs[tid] = o;
+            const Pose e = eval_pose(o), c = current_pose(o);
+            const Pose ps[4] = {e, e.inverse(), c, c.inverse()};
+            for (int q = 0; q < 4; q++) {
+                for (int k = 0; k < 4; k++) poses[tid][q][k] = ps[q].q[k];
+                for (int k = 0; k < 3; k++) poses[tid][q][4 + k] = ps[q].t[k];
+            }
         }
     } else if (tid == 64) {
         double *v = P.calib_val + 4 * blk;

@@ -360,17 +360,25 @@ LDSO_HD inline void frame_take_data_one(const ldso_ba_frame_state &F, float mode
 // (setting_solverMode = FIX_LAMBDA | ORTHOGONALIZE_X_LATER) at stepfac 1, for one frame:
 // step = -x.segment<8>(CPARS + 8 idx) (resubstituteF_MT, EnergyFunctional.cc:618-623), then
 // state = state_backup + step except head<6> = log(exp(step.head<6>) exp(state_backup.head<6>)).
-LDSO_HD inline void frame_step_one(const ldso_ba_frame_state &in, const double *x8, ldso_ba_frame_state &out) {
+// the step's tangent: pstepfac.head<6>().cwiseProduct(step.head<6>()), step = -x
+LDSO_HD inline void frame_step_tangent(const double *x8, double a[6]) {
+#pragma clang fp contract(off)
+    for (int i = 0; i < 6; i++) a[i] = 1.0 * -x8[i];
+}
+// the rest of the step once exp(a) and exp(state) are formed
+LDSO_HD inline void frame_step_finish(const ldso_ba_frame_state &in, const double *x8, const Pose &ea, const Pose &eb,
+                                      ldso_ba_frame_state &out) {
 #pragma clang fp contract(off)
     out = in;
-    double st[10], a[6], b[6], lg[6];
+    double st[10], lg[6];
     for (int i = 0; i < 10; i++) st[i] = i < 8 ? -x8[i] : 0.0;
-    for (int i = 0; i < 6; i++) {
-        a[i] = 1.0 * st[i];  // pstepfac.head<6>().cwiseProduct(step.head<6>())
-        b[i] = in.state[i];
-    }
-    (Pose::exp(a) * Pose::exp(b)).log(lg);
+    (ea * eb).log(lg);
     for (int i = 0; i < 10; i++) out.state[i] = i < 6 ? lg[i] : in.state[i] + 1.0 * st[i];
+}
+LDSO_HD inline void frame_step_one(const ldso_ba_frame_state &in, const double *x8, ldso_ba_frame_state &out) {
+    double a[6];
+    frame_step_tangent(x8, a);
+    frame_step_finish(in, x8, Pose::exp(a), Pose::exp(in.state), out);
 }
 
 // ... and the calibration: HCalib->step = -x.head<CPARS>(), setValue(value_backup + step)
