@@ -1,0 +1,75 @@
+"""Randomised tracker parity sweep: seeded draws of frame size (including
+sizes whose pyramid stops early: odd widths / heights), camera model, photometric response,
+affine exposure terms, pose magnitude (up to motions that push most points out of the frame) and
+outlier cut-off, through makeImages, calcRes and calcGSSSE on the GPU against the oracle:
+pyramid images, absSquaredGrad and the warped buffers bit for bit.  The reference sums calcRes's
+energy and shift terms in float, point by point (the oracle does too), the GPU in double: their
+gap is the float sum's own rounding, bounded by n u sum|x| (n terms, u = 2^-24; every term is
+non-negative, so sum|x| is the sum), which at 8000 points and large energies exceeds
+tests/test_tracker.py's fixed 1e-5 (one draw: 5.7e-5).  The bar here is that bound, and for
+calcGSSSE's H and b (Accumulator9's blocked float sums) max(1e-5, 2 n u) of their largest entry."""
+import numpy as np
+import pytest
+
+import oracle
+from ldso_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(640, 480), (752, 480), (424, 240), (317, 203), (1242, 375), (1232, 368), (160, 120)]
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_random_tracker_calls_match_oracle(built, case):
+    from ldso_amd.tracker import CoarseTracker
+    from test_tracker import pc_tuple
+
+    rng = np.random.default_rng(5000 + case)
+    w, h = SIZES[rng.integers(len(SIZES))]
+    color, make_pc = synth.make_tracker_scene(w, h, seed=int(rng.integers(1 << 30)))
+    B = (255 * (np.linspace(0, 1, 256) ** float(rng.uniform(0.6, 1.4)))).astype(np.float32) if rng.random() < 0.5 else None
+    levels = oracle.make_images(color, w, h, B)
+    pcs = make_pc([dI[:, 0] for dI, _ in levels])
+    f = float(rng.uniform(0.45, 1.1)) * w
+    calib = np.array([f, f * float(rng.uniform(0.95, 1.05)), (w - 1) / 2 + float(rng.uniform(-0.05, 0.05)) * w,
+                      (h - 1) / 2 + float(rng.uniform(-0.05, 0.05)) * h], np.float32)
+    aff6 = (float(rng.uniform(0.5, 2.0)), float(rng.uniform(0.5, 2.0)), float(rng.normal(0, 0.05)),
+            float(rng.normal(0, 5)), float(rng.normal(0, 0.05)), float(rng.normal(0, 5)))
+    print(f"case {case}: {w}x{h}, B {'yes' if B is not None else 'no'}, calib {calib}, aff6 {aff6}")
+    ct = CoarseTracker(w, h)
+    assert ct.levels == len(levels)
+    K = ct.make_k(calib)
+    np.testing.assert_array_equal(K, oracle.ct_make_k(calib, w, h))
+    ct.set_new_frame(color, aff6[1], B)
+    for l, (dI, ag) in enumerate(levels):
+        gdI, gag = ct.frame_level(l)
+        np.testing.assert_array_equal(gdI, dI)
+        np.testing.assert_array_equal(gag, ag)
+    ct.set_reference([pc_tuple(p) for p in pcs], aff6[0], aff6[2:4])
+    for l in range(len(levels)):
+        wl, hl = w >> l, h >> l
+        for _ in range(2):
+            scale = float(rng.choice([0.3, 1.0, 4.0, 20.0])) * 2.0 ** l
+            T = synth.se3_matrix(rng.normal(0, 2e-3, 3) * scale, rng.normal(0, 1e-2, 3) * scale)
+            cutoff = float(rng.uniform(6.0, 30.0))
+            rs_o, warped_o = oracle.ct_calc_res(l, wl, hl, K[l], levels[l][0], pc_tuple(pcs[l]), T, aff6, cutoff)
+            rs = ct.calc_res(l, T, aff6[4:6], cutoff)
+            assert rs[1] == rs_o[1]
+            u = 2.0 ** -24
+            n = max(float(len(pcs[l]["u"])), 1.0)  # float additions of the reference's sums
+            assert abs(rs[0] - rs_o[0]) <= n * u * abs(rs_o[0]) + 1e-6
+            for k in (2, 4):
+                assert abs(rs[k] - rs_o[k]) <= n * u * abs(rs_o[k]) + 1e-9, k
+            assert rs[3] == 0 and abs(rs[5] - rs_o[5]) <= 1e-7
+            np.testing.assert_array_equal(ct.warped(), warped_o)
+            if rs_o[1] > 0:
+                H, b = ct.calc_gs(l, T, aff6[4:6])
+                Ho, bo = oracle.ct_calc_gs(warped_o, K[l, 0], K[l, 1], aff6)
+                nw = warped_o.shape[0]
+                if nw == 0:  # every term saturated: calcGSSSE divides by zero rows, NaN on both sides
+                    assert np.isnan(Ho).all() and np.isnan(H).all() and np.isnan(b).all(), l
+                    continue
+                tol = max(1e-5, 2 * nw * u)
+                assert np.abs(H - Ho).max() <= tol * np.abs(Ho).max(), l
+                assert np.abs(b - bo).max() <= tol * np.abs(bo).max(), l
+    ct.close()
