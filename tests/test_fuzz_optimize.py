@@ -11,7 +11,7 @@ solve (about one float ulp: the size of the GPU's reassociated partial sums).  A
 stay 30-100x the convergence thresholds (most random draws here) passes such differences into x
 along its near-gauge directions and its later passes follow them (test_optimize's note): one
 two-keyframe draw differs from the host loop by 6.5e-5 at pass 1 and 1.3e-4 at pass 2, the
-perturbed host loops from each other by 7.0e-5 and 1.2e-4.  The loop runs three iterations.
+perturbed host loops from each other by 7.8e-5 and 2.6e-4.  The loop runs three iterations.
 Iteration count and exit status are compared only when the canbreak ratios of the host loop stay
 5 % away from the threshold at every iteration (the ratios and the decision are printed);
 otherwise the float reassociation of x may flip it, and that draw checks the passes both loops
