@@ -87,3 +87,62 @@ def test_random_trace_matches_oracle(built, case):
         assert bad.size == 0, (t, bad[:5], got[bad[:2]], ref[bad[:2]])
         np.testing.assert_array_equal(c, cr)
     ct.close()
+
+
+ACT_SIZES = [(160, 120), (317, 203), (640, 480), (1242, 375)]
+
+
+@pytest.mark.parametrize("case", range(10))
+def test_random_activation_matches_oracle(built, case):
+    """optimizeImmaturePoint (ldso_ba_activate_points) on random windows: 2-16 keyframes, the sizes,
+    camera models, motions and outliers of tests/test_fuzz_parity.py, interval spreads 1-60 % with
+    random offsets (true depth inside or outside), random colour offsets on a fraction of the
+    points, non-finite and empty intervals, energy thresholds and min_obs drawn at random, both
+    image layouts, and the activated window drawn from a context holding one to three windows:
+    every record (idepth, status, residual mask, energy) bit for bit against the oracle."""
+    from ldso_amd import BAContext, synth
+    from test_activation import differing as act_differing
+
+    rng = np.random.default_rng(17000 + case)
+    W, H = ACT_SIZES[rng.integers(len(ACT_SIZES))]
+    cfgs = []
+    for _ in range(int(rng.integers(1, 4))):
+        N = int(rng.integers(2, 17))
+        calib = None
+        if rng.random() < 0.5:
+            f = float(rng.uniform(0.4, 1.2)) * W
+            calib = [f, f * float(rng.uniform(0.95, 1.05)), W / 2 + float(rng.uniform(-0.1, 0.1)) * W,
+                     H / 2 + float(rng.uniform(-0.1, 0.1)) * H]
+        cfgs.append(dict(n_frames=N, n_points=int(rng.integers(1, 1200 if N <= 8 else 400)), width=W, height=H,
+                         seed=int(rng.integers(1 << 30)), outlier_frac=float(rng.uniform(0.0, 0.3)),
+                         motion=str(rng.choice(["sideways", "forward"])), calib=calib,
+                         edge_frac=float(rng.choice([0.0, 0.2])), plane_depth=max(25.0, 2.5 * (N - 1))))
+    k = int(rng.integers(len(cfgs)))
+    layout = int(rng.choice([1, 3]))
+    print(f"case {case}: layout {layout}, activating window {k} of {len(cfgs)}")
+    for c in cfgs:
+        print("  ", c)
+    w = synth.make_window(**cfgs[k])
+    pts = synth.immature_from_window(w, spread=float(rng.uniform(0.01, 0.6)), seed=case)
+    P = len(pts)
+    off = rng.uniform(-0.3, 0.3, P).astype(np.float32) * (rng.random(P) < 0.3)
+    pts["idepth_min"] *= 1 + off
+    pts["idepth_max"] *= 1 + off
+    bad = rng.random(P) < 0.1
+    pts["color"][bad] += rng.normal(0, 60, (int(bad.sum()), 1)).astype(np.float32)
+    pts["idepth_max"][rng.random(P) < 0.03] = np.nan
+    e = rng.random(P) < 0.03
+    pts["idepth_min"][e] = pts["idepth_max"][e] = 0.0
+    pts["energy_th"] = np.float32(rng.uniform(2, 12)) * np.float32(144)
+    ctx = BAContext(0)
+    ctx.set_tuning(2, layout)  # LDSO_BA_TUNE_TILED_IMAGES, before load
+    ctx.load([synth.make_window(**c) for c in cfgs])
+    ow = oracle.OracleWindow(synth.make_window(**cfgs[k]), threads=0)
+    for min_obs in sorted({1, int(rng.integers(1, cfgs[k]["n_frames"] + 1))}):
+        got = ctx.activate_points(k, pts, min_obs)
+        ref = ow.activate_points(pts, min_obs)
+        bad = act_differing(got, ref)
+        print(f"  min_obs {min_obs}: statuses {np.bincount(ref['status'], minlength=3).tolist()}")
+        assert bad.size == 0, (min_obs, bad[:5], got[bad[:3]], ref[bad[:3]])
+    ow.close()
+    ctx.close()
