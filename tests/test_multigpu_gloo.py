@@ -64,7 +64,7 @@ def _worker(rank, world, port, q):  # noqa: C901
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_shards_reduce_to_full_window(built, world):
     import oracle
     from ldso_amd import dist as ldist
@@ -211,10 +211,11 @@ def _opt_worker(rank, world, port, q, cfgs):
 
 
 @pytest.mark.timeout(600)
-def test_sharded_optimize_loop_matches_unsharded(built):
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_optimize_loop_matches_unsharded(built, world):
     """The whole sharded GN loop (shard, pass, one all-reduce + one all-gather, redundant solve,
     shard-local resubstitution, step, canbreak on the sumNID chain over the gathered runs) over gloo
-    at world 2: every rank leaves the loop at the same iteration with the same status as the
+    at world 2, 3 and 4: every rank leaves the loop at the same iteration with the same status as the
     unsharded loop, energies within 1e-5 (the ranks' float partials only reassociate), #IN equal,
     frame states within 5 % of the unsharded loop's total step; the first pass's sumNID (same
     idepths on both sides) bit-exact."""
@@ -222,7 +223,6 @@ def test_sharded_optimize_loop_matches_unsharded(built):
     from test_optimize import CONVERGES, RUNS_ALL
 
     cfgs = [CONVERGES, RUNS_ALL]
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
